@@ -1,0 +1,181 @@
+/*
+ * mq_aead.h — C ABI of the MI355X-native QUIC packet-protection library (libmq_aead.so).
+ *
+ * Drop-in boundary for milli-quic's packet-protection path (reference at
+ * computer-whisperer/milli-quic; all file:line citations below are relative to that tree):
+ *
+ *   trait Aead              src/crypto/aead.rs:8-42          -> mq_aead_* (per-packet, in place)
+ *   trait HeaderProtection  src/crypto/header_protection.rs:6-13 -> mq_hp_*
+ *   trait CryptoProvider    src/crypto/mod.rs:38-51          -> mq_aead_new / mq_hp_new (suite + key)
+ *   trait Hkdf + key_schedule src/crypto/hkdf.rs:7-16, src/crypto/key_schedule.rs:23-151 -> mq_hkdf_* / mq_derive_*
+ *   DirectionalKeys::nonce  src/crypto/mod.rs:66-74          -> mq_nonce
+ *
+ * plus a device-resident BATCH API (mq_batch_*), which the reference lacks: it runs the send
+ * composite of src/connection/transmit.rs:499-755 (seal + header protection) and the receive
+ * composite of src/connection/recv.rs:340-421,953-1025 (header-protection removal, decode_pn,
+ * open) over a whole arena of packets in HBM, one packet per GPU lane, ordered on a HIP stream.
+ *
+ * All entry points take plain pointers and sizes. Every compute path runs on the GPU (gfx950);
+ * there is no CPU fallback: without a usable device the calls return MQ_ERR_NO_DEVICE.
+ */
+#ifndef MQ_AEAD_H
+#define MQ_AEAD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (reference: src/error.rs:144-170) ------------------------------------- */
+#define MQ_OK                    0  /* Ok(..)                                               */
+#define MQ_ERR_CRYPTO            1  /* Error::Crypto: bad nonce length, short ciphertext,
+                                       tag mismatch, bad key length, sample out of range     */
+#define MQ_ERR_BUFFER_TOO_SMALL  2  /* Error::BufferTooSmall { needed }                     */
+#define MQ_ERR_INVALID_ARG       3  /* cases where the reference panics (index out of range:
+                                       rustcrypto.rs:83,154,180,201-204) or a NULL pointer   */
+#define MQ_ERR_PROTOCOL          4  /* Error::Transport(ProtocolViolation): decoded pn > 2^62-1
+                                       (recv.rs:393-395, 994-997)                             */
+#define MQ_ERR_SUITE             5  /* packet's key suite differs from the launched kernel's  */
+#define MQ_ERR_NO_DEVICE         6  /* no gfx950 device / HIP runtime failure                 */
+#define MQ_ERR_HIP               7  /* HIP runtime error during a call                        */
+
+/* ---- cipher suites (TLS_AES_128_GCM_SHA256 = 0x1301, TLS_CHACHA20_POLY1305_SHA256 = 0x1303;
+ *      reference tls/handshake.rs:636-654 maps KEY_LEN 16 -> 0x1301, 32 -> 0x1303) ----------- */
+#define MQ_SUITE_AES128GCM       1
+#define MQ_SUITE_CHACHA20        2
+#define MQ_SUITE_MIXED           0xFF /* batch hint: per-packet suite from the key table       */
+
+#define MQ_NONCE_LEN 12
+#define MQ_TAG_LEN   16
+#define MQ_SAMPLE_LEN 16
+#define MQ_MASK_LEN   5
+
+/* ---- key material (host side; what CryptoProvider::aead + ::header_protection consume) ---- */
+typedef struct mq_key_material {
+  uint32_t suite;      /* MQ_SUITE_AES128GCM or MQ_SUITE_CHACHA20                              */
+  uint32_t reserved;
+  uint8_t  key[32];    /* AEAD key: 16 B (AES) or 32 B (ChaCha20)                              */
+  uint8_t  iv[12];     /* DirectionalKeys::iv (src/crypto/mod.rs:57-59)                        */
+  uint8_t  pad[4];
+  uint8_t  hp[32];     /* header-protection key: 16 B (AES) or 32 B (ChaCha20)                 */
+} mq_key_material;     /* 88 bytes */
+
+/* ---- per-packet descriptor of the batch API (32 bytes, read once per packet) -------------- */
+#define MQ_PKT_LONG_HEADER  0x01  /* header protection masks byte 0 with 0x0f (else 0x1f)     */
+#define MQ_PKT_NO_HP        0x02  /* plain AEAD: no header protection, pn_len taken from the
+                                     descriptor on open, AAD = bytes [0, pn_offset + pn_len)  */
+
+typedef struct mq_pkt_desc {
+  uint64_t offset;     /* byte offset of the packet's first header byte in the arena            */
+  uint32_t len;        /* seal: bytes the protected packet occupies = pn_offset + pn_len +
+                          payload_len + 16 (the arena must hold them);
+                          open: protected length (pn_offset + Length for long headers)         */
+  uint32_t key_id;     /* row of the key table                                                  */
+  uint64_t pn;         /* seal: full packet number; open: largest_pn of the PN space (decode_pn) */
+  uint16_t pn_offset;  /* offset of the packet-number field (= 1 + dcid_len for short headers)  */
+  uint8_t  pn_len;     /* seal: encoded PN length 1..4 (already in the header); open: ignored
+                          unless MQ_PKT_NO_HP                                                     */
+  uint8_t  flags;      /* MQ_PKT_*                                                              */
+  uint32_t reserved;
+} mq_pkt_desc;
+
+/* ---- opaque handles ---------------------------------------------------------------------- */
+typedef struct mq_aead_ctx mq_aead_ctx;     /* one Aead instance (immutable after creation)      */
+typedef struct mq_hp_ctx mq_hp_ctx;         /* one HeaderProtection instance                     */
+typedef struct mq_keytable mq_keytable;     /* device-resident table of expanded keys            */
+
+/* ---- library / device ---------------------------------------------------------------------- */
+const char* mq_version(void);
+int mq_device_init(int device);            /* selects the HIP device used by this thread         */
+const char* mq_status_str(int status);
+
+/* ---- CryptoProvider::aead / Aead (per packet, host buffers; runs the HIP kernels) ----------- */
+/* provider.aead(key): key_len must equal KEY_LEN of the suite (rustcrypto.rs:234-236, 267-269) */
+int mq_aead_new(uint32_t suite, const uint8_t* key, size_t key_len, mq_aead_ctx** out);
+void mq_aead_free(mq_aead_ctx* ctx);
+size_t mq_aead_key_len(uint32_t suite);     /* Aead::KEY_LEN (16 / 32), 0 for an unknown suite   */
+/* Aead::seal_in_place (aead.rs:22-28, rustcrypto.rs:38-63 / 111-135): buf[..payload_len] holds
+ * plaintext; on MQ_OK buf[..payload_len+16] holds ciphertext||tag and *out_len = payload_len+16.
+ * MQ_ERR_CRYPTO if nonce_len != 12; MQ_ERR_BUFFER_TOO_SMALL (with *needed) if
+ * buf_len < payload_len + 16. */
+int mq_aead_seal_in_place(const mq_aead_ctx* ctx, const uint8_t* nonce, size_t nonce_len,
+                          const uint8_t* aad, size_t aad_len, uint8_t* buf, size_t buf_len,
+                          size_t payload_len, size_t* out_len, size_t* needed);
+/* Aead::open_in_place (aead.rs:35-41, rustcrypto.rs:65-94 / 137-165): buf[..ct_len] holds
+ * ciphertext||tag; on MQ_OK buf[..ct_len-16] holds plaintext and *out_len = ct_len - 16.
+ * MQ_ERR_CRYPTO on nonce_len != 12, ct_len < 16, or tag mismatch (buffer left unchanged);
+ * MQ_ERR_INVALID_ARG if ct_len > buf_len (the reference panics). */
+int mq_aead_open_in_place(const mq_aead_ctx* ctx, const uint8_t* nonce, size_t nonce_len,
+                          const uint8_t* aad, size_t aad_len, uint8_t* buf, size_t buf_len,
+                          size_t ct_len, size_t* out_len);
+
+/* ---- CryptoProvider::header_protection / HeaderProtection::mask ---------------------------- */
+int mq_hp_new(uint32_t suite, const uint8_t* key, size_t key_len, mq_hp_ctx** out);
+void mq_hp_free(mq_hp_ctx* ctx);
+/* HeaderProtection::mask (header_protection.rs:12; rustcrypto.rs:175-186 / 197-220):
+ * MQ_ERR_INVALID_ARG if sample_len < 16 (the reference panics). */
+int mq_hp_mask(const mq_hp_ctx* ctx, const uint8_t* sample, size_t sample_len, uint8_t mask[5]);
+
+/* ---- DirectionalKeys::nonce (src/crypto/mod.rs:66-74) -------------------------------------- */
+void mq_nonce(const uint8_t iv[12], uint64_t packet_number, uint8_t nonce[12]);
+
+/* ---- HKDF-SHA256 + QUIC key schedule (host; per connection, not per packet) ---------------- */
+/* Hkdf::extract / Hkdf::expand (rustcrypto.rs:9-24) */
+void mq_hkdf_extract(const uint8_t* salt, size_t salt_len, const uint8_t* ikm, size_t ikm_len,
+                     uint8_t prk[32]);
+int mq_hkdf_expand(const uint8_t* prk, size_t prk_len, const uint8_t* info, size_t info_len,
+                   uint8_t* okm, size_t okm_len);
+/* hkdf_expand_label (key_schedule.rs:23-55): MQ_ERR_CRYPTO if the info would exceed 80 bytes */
+int mq_hkdf_expand_label(const uint8_t* secret, size_t secret_len, const uint8_t* label,
+                         size_t label_len, const uint8_t* context, size_t context_len,
+                         uint8_t* out, size_t out_len);
+/* derive_initial_secrets (key_schedule.rs:60-72) */
+int mq_derive_initial_secrets(const uint8_t* dcid, size_t dcid_len, uint8_t client_secret[32],
+                              uint8_t server_secret[32]);
+/* derive_packet_keys + derive_directional_keys (key_schedule.rs:79-90, 123-151): fills key
+ * (KEY_LEN), iv, hp (max(KEY_LEN,16) bytes) of `out` for `suite` from a 32-byte secret */
+int mq_derive_key_material(uint32_t suite, const uint8_t* secret, size_t secret_len,
+                           mq_key_material* out);
+/* derive_next_application_secret (key_schedule.rs:114-120), label "quic ku" */
+int mq_derive_next_secret(const uint8_t* secret, size_t secret_len, uint8_t next[32]);
+
+/* ---- device key table ----------------------------------------------------------------------- */
+/* Expands every row (AES key schedules, GHASH subkey) on the host once and uploads the table. */
+int mq_keytable_create(const mq_key_material* rows, uint32_t n_rows, mq_keytable** out);
+int mq_keytable_update(mq_keytable* kt, uint32_t first_row, const mq_key_material* rows,
+                       uint32_t n_rows);
+uint32_t mq_keytable_rows(const mq_keytable* kt);
+void mq_keytable_free(mq_keytable* kt);
+
+/* ---- batch API (device pointers, stream-ordered, asynchronous) ------------------------------ */
+/* `arena` is device memory of `arena_len` bytes holding the packets; `desc` (n entries) and
+ * `status` (n bytes, written with MQ_* per packet) are device memory; `pn_out` (open only,
+ * may be NULL) receives each packet's decoded packet number. `suite_hint` is
+ * MQ_SUITE_CHACHA20 / MQ_SUITE_AES128GCM for a single-suite batch (one launch; rows of the
+ * other suite get MQ_ERR_SUITE) or MQ_SUITE_MIXED (packets are partitioned by suite on the
+ * device first; needs `workspace` of mq_batch_workspace_size(n) bytes of device memory).
+ * `stream` is a hipStream_t (NULL = default stream). Returns MQ_OK once the work is enqueued. */
+size_t mq_batch_workspace_size(uint32_t n);
+int mq_batch_seal(const mq_keytable* kt, uint8_t* arena, uint64_t arena_len,
+                  const mq_pkt_desc* desc, uint32_t n, uint8_t* status, uint32_t suite_hint,
+                  void* workspace, void* stream);
+int mq_batch_open(const mq_keytable* kt, uint8_t* arena, uint64_t arena_len,
+                  const mq_pkt_desc* desc, uint32_t n, uint8_t* status, uint64_t* pn_out,
+                  uint32_t suite_hint, void* workspace, void* stream);
+/* Batched HeaderProtection::mask: masks[i*5..] = mask(key_table[key_ids[i]].hp, samples[i*16..]) */
+int mq_batch_hp_mask(const mq_keytable* kt, const uint32_t* key_ids, const uint8_t* samples,
+                     uint8_t* masks, uint32_t n, void* stream);
+
+/* ---- timing hooks for bench.py (HIP events on the launch stream) ---------------------------- */
+/* Time `iters` back-to-back (seal, open) pairs on `stream`; returns per-kernel average ms. */
+int mq_batch_time_seal_open(const mq_keytable* kt, uint8_t* arena, uint64_t arena_len,
+                            const mq_pkt_desc* desc, uint32_t n, uint8_t* status, uint64_t* pn_out,
+                            uint32_t suite_hint, void* workspace, void* stream, int iters,
+                            float* seal_ms, float* open_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MQ_AEAD_H */

@@ -1,0 +1,115 @@
+"""Device-resident batch API: the send / receive composites of the reference over a whole arena.
+
+Reference composites reproduced per packet: send = build_and_encrypt_packet
+(src/connection/transmit.rs:625-755, Initial twin :499-622); receive = recv_short /
+decrypt_long_packet (src/connection/recv.rs:340-421, :953-1025). The reference processes one
+packet per call; here a batch of packets sitting in one HBM arena is protected in one launch.
+Torch supplies device memory and the stream only; the transforms are libmq_aead.so kernels.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .crypto import _raise
+
+DESC_DTYPE = np.dtype([
+    ("offset", "<u8"), ("len", "<u4"), ("key_id", "<u4"), ("pn", "<u8"),
+    ("pn_offset", "<u2"), ("pn_len", "u1"), ("flags", "u1"), ("reserved", "<u4"),
+])
+assert DESC_DTYPE.itemsize == 32
+
+
+def make_descs(offsets, lens, key_ids, pns, pn_offsets, pn_lens, flags):
+    """Build an mq_pkt_desc array (numpy structured, 32 B per packet)."""
+    n = len(offsets)
+    d = np.zeros(n, dtype=DESC_DTYPE)
+    d["offset"] = offsets
+    d["len"] = lens
+    d["key_id"] = key_ids
+    d["pn"] = pns
+    d["pn_offset"] = pn_offsets
+    d["pn_len"] = pn_lens
+    d["flags"] = flags
+    return d
+
+
+class KeyTable:
+    """Device key table (mq_keytable): AES schedules and GHASH powers expanded once on the host."""
+
+    def __init__(self, rows):
+        lib = _lib.load()
+        arr = (_lib.KeyMaterial * max(len(rows), 1))(*rows)
+        h = ctypes.c_void_p()
+        _raise(lib.mq_keytable_create(arr, len(rows), ctypes.byref(h)))
+        self._h = h
+        self.rows = len(rows)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def update(self, first_row, rows):
+        arr = (_lib.KeyMaterial * len(rows))(*rows)
+        _raise(_lib.load().mq_keytable_update(self._h, first_row, arr, len(rows)))
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            _lib.load().mq_keytable_free(h)
+            self._h = None
+
+
+def _stream_ptr(stream):
+    if stream is None:
+        import torch
+        return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    return ctypes.c_void_p(stream)
+
+
+def workspace_bytes(n):
+    return _lib.load().mq_batch_workspace_size(n)
+
+
+def seal(kt, arena, desc, status, suite_hint, workspace=None, stream=None):
+    """Seal + header-protect every packet of `desc` in the device `arena` (torch uint8 tensors)."""
+    n = desc.numel() // 32
+    ws = ctypes.c_void_p(workspace.data_ptr()) if workspace is not None else None
+    rc = _lib.load().mq_batch_seal(kt.handle, ctypes.c_void_p(arena.data_ptr()), arena.numel(),
+                                   ctypes.c_void_p(desc.data_ptr()), n, ctypes.c_void_p(status.data_ptr()),
+                                   suite_hint, ws, _stream_ptr(stream))
+    _raise(rc)
+
+
+def open_(kt, arena, desc, status, pn_out, suite_hint, workspace=None, stream=None):
+    """Remove header protection, decode PNs and open every packet of `desc` in place."""
+    n = desc.numel() // 32
+    ws = ctypes.c_void_p(workspace.data_ptr()) if workspace is not None else None
+    pn = ctypes.c_void_p(pn_out.data_ptr()) if pn_out is not None else None
+    rc = _lib.load().mq_batch_open(kt.handle, ctypes.c_void_p(arena.data_ptr()), arena.numel(),
+                                   ctypes.c_void_p(desc.data_ptr()), n, ctypes.c_void_p(status.data_ptr()),
+                                   pn, suite_hint, ws, _stream_ptr(stream))
+    _raise(rc)
+
+
+def hp_mask(kt, key_ids, samples, masks, stream=None):
+    """Batched HeaderProtection::mask: masks[i] = mask(row key_ids[i], samples[i])."""
+    n = key_ids.numel()
+    rc = _lib.load().mq_batch_hp_mask(kt.handle, ctypes.c_void_p(key_ids.data_ptr()),
+                                      ctypes.c_void_p(samples.data_ptr()), ctypes.c_void_p(masks.data_ptr()),
+                                      n, _stream_ptr(stream))
+    _raise(rc)
+
+
+def time_seal_open(kt, arena, desc, status, pn_out, suite_hint, iters, workspace=None, stream=None):
+    """Back-to-back (seal, open) pairs timed with HIP events on the launch stream.
+    Returns (seal_ms, open_ms) averaged per kernel pass."""
+    n = desc.numel() // 32
+    s_ms, o_ms = ctypes.c_float(), ctypes.c_float()
+    ws = ctypes.c_void_p(workspace.data_ptr()) if workspace is not None else None
+    rc = _lib.load().mq_batch_time_seal_open(
+        kt.handle, ctypes.c_void_p(arena.data_ptr()), arena.numel(), ctypes.c_void_p(desc.data_ptr()), n,
+        ctypes.c_void_p(status.data_ptr()), ctypes.c_void_p(pn_out.data_ptr()), suite_hint, ws,
+        _stream_ptr(stream), iters, ctypes.byref(s_ms), ctypes.byref(o_ms))
+    _raise(rc)
+    return s_ms.value, o_ms.value

@@ -1,0 +1,457 @@
+// mq_aes.hip — AEAD_AES_128_GCM packet protection (SP 800-38D, RFC 9001 §5) on gfx950.
+//
+// Replaces, per packet of a batch, the reference's Aes128GcmAead::seal_in_place /
+// open_in_place (src/crypto/rustcrypto.rs:38-94) and AesHeaderProtection::mask (:175-186),
+// composed as in src/connection/transmit.rs:499-755 and src/connection/recv.rs:340-421,953-1025.
+//
+// gfx950 has no AES or carry-less-multiply instructions, so:
+//   * AES-128 rounds use one T-table (T0, 1 KiB) in LDS replicated 8x per workgroup (entry x,
+//     replica lane&7 -> fewer bank conflicts), T1..T3 by rotation, round keys in VGPRs;
+//   * GHASH multiplies in the bit-reflected polynomial basis with 32x32 carry-less products
+//     built from integer v_mad_u64_u32 on bit-holed operands (4-bit spacing, <= 8 terms per
+//     output position, so no carry ever reaches the next kept bit), Karatsuba 128 -> 64 -> 32
+//     (9 products per multiply), then the x^128 + x^7 + x^2 + x + 1 fold.
+// Work split per tile (mq_tile.h): keystream block b of a packet (b = 0: E_K(J0), b >= 1:
+// counter b+1) on lane q = b / C; GHASH interleaved over the quad with H^4 (precomputed on the
+// host per key) and a final multiply by H^(4-q).
+#include "mq_tile.h"
+
+namespace mq {
+
+// FIPS-197 S-box (data table), used once per workgroup to build T0 in LDS.
+__constant__ uint8_t kSbox[256] = {
+    0x63, 0x7c, 0x77, 0x7b, 0xf2, 0x6b, 0x6f, 0xc5, 0x30, 0x01, 0x67, 0x2b, 0xfe, 0xd7, 0xab, 0x76,
+    0xca, 0x82, 0xc9, 0x7d, 0xfa, 0x59, 0x47, 0xf0, 0xad, 0xd4, 0xa2, 0xaf, 0x9c, 0xa4, 0x72, 0xc0,
+    0xb7, 0xfd, 0x93, 0x26, 0x36, 0x3f, 0xf7, 0xcc, 0x34, 0xa5, 0xe5, 0xf1, 0x71, 0xd8, 0x31, 0x15,
+    0x04, 0xc7, 0x23, 0xc3, 0x18, 0x96, 0x05, 0x9a, 0x07, 0x12, 0x80, 0xe2, 0xeb, 0x27, 0xb2, 0x75,
+    0x09, 0x83, 0x2c, 0x1a, 0x1b, 0x6e, 0x5a, 0xa0, 0x52, 0x3b, 0xd6, 0xb3, 0x29, 0xe3, 0x2f, 0x84,
+    0x53, 0xd1, 0x00, 0xed, 0x20, 0xfc, 0xb1, 0x5b, 0x6a, 0xcb, 0xbe, 0x39, 0x4a, 0x4c, 0x58, 0xcf,
+    0xd0, 0xef, 0xaa, 0xfb, 0x43, 0x4d, 0x33, 0x85, 0x45, 0xf9, 0x02, 0x7f, 0x50, 0x3c, 0x9f, 0xa8,
+    0x51, 0xa3, 0x40, 0x8f, 0x92, 0x9d, 0x38, 0xf5, 0xbc, 0xb6, 0xda, 0x21, 0x10, 0xff, 0xf3, 0xd2,
+    0xcd, 0x0c, 0x13, 0xec, 0x5f, 0x97, 0x44, 0x17, 0xc4, 0xa7, 0x7e, 0x3d, 0x64, 0x5d, 0x19, 0x73,
+    0x60, 0x81, 0x4f, 0xdc, 0x22, 0x2a, 0x90, 0x88, 0x46, 0xee, 0xb8, 0x14, 0xde, 0x5e, 0x0b, 0xdb,
+    0xe0, 0x32, 0x3a, 0x0a, 0x49, 0x06, 0x24, 0x5c, 0xc2, 0xd3, 0xac, 0x62, 0x91, 0x95, 0xe4, 0x79,
+    0xe7, 0xc8, 0x37, 0x6d, 0x8d, 0xd5, 0x4e, 0xa9, 0x6c, 0x56, 0xf4, 0xea, 0x65, 0x7a, 0xae, 0x08,
+    0xba, 0x78, 0x25, 0x2e, 0x1c, 0xa6, 0xb4, 0xc6, 0xe8, 0xdd, 0x74, 0x1f, 0x4b, 0xbd, 0x8b, 0x8a,
+    0x70, 0x3e, 0xb5, 0x66, 0x48, 0x03, 0xf6, 0x0e, 0x61, 0x35, 0x57, 0xb9, 0x86, 0xc1, 0x1d, 0x9e,
+    0xe1, 0xf8, 0x98, 0x11, 0x69, 0xd9, 0x8e, 0x94, 0x9b, 0x1e, 0x87, 0xe9, 0xce, 0x55, 0x28, 0xdf,
+    0x8c, 0xa1, 0x89, 0x0d, 0xbf, 0xe6, 0x42, 0x68, 0x41, 0x99, 0x2d, 0x0f, 0xb0, 0x54, 0xbb, 0x16};
+
+constexpr int kTReplicas = 8;
+constexpr int kAesWaves = 2;  // waves (tiles) per workgroup sharing one T-table
+__shared__ uint32_t g_t0[256 * kTReplicas];
+
+__device__ __forceinline__ void build_t0(int tid, int nthreads) {
+  for (int e = tid; e < 256 * kTReplicas; e += nthreads) {
+    const uint32_t s = kSbox[e / kTReplicas];
+    const uint32_t s2 = ((s << 1) ^ ((s & 0x80) ? 0x11b : 0)) & 0xff;
+    g_t0[e] = (s2 << 24) | (s << 16) | (s << 8) | (s2 ^ s);
+  }
+}
+
+__device__ __forceinline__ uint32_t ror(uint32_t x, int r) { return (x >> r) | (x << (32 - r)); }
+
+struct AesRk { uint32_t w[44]; };
+
+__device__ __forceinline__ void load_rk(const uint32_t* src, AesRk& rk) {
+#pragma unroll
+  for (int i = 0; i < 11; ++i) {
+    const uint4 v = *(const uint4*)(src + 4 * i);
+    rk.w[4 * i] = v.x; rk.w[4 * i + 1] = v.y; rk.w[4 * i + 2] = v.z; rk.w[4 * i + 3] = v.w;
+  }
+}
+
+// T0 lookup of byte k (0 = least significant) of s; `rb` = this lane's replica byte offset.
+__device__ __forceinline__ uint32_t tlook(uint32_t s, int k, uint32_t rb) {
+  const uint32_t idx = (s >> (8 * k)) & 0xff;
+  return *(const uint32_t*)((const uint8_t*)g_t0 + idx * (4 * kTReplicas) + rb);
+}
+
+// AES-128 encryption of a block given as big-endian column words (FIPS-197 §5.1).
+__device__ __forceinline__ void aes128_block(const AesRk& rk, uint32_t rb, uint32_t& s0, uint32_t& s1,
+                                             uint32_t& s2, uint32_t& s3) {
+  s0 ^= rk.w[0]; s1 ^= rk.w[1]; s2 ^= rk.w[2]; s3 ^= rk.w[3];
+#pragma unroll
+  for (int r = 1; r < 10; ++r) {
+    const uint32_t t0 = tlook(s0, 3, rb) ^ ror(tlook(s1, 2, rb), 8) ^ ror(tlook(s2, 1, rb), 16) ^ ror(tlook(s3, 0, rb), 24) ^ rk.w[4 * r];
+    const uint32_t t1 = tlook(s1, 3, rb) ^ ror(tlook(s2, 2, rb), 8) ^ ror(tlook(s3, 1, rb), 16) ^ ror(tlook(s0, 0, rb), 24) ^ rk.w[4 * r + 1];
+    const uint32_t t2 = tlook(s2, 3, rb) ^ ror(tlook(s3, 2, rb), 8) ^ ror(tlook(s0, 1, rb), 16) ^ ror(tlook(s1, 0, rb), 24) ^ rk.w[4 * r + 2];
+    const uint32_t t3 = tlook(s3, 3, rb) ^ ror(tlook(s0, 2, rb), 8) ^ ror(tlook(s1, 1, rb), 16) ^ ror(tlook(s2, 0, rb), 24) ^ rk.w[4 * r + 3];
+    s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+  }
+  // final round: SubBytes + ShiftRows (S[x] = byte 2 of T0[x]) + AddRoundKey
+  auto fin = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
+    return ((tlook(a, 3, rb) << 8) & 0xff000000u) ^ (tlook(b, 2, rb) & 0x00ff0000u) ^
+           ((tlook(c, 1, rb) >> 8) & 0x0000ff00u) ^ ((tlook(d, 0, rb) >> 16) & 0x000000ffu) ^ k;
+  };
+  const uint32_t o0 = fin(s0, s1, s2, s3, rk.w[40]), o1 = fin(s1, s2, s3, s0, rk.w[41]),
+                 o2 = fin(s2, s3, s0, s1, rk.w[42]), o3 = fin(s3, s0, s1, s2, rk.w[43]);
+  s0 = o0; s1 = o1; s2 = o2; s3 = o3;
+}
+
+// ---- GHASH in the bit-reflected basis: bit i of word k = coefficient of x^(32k+i) --------------
+__device__ __forceinline__ uint32_t brev(uint32_t x) { return __builtin_bitreverse32(x); }
+// memory dword (little-endian load of 4 GCM bytes) <-> reflected word
+__device__ __forceinline__ uint32_t refl(uint32_t le) { return brev(bswap32(le)); }
+
+// operand prepared for repeated multiplication: 9 Karatsuba words x 4 bit-hole masks
+struct GfOp { uint32_t y[9][4]; };
+
+__device__ __forceinline__ void holes(uint32_t v, uint32_t (&o)[4]) {
+  o[0] = v & 0x11111111u; o[1] = v & 0x22222222u; o[2] = v & 0x44444444u; o[3] = v & 0x88888888u;
+}
+
+__device__ __forceinline__ GfOp gf_prepare(const uint32_t (&b)[4]) {
+  GfOp op;
+  const uint32_t c0 = b[0] ^ b[2], c1 = b[1] ^ b[3];
+  const uint32_t k[9] = {b[0], b[1], b[0] ^ b[1], b[2], b[3], b[2] ^ b[3], c0, c1, c0 ^ c1};
+#pragma unroll
+  for (int i = 0; i < 9; ++i) holes(k[i], op.y[i]);
+  return op;
+}
+
+// 32x32 -> 64 carry-less product with holes
+__device__ __forceinline__ uint64_t bmul32(uint32_t x, const uint32_t (&y)[4]) {
+  uint32_t xh[4];
+  holes(x, xh);
+  const uint64_t z0 = (uint64_t)xh[0] * y[0] ^ (uint64_t)xh[1] * y[3] ^ (uint64_t)xh[2] * y[2] ^ (uint64_t)xh[3] * y[1];
+  const uint64_t z1 = (uint64_t)xh[0] * y[1] ^ (uint64_t)xh[1] * y[0] ^ (uint64_t)xh[2] * y[3] ^ (uint64_t)xh[3] * y[2];
+  const uint64_t z2 = (uint64_t)xh[0] * y[2] ^ (uint64_t)xh[1] * y[1] ^ (uint64_t)xh[2] * y[0] ^ (uint64_t)xh[3] * y[3];
+  const uint64_t z3 = (uint64_t)xh[0] * y[3] ^ (uint64_t)xh[1] * y[2] ^ (uint64_t)xh[2] * y[1] ^ (uint64_t)xh[3] * y[0];
+  return (z0 & 0x1111111111111111ull) | (z1 & 0x2222222222222222ull) | (z2 & 0x4444444444444444ull) |
+         (z3 & 0x8888888888888888ull);
+}
+
+// a = a * b mod (x^128 + x^7 + x^2 + x + 1), b prepared
+__device__ __forceinline__ void gf_mul(uint32_t (&a)[4], const GfOp& b) {
+  const uint32_t c0 = a[0] ^ a[2], c1 = a[1] ^ a[3];
+  // low half a1:a0 * b1:b0
+  const uint64_t l0 = bmul32(a[0], b.y[0]), l1 = bmul32(a[1], b.y[1]), l2 = bmul32(a[0] ^ a[1], b.y[2]) ^ l0 ^ l1;
+  // high half a3:a2 * b3:b2
+  const uint64_t h0 = bmul32(a[2], b.y[3]), h1 = bmul32(a[3], b.y[4]), h2 = bmul32(a[2] ^ a[3], b.y[5]) ^ h0 ^ h1;
+  // middle (a_lo ^ a_hi) * (b_lo ^ b_hi)
+  const uint64_t m0 = bmul32(c0, b.y[6]), m1 = bmul32(c1, b.y[7]), m2 = bmul32(c0 ^ c1, b.y[8]) ^ m0 ^ m1;
+  // 128-bit products as 4 words
+  uint32_t L[4] = {(uint32_t)l0, (uint32_t)(l0 >> 32) ^ (uint32_t)l2, (uint32_t)(l2 >> 32) ^ (uint32_t)l1, (uint32_t)(l1 >> 32)};
+  uint32_t H[4] = {(uint32_t)h0, (uint32_t)(h0 >> 32) ^ (uint32_t)h2, (uint32_t)(h2 >> 32) ^ (uint32_t)h1, (uint32_t)(h1 >> 32)};
+  uint32_t M[4] = {(uint32_t)m0, (uint32_t)(m0 >> 32) ^ (uint32_t)m2, (uint32_t)(m2 >> 32) ^ (uint32_t)m1, (uint32_t)(m1 >> 32)};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) M[i] ^= L[i] ^ H[i];
+  // P = L + M x^64 + H x^128  (8 words)
+  const uint32_t p0 = L[0], p1 = L[1], p2 = L[2] ^ M[0], p3 = L[3] ^ M[1];
+  const uint32_t p4 = H[0] ^ M[2], p5 = H[1] ^ M[3], p6 = H[2], p7 = H[3];
+  // fold x^(128+j) -> x^j + x^(j+1) + x^(j+2) + x^(j+7)
+  const uint32_t t = (p7 >> 31) ^ (p7 >> 30) ^ (p7 >> 25);
+  a[0] = p0 ^ p4 ^ (p4 << 1) ^ (p4 << 2) ^ (p4 << 7) ^ t ^ (t << 1) ^ (t << 2) ^ (t << 7);
+  a[1] = p1 ^ p5 ^ ((p5 << 1) | (p4 >> 31)) ^ ((p5 << 2) | (p4 >> 30)) ^ ((p5 << 7) | (p4 >> 25));
+  a[2] = p2 ^ p6 ^ ((p6 << 1) | (p5 >> 31)) ^ ((p6 << 2) | (p5 >> 30)) ^ ((p6 << 7) | (p5 >> 25));
+  a[3] = p3 ^ p7 ^ ((p7 << 1) | (p6 >> 31)) ^ ((p7 << 2) | (p6 >> 30)) ^ ((p7 << 7) | (p6 >> 25));
+}
+
+// Interleaved GHASH over AAD||pad||CT||pad||[len(A)]64||[len(C)]64 (bit lengths); every lane of
+// the quad returns the same value in the reflected basis.
+template <class S>
+__device__ __forceinline__ void ghash(const S& sp, typename S::off_t pkt, typename S::off_t pay,
+                                      uint32_t aad_len, uint32_t ct_len, const KeyRow* row, int q,
+                                      bool act, uint32_t (&y)[4]) {
+  uint32_t hp[4];
+  GfOp m4, mlast;
+  {
+#pragma unroll
+    for (int w = 0; w < 4; ++w) hp[w] = brev(row->H[3][w]);
+    m4 = gf_prepare(hp);
+    const int e = 3 - q;  // H^(4-q) is row->H[3-q]
+#pragma unroll
+    for (int w = 0; w < 4; ++w) hp[w] = brev(row->H[e][w]);
+    mlast = gf_prepare(hp);
+  }
+  const uint32_t A = (aad_len + 15) >> 4, T = (ct_len + 15) >> 4, nb = A + T + 1;
+  const uint32_t K = (nb + 3) >> 2;
+  const uint32_t Kmax = wave_max_u32(act ? K : 0u);
+  const int z = (int)(4 * Kmax) - (int)nb;
+  uint32_t acc[4] = {0, 0, 0, 0};
+  auto absorb = [&](uint32_t k) {
+    const int i = (int)(4 * k) + q - z;
+    typename S::off_t src = pkt;
+    int rem = 0;
+    bool lens = false;
+    if (act && i >= 0) {
+      if ((uint32_t)i < A) {
+        src = pkt + 16 * (uint32_t)i; rem = (int)aad_len - 16 * i;
+      } else if ((uint32_t)i < A + T) {
+        src = pay + 16 * ((uint32_t)i - A); rem = (int)ct_len - 16 * (i - (int)A);
+      } else {
+        lens = true;
+      }
+    }
+    uint32_t m[4];
+    load_words<4>(sp, src, m);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) m[w] = refl(m[w] & byte_mask(rem, w));
+    if (lens) {
+      const uint64_t ab = (uint64_t)aad_len * 8, cb = (uint64_t)ct_len * 8;
+      m[0] = brev((uint32_t)(ab >> 32)); m[1] = brev((uint32_t)ab);
+      m[2] = brev((uint32_t)(cb >> 32)); m[3] = brev((uint32_t)cb);
+    }
+#pragma unroll
+    for (int w = 0; w < 4; ++w) acc[w] ^= m[w];
+  };
+  for (uint32_t k = 0; k + 1 < Kmax; ++k) {
+    absorb(k);
+    gf_mul(acc, m4);
+  }
+  if (Kmax > 0) {
+    absorb(Kmax - 1);
+    gf_mul(acc, mlast);
+  }
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    acc[w] ^= quad_swap1(acc[w]);
+    acc[w] ^= quad_swap2(acc[w]);
+    y[w] = acc[w];
+  }
+}
+
+struct AesPolicy {
+  static constexpr uint32_t kSuite = MQ_SUITE_AES128GCM;
+
+  // keystream of block index b (0: E(J0), b >= 1: counter b + 1) as little-endian data words
+  static __device__ __forceinline__ void ctr_block(const AesRk& rk, uint32_t rb, const uint32_t (&nb)[3],
+                                                   uint32_t b, uint32_t (&ks)[4]) {
+    uint32_t s0 = nb[0], s1 = nb[1], s2 = nb[2], s3 = b == 0 ? 1u : b + 1;
+    aes128_block(rk, rb, s0, s1, s2, s3);
+    ks[0] = bswap32(s0); ks[1] = bswap32(s1); ks[2] = bswap32(s2); ks[3] = bswap32(s3);
+  }
+
+  template <class S>
+  static __device__ __forceinline__ void xor_block(const S& sp, typename S::off_t pay, uint32_t b,
+                                                   uint32_t P, const uint32_t (&ks)[4]) {
+    const uint32_t o = 16 * (b - 1);
+    const int ln = (int)min(16u, P - o);
+    uint32_t w[4];
+    load_words<4>(sp, pay + o, w);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] ^= ks[k];
+    store_words<4>(sp, pay + o, w, ln);
+  }
+
+  // AesHeaderProtection::mask (rustcrypto.rs:175-186): AES-ECB(hp, sample)[0..5]
+  template <class S>
+  static __device__ __forceinline__ void hp_mask(const S& sp, typename S::off_t sample_at,
+                                                 const KeyRow* row, uint32_t rb, uint32_t& m0, uint32_t& m1) {
+    uint32_t smp[4];
+    load_words<4>(sp, sample_at, smp);
+    AesRk hk;
+    load_rk(row->hp_rk, hk);
+    uint32_t s0 = bswap32(smp[0]), s1 = bswap32(smp[1]), s2 = bswap32(smp[2]), s3 = bswap32(smp[3]);
+    aes128_block(hk, rb, s0, s1, s2, s3);
+    m0 = bswap32(s0);
+    m1 = s1 >> 24;
+  }
+
+  static __device__ __forceinline__ void nonce_be(const KeyRow* row, uint64_t pn, uint32_t (&nb)[3]) {
+    // DirectionalKeys::nonce (src/crypto/mod.rs:66-74), as big-endian AES input words
+    nb[0] = bswap32(row->iv[0]);
+    nb[1] = bswap32(row->iv[1]) ^ (uint32_t)(pn >> 32);
+    nb[2] = bswap32(row->iv[2]) ^ (uint32_t)pn;
+  }
+
+  static __device__ __forceinline__ void tag_words(const uint32_t (&y)[4], const uint32_t (&ej0)[4],
+                                                   uint32_t (&tag)[4]) {
+#pragma unroll
+    for (int w = 0; w < 4; ++w) tag[w] = bswap32(brev(y[w])) ^ ej0[w];
+  }
+
+  template <class S>
+  static __device__ void seal(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int q) {
+    const mq_pkt_desc& d = c.d;
+    const uint32_t rb = (threadIdx.x & (kTReplicas - 1)) * 4;
+    const uint32_t aad_len = c.act ? (uint32_t)d.pn_offset + d.pn_len : 0u;
+    const uint32_t P = c.act ? d.len - aad_len - 16 : 0u;
+    const typename S::off_t pay = pkt + aad_len;
+    uint32_t nb[3];
+    nonce_be(row, c.pn, nb);
+    const uint32_t nblk = 1 + (P + 15) / 16;
+    const uint32_t C = (nblk + 3) >> 2;
+    const uint32_t Cmax = wave_max_u32(c.act ? C : 0u);
+    uint32_t ej0[4] = {0, 0, 0, 0};
+    {
+      AesRk rk;
+      load_rk(row->aes_rk, rk);
+      for (uint32_t it = 0; it < Cmax; ++it) {
+        const uint32_t b = q * C + it;
+        const bool a = c.act && it < C && b < nblk;
+        uint32_t ks[4];
+        ctr_block(rk, rb, nb, b, ks);
+        if (a && b == 0) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) ej0[k] = ks[k];
+        } else if (a) {
+          xor_block(sp, pay, b, P, ks);
+        }
+      }
+    }
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ej0[k] = quad_bcast0(ej0[k]);
+    uint32_t y[4], tag[4];
+    ghash(sp, pkt, pay, aad_len, P, row, q, c.act, y);
+    tag_words(y, ej0, tag);
+    if (c.act && q == 0) store_words<4>(sp, pay + P, tag, 16);
+    wave_sync();
+    if (c.act && !(d.flags & MQ_PKT_NO_HP)) {
+      uint32_t m0, m1;
+      hp_mask(sp, pkt + d.pn_offset + 4, row, rb, m0, m1);
+      if (q == 0) {
+        const uint8_t fb = (d.flags & MQ_PKT_LONG_HEADER) ? 0x0f : 0x1f;
+        sp.st8(pkt, sp.ld8(pkt) ^ ((uint8_t)m0 & fb));
+        const uint32_t mk = (m0 >> 8) | (m1 << 24);
+        for (uint32_t j = 0; j < d.pn_len; ++j)
+          sp.st8(pkt + d.pn_offset + j, sp.ld8(pkt + d.pn_offset + j) ^ (uint8_t)(mk >> (8 * j)));
+      }
+    }
+  }
+
+  template <class S>
+  static __device__ void open(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int q,
+                              bool direct) {
+    const mq_pkt_desc& d = c.d;
+    const uint32_t rb = (threadIdx.x & (kTReplicas - 1)) * 4;
+    uint32_t pn_len = d.pn_len;
+    uint8_t orig_b0 = 0;
+    uint32_t orig_pn = 0;
+    bool hdr_written = false;
+    if (c.act && !(d.flags & MQ_PKT_NO_HP)) {
+      uint32_t m0, m1;
+      hp_mask(sp, pkt + d.pn_offset + 4, row, rb, m0, m1);
+      const uint8_t fb = (d.flags & MQ_PKT_LONG_HEADER) ? 0x0f : 0x1f;
+      orig_b0 = sp.ld8(pkt);
+      const uint8_t b0 = orig_b0 ^ ((uint8_t)m0 & fb);
+      pn_len = (b0 & 3u) + 1;
+      const uint32_t mk = (m0 >> 8) | (m1 << 24);
+      uint32_t trunc = 0;
+      for (uint32_t j = 0; j < pn_len; ++j) {
+        const uint8_t e = sp.ld8(pkt + d.pn_offset + j);
+        orig_pn |= (uint32_t)e << (8 * j);
+        trunc = (trunc << 8) | (uint8_t)(e ^ (uint8_t)(mk >> (8 * j)));
+      }
+      c.pn = decode_pn(trunc, pn_len, d.pn);
+      if (c.pn > kMaxPn) {
+        c.st = MQ_ERR_PROTOCOL;
+        c.act = false;
+      } else if (q == 0) {
+        sp.st8(pkt, b0);
+        for (uint32_t j = 0; j < pn_len; ++j)
+          sp.st8(pkt + d.pn_offset + j, (uint8_t)(trunc >> (8 * (pn_len - 1 - j))));
+        hdr_written = true;
+      }
+    }
+    wave_sync();
+    const uint32_t aad_len = c.act ? (uint32_t)d.pn_offset + pn_len : 0u;
+    const uint32_t P = c.act ? d.len - aad_len - 16 : 0u;
+    const typename S::off_t pay = pkt + aad_len;
+    uint32_t nb[3];
+    nonce_be(row, c.pn, nb);
+    const uint32_t nblk = 1 + (P + 15) / 16;
+    const uint32_t C = (nblk + 3) >> 2;
+    const uint32_t Cmax = wave_max_u32(c.act ? C : 0u);
+    uint32_t y[4];
+    ghash(sp, pkt, pay, aad_len, P, row, q, c.act, y);
+    AesRk rk;
+    load_rk(row->aes_rk, rk);
+    uint32_t ej0[4];
+    ctr_block(rk, rb, nb, 0, ej0);
+    uint32_t tag[4], got[4];
+    tag_words(y, ej0, tag);
+    load_words<4>(sp, pay + P, got);
+    const uint32_t diff = (tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) | (tag[3] ^ got[3]);
+    if (c.act && diff != 0) {
+      c.st = MQ_ERR_CRYPTO;
+      c.act = false;
+    }
+    wave_sync();
+    // keystream blocks 1.. (block 0 = E(J0) is already used); spread b = 1 + q*C' + it
+    const uint32_t nks = nblk - 1;
+    const uint32_t C2 = (nks + 3) >> 2;
+    const uint32_t C2max = wave_max_u32(c.act ? C2 : 0u);
+    for (uint32_t it = 0; it < C2max; ++it) {
+      const uint32_t b = 1 + q * C2 + it;
+      const bool a = c.act && it < C2 && b < nblk;
+      uint32_t ks[4];
+      ctr_block(rk, rb, nb, b, ks);
+      if (a) xor_block(sp, pay, b, P, ks);
+    }
+    (void)Cmax;
+    if (direct && hdr_written && !c.act) {
+      sp.st8(pkt, orig_b0);
+      for (uint32_t j = 0; j < pn_len; ++j) sp.st8(pkt + d.pn_offset + j, (uint8_t)(orig_pn >> (8 * j)));
+    }
+  }
+};
+
+}  // namespace mq
+
+using namespace mq;
+
+extern "C" __global__ __launch_bounds__(64 * kAesWaves) void mq_aes_seal_kernel(
+    const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
+    const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,
+    const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  build_t0(threadIdx.x, blockDim.x);
+  __syncthreads();
+  const uint32_t w = threadIdx.x >> 6;
+  run_tile<AesPolicy, false>(smem + w * kLdsBytes, blockIdx.x * kAesWaves + w, kt, n_rows, arena, arena_len,
+                             desc, n, index, n_dev, status, nullptr);
+}
+
+extern "C" __global__ __launch_bounds__(64 * kAesWaves) void mq_aes_open_kernel(
+    const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
+    const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,
+    const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  build_t0(threadIdx.x, blockDim.x);
+  __syncthreads();
+  const uint32_t w = threadIdx.x >> 6;
+  run_tile<AesPolicy, true>(smem + w * kLdsBytes, blockIdx.x * kAesWaves + w, kt, n_rows, arena, arena_len,
+                            desc, n, index, n_dev, status, pn_out);
+}
+
+extern "C" __global__ __launch_bounds__(256) void mq_aes_hp_kernel(
+    const KeyRow* __restrict__ kt, uint32_t n_rows, const uint32_t* __restrict__ key_ids,
+    const uint8_t* __restrict__ samples, uint8_t* __restrict__ masks, uint32_t n) {
+  build_t0(threadIdx.x, blockDim.x);
+  __syncthreads();
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t kid = key_ids[i];
+  if (kid >= n_rows || kt[kid].suite != MQ_SUITE_AES128GCM) return;
+  GlobalSpace sp{const_cast<uint8_t*>(samples), (uint64_t)n * 16};
+  uint32_t m0, m1;
+  AesPolicy::hp_mask(sp, (uint64_t)i * 16, kt + kid, (threadIdx.x & (kTReplicas - 1)) * 4, m0, m1);
+  for (int b = 0; b < 4; ++b) masks[5 * (size_t)i + b] = (uint8_t)(m0 >> (8 * b));
+  masks[5 * (size_t)i + 4] = (uint8_t)m1;
+}
+
+hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena, uint64_t arena_len,
+                         const mq_pkt_desc* desc, uint32_t n, const uint32_t* index, const uint32_t* n_dev,
+                         uint8_t* status, uint64_t* pn_out, hipStream_t s) {
+  const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
+  if (tiles == 0) return hipSuccess;
+  const uint32_t blocks = (tiles + kAesWaves - 1) / kAesWaves;
+  if (open)
+    hipLaunchKernelGGL(mq_aes_open_kernel, dim3(blocks), dim3(64 * kAesWaves), kLdsBytes * kAesWaves, s, kt,
+                       n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out);
+  else
+    hipLaunchKernelGGL(mq_aes_seal_kernel, dim3(blocks), dim3(64 * kAesWaves), kLdsBytes * kAesWaves, s, kt,
+                       n_rows, arena, arena_len, desc, n, index, n_dev, status);
+  return hipGetLastError();
+}
+
+hipError_t mq_launch_aes_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t* key_ids, const uint8_t* samples,
+                            uint8_t* masks, uint32_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(mq_aes_hp_kernel, dim3((n + 255) / 256), dim3(256), 0, s, kt, n_rows, key_ids, samples,
+                     masks, n);
+  return hipGetLastError();
+}

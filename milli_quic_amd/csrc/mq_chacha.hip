@@ -1,0 +1,308 @@
+// mq_chacha.hip — AEAD_CHACHA20_POLY1305 packet protection (RFC 8439 / RFC 9001 §5) on gfx950.
+//
+// Replaces, per packet of a batch, the reference's ChaCha20Poly1305Aead::seal_in_place /
+// open_in_place (src/crypto/rustcrypto.rs:111-165) plus ChaChaHeaderProtection::mask
+// (:197-220), composed the way src/connection/transmit.rs:625-755 (send) and
+// src/connection/recv.rs:340-421,953-1025 (receive) compose them.
+//
+// Per tile (16 packets, one quad of lanes per packet; see mq_tile.h):
+//   seal: keystream blocks ctr = q*C + it (ctr 0 = Poly1305 one-time key) XORed into LDS ->
+//         interleaved Poly1305 over AAD||pad||CT||pad||lens -> tag -> HP mask from the sample
+//   open: HP mask -> unmask byte 0 / PN -> decode_pn -> nonce -> first keystream block (lane
+//         q=0: one-time key) -> Poly1305 over the untouched ciphertext -> tag check -> only
+//         then the keystream XOR (held first block + the rest); failed packets are never stored.
+#include "mq_tile.h"
+
+namespace mq {
+
+// Interleaved Poly1305 of the AEAD MAC input for the quad's packet. Every lane of the quad
+// returns the same tag. aad at `pkt` (aad_len bytes), ciphertext at `pay` (ct_len bytes).
+template <class S>
+__device__ __forceinline__ void poly_tag(const S& sp, typename S::off_t pkt, typename S::off_t pay,
+                                         uint32_t aad_len, uint32_t ct_len,
+                                         const uint32_t (&otk)[8], int q, bool act,
+                                         uint32_t (&tag)[4]) {
+  P26 r = p26_from_words(otk[0] & 0x0fffffffu, otk[1] & 0x0ffffffcu, otk[2] & 0x0ffffffcu,
+                         otk[3] & 0x0ffffffcu, 0);
+  const P26m m1 = p26_mult(r);
+  P26 r2 = r;
+  p26_mul(r2, m1);
+  P26 r3 = r2;
+  p26_mul(r3, m1);
+  P26 r4 = r2;
+  p26_mul(r4, p26_mult(r2));
+  P26 rq;
+#pragma unroll
+  for (int l = 0; l < 5; ++l)
+    rq.l[l] = q == 0 ? r4.l[l] : q == 1 ? r3.l[l] : q == 2 ? r2.l[l] : r.l[l];
+  const P26m m4 = p26_mult(r4), mlast = p26_mult(rq);
+
+  const uint32_t A = (aad_len + 15) >> 4, T = (ct_len + 15) >> 4, nb = A + T + 1;
+  const uint32_t K = (nb + 3) >> 2;
+  const uint32_t Kmax = wave_max_u32(act ? K : 0u);
+  // prepend zero blocks (no 2^128 bit) so every packet of the wave runs exactly Kmax steps
+  const int z = (int)(4 * Kmax) - (int)nb;
+  P26 acc;
+#pragma unroll
+  for (int l = 0; l < 5; ++l) acc.l[l] = 0;
+
+  auto absorb = [&](uint32_t k) {
+    const int i = (int)(4 * k) + q - z;
+    typename S::off_t src = pkt;
+    int rem = 0;
+    uint32_t hib = 0;
+    bool lens = false;
+    if (act && i >= 0) {
+      hib = 1;
+      if ((uint32_t)i < A) {
+        src = pkt + 16 * (uint32_t)i; rem = (int)aad_len - 16 * i;
+      } else if ((uint32_t)i < A + T) {
+        src = pay + 16 * ((uint32_t)i - A); rem = (int)ct_len - 16 * (i - (int)A);
+      } else {
+        lens = true;
+      }
+    }
+    uint32_t m[4];
+    load_words<4>(sp, src, m);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) m[w] &= byte_mask(rem, w);
+    if (lens) { m[0] = aad_len; m[1] = 0; m[2] = ct_len; m[3] = 0; }
+    P26 x = p26_from_words(m[0], m[1], m[2], m[3], hib);
+#pragma unroll
+    for (int l = 0; l < 5; ++l) acc.l[l] += x.l[l];
+  };
+  for (uint32_t k = 0; k + 1 < Kmax; ++k) {
+    absorb(k);
+    p26_mul(acc, m4);
+  }
+  if (Kmax > 0) {
+    absorb(Kmax - 1);
+    p26_mul(acc, mlast);
+  }
+#pragma unroll
+  for (int l = 0; l < 5; ++l) {
+    acc.l[l] += quad_swap1(acc.l[l]);
+    acc.l[l] += quad_swap2(acc.l[l]);
+  }
+  const uint32_t s[4] = {otk[4], otk[5], otk[6], otk[7]};
+  p26_finish(acc, s, tag);
+}
+
+__device__ __forceinline__ void load_key8(const uint32_t* src, uint32_t (&k)[8]) {
+  const uint4 a = *(const uint4*)src, b = *(const uint4*)(src + 4);
+  k[0] = a.x; k[1] = a.y; k[2] = a.z; k[3] = a.w; k[4] = b.x; k[5] = b.y; k[6] = b.z; k[7] = b.w;
+}
+
+struct ChaChaPolicy {
+  static constexpr uint32_t kSuite = MQ_SUITE_CHACHA20;
+
+  // XOR keystream block `ctr` (>= 1) into payload bytes [64(ctr-1), min(64 ctr, P)).
+  template <class S>
+  static __device__ __forceinline__ void xor_block(const S& sp, typename S::off_t pay, uint32_t ctr,
+                                                   uint32_t P, const uint32_t (&ks)[16]) {
+    const uint32_t o = 64 * (ctr - 1);
+    const int ln = (int)min(64u, P - o);
+    uint32_t w[16];
+    load_words<16>(sp, pay + o, w);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) w[k] ^= ks[k];
+    store_words<16>(sp, pay + o, w, ln);
+  }
+
+  // ChaChaHeaderProtection::mask (rustcrypto.rs:197-220): block(hp, ctr = sample[0..4] LE,
+  // nonce = sample[4..16]); the mask is keystream bytes 0..4.
+  template <class S>
+  static __device__ __forceinline__ void hp_mask(const S& sp, typename S::off_t sample_at,
+                                                 const KeyRow* row, uint32_t& m0, uint32_t& m1) {
+    uint32_t smp[4];
+    load_words<4>(sp, sample_at, smp);
+    uint32_t hk[8], blk[16];
+    load_key8(row->hp, hk);
+    chacha20_block(hk, smp[0], smp[1], smp[2], smp[3], blk);
+    m0 = blk[0];
+    m1 = blk[1];
+  }
+
+  template <class S>
+  static __device__ void seal(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int q) {
+    const mq_pkt_desc& d = c.d;
+    uint32_t key[8];
+    load_key8(row->key, key);
+    const uint32_t aad_len = c.act ? (uint32_t)d.pn_offset + d.pn_len : 0u;
+    const uint32_t P = c.act ? d.len - aad_len - 16 : 0u;
+    const typename S::off_t pay = pkt + aad_len;
+    // DirectionalKeys::nonce (src/crypto/mod.rs:66-74): iv ^ (0^32 || BE64(pn))
+    const uint32_t n0 = row->iv[0], n1 = row->iv[1] ^ bswap32((uint32_t)(c.pn >> 32)),
+                   n2 = row->iv[2] ^ bswap32((uint32_t)c.pn);
+    const uint32_t nblk = 1 + (P + 63) / 64;  // block 0 = Poly1305 key, 1.. = keystream
+    const uint32_t C = (nblk + 3) >> 2;
+    const uint32_t Cmax = wave_max_u32(c.act ? C : 0u);
+    uint32_t otk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t it = 0; it < Cmax; ++it) {
+      const uint32_t ctr = q * C + it;
+      const bool a = c.act && it < C && ctr < nblk;
+      uint32_t ks[16];
+      chacha20_block(key, ctr, n0, n1, n2, ks);
+      if (a && ctr == 0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) otk[k] = ks[k];
+      } else if (a) {
+        xor_block(sp, pay, ctr, P, ks);
+      }
+    }
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) otk[k] = quad_bcast0(otk[k]);
+    uint32_t tag[4];
+    poly_tag(sp, pkt, pay, aad_len, P, otk, q, c.act, tag);
+    if (c.act && q == 0) store_words<4>(sp, pay + P, tag, 16);
+    wave_sync();
+    // header protection (transmit.rs:721-738): sample at pn_offset + 4, after the tag exists
+    const bool hp = c.act && !(d.flags & MQ_PKT_NO_HP);
+    if (hp) {
+      uint32_t m0, m1;
+      hp_mask(sp, pkt + d.pn_offset + 4, row, m0, m1);
+      if (q == 0) {
+        const uint8_t fb = (d.flags & MQ_PKT_LONG_HEADER) ? 0x0f : 0x1f;
+        sp.st8(pkt, sp.ld8(pkt) ^ ((uint8_t)m0 & fb));
+        const uint32_t mk = (m0 >> 8) | (m1 << 24);  // mask[1..4]
+        for (uint32_t j = 0; j < d.pn_len; ++j)
+          sp.st8(pkt + d.pn_offset + j, sp.ld8(pkt + d.pn_offset + j) ^ (uint8_t)(mk >> (8 * j)));
+      }
+    }
+  }
+
+  template <class S>
+  static __device__ void open(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int q,
+                              bool direct) {
+    const mq_pkt_desc& d = c.d;
+    uint32_t pn_len = d.pn_len;
+    uint8_t orig_b0 = 0;
+    uint32_t orig_pn = 0;
+    bool hdr_written = false;
+    if (c.act && !(d.flags & MQ_PKT_NO_HP)) {
+      // recv.rs:363-391 / :968-992: mask, unmask byte 0, pn_len, unmask PN, decode_pn
+      uint32_t m0, m1;
+      hp_mask(sp, pkt + d.pn_offset + 4, row, m0, m1);
+      const uint8_t fb = (d.flags & MQ_PKT_LONG_HEADER) ? 0x0f : 0x1f;
+      orig_b0 = sp.ld8(pkt);
+      const uint8_t b0 = orig_b0 ^ ((uint8_t)m0 & fb);
+      pn_len = (b0 & 3u) + 1;
+      const uint32_t mk = (m0 >> 8) | (m1 << 24);
+      uint32_t trunc = 0;
+      for (uint32_t j = 0; j < pn_len; ++j) {
+        const uint8_t e = sp.ld8(pkt + d.pn_offset + j);
+        orig_pn |= (uint32_t)e << (8 * j);
+        trunc = (trunc << 8) | (uint8_t)(e ^ (uint8_t)(mk >> (8 * j)));
+      }
+      c.pn = decode_pn(trunc, pn_len, d.pn);
+      if (c.pn > kMaxPn) {  // recv.rs:393-395
+        c.st = MQ_ERR_PROTOCOL;
+        c.act = false;
+      } else if (q == 0) {
+        sp.st8(pkt, b0);
+        for (uint32_t j = 0; j < pn_len; ++j)
+          sp.st8(pkt + d.pn_offset + j, (uint8_t)(trunc >> (8 * (pn_len - 1 - j))));
+        hdr_written = true;
+      }
+    }
+    wave_sync();
+    uint32_t key[8];
+    load_key8(row->key, key);
+    const uint32_t aad_len = c.act ? (uint32_t)d.pn_offset + pn_len : 0u;
+    const uint32_t P = c.act ? d.len - aad_len - 16 : 0u;
+    const typename S::off_t pay = pkt + aad_len;
+    const uint32_t n0 = row->iv[0], n1 = row->iv[1] ^ bswap32((uint32_t)(c.pn >> 32)),
+                   n2 = row->iv[2] ^ bswap32((uint32_t)c.pn);
+    const uint32_t nblk = 1 + (P + 63) / 64;
+    const uint32_t C = (nblk + 3) >> 2;
+    const uint32_t Cmax = wave_max_u32(c.act ? C : 0u);
+    // first keystream block of every lane is computed before the MAC (lane q=0: one-time key)
+    const uint32_t ctr0 = q * C;
+    uint32_t ks0[16];
+    chacha20_block(key, ctr0, n0, n1, n2, ks0);
+    uint32_t otk[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) otk[k] = quad_bcast0(ks0[k]);
+    uint32_t tag[4], got[4];
+    poly_tag(sp, pkt, pay, aad_len, P, otk, q, c.act, tag);
+    load_words<4>(sp, pay + P, got);
+    const uint32_t diff = (tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) | (tag[3] ^ got[3]);
+    if (c.act && diff != 0) {  // Error::Crypto, buffer left as received
+      c.st = MQ_ERR_CRYPTO;
+      c.act = false;
+    }
+    wave_sync();  // every lane's MAC reads precede any plaintext write
+    if (c.act && Cmax > 0 && C > 0 && ctr0 >= 1 && ctr0 < nblk) xor_block(sp, pay, ctr0, P, ks0);
+    for (uint32_t it = 1; it < Cmax; ++it) {
+      const uint32_t ctr = q * C + it;
+      const bool a = c.act && it < C && ctr < nblk;
+      uint32_t ks[16];
+      chacha20_block(key, ctr, n0, n1, n2, ks);
+      if (a) xor_block(sp, pay, ctr, P, ks);
+    }
+    if (direct && hdr_written && !c.act) {  // direct path writes HBM in place: undo the unmask
+      sp.st8(pkt, orig_b0);
+      for (uint32_t j = 0; j < pn_len; ++j) sp.st8(pkt + d.pn_offset + j, (uint8_t)(orig_pn >> (8 * j)));
+    }
+  }
+};
+
+}  // namespace mq
+
+using namespace mq;
+
+extern "C" __global__ __launch_bounds__(64) void mq_chacha_seal_kernel(
+    const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
+    const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,
+    const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  run_tile<ChaChaPolicy, false>(smem, blockIdx.x, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr);
+}
+
+extern "C" __global__ __launch_bounds__(64) void mq_chacha_open_kernel(
+    const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
+    const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,
+    const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  run_tile<ChaChaPolicy, true>(smem, blockIdx.x, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out);
+}
+
+// Batched HeaderProtection::mask for ChaCha20 rows (one sample per lane).
+extern "C" __global__ __launch_bounds__(256) void mq_chacha_hp_kernel(
+    const KeyRow* __restrict__ kt, uint32_t n_rows, const uint32_t* __restrict__ key_ids,
+    const uint8_t* __restrict__ samples, uint8_t* __restrict__ masks, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t kid = key_ids[i];
+  if (kid >= n_rows || kt[kid].suite != MQ_SUITE_CHACHA20) return;
+  GlobalSpace sp{const_cast<uint8_t*>(samples), (uint64_t)n * 16};
+  uint32_t m0, m1;
+  ChaChaPolicy::hp_mask(sp, (uint64_t)i * 16, kt + kid, m0, m1);
+  for (int b = 0; b < 4; ++b) masks[5 * (size_t)i + b] = (uint8_t)(m0 >> (8 * b));
+  masks[5 * (size_t)i + 4] = (uint8_t)m1;
+}
+
+// ---- host-side launchers (called from mq_host.cpp) -------------------------------------------
+hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena,
+                            uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
+                            const uint32_t* index, const uint32_t* n_dev, uint8_t* status,
+                            uint64_t* pn_out, hipStream_t s) {
+  const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
+  if (tiles == 0) return hipSuccess;
+  if (open)
+    hipLaunchKernelGGL(mq_chacha_open_kernel, dim3(tiles), dim3(kWave), kLdsBytes, s, kt, n_rows, arena,
+                       arena_len, desc, n, index, n_dev, status, pn_out);
+  else
+    hipLaunchKernelGGL(mq_chacha_seal_kernel, dim3(tiles), dim3(kWave), kLdsBytes, s, kt, n_rows, arena,
+                       arena_len, desc, n, index, n_dev, status);
+  return hipGetLastError();
+}
+
+hipError_t mq_launch_chacha_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t* key_ids,
+                               const uint8_t* samples, uint8_t* masks, uint32_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(mq_chacha_hp_kernel, dim3((n + 255) / 256), dim3(256), 0, s, kt, n_rows, key_ids,
+                     samples, masks, n);
+  return hipGetLastError();
+}

@@ -1,0 +1,284 @@
+// mq_device.h — device-side building blocks of the MI355X (gfx950) packet-protection kernels.
+//
+// Execution model: one 64-lane wave per workgroup processes a TILE of
+// kPktsPerTile = 16 packets; each packet is owned by a QUAD of kLanesPerPkt = 4 lanes.
+//   * staging: the tile's packets are gathered HBM -> LDS with whole-packet contiguous
+//     16-B-per-lane loads (1 KiB per wave instruction), because one-packet-per-lane strided
+//     access measured 2.7 TB/s vs 5.5 TB/s contiguous on MI355X (tools/ubench/ubench3.hip);
+//   * keystream blocks of a packet are spread over its quad (ChaCha20 64-B blocks / AES-CTR
+//     16-B blocks), XORed in LDS;
+//   * the MAC (Poly1305 / GHASH) is a 4-way interleaved Horner evaluation (lane q takes MAC
+//     blocks i = 4k + q with multiplier r^4 / H^4, then one final multiply by r^(4-q) / H^(4-q))
+//     followed by a quad reduction through DPP;
+//   * header protection and the store back to HBM close the tile.
+// Tiles whose packets do not fit the LDS budget run the same code on HBM directly ("direct").
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mq_aead.h"
+
+namespace mq {
+
+constexpr int kWave = 64;
+constexpr int kPktsPerTile = 16;
+constexpr int kLanesPerPkt = kWave / kPktsPerTile;  // 4: one quad per packet
+constexpr uint32_t kLdsBytes = 20480;                // dynamic LDS per 1-wave workgroup -> 8 WG/CU
+constexpr uint32_t kTableBytes = kPktsPerTile * 16;  // per-packet slot table
+constexpr uint32_t kSlack = 64;                      // over-read room after the last slot
+constexpr uint32_t kSpanBudget = kLdsBytes - kTableBytes - kSlack;  // 20160 bytes of packet data
+
+// Device key-table row (512 B). Filled on the host by mq_keytable_create (mq_host.cpp).
+struct alignas(16) KeyRow {
+  uint32_t suite;
+  uint32_t pad0[3];
+  uint32_t iv[3];      // IV bytes as 3 little-endian words
+  uint32_t pad1;
+  uint32_t key[8];     // ChaCha20 key (LE words)
+  uint32_t hp[8];      // ChaCha20 HP key (LE words)
+  uint32_t aes_rk[44]; // AES-128 round keys of the AEAD key (FIPS-197 big-endian words)
+  uint32_t hp_rk[44];  // AES-128 round keys of the HP key
+  uint32_t H[4][4];    // GHASH H^1..H^4 (GCM byte order, big-endian words)
+};
+static_assert(sizeof(KeyRow) == 512, "KeyRow layout");
+
+// ------------------------------------------------------------------------------------------
+// byte-address spaces: LDS (staged tile) or the HBM arena (direct path)
+struct LdsSpace {
+  uint8_t* base;
+  typedef uint32_t off_t;
+  __device__ __forceinline__ uint32_t ld32(uint32_t a) const { return *(const uint32_t*)(base + a); }
+  __device__ __forceinline__ void st32(uint32_t a, uint32_t v) const { *(uint32_t*)(base + a) = v; }
+  __device__ __forceinline__ uint8_t ld8(uint32_t a) const { return base[a]; }
+  __device__ __forceinline__ void st8(uint32_t a, uint8_t v) const { base[a] = v; }
+};
+
+struct GlobalSpace {
+  uint8_t* base;
+  uint64_t len;  // reads at or beyond len return 0 (never fault)
+  typedef uint64_t off_t;
+  __device__ __forceinline__ uint32_t ld32(uint64_t a) const {
+    if (a + 4 <= len) return *(const uint32_t*)(base + a);
+    uint32_t w = 0;  // tail of an arena whose length is not a multiple of 4
+    for (int b = 0; b < 4; ++b)
+      if (a + b < len) w |= (uint32_t)base[a + b] << (8 * b);
+    return w;
+  }
+  __device__ __forceinline__ void st32(uint64_t a, uint32_t v) const { *(uint32_t*)(base + a) = v; }
+  __device__ __forceinline__ uint8_t ld8(uint64_t a) const { return a < len ? base[a] : (uint8_t)0; }
+  __device__ __forceinline__ void st8(uint64_t a, uint8_t v) const { base[a] = v; }
+};
+
+// v_perm_b32 selectors: loads realign memory dwords to a payload that starts `v` bytes into a
+// dword; stores realign payload words back to memory dwords. perm(hi, lo, sel) picks bytes of
+// the 8-byte {hi, lo} pair (lo = bytes 0..3).
+__device__ __forceinline__ uint32_t sel_load(uint32_t v) { return 0x03020100u + v * 0x01010101u; }
+__device__ __forceinline__ uint32_t sel_store(uint32_t v) { return 0x07060504u - v * 0x01010101u; }
+__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+  return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+// Read N payload-aligned words starting at byte address `a` (any alignment).
+template <int N, class S>
+__device__ __forceinline__ void load_words(const S& sp, typename S::off_t a, uint32_t (&w)[N]) {
+  typename S::off_t b = a & ~(typename S::off_t)3;
+  uint32_t sel = sel_load((uint32_t)(a & 3));
+  uint32_t m[N + 1];
+#pragma unroll
+  for (int k = 0; k <= N; ++k) m[k] = sp.ld32(b + 4 * k);
+#pragma unroll
+  for (int k = 0; k < N; ++k) w[k] = perm(m[k + 1], m[k], sel);
+}
+
+// Write bytes [a, a + len) (len <= 4N) from payload-aligned words w. Bytes outside the range
+// are never touched, so quads writing adjacent ranges never race on a shared dword.
+template <int N, class S>
+__device__ __forceinline__ void store_words(const S& sp, typename S::off_t a, const uint32_t (&w)[N],
+                                            int len) {
+  typename S::off_t b = a & ~(typename S::off_t)3;
+  int v = (int)(a & 3);
+  uint32_t sel = sel_store((uint32_t)v);
+#pragma unroll
+  for (int m = 0; m <= N; ++m) {
+    uint32_t hi = m < N ? w[m] : 0u, lo = m > 0 ? w[m - 1] : 0u;
+    uint32_t out = perm(hi, lo, sel);
+    int lo_idx = 4 * m - v;  // payload index of byte 0 of this memory dword
+    if (lo_idx >= 0 && lo_idx + 4 <= len) {
+      sp.st32(b + 4 * m, out);
+    } else if (lo_idx + 4 > 0 && lo_idx < len) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        int idx = lo_idx + k;
+        if (idx >= 0 && idx < len) sp.st8(b + 4 * m + k, (uint8_t)(out >> (8 * k)));
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t byte_mask(int rem, int k) {  // keep bytes < rem of word k
+  int r = rem - 4 * k;
+  return r >= 4 ? 0xffffffffu : (r <= 0 ? 0u : ((1u << (8 * r)) - 1u));
+}
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+// ------------------------------------------------------------------------------------------
+// DPP within a quad (lanes 4p..4p+3): quad_perm selectors
+__device__ __forceinline__ uint32_t quad_bcast0(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x00, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t quad_swap1(uint32_t x) {  // [1,0,3,2]
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t quad_swap2(uint32_t x) {  // [2,3,0,1]
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xf, 0xf, false);
+}
+
+// Wave-local barrier: tiles are private to one wave, so ordering the wave's own LDS / HBM
+// accesses (and keeping the compiler from moving them) is all a phase boundary needs. Unlike
+// __syncthreads() it is safe in multi-wave workgroups whose waves take different paths.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    uint32_t y = (uint32_t)__shfl_xor((int)x, d, 64);
+    x = x > y ? x : y;
+  }
+  return x;
+}
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    uint64_t y = __shfl_xor(x, d, 64);
+    x = x < y ? x : y;
+  }
+  return x;
+}
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    uint64_t y = __shfl_xor(x, d, 64);
+    x = x > y ? x : y;
+  }
+  return x;
+}
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+
+// ------------------------------------------------------------------------------------------
+// ChaCha20 block function (RFC 8439 §2.3): out = keystream words of block `ctr`.
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+#define MQ_QR(a, b, c, d)                 \
+  a += b; d ^= a; d = rotl(d, 16);        \
+  c += d; b ^= c; b = rotl(b, 12);        \
+  a += b; d ^= a; d = rotl(d, 8);         \
+  c += d; b ^= c; b = rotl(b, 7);
+
+__device__ __forceinline__ void chacha20_block(const uint32_t (&key)[8], uint32_t ctr,
+                                               uint32_t n0, uint32_t n1, uint32_t n2,
+                                               uint32_t (&out)[16]) {
+  uint32_t x0 = 0x61707865u, x1 = 0x3320646eu, x2 = 0x79622d32u, x3 = 0x6b206574u;
+  uint32_t x4 = key[0], x5 = key[1], x6 = key[2], x7 = key[3];
+  uint32_t x8 = key[4], x9 = key[5], x10 = key[6], x11 = key[7];
+  uint32_t x12 = ctr, x13 = n0, x14 = n1, x15 = n2;
+#pragma unroll 2
+  for (int i = 0; i < 10; ++i) {
+    MQ_QR(x0, x4, x8, x12) MQ_QR(x1, x5, x9, x13) MQ_QR(x2, x6, x10, x14) MQ_QR(x3, x7, x11, x15)
+    MQ_QR(x0, x5, x10, x15) MQ_QR(x1, x6, x11, x12) MQ_QR(x2, x7, x8, x13) MQ_QR(x3, x4, x9, x14)
+  }
+  out[0] = x0 + 0x61707865u; out[1] = x1 + 0x3320646eu; out[2] = x2 + 0x79622d32u;
+  out[3] = x3 + 0x6b206574u;
+  out[4] = x4 + key[0]; out[5] = x5 + key[1]; out[6] = x6 + key[2]; out[7] = x7 + key[3];
+  out[8] = x8 + key[4]; out[9] = x9 + key[5]; out[10] = x10 + key[6]; out[11] = x11 + key[7];
+  out[12] = x12 + ctr; out[13] = x13 + n0; out[14] = x14 + n1; out[15] = x15 + n2;
+}
+
+// ------------------------------------------------------------------------------------------
+// Poly1305 arithmetic mod 2^130-5 in radix 2^26 (5 limbs), general multiplier (r, r^2..r^4).
+struct P26 { uint32_t l[5]; };
+struct P26m { uint32_t r[5], s[4]; };  // multiplier with s[i] = 5 * r[i+1]
+
+__device__ __forceinline__ P26m p26_mult(const P26& r) {
+  P26m m;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) m.r[i] = r.l[i];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) m.s[i] = r.l[i + 1] * 5u;
+  return m;
+}
+
+__device__ __forceinline__ P26 p26_from_words(uint32_t t0, uint32_t t1, uint32_t t2, uint32_t t3,
+                                              uint32_t hibit) {
+  P26 h;
+  h.l[0] = t0 & 0x3ffffff;
+  h.l[1] = ((t0 >> 26) | (t1 << 6)) & 0x3ffffff;
+  h.l[2] = ((t1 >> 20) | (t2 << 12)) & 0x3ffffff;
+  h.l[3] = ((t2 >> 14) | (t3 << 18)) & 0x3ffffff;
+  h.l[4] = (t3 >> 8) | (hibit << 24);
+  return h;
+}
+
+// h = h * m (mod 2^130 - 5), partially reduced (limbs < 2^26, l[1] < 2^26 + 2^8).
+__device__ __forceinline__ void p26_mul(P26& h, const P26m& m) {
+  const uint32_t h0 = h.l[0], h1 = h.l[1], h2 = h.l[2], h3 = h.l[3], h4 = h.l[4];
+  uint64_t d0 = (uint64_t)h0 * m.r[0] + (uint64_t)h1 * m.s[3] + (uint64_t)h2 * m.s[2] + (uint64_t)h3 * m.s[1] + (uint64_t)h4 * m.s[0];
+  uint64_t d1 = (uint64_t)h0 * m.r[1] + (uint64_t)h1 * m.r[0] + (uint64_t)h2 * m.s[3] + (uint64_t)h3 * m.s[2] + (uint64_t)h4 * m.s[1];
+  uint64_t d2 = (uint64_t)h0 * m.r[2] + (uint64_t)h1 * m.r[1] + (uint64_t)h2 * m.r[0] + (uint64_t)h3 * m.s[3] + (uint64_t)h4 * m.s[2];
+  uint64_t d3 = (uint64_t)h0 * m.r[3] + (uint64_t)h1 * m.r[2] + (uint64_t)h2 * m.r[1] + (uint64_t)h3 * m.r[0] + (uint64_t)h4 * m.s[3];
+  uint64_t d4 = (uint64_t)h0 * m.r[4] + (uint64_t)h1 * m.r[3] + (uint64_t)h2 * m.r[2] + (uint64_t)h3 * m.r[1] + (uint64_t)h4 * m.r[0];
+  d1 += d0 >> 26;
+  d2 += d1 >> 26;
+  d3 += d2 >> 26;
+  d4 += d3 >> 26;
+  uint64_t t = (uint64_t)((uint32_t)d0 & 0x3ffffff) + (d4 >> 26) * 5u;
+  h.l[0] = (uint32_t)t & 0x3ffffff;
+  h.l[1] = ((uint32_t)d1 & 0x3ffffff) + (uint32_t)(t >> 26);
+  h.l[2] = (uint32_t)d2 & 0x3ffffff;
+  h.l[3] = (uint32_t)d3 & 0x3ffffff;
+  h.l[4] = (uint32_t)d4 & 0x3ffffff;
+}
+
+// Full reduction mod p and tag = (h + s) mod 2^128, as 4 LE words.
+__device__ __forceinline__ void p26_finish(P26 h, const uint32_t (&s)[4], uint32_t (&tag)[4]) {
+  uint32_t c;
+  c = h.l[0] >> 26; h.l[0] &= 0x3ffffff; h.l[1] += c;
+  c = h.l[1] >> 26; h.l[1] &= 0x3ffffff; h.l[2] += c;
+  c = h.l[2] >> 26; h.l[2] &= 0x3ffffff; h.l[3] += c;
+  c = h.l[3] >> 26; h.l[3] &= 0x3ffffff; h.l[4] += c;
+  c = h.l[4] >> 26; h.l[4] &= 0x3ffffff; h.l[0] += c * 5;
+  c = h.l[0] >> 26; h.l[0] &= 0x3ffffff; h.l[1] += c;
+  c = h.l[1] >> 26; h.l[1] &= 0x3ffffff; h.l[2] += c;
+  uint32_t g0, g1, g2, g3, g4;
+  g0 = h.l[0] + 5; c = g0 >> 26; g0 &= 0x3ffffff;
+  g1 = h.l[1] + c; c = g1 >> 26; g1 &= 0x3ffffff;
+  g2 = h.l[2] + c; c = g2 >> 26; g2 &= 0x3ffffff;
+  g3 = h.l[3] + c; c = g3 >> 26; g3 &= 0x3ffffff;
+  g4 = h.l[4] + c - (1u << 26);
+  bool use_g = (g4 >> 31) == 0;
+  uint32_t f0 = use_g ? g0 : h.l[0], f1 = use_g ? g1 : h.l[1], f2 = use_g ? g2 : h.l[2];
+  uint32_t f3 = use_g ? g3 : h.l[3], f4 = use_g ? g4 : h.l[4];
+  uint32_t w0 = f0 | (f1 << 26), w1 = (f1 >> 6) | (f2 << 20), w2 = (f2 >> 12) | (f3 << 14),
+           w3 = (f3 >> 18) | (f4 << 8);
+  uint64_t t = (uint64_t)w0 + s[0];
+  tag[0] = (uint32_t)t;
+  t = (uint64_t)w1 + s[1] + (t >> 32);
+  tag[1] = (uint32_t)t;
+  t = (uint64_t)w2 + s[2] + (t >> 32);
+  tag[2] = (uint32_t)t;
+  t = (uint64_t)w3 + s[3] + (t >> 32);
+  tag[3] = (uint32_t)t;
+}
+
+}  // namespace mq

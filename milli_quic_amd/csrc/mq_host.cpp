@@ -1,0 +1,699 @@
+// mq_host.cpp — C ABI of libmq_aead.so (include/mq_aead.h).
+//
+// Host side of the drop-in boundary: key contexts (CryptoProvider::aead/header_protection,
+// reference src/crypto/rustcrypto.rs:225-287), per-packet Aead/HeaderProtection calls that run
+// the HIP kernels on a batch of one, the HKDF/QUIC key schedule (src/crypto/key_schedule.rs),
+// device key tables and the stream-ordered batch API. No CPU fallback exists for any
+// cryptographic transform on packets: without a gfx950 device the calls fail with
+// MQ_ERR_NO_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "mq_device.h"
+
+using mq::KeyRow;
+
+// launchers defined in the .hip translation units
+hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena,
+                            uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
+                            const uint32_t* index, const uint32_t* n_dev, uint8_t* status,
+                            uint64_t* pn_out, hipStream_t s);
+hipError_t mq_launch_chacha_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t* key_ids,
+                               const uint8_t* samples, uint8_t* masks, uint32_t n, hipStream_t s);
+hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena,
+                         uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
+                         const uint32_t* index, const uint32_t* n_dev, uint8_t* status,
+                         uint64_t* pn_out, hipStream_t s);
+hipError_t mq_launch_aes_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t* key_ids,
+                            const uint8_t* samples, uint8_t* masks, uint32_t n, hipStream_t s);
+hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_desc* desc, uint32_t n,
+                               uint32_t* list, uint32_t* block_counts, uint32_t* counts,
+                               hipStream_t s);
+size_t mq_partition_workspace(uint32_t n);
+
+namespace {
+
+// ---------------------------------------------------------------------------------------------
+// device selection
+std::mutex g_dev_mu;
+int g_dev_state = 0;  // 0 unknown, 1 ok, -1 unusable
+int g_dev = 0;
+
+int ensure_device() {
+  std::lock_guard<std::mutex> lk(g_dev_mu);
+  if (g_dev_state == 1) {
+    hipSetDevice(g_dev);
+    return MQ_OK;
+  }
+  if (g_dev_state == -1) return MQ_ERR_NO_DEVICE;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= g_dev) { g_dev_state = -1; return MQ_ERR_NO_DEVICE; }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, g_dev) != hipSuccess ||
+      std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    g_dev_state = -1;
+    return MQ_ERR_NO_DEVICE;
+  }
+  if (hipSetDevice(g_dev) != hipSuccess) { g_dev_state = -1; return MQ_ERR_NO_DEVICE; }
+  g_dev_state = 1;
+  return MQ_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// AES-128 key expansion / block encryption (FIPS-197), host side: the reference computes the
+// key schedule and GHASH H once at construction (rustcrypto.rs:232-252); so does the key table.
+uint8_t g_sbox[256];
+std::once_flag g_sbox_once;
+
+uint8_t gmul(uint8_t a, uint8_t b) {
+  uint8_t r = 0;
+  while (b) {
+    if (b & 1) r ^= a;
+    a = (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0));
+    b >>= 1;
+  }
+  return r;
+}
+
+void init_sbox() {
+  // walk the multiplicative group with generator 3 to get inverses, then the affine map
+  uint8_t p = 1, qv = 1;
+  do {
+    p = (uint8_t)(p ^ (p << 1) ^ ((p & 0x80) ? 0x1b : 0));
+    qv ^= (uint8_t)(qv << 1); qv ^= (uint8_t)(qv << 2); qv ^= (uint8_t)(qv << 4);
+    if (qv & 0x80) qv ^= 0x09;
+    const uint8_t x = (uint8_t)(qv ^ ((qv << 1) | (qv >> 7)) ^ ((qv << 2) | (qv >> 6)) ^
+                                ((qv << 3) | (qv >> 5)) ^ ((qv << 4) | (qv >> 4)));
+    g_sbox[p] = x ^ 0x63;
+  } while (p != 1);
+  g_sbox[0] = 0x63;
+}
+
+const uint8_t* sbox() {
+  std::call_once(g_sbox_once, init_sbox);
+  return g_sbox;
+}
+
+uint32_t be32(const uint8_t* p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+uint32_t le32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+void aes_expand(const uint8_t key[16], uint32_t rk[44]) {
+  const uint8_t* S = sbox();
+  uint8_t rcon = 1;
+  for (int i = 0; i < 4; ++i) rk[i] = be32(key + 4 * i);
+  for (int i = 4; i < 44; ++i) {
+    uint32_t t = rk[i - 1];
+    if (i % 4 == 0) {
+      t = (t << 8) | (t >> 24);
+      t = ((uint32_t)S[t >> 24] << 24) | ((uint32_t)S[(t >> 16) & 0xff] << 16) |
+          ((uint32_t)S[(t >> 8) & 0xff] << 8) | S[t & 0xff];
+      t ^= (uint32_t)rcon << 24;
+      rcon = gmul(rcon, 2);
+    }
+    rk[i] = rk[i - 4] ^ t;
+  }
+}
+
+void aes_encrypt(const uint32_t rk[44], const uint8_t in[16], uint8_t out[16]) {
+  const uint8_t* S = sbox();
+  uint8_t s[16], t[16];
+  for (int c = 0; c < 4; ++c) {
+    uint32_t w = be32(in + 4 * c) ^ rk[c];
+    s[4 * c] = (uint8_t)(w >> 24); s[4 * c + 1] = (uint8_t)(w >> 16);
+    s[4 * c + 2] = (uint8_t)(w >> 8); s[4 * c + 3] = (uint8_t)w;
+  }
+  for (int r = 1; r <= 10; ++r) {
+    for (int c = 0; c < 4; ++c)
+      for (int i = 0; i < 4; ++i) t[4 * c + i] = S[s[4 * ((c + i) & 3) + i]];
+    if (r < 10) {
+      for (int c = 0; c < 4; ++c) {
+        const uint8_t a0 = t[4 * c], a1 = t[4 * c + 1], a2 = t[4 * c + 2], a3 = t[4 * c + 3];
+        s[4 * c] = gmul(a0, 2) ^ gmul(a1, 3) ^ a2 ^ a3;
+        s[4 * c + 1] = a0 ^ gmul(a1, 2) ^ gmul(a2, 3) ^ a3;
+        s[4 * c + 2] = a0 ^ a1 ^ gmul(a2, 2) ^ gmul(a3, 3);
+        s[4 * c + 3] = gmul(a0, 3) ^ a1 ^ a2 ^ gmul(a3, 2);
+      }
+    } else {
+      std::memcpy(s, t, 16);
+    }
+    for (int c = 0; c < 4; ++c) {
+      const uint32_t k = rk[4 * r + c];
+      s[4 * c] ^= (uint8_t)(k >> 24); s[4 * c + 1] ^= (uint8_t)(k >> 16);
+      s[4 * c + 2] ^= (uint8_t)(k >> 8); s[4 * c + 3] ^= (uint8_t)k;
+    }
+  }
+  std::memcpy(out, s, 16);
+}
+
+// GF(2^128) product in GCM bit order (SP 800-38D Alg. 1)
+void gf128_mul(const uint8_t x[16], const uint8_t y[16], uint8_t out[16]) {
+  uint8_t z[16] = {0}, v[16];
+  std::memcpy(v, y, 16);
+  for (int i = 0; i < 128; ++i) {
+    if ((x[i >> 3] >> (7 - (i & 7))) & 1)
+      for (int k = 0; k < 16; ++k) z[k] ^= v[k];
+    const int lsb = v[15] & 1;
+    for (int k = 15; k > 0; --k) v[k] = (uint8_t)((v[k] >> 1) | (v[k - 1] << 7));
+    v[0] >>= 1;
+    if (lsb) v[0] ^= 0xe1;
+  }
+  std::memcpy(out, z, 16);
+}
+
+size_t suite_key_len(uint32_t suite) {
+  return suite == MQ_SUITE_AES128GCM ? 16 : suite == MQ_SUITE_CHACHA20 ? 32 : 0;
+}
+
+// Build one device row from host key material. Returns false on a bad suite.
+bool build_row(const mq_key_material& km, KeyRow& row) {
+  std::memset(&row, 0, sizeof row);
+  if (!suite_key_len(km.suite)) return false;
+  row.suite = km.suite;
+  for (int i = 0; i < 3; ++i) row.iv[i] = le32(km.iv + 4 * i);
+  for (int i = 0; i < 8; ++i) row.key[i] = le32(km.key + 4 * i);
+  for (int i = 0; i < 8; ++i) row.hp[i] = le32(km.hp + 4 * i);
+  if (km.suite == MQ_SUITE_AES128GCM) {
+    aes_expand(km.key, row.aes_rk);
+    aes_expand(km.hp, row.hp_rk);
+    uint8_t h[4][16], zero[16] = {0};
+    aes_encrypt(row.aes_rk, zero, h[0]);
+    gf128_mul(h[0], h[0], h[1]);
+    gf128_mul(h[1], h[0], h[2]);
+    gf128_mul(h[2], h[0], h[3]);
+    for (int p = 0; p < 4; ++p)
+      for (int w = 0; w < 4; ++w) row.H[p][w] = be32(h[p] + 4 * w);
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------------------------------------
+// SHA-256 / HMAC / HKDF (FIPS 180-4, RFC 2104, RFC 5869): Hkdf trait, rustcrypto.rs:9-24
+const uint32_t kK256[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+struct Sha256 {
+  uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                   0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  uint8_t buf[64];
+  size_t fill = 0;
+  uint64_t total = 0;
+
+  static uint32_t ror(uint32_t x, int r) { return (x >> r) | (x << (32 - r)); }
+  void block(const uint8_t* p) {
+    uint32_t w[64];
+    for (int i = 0; i < 16; ++i) w[i] = be32(p + 4 * i);
+    for (int i = 16; i < 64; ++i)
+      w[i] = w[i - 16] + (ror(w[i - 15], 7) ^ ror(w[i - 15], 18) ^ (w[i - 15] >> 3)) + w[i - 7] +
+             (ror(w[i - 2], 17) ^ ror(w[i - 2], 19) ^ (w[i - 2] >> 10));
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+    for (int i = 0; i < 64; ++i) {
+      const uint32_t t1 = hh + (ror(e, 6) ^ ror(e, 11) ^ ror(e, 25)) + ((e & f) ^ (~e & g)) + kK256[i] + w[i];
+      const uint32_t t2 = (ror(a, 2) ^ ror(a, 13) ^ ror(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+      hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+    h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+  }
+  void update(const uint8_t* p, size_t n) {
+    total += n;
+    while (n) {
+      const size_t k = std::min(n, (size_t)64 - fill);
+      std::memcpy(buf + fill, p, k);
+      fill += k; p += k; n -= k;
+      if (fill == 64) { block(buf); fill = 0; }
+    }
+  }
+  void final(uint8_t out[32]) {
+    const uint64_t bits = total * 8;
+    const uint8_t one = 0x80, zero = 0;
+    update(&one, 1);
+    while (fill != 56) update(&zero, 1);
+    uint8_t len[8];
+    for (int i = 0; i < 8; ++i) len[i] = (uint8_t)(bits >> (56 - 8 * i));
+    update(len, 8);
+    for (int i = 0; i < 8; ++i) {
+      out[4 * i] = (uint8_t)(h[i] >> 24); out[4 * i + 1] = (uint8_t)(h[i] >> 16);
+      out[4 * i + 2] = (uint8_t)(h[i] >> 8); out[4 * i + 3] = (uint8_t)h[i];
+    }
+  }
+};
+
+void hmac_sha256(const uint8_t* key, size_t key_len, const uint8_t* m1, size_t l1, const uint8_t* m2,
+                 size_t l2, const uint8_t* m3, size_t l3, uint8_t out[32]) {
+  uint8_t k[64] = {0}, pad[64], inner[32];
+  if (key_len > 64) { Sha256 s; s.update(key, key_len); s.final(k); }
+  else std::memcpy(k, key, key_len);
+  Sha256 si, so;
+  for (int i = 0; i < 64; ++i) pad[i] = k[i] ^ 0x36;
+  si.update(pad, 64); si.update(m1, l1); si.update(m2, l2); si.update(m3, l3); si.final(inner);
+  for (int i = 0; i < 64; ++i) pad[i] = k[i] ^ 0x5c;
+  so.update(pad, 64); so.update(inner, 32); so.final(out);
+}
+
+// ---------------------------------------------------------------------------------------------
+// pinned staging + device scratch for the per-packet (batch of one) calls
+struct Scratch {
+  hipStream_t stream = nullptr;
+  uint8_t* dev = nullptr;   // [row 512][desc 32][status 16][pn 8][pad][packet ...]
+  uint8_t* host = nullptr;  // pinned mirror
+  size_t cap = 0;
+  std::mutex mu;
+
+  static constexpr size_t kHdr = 1024;  // row + desc + status + pn, then the packet at +1024
+
+  int ensure(size_t pkt_bytes) {
+    const size_t need = kHdr + ((pkt_bytes + 255) & ~(size_t)255) + 256;
+    if (!stream && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return MQ_ERR_HIP;
+    if (need <= cap) return MQ_OK;
+    if (dev) hipFree(dev);
+    if (host) hipHostFree(host);
+    dev = nullptr; host = nullptr; cap = 0;
+    if (hipMalloc(&dev, need) != hipSuccess) return MQ_ERR_HIP;
+    if (hipHostMalloc(&host, need, hipHostMallocDefault) != hipSuccess) return MQ_ERR_HIP;
+    cap = need;
+    return MQ_OK;
+  }
+  ~Scratch() {
+    if (dev) hipFree(dev);
+    if (host) hipHostFree(host);
+    if (stream) hipStreamDestroy(stream);
+  }
+};
+
+// Run one packet through the seal/open kernel of `row.suite`. pkt = aad || payload || tag area,
+// `len` bytes; descriptor in NO_HP mode with pn = 0 (the caller's nonce sits in row.iv).
+int run_one(Scratch& sc, const KeyRow& row, uint8_t* pkt, uint32_t len, uint32_t aad_len, bool open) {
+  int rc = ensure_device();
+  if (rc) return rc;
+  rc = sc.ensure(len);
+  if (rc) return rc;
+  std::memcpy(sc.host, &row, sizeof row);
+  mq_pkt_desc d;
+  std::memset(&d, 0, sizeof d);
+  d.offset = Scratch::kHdr;
+  d.len = len;
+  d.key_id = 0;
+  d.pn = 0;
+  d.pn_offset = (uint16_t)aad_len;
+  d.pn_len = 0;
+  d.flags = MQ_PKT_NO_HP;
+  std::memcpy(sc.host + 512, &d, sizeof d);
+  std::memset(sc.host + 544, 0xff, 16);
+  std::memcpy(sc.host + Scratch::kHdr, pkt, len);
+  const size_t bytes = Scratch::kHdr + len;
+  if (hipMemcpyAsync(sc.dev, sc.host, bytes, hipMemcpyHostToDevice, sc.stream) != hipSuccess) return MQ_ERR_HIP;
+  const KeyRow* kt = (const KeyRow*)sc.dev;
+  const mq_pkt_desc* dd = (const mq_pkt_desc*)(sc.dev + 512);
+  uint8_t* st = sc.dev + 544;
+  uint64_t* pn = (uint64_t*)(sc.dev + 560);
+  // the arena is the whole scratch buffer; the packet sits at offset kHdr
+  hipError_t e = row.suite == MQ_SUITE_CHACHA20
+                     ? mq_launch_chacha(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, st, pn, sc.stream)
+                     : mq_launch_aes(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, st, pn, sc.stream);
+  if (e != hipSuccess) return MQ_ERR_HIP;
+  if (hipMemcpyAsync(sc.host + 544, st, 16, hipMemcpyDeviceToHost, sc.stream) != hipSuccess) return MQ_ERR_HIP;
+  if (hipMemcpyAsync(sc.host + Scratch::kHdr, sc.dev + Scratch::kHdr, len, hipMemcpyDeviceToHost,
+                     sc.stream) != hipSuccess)
+    return MQ_ERR_HIP;
+  if (hipStreamSynchronize(sc.stream) != hipSuccess) return MQ_ERR_HIP;
+  const int status = sc.host[544];
+  if (status == MQ_OK) std::memcpy(pkt, sc.host + Scratch::kHdr, len);
+  return status;
+}
+
+}  // namespace
+
+// =============================================================================================
+// opaque handle definitions
+struct mq_aead_ctx {
+  uint32_t suite;
+  KeyRow row;  // key schedule, H powers; iv is overwritten by the per-call nonce
+  mutable Scratch sc;
+};
+struct mq_hp_ctx {
+  uint32_t suite;
+  KeyRow row;
+  mutable Scratch sc;
+};
+struct mq_keytable {
+  KeyRow* dev = nullptr;
+  uint32_t rows = 0;
+};
+
+extern "C" {
+
+const char* mq_version(void) { return "mq_aead 0.1.0 (gfx950)"; }
+
+int mq_device_init(int device) {
+  {
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    g_dev = device;
+    g_dev_state = 0;
+  }
+  return ensure_device();
+}
+
+const char* mq_status_str(int status) {
+  switch (status) {
+    case MQ_OK: return "ok";
+    case MQ_ERR_CRYPTO: return "crypto";
+    case MQ_ERR_BUFFER_TOO_SMALL: return "buffer too small";
+    case MQ_ERR_INVALID_ARG: return "invalid argument";
+    case MQ_ERR_PROTOCOL: return "protocol violation";
+    case MQ_ERR_SUITE: return "suite mismatch";
+    case MQ_ERR_NO_DEVICE: return "no gfx950 device";
+    case MQ_ERR_HIP: return "hip runtime error";
+    default: return "unknown";
+  }
+}
+
+size_t mq_aead_key_len(uint32_t suite) { return suite_key_len(suite); }
+
+int mq_aead_new(uint32_t suite, const uint8_t* key, size_t key_len, mq_aead_ctx** out) {
+  if (!out) return MQ_ERR_INVALID_ARG;
+  *out = nullptr;
+  if (!suite_key_len(suite) || !key || key_len != suite_key_len(suite)) return MQ_ERR_CRYPTO;
+  const int rc = ensure_device();
+  if (rc) return rc;
+  mq_key_material km;
+  std::memset(&km, 0, sizeof km);
+  km.suite = suite;
+  std::memcpy(km.key, key, key_len);
+  mq_aead_ctx* c = new mq_aead_ctx();
+  c->suite = suite;
+  build_row(km, c->row);
+  *out = c;
+  return MQ_OK;
+}
+
+void mq_aead_free(mq_aead_ctx* ctx) { delete ctx; }
+
+int mq_aead_seal_in_place(const mq_aead_ctx* ctx, const uint8_t* nonce, size_t nonce_len,
+                          const uint8_t* aad, size_t aad_len, uint8_t* buf, size_t buf_len,
+                          size_t payload_len, size_t* out_len, size_t* needed) {
+  if (!ctx) return MQ_ERR_INVALID_ARG;
+  if (!nonce || nonce_len != 12) return MQ_ERR_CRYPTO;  // rustcrypto.rs:48-50,120-122
+  const size_t total = payload_len + 16;
+  if (buf_len < total) {  // rustcrypto.rs:51-54,123-126
+    if (needed) *needed = total;
+    return MQ_ERR_BUFFER_TOO_SMALL;
+  }
+  if ((aad_len && !aad) || !buf || aad_len > 0xffff || aad_len + total > 0xffffffffu) return MQ_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(ctx->sc.mu);
+  KeyRow row = ctx->row;
+  for (int i = 0; i < 3; ++i) row.iv[i] = le32(nonce + 4 * i);
+  std::vector<uint8_t> pkt(aad_len + total);
+  if (aad_len) std::memcpy(pkt.data(), aad, aad_len);
+  std::memcpy(pkt.data() + aad_len, buf, payload_len);
+  const int rc = run_one(ctx->sc, row, pkt.data(), (uint32_t)pkt.size(), (uint32_t)aad_len, false);
+  if (rc) return rc;
+  std::memcpy(buf, pkt.data() + aad_len, total);
+  if (out_len) *out_len = total;
+  return MQ_OK;
+}
+
+int mq_aead_open_in_place(const mq_aead_ctx* ctx, const uint8_t* nonce, size_t nonce_len,
+                          const uint8_t* aad, size_t aad_len, uint8_t* buf, size_t buf_len,
+                          size_t ct_len, size_t* out_len) {
+  if (!ctx) return MQ_ERR_INVALID_ARG;
+  if (!nonce || nonce_len != 12) return MQ_ERR_CRYPTO;  // rustcrypto.rs:75-77,146-148
+  if (ct_len < 16) return MQ_ERR_CRYPTO;                // :78-80,149-151
+  if (ct_len > buf_len) return MQ_ERR_INVALID_ARG;      // the reference panics (:83,154)
+  if ((aad_len && !aad) || !buf || aad_len > 0xffff || aad_len + ct_len > 0xffffffffu) return MQ_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(ctx->sc.mu);
+  KeyRow row = ctx->row;
+  for (int i = 0; i < 3; ++i) row.iv[i] = le32(nonce + 4 * i);
+  std::vector<uint8_t> pkt(aad_len + ct_len);
+  if (aad_len) std::memcpy(pkt.data(), aad, aad_len);
+  std::memcpy(pkt.data() + aad_len, buf, ct_len);
+  const int rc = run_one(ctx->sc, row, pkt.data(), (uint32_t)pkt.size(), (uint32_t)aad_len, true);
+  if (rc) return rc;  // buffer untouched on failure
+  std::memcpy(buf, pkt.data() + aad_len, ct_len - 16);
+  if (out_len) *out_len = ct_len - 16;
+  return MQ_OK;
+}
+
+int mq_hp_new(uint32_t suite, const uint8_t* key, size_t key_len, mq_hp_ctx** out) {
+  if (!out) return MQ_ERR_INVALID_ARG;
+  *out = nullptr;
+  const size_t want = suite == MQ_SUITE_AES128GCM ? 16 : suite == MQ_SUITE_CHACHA20 ? 32 : 0;
+  if (!want || !key || key_len != want) return MQ_ERR_CRYPTO;  // rustcrypto.rs:247-249,280-282
+  const int rc = ensure_device();
+  if (rc) return rc;
+  mq_key_material km;
+  std::memset(&km, 0, sizeof km);
+  km.suite = suite;
+  std::memcpy(km.hp, key, key_len);
+  if (suite == MQ_SUITE_AES128GCM) std::memset(km.key, 0, 16);
+  mq_hp_ctx* c = new mq_hp_ctx();
+  c->suite = suite;
+  build_row(km, c->row);
+  *out = c;
+  return MQ_OK;
+}
+
+void mq_hp_free(mq_hp_ctx* ctx) { delete ctx; }
+
+int mq_hp_mask(const mq_hp_ctx* ctx, const uint8_t* sample, size_t sample_len, uint8_t mask[5]) {
+  if (!ctx || !mask || !sample || sample_len < 16) return MQ_ERR_INVALID_ARG;
+  int rc = ensure_device();
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(ctx->sc.mu);
+  Scratch& sc = ctx->sc;
+  rc = sc.ensure(64);
+  if (rc) return rc;
+  // layout: row 512 | key id (4) @512 | sample 16 @528 | mask 5 @544
+  std::memcpy(sc.host, &ctx->row, sizeof(KeyRow));
+  const uint32_t kid = 0;
+  std::memcpy(sc.host + 512, &kid, 4);
+  std::memcpy(sc.host + 528, sample, 16);
+  std::memset(sc.host + 544, 0, 8);
+  if (hipMemcpyAsync(sc.dev, sc.host, 560, hipMemcpyHostToDevice, sc.stream) != hipSuccess) return MQ_ERR_HIP;
+  const KeyRow* kt = (const KeyRow*)sc.dev;
+  hipError_t e = ctx->suite == MQ_SUITE_CHACHA20
+                     ? mq_launch_chacha_hp(kt, 1, (const uint32_t*)(sc.dev + 512), sc.dev + 528, sc.dev + 544, 1, sc.stream)
+                     : mq_launch_aes_hp(kt, 1, (const uint32_t*)(sc.dev + 512), sc.dev + 528, sc.dev + 544, 1, sc.stream);
+  if (e != hipSuccess) return MQ_ERR_HIP;
+  if (hipMemcpyAsync(sc.host + 544, sc.dev + 544, 8, hipMemcpyDeviceToHost, sc.stream) != hipSuccess) return MQ_ERR_HIP;
+  if (hipStreamSynchronize(sc.stream) != hipSuccess) return MQ_ERR_HIP;
+  std::memcpy(mask, sc.host + 544, 5);
+  return MQ_OK;
+}
+
+void mq_nonce(const uint8_t iv[12], uint64_t packet_number, uint8_t nonce[12]) {
+  std::memcpy(nonce, iv, 12);
+  for (int i = 0; i < 8; ++i) nonce[4 + i] ^= (uint8_t)(packet_number >> (56 - 8 * i));
+}
+
+void mq_hkdf_extract(const uint8_t* salt, size_t salt_len, const uint8_t* ikm, size_t ikm_len,
+                     uint8_t prk[32]) {
+  hmac_sha256(salt, salt_len, ikm, ikm_len, nullptr, 0, nullptr, 0, prk);
+}
+
+int mq_hkdf_expand(const uint8_t* prk, size_t prk_len, const uint8_t* info, size_t info_len,
+                   uint8_t* okm, size_t okm_len) {
+  if (prk_len < 32 || okm_len > 255 * 32 || (!okm && okm_len)) return MQ_ERR_CRYPTO;
+  uint8_t t[32];
+  size_t tlen = 0, done = 0;
+  for (uint8_t i = 1; done < okm_len; ++i) {
+    hmac_sha256(prk, prk_len, t, tlen, info, info_len, &i, 1, t);
+    tlen = 32;
+    const size_t n = std::min(okm_len - done, (size_t)32);
+    std::memcpy(okm + done, t, n);
+    done += n;
+  }
+  return MQ_OK;
+}
+
+int mq_hkdf_expand_label(const uint8_t* secret, size_t secret_len, const uint8_t* label,
+                         size_t label_len, const uint8_t* context, size_t context_len,
+                         uint8_t* out, size_t out_len) {
+  // key_schedule.rs:23-55: HkdfLabel = u16 length || u8 len || "tls13 " label || u8 len || ctx
+  const size_t full = 6 + label_len, info_len = 2 + 1 + full + 1 + context_len;
+  if (info_len > 80) return MQ_ERR_CRYPTO;
+  uint8_t info[80];
+  info[0] = (uint8_t)(out_len >> 8);
+  info[1] = (uint8_t)out_len;
+  info[2] = (uint8_t)full;
+  std::memcpy(info + 3, "tls13 ", 6);
+  if (label_len) std::memcpy(info + 9, label, label_len);
+  info[3 + full] = (uint8_t)context_len;
+  if (context_len) std::memcpy(info + 4 + full, context, context_len);
+  return mq_hkdf_expand(secret, secret_len, info, info_len, out, out_len);
+}
+
+int mq_derive_initial_secrets(const uint8_t* dcid, size_t dcid_len, uint8_t client_secret[32],
+                              uint8_t server_secret[32]) {
+  static const uint8_t salt[20] = {0x38, 0x76, 0x2c, 0xf7, 0xf5, 0x59, 0x34, 0xb3, 0x4d, 0x17,
+                                   0x9a, 0xe6, 0xa4, 0xc8, 0x0c, 0xad, 0xcc, 0xbb, 0x7f, 0x0a};
+  uint8_t initial[32];
+  mq_hkdf_extract(salt, 20, dcid, dcid_len, initial);
+  int rc = mq_hkdf_expand_label(initial, 32, (const uint8_t*)"client in", 9, nullptr, 0, client_secret, 32);
+  if (rc) return rc;
+  return mq_hkdf_expand_label(initial, 32, (const uint8_t*)"server in", 9, nullptr, 0, server_secret, 32);
+}
+
+int mq_derive_key_material(uint32_t suite, const uint8_t* secret, size_t secret_len,
+                           mq_key_material* out) {
+  const size_t klen = suite_key_len(suite);
+  if (!klen || !out) return MQ_ERR_CRYPTO;
+  std::memset(out, 0, sizeof *out);
+  out->suite = suite;
+  int rc = mq_hkdf_expand_label(secret, secret_len, (const uint8_t*)"quic key", 8, nullptr, 0, out->key, klen);
+  if (!rc) rc = mq_hkdf_expand_label(secret, secret_len, (const uint8_t*)"quic iv", 7, nullptr, 0, out->iv, 12);
+  if (!rc)  // hp_key_len = max(KEY_LEN, 16), key_schedule.rs:133
+    rc = mq_hkdf_expand_label(secret, secret_len, (const uint8_t*)"quic hp", 7, nullptr, 0, out->hp,
+                              klen > 16 ? klen : 16);
+  return rc;
+}
+
+int mq_derive_next_secret(const uint8_t* secret, size_t secret_len, uint8_t next[32]) {
+  return mq_hkdf_expand_label(secret, secret_len, (const uint8_t*)"quic ku", 7, nullptr, 0, next, 32);
+}
+
+int mq_keytable_create(const mq_key_material* rows, uint32_t n_rows, mq_keytable** out) {
+  if (!out || (!rows && n_rows)) return MQ_ERR_INVALID_ARG;
+  *out = nullptr;
+  int rc = ensure_device();
+  if (rc) return rc;
+  mq_keytable* kt = new mq_keytable();
+  kt->rows = n_rows;
+  if (hipMalloc(&kt->dev, sizeof(KeyRow) * (n_rows ? n_rows : 1)) != hipSuccess) {
+    delete kt;
+    return MQ_ERR_HIP;
+  }
+  rc = mq_keytable_update(kt, 0, rows, n_rows);
+  if (rc) {
+    mq_keytable_free(kt);
+    return rc;
+  }
+  *out = kt;
+  return MQ_OK;
+}
+
+int mq_keytable_update(mq_keytable* kt, uint32_t first_row, const mq_key_material* rows, uint32_t n_rows) {
+  if (!kt || (uint64_t)first_row + n_rows > kt->rows) return MQ_ERR_INVALID_ARG;
+  if (!n_rows) return MQ_OK;
+  std::vector<KeyRow> host(n_rows);
+  for (uint32_t i = 0; i < n_rows; ++i)
+    if (!build_row(rows[i], host[i])) std::memset(&host[i], 0, sizeof(KeyRow));  // suite 0: rejected per packet
+  if (hipMemcpy(kt->dev + first_row, host.data(), sizeof(KeyRow) * n_rows, hipMemcpyHostToDevice) != hipSuccess)
+    return MQ_ERR_HIP;
+  return MQ_OK;
+}
+
+uint32_t mq_keytable_rows(const mq_keytable* kt) { return kt ? kt->rows : 0; }
+
+void mq_keytable_free(mq_keytable* kt) {
+  if (!kt) return;
+  if (kt->dev) hipFree(kt->dev);
+  delete kt;
+}
+
+size_t mq_batch_workspace_size(uint32_t n) { return mq_partition_workspace(n); }
+
+static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t arena_len,
+                 const mq_pkt_desc* desc, uint32_t n, uint8_t* status, uint64_t* pn_out,
+                 uint32_t suite_hint, void* workspace, void* stream) {
+  if (!kt || (n && (!arena || !desc || !status))) return MQ_ERR_INVALID_ARG;
+  if (((uintptr_t)arena & 15) != 0) return MQ_ERR_INVALID_ARG;  // 16-B staging chunks
+  int rc = ensure_device();
+  if (rc) return rc;
+  if (n == 0) return MQ_OK;
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e;
+  if (suite_hint == MQ_SUITE_CHACHA20) {
+    e = mq_launch_chacha(open, kt->dev, kt->rows, arena, arena_len, desc, n, nullptr, nullptr, status, pn_out, s);
+  } else if (suite_hint == MQ_SUITE_AES128GCM) {
+    e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, n, nullptr, nullptr, status, pn_out, s);
+  } else if (suite_hint == MQ_SUITE_MIXED) {
+    if (!workspace) return MQ_ERR_INVALID_ARG;
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    uint8_t* ws = (uint8_t*)workspace;
+    uint32_t* list = (uint32_t*)ws;
+    const size_t nblocks = ((size_t)n + 1023) / 1024;
+    uint32_t* bc = (uint32_t*)(ws + al(sizeof(uint32_t) * 2 * (size_t)n));
+    uint32_t* counts = (uint32_t*)(ws + al(sizeof(uint32_t) * 2 * (size_t)n) + al(sizeof(uint32_t) * 2 * nblocks));
+    e = mq_launch_partition(kt->dev, kt->rows, desc, n, list, bc, counts, s);
+    if (e == hipSuccess)
+      e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, n, list, counts, status, pn_out, s);
+    if (e == hipSuccess)
+      e = mq_launch_chacha(open, kt->dev, kt->rows, arena, arena_len, desc, n, list + n, counts + 1, status,
+                           pn_out, s);
+  } else {
+    return MQ_ERR_INVALID_ARG;
+  }
+  return e == hipSuccess ? MQ_OK : MQ_ERR_HIP;
+}
+
+int mq_batch_seal(const mq_keytable* kt, uint8_t* arena, uint64_t arena_len, const mq_pkt_desc* desc,
+                  uint32_t n, uint8_t* status, uint32_t suite_hint, void* workspace, void* stream) {
+  return batch(false, kt, arena, arena_len, desc, n, status, nullptr, suite_hint, workspace, stream);
+}
+
+int mq_batch_open(const mq_keytable* kt, uint8_t* arena, uint64_t arena_len, const mq_pkt_desc* desc,
+                  uint32_t n, uint8_t* status, uint64_t* pn_out, uint32_t suite_hint, void* workspace,
+                  void* stream) {
+  return batch(true, kt, arena, arena_len, desc, n, status, pn_out, suite_hint, workspace, stream);
+}
+
+int mq_batch_hp_mask(const mq_keytable* kt, const uint32_t* key_ids, const uint8_t* samples,
+                     uint8_t* masks, uint32_t n, void* stream) {
+  if (!kt || (n && (!key_ids || !samples || !masks))) return MQ_ERR_INVALID_ARG;
+  int rc = ensure_device();
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = mq_launch_chacha_hp(kt->dev, kt->rows, key_ids, samples, masks, n, s);
+  if (e == hipSuccess) e = mq_launch_aes_hp(kt->dev, kt->rows, key_ids, samples, masks, n, s);
+  return e == hipSuccess ? MQ_OK : MQ_ERR_HIP;
+}
+
+int mq_batch_time_seal_open(const mq_keytable* kt, uint8_t* arena, uint64_t arena_len,
+                            const mq_pkt_desc* desc, uint32_t n, uint8_t* status, uint64_t* pn_out,
+                            uint32_t suite_hint, void* workspace, void* stream, int iters,
+                            float* seal_ms, float* open_ms) {
+  if (iters <= 0 || !seal_ms || !open_ms) return MQ_ERR_INVALID_ARG;
+  int rc = ensure_device();
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  std::vector<hipEvent_t> ev(2 * iters + 1);
+  for (auto& x : ev)
+    if (hipEventCreate(&x) != hipSuccess) return MQ_ERR_HIP;
+  hipEventRecord(ev[0], s);
+  for (int i = 0; i < iters && rc == MQ_OK; ++i) {
+    rc = mq_batch_seal(kt, arena, arena_len, desc, n, status, suite_hint, workspace, stream);
+    hipEventRecord(ev[2 * i + 1], s);
+    if (rc == MQ_OK) rc = mq_batch_open(kt, arena, arena_len, desc, n, status, pn_out, suite_hint, workspace, stream);
+    hipEventRecord(ev[2 * i + 2], s);
+  }
+  hipEventSynchronize(ev[2 * iters]);
+  double ts = 0, to = 0;
+  for (int i = 0; i < iters; ++i) {
+    float a = 0, b = 0;
+    hipEventElapsedTime(&a, ev[2 * i], ev[2 * i + 1]);
+    hipEventElapsedTime(&b, ev[2 * i + 1], ev[2 * i + 2]);
+    ts += a;
+    to += b;
+  }
+  for (auto& x : ev) hipEventDestroy(x);
+  *seal_ms = (float)(ts / iters);
+  *open_ms = (float)(to / iters);
+  return rc;
+}
+
+}  // extern "C"
