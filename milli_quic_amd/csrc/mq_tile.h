@@ -170,7 +170,10 @@ __device__ __forceinline__ void run_tile(uint8_t* smem, uint32_t tile_id, const 
   c.pn = c.d.pn;
   const KeyRow* row = kt + (c.act ? c.d.key_id : 0u);
   const uint64_t off = c.act ? c.d.offset : 0;
-  const uint32_t nch = c.act ? (uint32_t)(((off + c.d.len + 15) >> 4) - (off >> 4)) : 0u;
+  // chunks of the packet's LDS image, clamped so the 16-packet scan cannot overflow; a clamped
+  // (huge) packet always exceeds the budget and sends the tile down the direct path
+  const uint64_t nch64 = c.act ? ((off + c.d.len + 15) >> 4) - (off >> 4) : 0u;
+  const uint32_t nch = (uint32_t)(nch64 < 0xFFFFu ? nch64 : 0xFFFFu);
   const uint32_t mine = (q == 0) ? nch : 0u;
   const uint32_t incl = wave_incl_scan(mine, lane);
   const uint32_t total = (uint32_t)__shfl((int)incl, 63, 64);

@@ -1,0 +1,316 @@
+"""Parity of the HIP kernels (through the C ABI) with the oracle and the golden vectors.
+
+Bar: bit-exact ciphertext, tag, header-protection mask and protected packet bytes; identical
+per-packet status; packets that fail are left byte-for-byte unchanged. Mirrors the reference's
+crypto unit tests (src/crypto/rustcrypto.rs:289-434, src/crypto/key_schedule.rs:160-360) and
+adds the differential batch tests the reference lacks.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from milli_quic_amd import _lib, batch, crypto, key_schedule, workload  # noqa: E402
+from milli_quic_amd.batch import DESC_DTYPE, KeyTable, make_descs  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device(mqlib):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    assert mqlib.mq_device_init(0) == 0, "libmq_aead.so must find a gfx950 device"
+
+
+def to_dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).to(DEV)
+
+
+def gpu_run(keys, arena, desc, hint, open_=False):
+    kt = KeyTable(keys)
+    n = len(desc)
+    a, d = to_dev(arena), to_dev(desc)
+    st = torch.full((max(n, 1),), 0xEE, dtype=torch.uint8, device=DEV)
+    pn = torch.zeros(max(n, 1), dtype=torch.int64, device=DEV)
+    ws = torch.empty(max(batch.workspace_bytes(n), 256), dtype=torch.uint8, device=DEV)
+    if open_:
+        batch.open_(kt, a, d, st, pn, hint, ws)
+    else:
+        batch.seal(kt, a, d, st, hint, ws)
+    torch.cuda.synchronize()
+    return a.cpu().numpy(), st.cpu().numpy()[:n], pn.cpu().numpy().view(np.uint64)[:n]
+
+
+def km_from(p):
+    return key_schedule.make_key_material(p["suite"], bytes.fromhex(p["key"]), bytes.fromhex(p["iv"]),
+                                          bytes.fromhex(p["hp"]))
+
+
+# ---------------------------------------------------------------------------------------------
+# per-packet trait API (Aead / HeaderProtection), mirrors of rustcrypto.rs tests
+def test_aead_vectors_per_packet(aead_vectors):
+    for c in aead_vectors:
+        key, nonce, aad, pt = (bytes.fromhex(c[k]) for k in ("key", "nonce", "aad", "pt"))
+        prov = crypto.Aes128GcmProvider() if c["suite"] == 1 else crypto.ChaCha20Provider()
+        aead = prov.aead(key)
+        buf = bytearray(pt) + bytearray(16)
+        n = aead.seal_in_place(nonce, aad, buf, len(pt))
+        assert n == len(pt) + 16 and bytes(buf).hex() == c["ct_tag"], (c["suite"], len(pt), len(aad))
+        m = aead.open_in_place(nonce, aad, buf, n)
+        assert m == len(pt) and bytes(buf[:m]) == pt
+
+
+@pytest.mark.parametrize("prov_cls,klen", [(crypto.Aes128GcmProvider, 16), (crypto.ChaCha20Provider, 32)])
+def test_reference_unit_mirrors(prov_cls, klen):
+    prov = prov_cls()
+    aead = prov.aead(bytes([0x42] * klen))                      # rustcrypto.rs:295-315 / 340-361
+    nonce, aad, pt = bytes(12), b"associated data", b"hello world"
+    buf = bytearray(128)
+    buf[: len(pt)] = pt
+    ct_len = aead.seal_in_place(nonce, aad, buf, len(pt))
+    assert ct_len == len(pt) + 16
+    assert aead.open_in_place(nonce, aad, buf, ct_len) == len(pt) and bytes(buf[: len(pt)]) == pt
+    buf = bytearray(128)                                          # :317-338 / 363-384 tamper
+    buf[:6] = b"secret"
+    ct_len = aead.seal_in_place(nonce, b"aad", buf, 6)
+    buf[0] ^= 0xFF
+    before = bytes(buf)
+    with pytest.raises(crypto.CryptoError):
+        aead.open_in_place(nonce, b"aad", buf, ct_len)
+    assert bytes(buf) == before                                   # nothing released
+    with pytest.raises(crypto.CryptoError):                      # nonce.len() != 12
+        aead.seal_in_place(bytes(11), b"", bytearray(32), 4)
+    with pytest.raises(crypto.BufferTooSmall) as e:              # buf.len() < payload + 16
+        aead.seal_in_place(nonce, b"", bytearray(20), 10)
+    assert e.value.needed == 26
+    with pytest.raises(crypto.CryptoError):                      # ct < 16
+        aead.open_in_place(nonce, b"", bytearray(32), 15)
+    with pytest.raises(crypto.InvalidArgument):                  # ct_len > buf.len(): reference panics
+        aead.open_in_place(nonce, b"", bytearray(20), 40)
+    with pytest.raises(crypto.CryptoError):                      # key length check
+        prov.aead(bytes(klen + 1))
+    assert prov.Aead.KEY_LEN == klen and prov.Aead.NONCE_LEN == 12 and prov.Aead.TAG_LEN == 16
+    hp = prov.header_protection(bytes([0x55] * klen))           # :388-416 (+ actual mask bytes)
+    m = hp.mask(bytes([0xAA] * 16))
+    assert len(m) == 5
+    hb = 0xC0 ^ (m[0] & 0x0F) ^ (m[0] & 0x0F)
+    assert hb == 0xC0
+    with pytest.raises(crypto.InvalidArgument):
+        hp.mask(bytes(15))
+
+
+def test_hp_vectors(hp_vectors):
+    for c in hp_vectors:
+        cls = crypto.AesHeaderProtection if c["suite"] == 1 else crypto.ChaChaHeaderProtection
+        assert cls(bytes.fromhex(c["hp"])).mask(bytes.fromhex(c["sample"])).hex() == c["mask"]
+    # batched form through a key table
+    rows = [key_schedule.make_key_material(c["suite"], bytes(32), bytes(12), bytes.fromhex(c["hp"]))
+            for c in hp_vectors]
+    kt = KeyTable(rows)
+    ids = torch.arange(len(rows), dtype=torch.int32, device=DEV)
+    samples = to_dev(np.frombuffer(b"".join(bytes.fromhex(c["sample"]) for c in hp_vectors), dtype=np.uint8))
+    masks = torch.zeros(5 * len(rows), dtype=torch.uint8, device=DEV)
+    batch.hp_mask(kt, ids, samples, masks)
+    got = masks.cpu().numpy().tobytes()
+    for i, c in enumerate(hp_vectors):
+        assert got[5 * i:5 * i + 5].hex() == c["mask"]
+
+
+def test_key_schedule_roundtrip(ref_fixtures):
+    # key_schedule.rs:268-305: derive from the A.1 client secret, seal/open roundtrip
+    a1 = ref_fixtures["rfc9001"]["a1"]
+    c, s = key_schedule.derive_initial_secrets(bytes.fromhex(ref_fixtures["rfc9001"]["dcid"]))
+    assert c.hex() == a1["client_initial_secret"] and s.hex() == a1["server_initial_secret"]
+    keys = key_schedule.derive_directional_keys(crypto.Aes128GcmProvider(), c)
+    assert keys.iv.hex() == a1["client_iv"]
+    assert keys.nonce(2).hex() == "fa044b2f42a3fd3b46fb255e"
+    buf = bytearray(b"quic payload" + bytes(16))
+    n = keys.aead.seal_in_place(keys.nonce(7), b"hdr", buf, 12)
+    assert keys.aead.open_in_place(keys.nonce(7), b"hdr", buf, n) == 12 and bytes(buf[:12]) == b"quic payload"
+
+
+# ---------------------------------------------------------------------------------------------
+# batch API: golden packets, RFC packets, curl Initial
+def _pack(packets, field, align=1, gap=0):
+    offs, blobs, pos = [], [], 0
+    for p in packets:
+        pos = (pos + align - 1) // align * align
+        offs.append(pos)
+        blobs.append((pos, bytes.fromhex(p[field])))
+        pos += p["len"] + gap
+    arena = np.zeros(pos + 64, dtype=np.uint8)
+    arena[:] = 0x5A  # gap filler must survive untouched
+    for o, b in blobs:
+        arena[o:o + len(b)] = np.frombuffer(b, dtype=np.uint8)
+    return arena, np.array(offs, dtype=np.uint64)
+
+
+@pytest.mark.parametrize("align,gap", [(1, 0), (16, 0), (1, 7)])
+def test_packet_vectors_batch(packet_vectors, align, gap):
+    pk = packet_vectors
+    keys = [km_from(p) for p in pk]
+    flags = [_lib.MQ_PKT_LONG_HEADER if p["long_header"] else 0 for p in pk]
+    arena, offs = _pack(pk, "unprotected", align, gap)
+    lens = [p["len"] for p in pk]
+    seal = make_descs(offs, lens, range(len(pk)), [p["pn"] for p in pk], [p["pn_offset"] for p in pk],
+                      [p["pn_len"] for p in pk], flags)
+    out, st, _ = gpu_run(keys, arena, seal, _lib.MQ_SUITE_MIXED)
+    assert (st == 0).all(), st
+    want, _ = _pack(pk, "protected", align, gap)
+    for i, p in enumerate(pk):
+        o = int(offs[i])
+        assert out[o:o + p["len"]].tobytes().hex() == p["protected"], p["name"]
+    assert out.tobytes() == want.tobytes()  # gap bytes untouched
+    opn = make_descs(offs, lens, range(len(pk)), [p["largest_pn"] for p in pk], [p["pn_offset"] for p in pk],
+                     0, flags)
+    back, st, pn = gpu_run(keys, out, opn, _lib.MQ_SUITE_MIXED, open_=True)
+    assert (st == 0).all()
+    assert [int(x) for x in pn] == [p["pn"] for p in pk]
+    for i, p in enumerate(pk):
+        o = int(offs[i])
+        assert back[o:o + p["len"] - 16].tobytes().hex() == p["unprotected"][:-32], p["name"]
+
+
+def test_single_suite_hints(packet_vectors):
+    for suite in (1, 2):
+        pk = [p for p in packet_vectors if p["suite"] == suite]
+        keys = [km_from(p) for p in pk]
+        arena, offs = _pack(pk, "unprotected")
+        flags = [_lib.MQ_PKT_LONG_HEADER if p["long_header"] else 0 for p in pk]
+        seal = make_descs(offs, [p["len"] for p in pk], range(len(pk)), [p["pn"] for p in pk],
+                          [p["pn_offset"] for p in pk], [p["pn_len"] for p in pk], flags)
+        out, st, _ = gpu_run(keys, arena, seal, suite)
+        assert (st == 0).all()
+        for i, p in enumerate(pk):
+            o = int(offs[i])
+            assert out[o:o + p["len"]].tobytes().hex() == p["protected"]
+        # the other suite's kernel rejects these rows with MQ_ERR_SUITE and leaves them alone
+        out2, st2, _ = gpu_run(keys, arena, seal, 3 - suite)
+        assert (st2 == _lib.MQ_ERR_SUITE).all() and out2.tobytes() == arena.tobytes()
+
+
+def test_curl_initial_batch(ref_fixtures):
+    from helpers import curl_desc_and_keys
+    data, dcid, pn_offset, length, client = curl_desc_and_keys(None, ref_fixtures,
+                                                               key_schedule.derive_initial_secrets)
+    km = key_schedule.key_material(_lib.MQ_SUITE_AES128GCM, client)
+    arena = np.frombuffer(data, dtype=np.uint8).copy()
+    opn = make_descs([0], [pn_offset + length], [0], [0], [pn_offset], [0], [_lib.MQ_PKT_LONG_HEADER])
+    out, st, pn = gpu_run([km], arena, opn, _lib.MQ_SUITE_AES128GCM, open_=True)
+    assert st[0] == 0 and int(pn[0]) == 0 and out[pn_offset + 1] == 0x06
+
+
+# ---------------------------------------------------------------------------------------------
+# differential vs oracle on random batches
+def oracle_run(orc, keys, arena, desc, hint, open_=False):
+    a = arena.copy()
+    if open_:
+        st, pn = orc.batch_open(keys, a, desc, hint, threads=8)
+        return a, st, pn
+    return a, orc.batch_seal(keys, a, desc, hint, threads=8), None
+
+
+def test_mixed_batch_vs_oracle(orc):
+    w = workload.config_e(20000, seed=0x1234)
+    g_out, g_st, _ = gpu_run(w.keys, w.arena, w.seal_desc, w.suite_hint)
+    o_out, o_st, _ = oracle_run(orc, w.keys, w.arena, w.seal_desc, w.suite_hint)
+    assert (o_st == 0).all()
+    assert (g_st == o_st).all()
+    assert g_out.tobytes() == o_out.tobytes()
+    g_back, g_st, g_pn = gpu_run(w.keys, g_out, w.open_desc, w.suite_hint, open_=True)
+    o_back, o_st, o_pn = oracle_run(orc, w.keys, o_out, w.open_desc, w.suite_hint, open_=True)
+    assert (g_st == 0).all() and (g_st == o_st).all()
+    assert (g_pn == o_pn).all() and (g_pn == w.pns).all()
+    assert g_back.tobytes() == o_back.tobytes()
+
+
+@pytest.mark.parametrize("suite", [1, 2])
+def test_failures_match_oracle(orc, suite):
+    w = workload.uniform(2048, suite, L=300)
+    sealed, st, _ = oracle_run(orc, w.keys, w.arena, w.seal_desc, suite)
+    rng = np.random.default_rng(suite)
+    bad = sealed.copy()
+    victims = rng.choice(w.n, size=200, replace=False)
+    for v in victims:  # flip one byte anywhere in the packet: header, payload or tag
+        o = int(w.seal_desc["offset"][v])
+        bad[o + int(rng.integers(0, 300))] ^= 1 << int(rng.integers(0, 8))
+    od = w.open_desc.copy()
+    od["key_id"][5] = 99                     # key id out of range
+    od["len"][6] = 24                        # sample out of range -> Crypto
+    od["offset"][7] = len(bad) - 10          # past the arena end
+    od["pn"][8] = (1 << 62) - 2              # decode_pn lands above 2^62-1 -> ProtocolViolation
+    g_out, g_st, g_pn = gpu_run(w.keys, bad, od, suite, open_=True)
+    o_out, o_st, o_pn = oracle_run(orc, w.keys, bad, od, suite, open_=True)
+    assert (g_st == o_st).all(), np.nonzero(g_st != o_st)
+    assert (o_st != 0).sum() >= 150
+    assert g_out.tobytes() == o_out.tobytes()
+    ok = o_st == 0
+    assert (g_pn[ok] == o_pn[ok]).all()
+    sd = w.seal_desc.copy()
+    sd["pn_len"][3] = 0                      # invalid pn_len
+    sd["pn_len"][4] = 5
+    sd["len"][9] = 20                        # len < pn_offset + pn_len + 16
+    sd["key_id"][10] = 1 << 20
+    g_out, g_st, _ = gpu_run(w.keys, w.arena, sd, suite)
+    o_out, o_st, _ = oracle_run(orc, w.keys, w.arena, sd, suite)
+    assert (g_st == o_st).all() and g_out.tobytes() == o_out.tobytes()
+
+
+@pytest.mark.parametrize("suite", [1, 2])
+def test_direct_path_and_disorder(orc, suite):
+    # tiles whose packets exceed the LDS budget (16 x 1500 B) and out-of-order descriptors
+    w = workload.uniform(512, suite, L=1500)
+    rng = np.random.default_rng(3)
+    for order in (np.arange(w.n), np.arange(w.n)[::-1], rng.permutation(w.n)):
+        sd, od = w.seal_desc[order].copy(), w.open_desc[order].copy()
+        g_out, g_st, _ = gpu_run(w.keys, w.arena, sd, suite)
+        o_out, o_st, _ = oracle_run(orc, w.keys, w.arena, sd, suite)
+        assert (g_st == 0).all() and (g_st == o_st).all()
+        assert g_out.tobytes() == o_out.tobytes()
+        g_back, g_st, g_pn = gpu_run(w.keys, g_out, od, suite, open_=True)
+        assert (g_st == 0).all() and (g_pn == w.pns[order]).all()
+        keep = w.arena.reshape(w.n, 1500)[:, :1484].tobytes()
+        assert g_back.reshape(w.n, 1500)[:, :1484].tobytes() == keep
+
+
+@pytest.mark.parametrize("L", [21, 36, 63, 64, 65, 100, 1350])
+def test_small_and_odd_sizes(orc, L):
+    for suite in (1, 2):
+        w = workload.uniform(96, suite, L=L, pn_len=1 + (L % 4))
+        g_out, g_st, _ = gpu_run(w.keys, w.arena, w.seal_desc, suite)
+        o_out, o_st, _ = oracle_run(orc, w.keys, w.arena, w.seal_desc, suite)
+        assert (g_st == o_st).all() and g_out.tobytes() == o_out.tobytes(), (suite, L)
+
+
+def test_full_size_roundtrip_config_b(orc):
+    # BASELINE configs[1] at full size: 2^20 x 1200 B ChaCha20-Poly1305
+    w = workload.config_b(1 << 20)
+    kt = KeyTable(w.keys)
+    a = to_dev(w.arena)
+    sd, od = to_dev(w.seal_desc), to_dev(w.open_desc)
+    st = torch.full((w.n,), 0xEE, dtype=torch.uint8, device=DEV)
+    pn = torch.zeros(w.n, dtype=torch.int64, device=DEV)
+    batch.seal(kt, a, sd, st, w.suite_hint)
+    torch.cuda.synchronize()
+    assert int((st != 0).sum()) == 0
+    sealed = a.cpu().numpy()
+    # sampled oracle parity on the full-size arena
+    rng = np.random.default_rng(11)
+    idx = np.sort(rng.choice(w.n, size=512, replace=False))
+    sub_desc = w.seal_desc[idx].copy()
+    o_arena = w.arena.copy()
+    o_st = orc.batch_seal(w.keys, o_arena, sub_desc, w.suite_hint, threads=8)
+    assert (o_st == 0).all()
+    for i in idx:
+        lo = int(w.seal_desc["offset"][i])
+        assert sealed[lo:lo + 1200].tobytes() == o_arena[lo:lo + 1200].tobytes()
+    batch.open_(kt, a, od, st, pn, w.suite_hint)
+    torch.cuda.synchronize()
+    assert int((st != 0).sum()) == 0
+    assert (pn.cpu().numpy().view(np.uint64) == w.pns).all()
+    back = a.cpu().numpy()
+    v = back.reshape(w.n, 1200)[:, :1184]
+    assert v.tobytes() == w.arena.reshape(w.n, 1200)[:, :1184].tobytes()

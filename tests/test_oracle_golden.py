@@ -14,6 +14,8 @@ import pytest
 from milli_quic_amd import _lib
 from milli_quic_amd.batch import make_descs
 
+from helpers import curl_desc_and_keys
+
 A1 = {
     "initial_secret": "7db5df06e7a69e432496adedb00851923595221596ae2ae9fb8115c1e9ed0a44",
 }
@@ -106,24 +108,6 @@ def test_rfc9001_packets_match_rfc_text(packet_vectors, ref_fixtures):
     assert by["rfc9001-A.2"]["protected"] == ref_fixtures["rfc9001"]["a2_protected"]
     assert by["rfc9001-A.3"]["protected"] == ref_fixtures["rfc9001"]["a3_protected"]
     assert by["rfc9001-A.5"]["protected"] == ref_fixtures["rfc9001"]["a5_packet"]
-
-
-def curl_desc_and_keys(orc_or_none, ref_fixtures, derive):
-    """The curl Initial: long header, DCID 20 B at byte 6; keys from the client initial secret."""
-    data = bytes.fromhex(ref_fixtures["curl_initial"]["hex"])
-    dcid_len = data[5]
-    dcid = data[6:6 + dcid_len]
-    pos = 6 + dcid_len
-    scid_len = data[pos]
-    pos += 1 + scid_len
-    tok_len = data[pos]  # 1-byte varint in this capture
-    assert tok_len < 64
-    pos += 1 + tok_len
-    vlen = 1 << (data[pos] >> 6)  # RFC 9000 §16 varint (this capture: 4-byte Length)
-    length = int.from_bytes(data[pos:pos + vlen], "big") & ((1 << (8 * vlen - 2)) - 1)
-    pn_offset = pos + vlen
-    client, _ = derive(dcid)
-    return data, dcid, pn_offset, length, client
 
 
 def test_curl_initial_opens(orc, ref_fixtures):
