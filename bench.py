@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident AEAD seal+open throughput on MI355X (BASELINE.json metric).
+
+One "step" = seal (AEAD + header protection) then open (HP removal + decode_pn + AEAD open) of
+the whole per-GPU batch, in place in HBM. Default workload = BASELINE configs[1]: 2^20 x 1200-B
+1-RTT packets, ChaCha20-Poly1305. With --gpus N (torch.distributed.run,
+one rank per GPU) every rank protects its own 2^20-packet shard (config D; packets are
+independent, so there is no data-path collective: scaling "weak").
+
+  value  = sum over ranks of wire bytes x 2 / (t_seal + t_open) / 2^30   [GiB/s]
+  roofline.achieved = algorithmic bytes of one launch (2 x L per packet: read + write) / the
+                      average duration of the dominant kernel, from events on the launch stream
+  cpu_baseline = the C oracle (oracle/, "port") on a bounded sample, host threads stated
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config b|c|e] [--packets P]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="b", choices=["b", "c", "e"])
+    ap.add_argument("--packets", type=int, default=1 << 20, help="packets per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=1 << 17, help="packets in the CPU baseline sample")
+    return ap.parse_args()
+
+
+def build_workload(cfg, n, rank):
+    from milli_quic_amd import workload
+    seed = workload.SEED ^ (rank * 0x9E3779B97F4A7C15 & 0xFFFFFFFFFFFFFFFF)
+    if cfg == "b":
+        return workload.config_b(n, seed=seed)
+    if cfg == "c":
+        return workload.config_c(n, seed=seed)
+    return workload.config_e(n, seed=seed)
+
+
+def cpu_baseline(w, sample, threads):
+    """Time the CPU oracle (seal + open) on the first `sample` packets of the same workload."""
+    from oracle import oracle
+    oracle.load()
+    n = min(sample, w.n)
+    end = int(w.seal_desc["offset"][n - 1]) + int(w.seal_desc["len"][n - 1])
+    arena = w.arena[:end].copy()
+    sd, od = w.seal_desc[:n].copy(), w.open_desc[:n].copy()
+    oracle.batch_seal(w.keys, arena.copy(), sd[: min(n, 256)].copy(), w.suite_hint, threads)  # warm
+    t0 = time.perf_counter()
+    st = oracle.batch_seal(w.keys, arena, sd, w.suite_hint, threads)
+    t1 = time.perf_counter()
+    st2, _ = oracle.batch_open(w.keys, arena, od, w.suite_hint, threads)
+    t2 = time.perf_counter()
+    assert (st == 0).all() and (st2 == 0).all(), "CPU oracle failed on its sample"
+    wire = int(sd["len"].astype(np.int64).sum())
+    gibs = wire * 2 / (t2 - t0) / 2 ** 30
+    return {"value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{n} packets ({wire / 1e6:.1f} MB) of the same workload, seal {t1 - t0:.2f}s + "
+                      f"open {t2 - t1:.2f}s, oracle/mq_oracle.c with {threads} host threads"}
+
+
+def load_traffic(cfg):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(cfg)
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+
+    from milli_quic_amd import _lib, batch
+    from milli_quic_amd.batch import KeyTable
+    lib = _lib.load()
+    rc = lib.mq_device_init(local)
+    if rc != 0:
+        raise SystemExit(f"libmq_aead: no usable gfx950 device ({_lib.status_str(rc)})")
+
+    w = build_workload(args.config, args.packets, rank)
+    dev = torch.device("cuda", local)
+    kt = KeyTable(w.keys)
+    arena = torch.from_numpy(w.arena).to(dev)
+    sd = torch.from_numpy(w.seal_desc.view(np.uint8)).to(dev)
+    od = torch.from_numpy(w.open_desc.view(np.uint8)).to(dev)
+    st = torch.zeros(w.n, dtype=torch.uint8, device=dev)
+    pn = torch.zeros(w.n, dtype=torch.int64, device=dev)
+    ws = torch.empty(max(batch.workspace_bytes(w.n), 256), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+
+    def step(ev=None, i=0):
+        if ev is not None:
+            ev[3 * i].record(stream)
+        batch.seal(kt, arena, sd, st, w.suite_hint, ws, sh)
+        if ev is not None:
+            ev[3 * i + 1].record(stream)
+        batch.open_(kt, arena, od, st, pn, w.suite_hint, ws, sh)
+        if ev is not None:
+            ev[3 * i + 2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # correctness gate before timing: the roundtrip must succeed for every packet
+    fails = int((st != 0).sum())
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3 * args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(ev, i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    fails += int((st != 0).sum())
+    seal_ms = float(np.mean([ev[3 * i].elapsed_time(ev[3 * i + 1]) for i in range(args.steps)]))
+    open_ms = float(np.mean([ev[3 * i + 1].elapsed_time(ev[3 * i + 2]) for i in range(args.steps)]))
+
+    wire = w.wire_bytes
+    t = torch.tensor([elapsed, float(fails), float(wire)], dtype=torch.float64, device=dev)
+    if world > 1:
+        tmax = t[:1].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = t[1:].clone()
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        elapsed, fails, total_wire = float(tmax[0]), int(tsum[0]), float(tsum[1])
+    else:
+        total_wire = float(wire)
+    ms_per_step = elapsed / args.steps * 1e3
+    value = total_wire * 2 / (elapsed / args.steps) / 2 ** 30
+
+    if rank == 0:
+        dom_ms = max(seal_ms, open_ms)
+        algo_bytes = 2.0 * wire  # per launch: read + write of every wire byte
+        achieved = algo_bytes / (dom_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config),
+                "kernel": "open" if open_ms >= seal_ms else "seal",
+                "seal_ms": round(seal_ms, 4), "open_ms": round(open_ms, 4),
+                "algorithmic_bytes_per_launch": int(algo_bytes)}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(w, args.cpu_sample, min(16, os.cpu_count() or 1))
+        names = {"b": "configs[1]: 1M x 1200B ChaCha20-Poly1305 seal+open, 1-RTT short header",
+                 "c": "configs[2]: 1M x 1200B AES-128-GCM seal+open + header protection",
+                 "e": "configs[4]: mixed 64-1350B batch, Initial + 1-RTT, ChaCha20/AES-GCM interleaved"}
+        out = {
+            "metric": "GiB/s device-resident AEAD seal+open, 1M×1200B QUIC packets, 1/2/4/8 GPU",
+            "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+            "config": {"workload": names[args.config], "packets_per_gpu": w.n,
+                       "wire_bytes_per_gpu": wire, "parallelism": f"dp{world} (independent packet shards)",
+                       "seal_failures_or_open_failures": fails},
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -12,8 +12,8 @@
 //     output position, so no carry ever reaches the next kept bit), Karatsuba 128 -> 64 -> 32
 //     (9 products per multiply), then the x^128 + x^7 + x^2 + x + 1 fold.
 // Work split per tile (mq_tile.h): keystream block b of a packet (b = 0: E_K(J0), b >= 1:
-// counter b+1) on lane q = b / C; GHASH interleaved over the quad with H^4 (precomputed on the
-// host per key) and a final multiply by H^(4-q).
+// counter b+1) on lane b % 8; GHASH interleaved over the octet with H^8 (precomputed on the
+// host per key) and a final multiply by H^(8-j).
 #include "mq_tile.h"
 
 namespace mq {
@@ -38,7 +38,7 @@ __constant__ uint8_t kSbox[256] = {
     0x8c, 0xa1, 0x89, 0x0d, 0xbf, 0xe6, 0x42, 0x68, 0x41, 0x99, 0x2d, 0x0f, 0xb0, 0x54, 0xbb, 0x16};
 
 constexpr int kTReplicas = 8;
-constexpr int kAesWaves = 2;  // waves (tiles) per workgroup sharing one T-table
+constexpr int kAesWaves = 4;  // waves (tiles) per workgroup sharing one T-table
 __shared__ uint32_t g_t0[256 * kTReplicas];
 
 __device__ __forceinline__ void build_t0(int tid, int nthreads) {
@@ -148,47 +148,49 @@ __device__ __forceinline__ void gf_mul(uint32_t (&a)[4], const GfOp& b) {
   a[3] = p3 ^ p7 ^ ((p7 << 1) | (p6 >> 31)) ^ ((p7 << 2) | (p6 >> 30)) ^ ((p7 << 7) | (p6 >> 25));
 }
 
-// Interleaved GHASH over AAD||pad||CT||pad||[len(A)]64||[len(C)]64 (bit lengths); every lane of
-// the quad returns the same value in the reflected basis.
+// Interleaved GHASH over AAD||pad||CT||pad||[len(A)]64||[len(C)]64 (bit lengths): lane j takes
+// blocks 8k + j with multiplier H^8, then one final multiply by H^(8-j) (row->H[7-j], computed on
+// the host per key), then the octet XOR. Every lane of the octet returns the same value
+// (reflected basis).
 template <class S>
 __device__ __forceinline__ void ghash(const S& sp, typename S::off_t pkt, typename S::off_t pay,
-                                      uint32_t aad_len, uint32_t ct_len, const KeyRow* row, int q,
+                                      uint32_t aad_len, uint32_t ct_len, const KeyRow* row, int j,
                                       bool act, uint32_t (&y)[4]) {
   uint32_t hp[4];
-  GfOp m4, mlast;
+  GfOp m8, mlast;
   {
 #pragma unroll
-    for (int w = 0; w < 4; ++w) hp[w] = brev(row->H[3][w]);
-    m4 = gf_prepare(hp);
-    const int e = 3 - q;  // H^(4-q) is row->H[3-q]
+    for (int w = 0; w < 4; ++w) hp[w] = brev(row->H[7][w]);
+    m8 = gf_prepare(hp);
+    const int e = 7 - j;  // H^(8-j)
 #pragma unroll
     for (int w = 0; w < 4; ++w) hp[w] = brev(row->H[e][w]);
     mlast = gf_prepare(hp);
   }
   const uint32_t A = (aad_len + 15) >> 4, T = (ct_len + 15) >> 4, nb = A + T + 1;
-  const uint32_t K = (nb + 3) >> 2;
+  const uint32_t K = (nb + kLanesPerPkt - 1) / kLanesPerPkt;
   const uint32_t Kmax = wave_max_u32(act ? K : 0u);
-  const int z = (int)(4 * Kmax) - (int)nb;
+  const int z = (int)(kLanesPerPkt * Kmax) - (int)nb;
   uint32_t acc[4] = {0, 0, 0, 0};
-  auto absorb = [&](uint32_t k) {
-    const int i = (int)(4 * k) + q - z;
-    typename S::off_t src = pkt;
-    int rem = 0;
-    bool lens = false;
+  struct Blk { typename S::off_t src; int rem; bool lens; };
+  auto where = [&](uint32_t k) {
+    const int i = (int)(kLanesPerPkt * k) + j - z;
+    Blk b{pkt, 0, false};
     if (act && i >= 0) {
       if ((uint32_t)i < A) {
-        src = pkt + 16 * (uint32_t)i; rem = (int)aad_len - 16 * i;
+        b.src = pkt + 16 * (uint32_t)i; b.rem = (int)aad_len - 16 * i;
       } else if ((uint32_t)i < A + T) {
-        src = pay + 16 * ((uint32_t)i - A); rem = (int)ct_len - 16 * (i - (int)A);
+        b.src = pay + 16 * ((uint32_t)i - A); b.rem = (int)ct_len - 16 * (i - (int)A);
       } else {
-        lens = true;
+        b.lens = true;
       }
     }
-    uint32_t m[4];
-    load_words<4>(sp, src, m);
+    return b;
+  };
+  auto absorb = [&](const Blk& b, uint32_t (&m)[4]) {
 #pragma unroll
-    for (int w = 0; w < 4; ++w) m[w] = refl(m[w] & byte_mask(rem, w));
-    if (lens) {
+    for (int w = 0; w < 4; ++w) m[w] = refl(m[w] & byte_mask(b.rem, w));
+    if (b.lens) {
       const uint64_t ab = (uint64_t)aad_len * 8, cb = (uint64_t)ct_len * 8;
       m[0] = brev((uint32_t)(ab >> 32)); m[1] = brev((uint32_t)ab);
       m[2] = brev((uint32_t)(cb >> 32)); m[3] = brev((uint32_t)cb);
@@ -196,20 +198,21 @@ __device__ __forceinline__ void ghash(const S& sp, typename S::off_t pkt, typena
 #pragma unroll
     for (int w = 0; w < 4; ++w) acc[w] ^= m[w];
   };
-  for (uint32_t k = 0; k + 1 < Kmax; ++k) {
-    absorb(k);
-    gf_mul(acc, m4);
-  }
   if (Kmax > 0) {
-    absorb(Kmax - 1);
+    Blk b = where(0);
+    uint32_t m[4];
+    load_words<4>(sp, b.src, m);
+    for (uint32_t k = 0; k + 1 < Kmax; ++k) {
+      absorb(b, m);
+      b = where(k + 1);
+      load_words<4>(sp, b.src, m);
+      gf_mul(acc, m8);
+    }
+    absorb(b, m);
     gf_mul(acc, mlast);
   }
 #pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    acc[w] ^= quad_swap1(acc[w]);
-    acc[w] ^= quad_swap2(acc[w]);
-    y[w] = acc[w];
-  }
+  for (int w = 0; w < 4; ++w) y[w] = oct_xor(acc[w]);
 }
 
 struct AesPolicy {
@@ -228,11 +231,9 @@ struct AesPolicy {
                                                    uint32_t P, const uint32_t (&ks)[4]) {
     const uint32_t o = 16 * (b - 1);
     const int ln = (int)min(16u, P - o);
-    uint32_t w[4];
-    load_words<4>(sp, pay + o, w);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) w[k] ^= ks[k];
-    store_words<4>(sp, pay + o, w, ln);
+    uint32_t raw[5];
+    load_raw<4>(sp, pay + o, raw);
+    xor_words<4>(sp, pay + o, ks, ln, raw);
   }
 
   // AesHeaderProtection::mask (rustcrypto.rs:175-186): AES-ECB(hp, sample)[0..5]
@@ -263,7 +264,20 @@ struct AesPolicy {
   }
 
   template <class S>
-  static __device__ void seal(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int q) {
+  static __device__ __forceinline__ void apply_hp(const S& sp, typename S::off_t pkt, const mq_pkt_desc& d,
+                                                  uint32_t m0, uint32_t m1) {
+    const uint8_t fb = (d.flags & MQ_PKT_LONG_HEADER) ? 0x0f : 0x1f;
+    sp.st8(pkt, sp.ld8(pkt) ^ ((uint8_t)m0 & fb));
+    const uint32_t mk = (m0 >> 8) | (m1 << 24);
+    for (uint32_t b = 0; b < d.pn_len; ++b)
+      sp.st8(pkt + d.pn_offset + b, sp.ld8(pkt + d.pn_offset + b) ^ (uint8_t)(mk >> (8 * b)));
+  }
+
+  // send composite: CTR block b (0 = E_K(J0)) on lane b % 8 in iteration b / 8; the HP block runs
+  // in the first free slot after the blocks holding the sample (b = 1, 2), or in a separate phase
+  // when the sample reaches into the tag.
+  template <class S, class G>
+  static __device__ void seal(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j, G& stg) {
     const mq_pkt_desc& d = c.d;
     const uint32_t rb = (threadIdx.x & (kTReplicas - 1)) * 4;
     const uint32_t aad_len = c.act ? (uint32_t)d.pn_offset + d.pn_len : 0u;
@@ -272,50 +286,74 @@ struct AesPolicy {
     uint32_t nb[3];
     nonce_be(row, c.pn, nb);
     const uint32_t nblk = 1 + (P + 15) / 16;
-    const uint32_t C = (nblk + 3) >> 2;
-    const uint32_t Cmax = wave_max_u32(c.act ? C : 0u);
+    const bool hp_on = c.act && !(d.flags & MQ_PKT_NO_HP);
+    const bool hp_post = hp_on && 20 > P + d.pn_len;
+    uint32_t hp_it = nblk / kLanesPerPkt, hp_lane = nblk % kLanesPerPkt;
+    if (hp_it == 0) { hp_it = 1; hp_lane = 0; }
+    const uint32_t iters = max((nblk + kLanesPerPkt - 1) / kLanesPerPkt, (hp_on && !hp_post) ? hp_it + 1 : 0u);
+    const uint32_t Imax = wave_max_u32(c.act ? iters : 0u);
     uint32_t ej0[4] = {0, 0, 0, 0};
+    uint32_t m0 = 0, m1 = 0;
+    bool have_mask = false;
     {
       AesRk rk;
       load_rk(row->aes_rk, rk);
-      for (uint32_t it = 0; it < Cmax; ++it) {
-        const uint32_t b = q * C + it;
-        const bool a = c.act && it < C && b < nblk;
+#pragma unroll
+      for (int k = 0; k < 44; ++k) pin(rk.w[k]);
+      pin(nb[0]); pin(nb[1]); pin(nb[2]);
+      stg.issue();
+      for (uint32_t it = 0; it < Imax; ++it) {
+        const uint32_t b = (uint32_t)j + kLanesPerPkt * it;
+        const bool a = c.act && b < nblk;
+        const bool is_hp = hp_on && !hp_post && it == hp_it && (uint32_t)j == hp_lane;
         uint32_t ks[4];
-        ctr_block(rk, rb, nb, b, ks);
+        if (wave_max_u32(is_hp ? 1u : 0u)) {  // iteration carrying HP blocks: per-lane key/input
+          AesRk hk;
+          load_rk(row->hp_rk, hk);
+          uint32_t smp[4];
+          load_words<4>(sp, pkt + (c.act ? d.pn_offset + 4u : 0u), smp);
+#pragma unroll
+          for (int k = 0; k < 44; ++k) hk.w[k] = is_hp ? hk.w[k] : rk.w[k];
+          uint32_t s0 = nb[0], s1 = nb[1], s2 = nb[2], s3 = b == 0 ? 1u : b + 1;
+          if (is_hp) { s0 = bswap32(smp[0]); s1 = bswap32(smp[1]); s2 = bswap32(smp[2]); s3 = bswap32(smp[3]); }
+          aes128_block(hk, rb, s0, s1, s2, s3);
+          ks[0] = bswap32(s0); ks[1] = bswap32(s1); ks[2] = bswap32(s2); ks[3] = bswap32(s3);
+          if (is_hp) { m0 = ks[0]; m1 = s1 >> 24; have_mask = true; }
+        } else {
+          ctr_block(rk, rb, nb, b, ks);
+        }
+        if (it == 0) stg.complete();
         if (a && b == 0) {
 #pragma unroll
           for (int k = 0; k < 4; ++k) ej0[k] = ks[k];
         } else if (a) {
           xor_block(sp, pay, b, P, ks);
         }
+        wave_sync();
       }
+      if (Imax == 0) stg.complete();
     }
-    wave_sync();
 #pragma unroll
-    for (int k = 0; k < 4; ++k) ej0[k] = quad_bcast0(ej0[k]);
+    for (int k = 0; k < 4; ++k) ej0[k] = oct_bcast0(ej0[k]);
     uint32_t y[4], tag[4];
-    ghash(sp, pkt, pay, aad_len, P, row, q, c.act, y);
+    ghash(sp, pkt, pay, aad_len, P, row, j, c.act, y);
     tag_words(y, ej0, tag);
-    if (c.act && q == 0) store_words<4>(sp, pay + P, tag, 16);
+    if (c.act && j == 0) store_words<4>(sp, pay + P, tag);
     wave_sync();
-    if (c.act && !(d.flags & MQ_PKT_NO_HP)) {
-      uint32_t m0, m1;
-      hp_mask(sp, pkt + d.pn_offset + 4, row, rb, m0, m1);
-      if (q == 0) {
-        const uint8_t fb = (d.flags & MQ_PKT_LONG_HEADER) ? 0x0f : 0x1f;
-        sp.st8(pkt, sp.ld8(pkt) ^ ((uint8_t)m0 & fb));
-        const uint32_t mk = (m0 >> 8) | (m1 << 24);
-        for (uint32_t j = 0; j < d.pn_len; ++j)
-          sp.st8(pkt + d.pn_offset + j, sp.ld8(pkt + d.pn_offset + j) ^ (uint8_t)(mk >> (8 * j)));
-      }
+    if (wave_max_u32(hp_post ? 1u : 0u)) {
+      uint32_t t0, t1;
+      hp_mask(sp, pkt + (c.act ? d.pn_offset + 4u : 0u), row, rb, t0, t1);
+      if (hp_post && j == 0) { m0 = t0; m1 = t1; have_mask = true; }
     }
+    if (have_mask) apply_hp(sp, pkt, d, m0, m1);
   }
 
-  template <class S>
-  static __device__ void open(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int q,
-                              bool direct) {
+  template <class S, class G>
+  static __device__ void open(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j,
+                              bool direct, G& stg) {
     const mq_pkt_desc& d = c.d;
+    stg.issue();
+    stg.complete();
     const uint32_t rb = (threadIdx.x & (kTReplicas - 1)) * 4;
     uint32_t pn_len = d.pn_len;
     uint8_t orig_b0 = 0;
@@ -330,19 +368,19 @@ struct AesPolicy {
       pn_len = (b0 & 3u) + 1;
       const uint32_t mk = (m0 >> 8) | (m1 << 24);
       uint32_t trunc = 0;
-      for (uint32_t j = 0; j < pn_len; ++j) {
-        const uint8_t e = sp.ld8(pkt + d.pn_offset + j);
-        orig_pn |= (uint32_t)e << (8 * j);
-        trunc = (trunc << 8) | (uint8_t)(e ^ (uint8_t)(mk >> (8 * j)));
+      for (uint32_t b = 0; b < pn_len; ++b) {
+        const uint8_t e = sp.ld8(pkt + d.pn_offset + b);
+        orig_pn |= (uint32_t)e << (8 * b);
+        trunc = (trunc << 8) | (uint8_t)(e ^ (uint8_t)(mk >> (8 * b)));
       }
       c.pn = decode_pn(trunc, pn_len, d.pn);
       if (c.pn > kMaxPn) {
         c.st = MQ_ERR_PROTOCOL;
         c.act = false;
-      } else if (q == 0) {
+      } else if (j == 0) {
         sp.st8(pkt, b0);
-        for (uint32_t j = 0; j < pn_len; ++j)
-          sp.st8(pkt + d.pn_offset + j, (uint8_t)(trunc >> (8 * (pn_len - 1 - j))));
+        for (uint32_t b = 0; b < pn_len; ++b)
+          sp.st8(pkt + d.pn_offset + b, (uint8_t)(trunc >> (8 * (pn_len - 1 - b))));
         hdr_written = true;
       }
     }
@@ -353,14 +391,17 @@ struct AesPolicy {
     uint32_t nb[3];
     nonce_be(row, c.pn, nb);
     const uint32_t nblk = 1 + (P + 15) / 16;
-    const uint32_t C = (nblk + 3) >> 2;
+    const uint32_t C = (nblk + kLanesPerPkt - 1) / kLanesPerPkt;
     const uint32_t Cmax = wave_max_u32(c.act ? C : 0u);
     uint32_t y[4];
-    ghash(sp, pkt, pay, aad_len, P, row, q, c.act, y);
+    ghash(sp, pkt, pay, aad_len, P, row, j, c.act, y);
     AesRk rk;
     load_rk(row->aes_rk, rk);
+    uint32_t ks0[4];  // block j: E(J0) on lane 0, keystream elsewhere
+    ctr_block(rk, rb, nb, (uint32_t)j, ks0);
     uint32_t ej0[4];
-    ctr_block(rk, rb, nb, 0, ej0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ej0[k] = oct_bcast0(ks0[k]);
     uint32_t tag[4], got[4];
     tag_words(y, ej0, tag);
     load_words<4>(sp, pay + P, got);
@@ -370,21 +411,17 @@ struct AesPolicy {
       c.act = false;
     }
     wave_sync();
-    // keystream blocks 1.. (block 0 = E(J0) is already used); spread b = 1 + q*C' + it
-    const uint32_t nks = nblk - 1;
-    const uint32_t C2 = (nks + 3) >> 2;
-    const uint32_t C2max = wave_max_u32(c.act ? C2 : 0u);
-    for (uint32_t it = 0; it < C2max; ++it) {
-      const uint32_t b = 1 + q * C2 + it;
-      const bool a = c.act && it < C2 && b < nblk;
+    if (c.act && j >= 1 && (uint32_t)j < nblk) xor_block(sp, pay, (uint32_t)j, P, ks0);
+    for (uint32_t it = 1; it < Cmax; ++it) {
+      const uint32_t b = (uint32_t)j + kLanesPerPkt * it;
+      const bool a = c.act && b < nblk;
       uint32_t ks[4];
       ctr_block(rk, rb, nb, b, ks);
       if (a) xor_block(sp, pay, b, P, ks);
     }
-    (void)Cmax;
     if (direct && hdr_written && !c.act) {
       sp.st8(pkt, orig_b0);
-      for (uint32_t j = 0; j < pn_len; ++j) sp.st8(pkt + d.pn_offset + j, (uint8_t)(orig_pn >> (8 * j)));
+      for (uint32_t b = 0; b < pn_len; ++b) sp.st8(pkt + d.pn_offset + b, (uint8_t)(orig_pn >> (8 * b)));
     }
   }
 };
@@ -455,3 +492,7 @@ hipError_t mq_launch_aes_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t* k
                      masks, n);
   return hipGetLastError();
 }
+
+#ifdef MQ_STAMPS
+void mq_stamps_set_aes(uint64_t* p) { (void)hipMemcpyToSymbol(HIP_SYMBOL(mq_stamp_buf), &p, sizeof p); }
+#endif

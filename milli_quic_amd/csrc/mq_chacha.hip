@@ -5,85 +5,102 @@
 // (:197-220), composed the way src/connection/transmit.rs:625-755 (send) and
 // src/connection/recv.rs:340-421,953-1025 (receive) compose them.
 //
-// Per tile (16 packets, one quad of lanes per packet; see mq_tile.h):
-//   seal: keystream blocks ctr = q*C + it (ctr 0 = Poly1305 one-time key) XORed into LDS ->
-//         interleaved Poly1305 over AAD||pad||CT||pad||lens -> tag -> HP mask from the sample
-//   open: HP mask -> unmask byte 0 / PN -> decode_pn -> nonce -> first keystream block (lane
-//         q=0: one-time key) -> Poly1305 over the untouched ciphertext -> tag check -> only
-//         then the keystream XOR (held first block + the rest); failed packets are never stored.
+// Per tile (8 packets, one octet of lanes per packet; see mq_tile.h):
+//   seal: keystream block ctr on lane ctr % 8 (ctr 0 = Poly1305 one-time key) XORed into LDS,
+//         HP block in the first free slot -> interleaved Poly1305 over AAD||pad||CT||pad||lens
+//         -> tag -> header mask applied
+//   open: HP mask -> unmask byte 0 / PN -> decode_pn -> nonce -> first keystream block (lane 0:
+//         one-time key) -> Poly1305 over the untouched ciphertext -> tag check -> only then the
+//         keystream XOR (held first block + the rest); failed packets are never stored.
 #include "mq_tile.h"
 
 namespace mq {
 
-// Interleaved Poly1305 of the AEAD MAC input for the quad's packet. Every lane of the quad
-// returns the same tag. aad at `pkt` (aad_len bytes), ciphertext at `pay` (ct_len bytes).
+// Interleaved Poly1305 of the AEAD MAC input for the octet's packet (RFC 8439 §2.8: AAD||pad16||
+// CT||pad16||LE64(len AAD)||LE64(len CT)): lane j takes MAC blocks 8k + j, Horner with r^8, one
+// final multiply by r^(8-j), then the octet sum. Every lane of the octet returns the same tag.
 template <class S>
 __device__ __forceinline__ void poly_tag(const S& sp, typename S::off_t pkt, typename S::off_t pay,
                                          uint32_t aad_len, uint32_t ct_len,
-                                         const uint32_t (&otk)[8], int q, bool act,
+                                         const uint32_t (&otk)[8], int j, bool act,
                                          uint32_t (&tag)[4]) {
-  P26 r = p26_from_words(otk[0] & 0x0fffffffu, otk[1] & 0x0ffffffcu, otk[2] & 0x0ffffffcu,
-                         otk[3] & 0x0ffffffcu, 0);
+  const P26 r = p26_from_words(otk[0] & 0x0fffffffu, otk[1] & 0x0ffffffcu, otk[2] & 0x0ffffffcu,
+                               otk[3] & 0x0ffffffcu, 0);
   const P26m m1 = p26_mult(r);
   P26 r2 = r;
   p26_mul(r2, m1);
-  P26 r3 = r2;
-  p26_mul(r3, m1);
+  const P26m m2 = p26_mult(r2);
   P26 r4 = r2;
-  p26_mul(r4, p26_mult(r2));
-  P26 rq;
+  p26_mul(r4, m2);
+  const P26m m4p = p26_mult(r4);
+  P26 r8 = r4;
+  p26_mul(r8, m4p);
+  // r^(8-j) from the bits of e = 8 - j (e = 8 -> r^8)
+  const uint32_t e = 8u - (uint32_t)j;
+  P26 rj;
 #pragma unroll
-  for (int l = 0; l < 5; ++l)
-    rq.l[l] = q == 0 ? r4.l[l] : q == 1 ? r3.l[l] : q == 2 ? r2.l[l] : r.l[l];
-  const P26m m4 = p26_mult(r4), mlast = p26_mult(rq);
+  for (int l = 0; l < 5; ++l) rj.l[l] = (e & 1) ? r.l[l] : (l == 0 ? 1u : 0u);
+  {
+    P26 t = rj;
+    p26_mul(t, m2);
+#pragma unroll
+    for (int l = 0; l < 5; ++l) rj.l[l] = (e & 2) ? t.l[l] : rj.l[l];
+    t = rj;
+    p26_mul(t, m4p);
+#pragma unroll
+    for (int l = 0; l < 5; ++l) rj.l[l] = (e & 4) ? t.l[l] : (e == 8 ? r8.l[l] : rj.l[l]);
+  }
+  const P26m m8 = p26_mult(r8), mlast = p26_mult(rj);
 
   const uint32_t A = (aad_len + 15) >> 4, T = (ct_len + 15) >> 4, nb = A + T + 1;
-  const uint32_t K = (nb + 3) >> 2;
+  const uint32_t K = (nb + kLanesPerPkt - 1) / kLanesPerPkt;
   const uint32_t Kmax = wave_max_u32(act ? K : 0u);
   // prepend zero blocks (no 2^128 bit) so every packet of the wave runs exactly Kmax steps
-  const int z = (int)(4 * Kmax) - (int)nb;
+  const int z = (int)(kLanesPerPkt * Kmax) - (int)nb;
   P26 acc;
 #pragma unroll
   for (int l = 0; l < 5; ++l) acc.l[l] = 0;
 
-  auto absorb = [&](uint32_t k) {
-    const int i = (int)(4 * k) + q - z;
-    typename S::off_t src = pkt;
-    int rem = 0;
-    uint32_t hib = 0;
-    bool lens = false;
+  // MAC block k of this lane: where it lives and how many of its bytes are real
+  struct Blk { typename S::off_t src; int rem; uint32_t hib; bool lens; };
+  auto where = [&](uint32_t k) {
+    const int i = (int)(kLanesPerPkt * k) + j - z;
+    Blk b{pkt, 0, 0u, false};
     if (act && i >= 0) {
-      hib = 1;
+      b.hib = 1;
       if ((uint32_t)i < A) {
-        src = pkt + 16 * (uint32_t)i; rem = (int)aad_len - 16 * i;
+        b.src = pkt + 16 * (uint32_t)i; b.rem = (int)aad_len - 16 * i;
       } else if ((uint32_t)i < A + T) {
-        src = pay + 16 * ((uint32_t)i - A); rem = (int)ct_len - 16 * (i - (int)A);
+        b.src = pay + 16 * ((uint32_t)i - A); b.rem = (int)ct_len - 16 * (i - (int)A);
       } else {
-        lens = true;
+        b.lens = true;
       }
     }
-    uint32_t m[4];
-    load_words<4>(sp, src, m);
+    return b;
+  };
+  auto absorb = [&](const Blk& b, uint32_t (&m)[4]) {
 #pragma unroll
-    for (int w = 0; w < 4; ++w) m[w] &= byte_mask(rem, w);
-    if (lens) { m[0] = aad_len; m[1] = 0; m[2] = ct_len; m[3] = 0; }
-    P26 x = p26_from_words(m[0], m[1], m[2], m[3], hib);
+    for (int w = 0; w < 4; ++w) m[w] &= byte_mask(b.rem, w);
+    if (b.lens) { m[0] = aad_len; m[1] = 0; m[2] = ct_len; m[3] = 0; }
+    const P26 x = p26_from_words(m[0], m[1], m[2], m[3], b.hib);
 #pragma unroll
     for (int l = 0; l < 5; ++l) acc.l[l] += x.l[l];
   };
-  for (uint32_t k = 0; k + 1 < Kmax; ++k) {
-    absorb(k);
-    p26_mul(acc, m4);
-  }
   if (Kmax > 0) {
-    absorb(Kmax - 1);
+    Blk b = where(0);
+    uint32_t m[4];
+    load_words<4>(sp, b.src, m);
+    for (uint32_t k = 0; k + 1 < Kmax; ++k) {
+      absorb(b, m);
+      b = where(k + 1);
+      load_words<4>(sp, b.src, m);  // next block's LDS reads overlap this multiply
+      p26_mul(acc, m8);
+    }
+    absorb(b, m);
     p26_mul(acc, mlast);
   }
 #pragma unroll
-  for (int l = 0; l < 5; ++l) {
-    acc.l[l] += quad_swap1(acc.l[l]);
-    acc.l[l] += quad_swap2(acc.l[l]);
-  }
+  for (int l = 0; l < 5; ++l) acc.l[l] = oct_sum(acc.l[l]);
   const uint32_t s[4] = {otk[4], otk[5], otk[6], otk[7]};
   p26_finish(acc, s, tag);
 }
@@ -93,20 +110,31 @@ __device__ __forceinline__ void load_key8(const uint32_t* src, uint32_t (&k)[8])
   k[0] = a.x; k[1] = a.y; k[2] = a.z; k[3] = a.w; k[4] = b.x; k[5] = b.y; k[6] = b.z; k[7] = b.w;
 }
 
+// RFC 9001 §5.4.1: apply the 5-byte mask to byte 0 (low 4 / 5 bits) and the PN bytes.
+template <class S>
+__device__ __forceinline__ void apply_hp(const S& sp, typename S::off_t pkt, const mq_pkt_desc& d,
+                                         uint32_t m0, uint32_t m1) {
+  const uint8_t fb = (d.flags & MQ_PKT_LONG_HEADER) ? 0x0f : 0x1f;
+  sp.st8(pkt, sp.ld8(pkt) ^ ((uint8_t)m0 & fb));
+  const uint32_t mk = (m0 >> 8) | (m1 << 24);  // mask[1..4]
+  for (uint32_t b = 0; b < d.pn_len; ++b)
+    sp.st8(pkt + d.pn_offset + b, sp.ld8(pkt + d.pn_offset + b) ^ (uint8_t)(mk >> (8 * b)));
+}
+
 struct ChaChaPolicy {
   static constexpr uint32_t kSuite = MQ_SUITE_CHACHA20;
 
-  // XOR keystream block `ctr` (>= 1) into payload bytes [64(ctr-1), min(64 ctr, P)).
+  // raw LDS/HBM dwords under keystream block `ctr` (>= 1): payload [64(ctr-1), min(64 ctr, P))
   template <class S>
-  static __device__ __forceinline__ void xor_block(const S& sp, typename S::off_t pay, uint32_t ctr,
-                                                   uint32_t P, const uint32_t (&ks)[16]) {
+  static __device__ __forceinline__ void load_block(const S& sp, typename S::off_t pay, uint32_t ctr,
+                                                    uint32_t (&raw)[17]) {
+    load_raw<16>(sp, pay + 64 * (ctr > 0 ? ctr - 1 : 0), raw);
+  }
+  template <class S>
+  static __device__ __forceinline__ void store_block(const S& sp, typename S::off_t pay, uint32_t ctr, uint32_t P,
+                                                     const uint32_t (&ks)[16], const uint32_t (&raw)[17]) {
     const uint32_t o = 64 * (ctr - 1);
-    const int ln = (int)min(64u, P - o);
-    uint32_t w[16];
-    load_words<16>(sp, pay + o, w);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) w[k] ^= ks[k];
-    store_words<16>(sp, pay + o, w, ln);
+    xor_words<16>(sp, pay + o, ks, (int)min(64u, P - o), raw);
   }
 
   // ChaChaHeaderProtection::mask (rustcrypto.rs:197-220): block(hp, ctr = sample[0..4] LE,
@@ -123,59 +151,92 @@ struct ChaChaPolicy {
     m1 = blk[1];
   }
 
-  template <class S>
-  static __device__ void seal(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int q) {
+  // send composite (transmit.rs:625-755): seal, then header protection from the sample.
+  // Keystream block ctr of the packet runs on lane ctr % 8 in iteration ctr / 8 (ctr 0 = the
+  // Poly1305 key); the HP block runs in the first free slot after ctr 1 (whose ciphertext holds
+  // the sample) unless the sample reaches into the tag (tiny payloads: a separate phase).
+  template <class S, class G>
+  static __device__ void seal(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j, G& stg) {
     const mq_pkt_desc& d = c.d;
-    uint32_t key[8];
+    uint32_t key[8], hk[8];
     load_key8(row->key, key);
+    load_key8(row->hp, hk);
     const uint32_t aad_len = c.act ? (uint32_t)d.pn_offset + d.pn_len : 0u;
     const uint32_t P = c.act ? d.len - aad_len - 16 : 0u;
     const typename S::off_t pay = pkt + aad_len;
     // DirectionalKeys::nonce (src/crypto/mod.rs:66-74): iv ^ (0^32 || BE64(pn))
-    const uint32_t n0 = row->iv[0], n1 = row->iv[1] ^ bswap32((uint32_t)(c.pn >> 32)),
-                   n2 = row->iv[2] ^ bswap32((uint32_t)c.pn);
+    uint32_t n0 = row->iv[0], n1 = row->iv[1] ^ bswap32((uint32_t)(c.pn >> 32)),
+             n2 = row->iv[2] ^ bswap32((uint32_t)c.pn);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { pin(key[k]); pin(hk[k]); }
+    pin(n0); pin(n1); pin(n2);
+    stg.issue();  // packet bytes stream into LDS while the first keystream block is computed
     const uint32_t nblk = 1 + (P + 63) / 64;  // block 0 = Poly1305 key, 1.. = keystream
-    const uint32_t C = (nblk + 3) >> 2;
-    const uint32_t Cmax = wave_max_u32(c.act ? C : 0u);
+    const bool hp_on = c.act && !(d.flags & MQ_PKT_NO_HP);
+    const bool hp_post = hp_on && 20 > P + d.pn_len;  // sample reaches into the tag
+    uint32_t hp_it = nblk / kLanesPerPkt, hp_lane = nblk % kLanesPerPkt;
+    if (hp_it == 0) { hp_it = 1; hp_lane = 0; }
+    const uint32_t iters = max((nblk + kLanesPerPkt - 1) / kLanesPerPkt, (hp_on && !hp_post) ? hp_it + 1 : 0u);
+    const uint32_t Imax = wave_max_u32(c.act ? iters : 0u);
     uint32_t otk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (uint32_t it = 0; it < Cmax; ++it) {
-      const uint32_t ctr = q * C + it;
-      const bool a = c.act && it < C && ctr < nblk;
+    uint32_t m0 = 0, m1 = 0;
+    bool have_mask = false;
+    for (uint32_t it = 0; it < Imax; ++it) {
+      const uint32_t ctr = (uint32_t)j + kLanesPerPkt * it;
+      const bool a = c.act && ctr < nblk;
+      const bool is_hp = hp_on && !hp_post && it == hp_it && (uint32_t)j == hp_lane;
+      uint32_t w[17];
+      if (it > 0) load_block(sp, pay, a ? ctr : 0u, w);  // LDS reads in flight during the block function
+      uint32_t kk[8], cc = ctr, x0 = n0, x1 = n1, x2 = n2;
+      if (it > 0) {
+        uint32_t smp[4];
+        load_words<4>(sp, pkt + (c.act ? d.pn_offset + 4u : 0u), smp);
+        if (is_hp) { cc = smp[0]; x0 = smp[1]; x1 = smp[2]; x2 = smp[3]; }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) kk[k] = is_hp ? hk[k] : key[k];
       uint32_t ks[16];
-      chacha20_block(key, ctr, n0, n1, n2, ks);
+      chacha20_block(kk, cc, x0, x1, x2, ks);
+      if (it == 0) {
+        stg.complete();
+        MQ_STAMP(c.tile, 2);
+        load_block(sp, pay, a ? ctr : 0u, w);
+      }
       if (a && ctr == 0) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) otk[k] = ks[k];
       } else if (a) {
-        xor_block(sp, pay, ctr, P, ks);
+        store_block(sp, pay, ctr, P, ks, w);
       }
+      if (is_hp) { m0 = ks[0]; m1 = ks[1]; have_mask = true; }
+      wave_sync();  // this iteration's ciphertext (the HP sample) is visible to the next
     }
-    wave_sync();
+    if (Imax == 0) stg.complete();
+    MQ_STAMP(c.tile, 3);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) otk[k] = quad_bcast0(otk[k]);
+    for (int k = 0; k < 8; ++k) otk[k] = oct_bcast0(otk[k]);
     uint32_t tag[4];
-    poly_tag(sp, pkt, pay, aad_len, P, otk, q, c.act, tag);
-    if (c.act && q == 0) store_words<4>(sp, pay + P, tag, 16);
+    poly_tag(sp, pkt, pay, aad_len, P, otk, j, c.act, tag);
+    if (c.act && j == 0) store_words<4>(sp, pay + P, tag);
     wave_sync();
-    // header protection (transmit.rs:721-738): sample at pn_offset + 4, after the tag exists
-    const bool hp = c.act && !(d.flags & MQ_PKT_NO_HP);
-    if (hp) {
-      uint32_t m0, m1;
-      hp_mask(sp, pkt + d.pn_offset + 4, row, m0, m1);
-      if (q == 0) {
-        const uint8_t fb = (d.flags & MQ_PKT_LONG_HEADER) ? 0x0f : 0x1f;
-        sp.st8(pkt, sp.ld8(pkt) ^ ((uint8_t)m0 & fb));
-        const uint32_t mk = (m0 >> 8) | (m1 << 24);  // mask[1..4]
-        for (uint32_t j = 0; j < d.pn_len; ++j)
-          sp.st8(pkt + d.pn_offset + j, sp.ld8(pkt + d.pn_offset + j) ^ (uint8_t)(mk >> (8 * j)));
-      }
+    MQ_STAMP(c.tile, 4);
+    if (wave_max_u32(hp_post ? 1u : 0u)) {  // rare: sample includes tag bytes
+      uint32_t t0, t1;
+      hp_mask(sp, pkt + (c.act ? d.pn_offset + 4u : 0u), row, t0, t1);
+      if (hp_post && j == 0) { m0 = t0; m1 = t1; have_mask = true; }
     }
+    if (have_mask) apply_hp(sp, pkt, d, m0, m1);  // after the MAC read the unprotected header
+    MQ_STAMP(c.tile, 5);
   }
 
-  template <class S>
-  static __device__ void open(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int q,
-                              bool direct) {
+  // receive composite (recv.rs:340-421 / 953-1025): HP removal, decode_pn, open.
+  template <class S, class G>
+  static __device__ void open(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j,
+                              bool direct, G& stg) {
     const mq_pkt_desc& d = c.d;
+    stg.issue();
+    stg.complete();
+    MQ_STAMP(c.tile, 2);
     uint32_t pn_len = d.pn_len;
     uint8_t orig_b0 = 0;
     uint32_t orig_pn = 0;
@@ -190,23 +251,24 @@ struct ChaChaPolicy {
       pn_len = (b0 & 3u) + 1;
       const uint32_t mk = (m0 >> 8) | (m1 << 24);
       uint32_t trunc = 0;
-      for (uint32_t j = 0; j < pn_len; ++j) {
-        const uint8_t e = sp.ld8(pkt + d.pn_offset + j);
-        orig_pn |= (uint32_t)e << (8 * j);
-        trunc = (trunc << 8) | (uint8_t)(e ^ (uint8_t)(mk >> (8 * j)));
+      for (uint32_t b = 0; b < pn_len; ++b) {
+        const uint8_t e = sp.ld8(pkt + d.pn_offset + b);
+        orig_pn |= (uint32_t)e << (8 * b);
+        trunc = (trunc << 8) | (uint8_t)(e ^ (uint8_t)(mk >> (8 * b)));
       }
       c.pn = decode_pn(trunc, pn_len, d.pn);
       if (c.pn > kMaxPn) {  // recv.rs:393-395
         c.st = MQ_ERR_PROTOCOL;
         c.act = false;
-      } else if (q == 0) {
+      } else if (j == 0) {
         sp.st8(pkt, b0);
-        for (uint32_t j = 0; j < pn_len; ++j)
-          sp.st8(pkt + d.pn_offset + j, (uint8_t)(trunc >> (8 * (pn_len - 1 - j))));
+        for (uint32_t b = 0; b < pn_len; ++b)
+          sp.st8(pkt + d.pn_offset + b, (uint8_t)(trunc >> (8 * (pn_len - 1 - b))));
         hdr_written = true;
       }
     }
     wave_sync();
+    MQ_STAMP(c.tile, 3);
     uint32_t key[8];
     load_key8(row->key, key);
     const uint32_t aad_len = c.act ? (uint32_t)d.pn_offset + pn_len : 0u;
@@ -215,17 +277,17 @@ struct ChaChaPolicy {
     const uint32_t n0 = row->iv[0], n1 = row->iv[1] ^ bswap32((uint32_t)(c.pn >> 32)),
                    n2 = row->iv[2] ^ bswap32((uint32_t)c.pn);
     const uint32_t nblk = 1 + (P + 63) / 64;
-    const uint32_t C = (nblk + 3) >> 2;
+    const uint32_t C = (nblk + kLanesPerPkt - 1) / kLanesPerPkt;
     const uint32_t Cmax = wave_max_u32(c.act ? C : 0u);
-    // first keystream block of every lane is computed before the MAC (lane q=0: one-time key)
-    const uint32_t ctr0 = q * C;
+    // first keystream block of every lane is computed before the MAC (lane 0: one-time key)
+    const uint32_t ctr0 = (uint32_t)j;
     uint32_t ks0[16];
     chacha20_block(key, ctr0, n0, n1, n2, ks0);
     uint32_t otk[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) otk[k] = quad_bcast0(ks0[k]);
+    for (int k = 0; k < 8; ++k) otk[k] = oct_bcast0(ks0[k]);
     uint32_t tag[4], got[4];
-    poly_tag(sp, pkt, pay, aad_len, P, otk, q, c.act, tag);
+    poly_tag(sp, pkt, pay, aad_len, P, otk, j, c.act, tag);
     load_words<4>(sp, pay + P, got);
     const uint32_t diff = (tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) | (tag[3] ^ got[3]);
     if (c.act && diff != 0) {  // Error::Crypto, buffer left as received
@@ -233,17 +295,25 @@ struct ChaChaPolicy {
       c.act = false;
     }
     wave_sync();  // every lane's MAC reads precede any plaintext write
-    if (c.act && Cmax > 0 && C > 0 && ctr0 >= 1 && ctr0 < nblk) xor_block(sp, pay, ctr0, P, ks0);
+    MQ_STAMP(c.tile, 4);
+    if (c.act && ctr0 >= 1 && ctr0 < nblk) {
+      uint32_t w[17];
+      load_block(sp, pay, ctr0, w);
+      store_block(sp, pay, ctr0, P, ks0, w);
+    }
     for (uint32_t it = 1; it < Cmax; ++it) {
-      const uint32_t ctr = q * C + it;
-      const bool a = c.act && it < C && ctr < nblk;
+      const uint32_t ctr = (uint32_t)j + kLanesPerPkt * it;
+      const bool a = c.act && ctr < nblk;
+      uint32_t w[17];
+      load_block(sp, pay, a ? ctr : 0u, w);
       uint32_t ks[16];
       chacha20_block(key, ctr, n0, n1, n2, ks);
-      if (a) xor_block(sp, pay, ctr, P, ks);
+      if (a) store_block(sp, pay, ctr, P, ks, w);
     }
+    MQ_STAMP(c.tile, 5);
     if (direct && hdr_written && !c.act) {  // direct path writes HBM in place: undo the unmask
       sp.st8(pkt, orig_b0);
-      for (uint32_t j = 0; j < pn_len; ++j) sp.st8(pkt + d.pn_offset + j, (uint8_t)(orig_pn >> (8 * j)));
+      for (uint32_t b = 0; b < pn_len; ++b) sp.st8(pkt + d.pn_offset + b, (uint8_t)(orig_pn >> (8 * b)));
     }
   }
 };
@@ -306,3 +376,7 @@ hipError_t mq_launch_chacha_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t
                      samples, masks, n);
   return hipGetLastError();
 }
+
+#ifdef MQ_STAMPS
+void mq_stamps_set_chacha(uint64_t* p) { (void)hipMemcpyToSymbol(HIP_SYMBOL(mq_stamp_buf), &p, sizeof p); }
+#endif

@@ -1,15 +1,15 @@
 // mq_device.h — device-side building blocks of the MI355X (gfx950) packet-protection kernels.
 //
-// Execution model: one 64-lane wave per workgroup processes a TILE of
-// kPktsPerTile = 16 packets; each packet is owned by a QUAD of kLanesPerPkt = 4 lanes.
+// Execution model: one 64-lane wave processes a TILE of kPktsPerTile = 8
+// packets; each packet is owned by an OCTET of kLanesPerPkt = 8 lanes (lane = 8*p + j).
 //   * staging: the tile's packets are gathered HBM -> LDS with whole-packet contiguous
 //     16-B-per-lane loads (1 KiB per wave instruction), because one-packet-per-lane strided
 //     access measured 2.7 TB/s vs 5.5 TB/s contiguous on MI355X (tools/ubench/ubench3.hip);
-//   * keystream blocks of a packet are spread over its quad (ChaCha20 64-B blocks / AES-CTR
-//     16-B blocks), XORed in LDS;
-//   * the MAC (Poly1305 / GHASH) is a 4-way interleaved Horner evaluation (lane q takes MAC
-//     blocks i = 4k + q with multiplier r^4 / H^4, then one final multiply by r^(4-q) / H^(4-q))
-//     followed by a quad reduction through DPP;
+//   * keystream blocks of a packet are spread over its octet (ChaCha20 64-B blocks / AES-CTR
+//     16-B blocks, block b on lane b % 8), XORed in LDS;
+//   * the MAC (Poly1305 / GHASH) is an 8-way interleaved Horner evaluation (lane j takes MAC
+//     blocks i = 8k + j with multiplier r^8 / H^8, then one final multiply by r^(8-j) / H^(8-j))
+//     followed by an octet reduction through DPP;
 //   * header protection and the store back to HBM close the tile.
 // Tiles whose packets do not fit the LDS budget run the same code on HBM directly ("direct").
 #pragma once
@@ -21,14 +21,12 @@
 namespace mq {
 
 constexpr int kWave = 64;
-constexpr int kPktsPerTile = 16;
-constexpr int kLanesPerPkt = kWave / kPktsPerTile;  // 4: one quad per packet
-constexpr uint32_t kLdsBytes = 20480;                // dynamic LDS per 1-wave workgroup -> 8 WG/CU
-constexpr uint32_t kTableBytes = kPktsPerTile * 16;  // per-packet slot table
+constexpr int kPktsPerTile = 8;
+constexpr int kLanesPerPkt = kWave / kPktsPerTile;  // 8: one octet of lanes per packet
+constexpr uint32_t kLdsBytes = 10240;                // LDS per tile (wave) -> 16 waves/CU
 constexpr uint32_t kSlack = 64;                      // over-read room after the last slot
-constexpr uint32_t kSpanBudget = kLdsBytes - kTableBytes - kSlack;  // 20160 bytes of packet data
 
-// Device key-table row (512 B). Filled on the host by mq_keytable_create (mq_host.cpp).
+// Device key-table row (576 B). Filled on the host by mq_keytable_create (mq_host.cpp).
 struct alignas(16) KeyRow {
   uint32_t suite;
   uint32_t pad0[3];
@@ -38,9 +36,9 @@ struct alignas(16) KeyRow {
   uint32_t hp[8];      // ChaCha20 HP key (LE words)
   uint32_t aes_rk[44]; // AES-128 round keys of the AEAD key (FIPS-197 big-endian words)
   uint32_t hp_rk[44];  // AES-128 round keys of the HP key
-  uint32_t H[4][4];    // GHASH H^1..H^4 (GCM byte order, big-endian words)
+  uint32_t H[8][4];    // GHASH H^1..H^8 (GCM byte order, big-endian words)
 };
-static_assert(sizeof(KeyRow) == 512, "KeyRow layout");
+static_assert(sizeof(KeyRow) == 576, "KeyRow layout");
 
 // ------------------------------------------------------------------------------------------
 // byte-address spaces: LDS (staged tile) or the HBM arena (direct path)
@@ -51,6 +49,7 @@ struct LdsSpace {
   __device__ __forceinline__ void st32(uint32_t a, uint32_t v) const { *(uint32_t*)(base + a) = v; }
   __device__ __forceinline__ uint8_t ld8(uint32_t a) const { return base[a]; }
   __device__ __forceinline__ void st8(uint32_t a, uint8_t v) const { base[a] = v; }
+  __device__ __forceinline__ void xor32(uint32_t a, uint32_t v) const { atomicXor((uint32_t*)(base + a), v); }
 };
 
 struct GlobalSpace {
@@ -67,6 +66,7 @@ struct GlobalSpace {
   __device__ __forceinline__ void st32(uint64_t a, uint32_t v) const { *(uint32_t*)(base + a) = v; }
   __device__ __forceinline__ uint8_t ld8(uint64_t a) const { return a < len ? base[a] : (uint8_t)0; }
   __device__ __forceinline__ void st8(uint64_t a, uint8_t v) const { base[a] = v; }
+  __device__ __forceinline__ void xor32(uint64_t a, uint32_t v) const { atomicXor((uint32_t*)(base + a), v); }
 };
 
 // v_perm_b32 selectors: loads realign memory dwords to a payload that starts `v` bytes into a
@@ -90,30 +90,74 @@ __device__ __forceinline__ void load_words(const S& sp, typename S::off_t a, uin
   for (int k = 0; k < N; ++k) w[k] = perm(m[k + 1], m[k], sel);
 }
 
-// Write bytes [a, a + len) (len <= 4N) from payload-aligned words w. Bytes outside the range
-// are never touched, so quads writing adjacent ranges never race on a shared dword.
+// bytes [lo, hi) of a dword
+__device__ __forceinline__ uint32_t range_mask(int lo, int hi) {
+  const uint32_t h = hi >= 4 ? 0xffffffffu : ((1u << (8 * hi)) - 1u);
+  const uint32_t l = lo <= 0 ? 0u : ((1u << (8 * lo)) - 1u);
+  return h & ~l;
+}
+
+// Raw memory dwords covering N payload words at byte address `a` (for xor_words).
 template <int N, class S>
-__device__ __forceinline__ void store_words(const S& sp, typename S::off_t a, const uint32_t (&w)[N],
-                                            int len) {
-  typename S::off_t b = a & ~(typename S::off_t)3;
-  int v = (int)(a & 3);
-  uint32_t sel = sel_store((uint32_t)v);
+__device__ __forceinline__ void load_raw(const S& sp, typename S::off_t a, uint32_t (&raw)[N + 1]) {
+  const typename S::off_t b = a & ~(typename S::off_t)3;
+#pragma unroll
+  for (int m = 0; m <= N; ++m) raw[m] = sp.ld32(b + 4 * m);
+}
+
+// bytes [a, a + len) ^= payload-aligned keystream words ks (len <= 4N); `raw` = load_raw(a).
+// Dwords wholly inside the range are rewritten from raw; the (at most two) edge dwords, which
+// other lanes of the octet may be updating in the same instruction, take an atomic XOR of only
+// this lane's bytes (ds_xor_b32), so neighbouring ranges never race.
+template <int N, class S>
+__device__ __forceinline__ void xor_words(const S& sp, typename S::off_t a, const uint32_t (&ks)[N], int len,
+                                          const uint32_t (&raw)[N + 1]) {
+  const typename S::off_t b = a & ~(typename S::off_t)3;
+  const int v = (int)(a & 3);
+  const uint32_t sel = sel_store((uint32_t)v);
+  if (len == 4 * N) {
+#pragma unroll
+    for (int m = 1; m < N; ++m) sp.st32(b + 4 * m, raw[m] ^ perm(ks[m], ks[m - 1], sel));
+    sp.xor32(b, perm(ks[0], 0u, sel) & range_mask(v, 4));
+    if (v) sp.xor32(b + 4 * N, perm(0u, ks[N - 1], sel) & range_mask(0, v));
+    return;
+  }
 #pragma unroll
   for (int m = 0; m <= N; ++m) {
-    uint32_t hi = m < N ? w[m] : 0u, lo = m > 0 ? w[m - 1] : 0u;
-    uint32_t out = perm(hi, lo, sel);
-    int lo_idx = 4 * m - v;  // payload index of byte 0 of this memory dword
+    const uint32_t out = perm(m < N ? ks[m] : 0u, m > 0 ? ks[m - 1] : 0u, sel);
+    const int lo_idx = 4 * m - v;  // payload index of byte 0 of this memory dword
     if (lo_idx >= 0 && lo_idx + 4 <= len) {
-      sp.st32(b + 4 * m, out);
+      sp.st32(b + 4 * m, raw[m] ^ out);
     } else if (lo_idx + 4 > 0 && lo_idx < len) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        int idx = lo_idx + k;
-        if (idx >= 0 && idx < len) sp.st8(b + 4 * m + k, (uint8_t)(out >> (8 * k)));
-      }
+      sp.xor32(b + 4 * m, out & range_mask(-lo_idx, len - lo_idx));
     }
   }
 }
+
+// Write N payload-aligned words at byte address `a` (any alignment), preserving the bytes of
+// the two edge dwords outside the range by read-modify-write. Only for a single writer per
+// packet (e.g. the tag, written by lane j == 0 after every keystream update of its packet).
+template <int N, class S>
+__device__ __forceinline__ void store_words(const S& sp, typename S::off_t a, const uint32_t (&w)[N]) {
+  const typename S::off_t b = a & ~(typename S::off_t)3;
+  const int v = (int)(a & 3);
+  const uint32_t sel = sel_store((uint32_t)v);
+  if (v == 0) {
+#pragma unroll
+    for (int m = 0; m < N; ++m) sp.st32(b + 4 * m, w[m]);
+    return;
+  }
+  const uint32_t keep = range_mask(0, v);
+  const uint32_t e0 = sp.ld32(b), eN = sp.ld32(b + 4 * N);
+#pragma unroll
+  for (int m = 1; m < N; ++m) sp.st32(b + 4 * m, perm(w[m], w[m - 1], sel));
+  sp.st32(b, (e0 & keep) | (perm(w[0], 0u, sel) & ~keep));
+  sp.st32(b + 4 * N, (eN & ~keep) | (perm(0u, w[N - 1], sel) & keep));
+}
+
+// Keep the compiler from sinking the wait for `x`'s load past this point (used to retire the
+// key loads before LDS-DMA is issued: hipcc would otherwise wait vmcnt(0) on the DMA too).
+__device__ __forceinline__ void pin(uint32_t& x) { asm volatile("" : "+v"(x)); }
 
 __device__ __forceinline__ uint32_t byte_mask(int rem, int k) {  // keep bytes < rem of word k
   int r = rem - 4 * k;
@@ -121,6 +165,25 @@ __device__ __forceinline__ uint32_t byte_mask(int rem, int k) {  // keep bytes <
 }
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+// ------------------------------------------------------------------------------------------
+// Diagnostic phase stamps (only in the -DMQ_STAMPS build, libmq_aead_stamps.so): lane 0 of each
+// tile records s_memtime at phase boundaries into mq_stamp_buf[tile][slot]. Never compiled into
+// the product library; read by tools/stamps.py.
+#ifdef MQ_STAMPS
+constexpr int kStampSlots = 8;
+static __device__ uint64_t* mq_stamp_buf;  // one copy per translation unit, set by mq_debug_set_stamps
+#define MQ_STAMP(tile, slot)                                                        \
+  do {                                                                              \
+    __builtin_amdgcn_sched_barrier(0);                                              \
+    uint64_t _t = __builtin_amdgcn_s_memtime();                                     \
+    if ((threadIdx.x & 63) == 0 && mq_stamp_buf)                                    \
+      mq_stamp_buf[(size_t)(tile) * kStampSlots + (slot)] = _t;                     \
+    __builtin_amdgcn_sched_barrier(0);                                              \
+  } while (0)
+#else
+#define MQ_STAMP(tile, slot) do { } while (0)
+#endif
 
 // ------------------------------------------------------------------------------------------
 // DPP within a quad (lanes 4p..4p+3): quad_perm selectors
@@ -132,6 +195,23 @@ __device__ __forceinline__ uint32_t quad_swap1(uint32_t x) {  // [1,0,3,2]
 }
 __device__ __forceinline__ uint32_t quad_swap2(uint32_t x) {  // [2,3,0,1]
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t half_mirror(uint32_t x) {  // lane i <- lane 7-i within 8
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xf, 0xf, false);
+}
+// octet (8-lane group) broadcast of lane 0 / sums: ds_swizzle bit mode, and_mask 0x18
+__device__ __forceinline__ uint32_t oct_bcast0(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x18);
+}
+__device__ __forceinline__ uint32_t oct_sum(uint32_t x) {
+  x += quad_swap1(x);
+  x += quad_swap2(x);
+  return x + half_mirror(x);
+}
+__device__ __forceinline__ uint32_t oct_xor(uint32_t x) {
+  x ^= quad_swap1(x);
+  x ^= quad_swap2(x);
+  return x ^ half_mirror(x);
 }
 
 // Wave-local barrier: tiles are private to one wave, so ordering the wave's own LDS / HBM

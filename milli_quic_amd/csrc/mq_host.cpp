@@ -35,6 +35,10 @@ hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_d
                                uint32_t* list, uint32_t* block_counts, uint32_t* counts,
                                hipStream_t s);
 size_t mq_partition_workspace(uint32_t n);
+#ifdef MQ_STAMPS
+void mq_stamps_set_chacha(uint64_t* p);
+void mq_stamps_set_aes(uint64_t* p);
+#endif
 
 namespace {
 
@@ -184,12 +188,10 @@ bool build_row(const mq_key_material& km, KeyRow& row) {
   if (km.suite == MQ_SUITE_AES128GCM) {
     aes_expand(km.key, row.aes_rk);
     aes_expand(km.hp, row.hp_rk);
-    uint8_t h[4][16], zero[16] = {0};
-    aes_encrypt(row.aes_rk, zero, h[0]);
-    gf128_mul(h[0], h[0], h[1]);
-    gf128_mul(h[1], h[0], h[2]);
-    gf128_mul(h[2], h[0], h[3]);
-    for (int p = 0; p < 4; ++p)
+    uint8_t h[8][16], zero[16] = {0};
+    aes_encrypt(row.aes_rk, zero, h[0]);  // H = E_K(0^128), then H^2..H^8
+    for (int p = 1; p < 8; ++p) gf128_mul(h[p - 1], h[0], h[p]);
+    for (int p = 0; p < 8; ++p)
       for (int w = 0; w < 4; ++w) row.H[p][w] = be32(h[p] + 4 * w);
   }
   return true;
@@ -269,12 +271,17 @@ void hmac_sha256(const uint8_t* key, size_t key_len, const uint8_t* m1, size_t l
 // pinned staging + device scratch for the per-packet (batch of one) calls
 struct Scratch {
   hipStream_t stream = nullptr;
-  uint8_t* dev = nullptr;   // [row 512][desc 32][status 16][pn 8][pad][packet ...]
+  uint8_t* dev = nullptr;   // [row][desc 32][status 16][pn 8][pad][packet ...]
   uint8_t* host = nullptr;  // pinned mirror
   size_t cap = 0;
   std::mutex mu;
 
-  static constexpr size_t kHdr = 1024;  // row + desc + status + pn, then the packet at +1024
+  static constexpr size_t kDesc = sizeof(KeyRow);  // descriptor (AEAD) / key id (HP)
+  static constexpr size_t kStatus = kDesc + 32;     // status (AEAD) / mask (HP)
+  static constexpr size_t kPn = kStatus + 16;       // decoded pn (AEAD)
+  static constexpr size_t kSample = kDesc + 16;     // HP sample
+  static constexpr size_t kHdr = 1024;              // the packet
+  static_assert(kPn + 8 <= kHdr && kPn % 8 == 0, "scratch header layout");
 
   int ensure(size_t pkt_bytes) {
     const size_t need = kHdr + ((pkt_bytes + 255) & ~(size_t)255) + 256;
@@ -312,26 +319,27 @@ int run_one(Scratch& sc, const KeyRow& row, uint8_t* pkt, uint32_t len, uint32_t
   d.pn_offset = (uint16_t)aad_len;
   d.pn_len = 0;
   d.flags = MQ_PKT_NO_HP;
-  std::memcpy(sc.host + 512, &d, sizeof d);
-  std::memset(sc.host + 544, 0xff, 16);
+  std::memcpy(sc.host + Scratch::kDesc, &d, sizeof d);
+  std::memset(sc.host + Scratch::kStatus, 0xff, 16);
   std::memcpy(sc.host + Scratch::kHdr, pkt, len);
   const size_t bytes = Scratch::kHdr + len;
   if (hipMemcpyAsync(sc.dev, sc.host, bytes, hipMemcpyHostToDevice, sc.stream) != hipSuccess) return MQ_ERR_HIP;
   const KeyRow* kt = (const KeyRow*)sc.dev;
-  const mq_pkt_desc* dd = (const mq_pkt_desc*)(sc.dev + 512);
-  uint8_t* st = sc.dev + 544;
-  uint64_t* pn = (uint64_t*)(sc.dev + 560);
+  const mq_pkt_desc* dd = (const mq_pkt_desc*)(sc.dev + Scratch::kDesc);
+  uint8_t* st = sc.dev + Scratch::kStatus;
+  uint64_t* pn = (uint64_t*)(sc.dev + Scratch::kPn);
   // the arena is the whole scratch buffer; the packet sits at offset kHdr
   hipError_t e = row.suite == MQ_SUITE_CHACHA20
                      ? mq_launch_chacha(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, st, pn, sc.stream)
                      : mq_launch_aes(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, st, pn, sc.stream);
   if (e != hipSuccess) return MQ_ERR_HIP;
-  if (hipMemcpyAsync(sc.host + 544, st, 16, hipMemcpyDeviceToHost, sc.stream) != hipSuccess) return MQ_ERR_HIP;
+  if (hipMemcpyAsync(sc.host + Scratch::kStatus, st, 16, hipMemcpyDeviceToHost, sc.stream) != hipSuccess)
+    return MQ_ERR_HIP;
   if (hipMemcpyAsync(sc.host + Scratch::kHdr, sc.dev + Scratch::kHdr, len, hipMemcpyDeviceToHost,
                      sc.stream) != hipSuccess)
     return MQ_ERR_HIP;
   if (hipStreamSynchronize(sc.stream) != hipSuccess) return MQ_ERR_HIP;
-  const int status = sc.host[544];
+  const int status = sc.host[Scratch::kStatus];
   if (status == MQ_OK) std::memcpy(pkt, sc.host + Scratch::kHdr, len);
   return status;
 }
@@ -477,21 +485,25 @@ int mq_hp_mask(const mq_hp_ctx* ctx, const uint8_t* sample, size_t sample_len, u
   Scratch& sc = ctx->sc;
   rc = sc.ensure(64);
   if (rc) return rc;
-  // layout: row 512 | key id (4) @512 | sample 16 @528 | mask 5 @544
+  // layout: row | key id (4) @kDesc | sample 16 @kSample | mask 5 @kStatus
   std::memcpy(sc.host, &ctx->row, sizeof(KeyRow));
   const uint32_t kid = 0;
-  std::memcpy(sc.host + 512, &kid, 4);
-  std::memcpy(sc.host + 528, sample, 16);
-  std::memset(sc.host + 544, 0, 8);
-  if (hipMemcpyAsync(sc.dev, sc.host, 560, hipMemcpyHostToDevice, sc.stream) != hipSuccess) return MQ_ERR_HIP;
+  std::memcpy(sc.host + Scratch::kDesc, &kid, 4);
+  std::memcpy(sc.host + Scratch::kSample, sample, 16);
+  std::memset(sc.host + Scratch::kStatus, 0, 8);
+  if (hipMemcpyAsync(sc.dev, sc.host, Scratch::kStatus + 8, hipMemcpyHostToDevice, sc.stream) != hipSuccess)
+    return MQ_ERR_HIP;
   const KeyRow* kt = (const KeyRow*)sc.dev;
+  const uint32_t* kids = (const uint32_t*)(sc.dev + Scratch::kDesc);
   hipError_t e = ctx->suite == MQ_SUITE_CHACHA20
-                     ? mq_launch_chacha_hp(kt, 1, (const uint32_t*)(sc.dev + 512), sc.dev + 528, sc.dev + 544, 1, sc.stream)
-                     : mq_launch_aes_hp(kt, 1, (const uint32_t*)(sc.dev + 512), sc.dev + 528, sc.dev + 544, 1, sc.stream);
+                     ? mq_launch_chacha_hp(kt, 1, kids, sc.dev + Scratch::kSample, sc.dev + Scratch::kStatus, 1, sc.stream)
+                     : mq_launch_aes_hp(kt, 1, kids, sc.dev + Scratch::kSample, sc.dev + Scratch::kStatus, 1, sc.stream);
   if (e != hipSuccess) return MQ_ERR_HIP;
-  if (hipMemcpyAsync(sc.host + 544, sc.dev + 544, 8, hipMemcpyDeviceToHost, sc.stream) != hipSuccess) return MQ_ERR_HIP;
+  if (hipMemcpyAsync(sc.host + Scratch::kStatus, sc.dev + Scratch::kStatus, 8, hipMemcpyDeviceToHost, sc.stream) !=
+      hipSuccess)
+    return MQ_ERR_HIP;
   if (hipStreamSynchronize(sc.stream) != hipSuccess) return MQ_ERR_HIP;
-  std::memcpy(mask, sc.host + 544, 5);
+  std::memcpy(mask, sc.host + Scratch::kStatus, 5);
   return MQ_OK;
 }
 
@@ -695,5 +707,13 @@ int mq_batch_time_seal_open(const mq_keytable* kt, uint8_t* arena, uint64_t aren
   *open_ms = (float)(to / iters);
   return rc;
 }
+
+#ifdef MQ_STAMPS
+// Diagnostic build only: route phase stamps to a device buffer of tiles x 8 uint64.
+void mq_debug_set_stamps(uint64_t* dev) {
+  mq_stamps_set_chacha(dev);
+  mq_stamps_set_aes(dev);
+}
+#endif
 
 }  // extern "C"
