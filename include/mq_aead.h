@@ -156,6 +156,9 @@ void mq_keytable_free(mq_keytable* kt);
  * MQ_SUITE_CHACHA20 / MQ_SUITE_AES128GCM for a single-suite batch (one launch; rows of the
  * other suite get MQ_ERR_SUITE) or MQ_SUITE_MIXED (packets are partitioned by suite on the
  * device first; needs `workspace` of mq_batch_workspace_size(n) bytes of device memory).
+ * `workspace` is optional for single-suite batches; given to mq_batch_open it also enables the
+ * header-protection pre-pass (one lane per packet computes the mask, so the packet kernel spends
+ * no keystream slot on it) — same results, faster. Workspace contents need not be initialised.
  * `stream` is a hipStream_t (NULL = default stream). Returns MQ_OK once the work is enqueued. */
 size_t mq_batch_workspace_size(uint32_t n);
 int mq_batch_seal(const mq_keytable* kt, uint8_t* arena, uint64_t arena_len,

@@ -11,6 +11,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
+from . import crypto
 from .crypto import _raise
 
 DESC_DTYPE = np.dtype([
@@ -71,10 +72,26 @@ def workspace_bytes(n):
     return _lib.load().mq_batch_workspace_size(n)
 
 
+def _ws_ptr(workspace, n):
+    if workspace is None:
+        return None
+    if workspace.numel() * workspace.element_size() < workspace_bytes(n):
+        raise crypto.InvalidArgument(f"workspace needs {workspace_bytes(n)} bytes for {n} packets")
+    return ctypes.c_void_p(workspace.data_ptr())
+
+
+def _check_out(status, pn_out, n):
+    if status.numel() < n:
+        raise crypto.InvalidArgument("status needs one byte per packet")
+    if pn_out is not None and pn_out.numel() * pn_out.element_size() < 8 * n:
+        raise crypto.InvalidArgument("pn_out needs 8 bytes per packet")
+
+
 def seal(kt, arena, desc, status, suite_hint, workspace=None, stream=None):
     """Seal + header-protect every packet of `desc` in the device `arena` (torch uint8 tensors)."""
     n = desc.numel() // 32
-    ws = ctypes.c_void_p(workspace.data_ptr()) if workspace is not None else None
+    _check_out(status, None, n)
+    ws = _ws_ptr(workspace, n)
     rc = _lib.load().mq_batch_seal(kt.handle, ctypes.c_void_p(arena.data_ptr()), arena.numel(),
                                    ctypes.c_void_p(desc.data_ptr()), n, ctypes.c_void_p(status.data_ptr()),
                                    suite_hint, ws, _stream_ptr(stream))
@@ -84,7 +101,8 @@ def seal(kt, arena, desc, status, suite_hint, workspace=None, stream=None):
 def open_(kt, arena, desc, status, pn_out, suite_hint, workspace=None, stream=None):
     """Remove header protection, decode PNs and open every packet of `desc` in place."""
     n = desc.numel() // 32
-    ws = ctypes.c_void_p(workspace.data_ptr()) if workspace is not None else None
+    _check_out(status, pn_out, n)
+    ws = _ws_ptr(workspace, n)
     pn = ctypes.c_void_p(pn_out.data_ptr()) if pn_out is not None else None
     rc = _lib.load().mq_batch_open(kt.handle, ctypes.c_void_p(arena.data_ptr()), arena.numel(),
                                    ctypes.c_void_p(desc.data_ptr()), n, ctypes.c_void_p(status.data_ptr()),

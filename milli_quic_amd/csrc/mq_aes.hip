@@ -70,6 +70,10 @@ __device__ __forceinline__ uint32_t tlook(uint32_t s, int k, uint32_t rb) {
 // AES-128 encryption of a block given as big-endian column words (FIPS-197 §5.1).
 __device__ __forceinline__ void aes128_block(const AesRk& rk, uint32_t rb, uint32_t& s0, uint32_t& s1,
                                              uint32_t& s2, uint32_t& s3) {
+#if MQ_PROF_SKIP & 16
+  s0 ^= rk.w[0]; s1 ^= rk.w[41]; s2 ^= rk.w[42] ^ rb; s3 ^= rk.w[43];
+  return;
+#endif
   s0 ^= rk.w[0]; s1 ^= rk.w[1]; s2 ^= rk.w[2]; s3 ^= rk.w[3];
 #pragma unroll
   for (int r = 1; r < 10; ++r) {
@@ -156,6 +160,10 @@ template <class S>
 __device__ __forceinline__ void ghash(const S& sp, typename S::off_t pkt, typename S::off_t pay,
                                       uint32_t aad_len, uint32_t ct_len, const KeyRow* row, int j,
                                       bool act, uint32_t (&y)[4]) {
+#if MQ_PROF_SKIP & 2
+  for (int w = 0; w < 4; ++w) y[w] = row->H[0][w] ^ aad_len ^ ct_len;
+  return;
+#endif
   uint32_t hp[4];
   GfOp m8, mlast;
   {
@@ -360,8 +368,8 @@ struct AesPolicy {
     uint32_t orig_pn = 0;
     bool hdr_written = false;
     if (c.act && !(d.flags & MQ_PKT_NO_HP)) {
-      uint32_t m0, m1;
-      hp_mask(sp, pkt + d.pn_offset + 4, row, rb, m0, m1);
+      uint32_t m0 = c.hm0, m1 = c.hm1;
+      if (!c.pre_hp) hp_mask(sp, pkt + d.pn_offset + 4, row, rb, m0, m1);
       const uint8_t fb = (d.flags & MQ_PKT_LONG_HEADER) ? 0x0f : 0x1f;
       orig_b0 = sp.ld8(pkt);
       const uint8_t b0 = orig_b0 ^ ((uint8_t)m0 & fb);
@@ -439,19 +447,20 @@ extern "C" __global__ __launch_bounds__(64 * kAesWaves) void mq_aes_seal_kernel(
   __syncthreads();
   const uint32_t w = threadIdx.x >> 6;
   run_tile<AesPolicy, false>(smem + w * kLdsBytes, blockIdx.x * kAesWaves + w, kt, n_rows, arena, arena_len,
-                             desc, n, index, n_dev, status, nullptr);
+                             desc, n, index, n_dev, status, nullptr, nullptr);
 }
 
 extern "C" __global__ __launch_bounds__(64 * kAesWaves) void mq_aes_open_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
     const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,
-    const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out) {
+    const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,
+    const uint2* __restrict__ hpm) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   build_t0(threadIdx.x, blockDim.x);
   __syncthreads();
   const uint32_t w = threadIdx.x >> 6;
   run_tile<AesPolicy, true>(smem + w * kLdsBytes, blockIdx.x * kAesWaves + w, kt, n_rows, arena, arena_len,
-                            desc, n, index, n_dev, status, pn_out);
+                            desc, n, index, n_dev, status, pn_out, hpm);
 }
 
 extern "C" __global__ __launch_bounds__(256) void mq_aes_hp_kernel(
@@ -470,15 +479,40 @@ extern "C" __global__ __launch_bounds__(256) void mq_aes_hp_kernel(
   masks[5 * (size_t)i + 4] = (uint8_t)m1;
 }
 
+// Open pre-pass: AesHeaderProtection::mask of every packet's sample, one packet per lane.
+extern "C" __global__ __launch_bounds__(256) void mq_aes_open_hp_kernel(
+    const KeyRow* __restrict__ kt, uint32_t n_rows, const uint8_t* __restrict__ arena, uint64_t arena_len,
+    const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,
+    const uint32_t* __restrict__ n_dev, uint2* __restrict__ hpm) {
+  build_t0(threadIdx.x, blockDim.x);
+  __syncthreads();
+  uint32_t i;
+  const KeyRow* row;
+  uint64_t at;
+  if (!prepass_pick(blockIdx.x * blockDim.x + threadIdx.x, MQ_SUITE_AES128GCM, kt, n_rows, arena_len, desc, n,
+                    index, n_dev, i, row, at))
+    return;
+  GlobalSpace sp{const_cast<uint8_t*>(arena), arena_len};
+  uint32_t m0, m1;
+  AesPolicy::hp_mask(sp, at, row, (threadIdx.x & (kTReplicas - 1)) * 4, m0, m1);
+  hpm[i] = make_uint2(m0, m1);
+}
+
 hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena, uint64_t arena_len,
                          const mq_pkt_desc* desc, uint32_t n, const uint32_t* index, const uint32_t* n_dev,
-                         uint8_t* status, uint64_t* pn_out, hipStream_t s) {
+                         uint8_t* status, uint64_t* pn_out, uint2* hpm, hipStream_t s) {
   const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
   if (tiles == 0) return hipSuccess;
   const uint32_t blocks = (tiles + kAesWaves - 1) / kAesWaves;
+  if (open && hpm) {
+    hipLaunchKernelGGL(mq_aes_open_hp_kernel, dim3((n + 255) / 256), dim3(256), 0, s, kt, n_rows, arena,
+                       arena_len, desc, n, index, n_dev, hpm);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
   if (open)
     hipLaunchKernelGGL(mq_aes_open_kernel, dim3(blocks), dim3(64 * kAesWaves), kLdsBytes * kAesWaves, s, kt,
-                       n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out);
+                       n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm);
   else
     hipLaunchKernelGGL(mq_aes_seal_kernel, dim3(blocks), dim3(64 * kAesWaves), kLdsBytes * kAesWaves, s, kt,
                        n_rows, arena, arena_len, desc, n, index, n_dev, status);

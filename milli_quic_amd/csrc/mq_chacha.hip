@@ -24,6 +24,10 @@ __device__ __forceinline__ void poly_tag(const S& sp, typename S::off_t pkt, typ
                                          uint32_t aad_len, uint32_t ct_len,
                                          const uint32_t (&otk)[8], int j, bool act,
                                          uint32_t (&tag)[4]) {
+#if MQ_PROF_SKIP & 2
+  for (int w = 0; w < 4; ++w) tag[w] = otk[4 + w] ^ aad_len ^ ct_len;
+  return;
+#endif
   const P26 r = p26_from_words(otk[0] & 0x0fffffffu, otk[1] & 0x0ffffffcu, otk[2] & 0x0ffffffcu,
                                otk[3] & 0x0ffffffcu, 0);
   const P26m m1 = p26_mult(r);
@@ -243,8 +247,8 @@ struct ChaChaPolicy {
     bool hdr_written = false;
     if (c.act && !(d.flags & MQ_PKT_NO_HP)) {
       // recv.rs:363-391 / :968-992: mask, unmask byte 0, pn_len, unmask PN, decode_pn
-      uint32_t m0, m1;
-      hp_mask(sp, pkt + d.pn_offset + 4, row, m0, m1);
+      uint32_t m0 = c.hm0, m1 = c.hm1;
+      if (!c.pre_hp) hp_mask(sp, pkt + d.pn_offset + 4, row, m0, m1);
       const uint8_t fb = (d.flags & MQ_PKT_LONG_HEADER) ? 0x0f : 0x1f;
       orig_b0 = sp.ld8(pkt);
       const uint8_t b0 = orig_b0 ^ ((uint8_t)m0 & fb);
@@ -327,15 +331,16 @@ extern "C" __global__ __launch_bounds__(64) void mq_chacha_seal_kernel(
     const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,
     const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  run_tile<ChaChaPolicy, false>(smem, blockIdx.x, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr);
+  run_tile<ChaChaPolicy, false>(smem, blockIdx.x, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr, nullptr);
 }
 
 extern "C" __global__ __launch_bounds__(64) void mq_chacha_open_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
     const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,
-    const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out) {
+    const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,
+    const uint2* __restrict__ hpm) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  run_tile<ChaChaPolicy, true>(smem, blockIdx.x, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out);
+  run_tile<ChaChaPolicy, true>(smem, blockIdx.x, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm);
 }
 
 // Batched HeaderProtection::mask for ChaCha20 rows (one sample per lane).
@@ -353,16 +358,40 @@ extern "C" __global__ __launch_bounds__(256) void mq_chacha_hp_kernel(
   masks[5 * (size_t)i + 4] = (uint8_t)m1;
 }
 
+// Open pre-pass: ChaChaHeaderProtection::mask of every packet's sample, one packet per lane, so
+// the tile kernel spends no keystream slot of its octet on it.
+extern "C" __global__ __launch_bounds__(256) void mq_chacha_open_hp_kernel(
+    const KeyRow* __restrict__ kt, uint32_t n_rows, const uint8_t* __restrict__ arena, uint64_t arena_len,
+    const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,
+    const uint32_t* __restrict__ n_dev, uint2* __restrict__ hpm) {
+  uint32_t i;
+  const KeyRow* row;
+  uint64_t at;
+  if (!prepass_pick(blockIdx.x * blockDim.x + threadIdx.x, MQ_SUITE_CHACHA20, kt, n_rows, arena_len, desc, n,
+                    index, n_dev, i, row, at))
+    return;
+  GlobalSpace sp{const_cast<uint8_t*>(arena), arena_len};
+  uint32_t m0, m1;
+  ChaChaPolicy::hp_mask(sp, at, row, m0, m1);
+  hpm[i] = make_uint2(m0, m1);
+}
+
 // ---- host-side launchers (called from mq_host.cpp) -------------------------------------------
 hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena,
                             uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
                             const uint32_t* index, const uint32_t* n_dev, uint8_t* status,
-                            uint64_t* pn_out, hipStream_t s) {
+                            uint64_t* pn_out, uint2* hpm, hipStream_t s) {
   const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
   if (tiles == 0) return hipSuccess;
+  if (open && hpm) {
+    hipLaunchKernelGGL(mq_chacha_open_hp_kernel, dim3((n + 255) / 256), dim3(256), 0, s, kt, n_rows, arena,
+                       arena_len, desc, n, index, n_dev, hpm);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
   if (open)
     hipLaunchKernelGGL(mq_chacha_open_kernel, dim3(tiles), dim3(kWave), kLdsBytes, s, kt, n_rows, arena,
-                       arena_len, desc, n, index, n_dev, status, pn_out);
+                       arena_len, desc, n, index, n_dev, status, pn_out, hpm);
   else
     hipLaunchKernelGGL(mq_chacha_seal_kernel, dim3(tiles), dim3(kWave), kLdsBytes, s, kt, n_rows, arena,
                        arena_len, desc, n, index, n_dev, status);

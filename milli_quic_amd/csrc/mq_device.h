@@ -167,6 +167,13 @@ __device__ __forceinline__ uint32_t byte_mask(int rem, int k) {  // keep bytes <
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
 // ------------------------------------------------------------------------------------------
+// MQ_PROF_SKIP (diagnostic builds from `make prof-variants`, never the product library): bit 1
+// skips the ChaCha rounds, 2 the MAC, 4 the LDS->HBM store, 8 the HBM->LDS staging, 16 the AES
+// rounds; the timing differences give each phase's cost under full load (tools/phase_cost.py).
+#ifndef MQ_PROF_SKIP
+#define MQ_PROF_SKIP 0
+#endif
+
 // Diagnostic phase stamps (only in the -DMQ_STAMPS build, libmq_aead_stamps.so): lane 0 of each
 // tile records s_memtime at phase boundaries into mq_stamp_buf[tile][slot]. Never compiled into
 // the product library; read by tools/stamps.py.
@@ -269,6 +276,11 @@ __device__ __forceinline__ uint32_t rotl(uint32_t x, int r) { return (x << r) | 
 __device__ __forceinline__ void chacha20_block(const uint32_t (&key)[8], uint32_t ctr,
                                                uint32_t n0, uint32_t n1, uint32_t n2,
                                                uint32_t (&out)[16]) {
+#if MQ_PROF_SKIP & 1  // phase-cost diagnostic build only (tools/phase_cost.py): no rounds
+#pragma unroll
+  for (int k = 0; k < 16; ++k) out[k] = key[k & 7] ^ ctr ^ n0 ^ (k == 13 ? n1 : n2);
+  return;
+#endif
   uint32_t x0 = 0x61707865u, x1 = 0x3320646eu, x2 = 0x79622d32u, x3 = 0x6b206574u;
   uint32_t x4 = key[0], x5 = key[1], x6 = key[2], x7 = key[3];
   uint32_t x8 = key[4], x9 = key[5], x10 = key[6], x11 = key[7];

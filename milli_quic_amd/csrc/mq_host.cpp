@@ -22,13 +22,13 @@ using mq::KeyRow;
 hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena,
                             uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
                             const uint32_t* index, const uint32_t* n_dev, uint8_t* status,
-                            uint64_t* pn_out, hipStream_t s);
+                            uint64_t* pn_out, uint2* hpm, hipStream_t s);
 hipError_t mq_launch_chacha_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t* key_ids,
                                const uint8_t* samples, uint8_t* masks, uint32_t n, hipStream_t s);
 hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena,
                          uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
                          const uint32_t* index, const uint32_t* n_dev, uint8_t* status,
-                         uint64_t* pn_out, hipStream_t s);
+                         uint64_t* pn_out, uint2* hpm, hipStream_t s);
 hipError_t mq_launch_aes_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t* key_ids,
                             const uint8_t* samples, uint8_t* masks, uint32_t n, hipStream_t s);
 hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_desc* desc, uint32_t n,
@@ -330,8 +330,8 @@ int run_one(Scratch& sc, const KeyRow& row, uint8_t* pkt, uint32_t len, uint32_t
   uint64_t* pn = (uint64_t*)(sc.dev + Scratch::kPn);
   // the arena is the whole scratch buffer; the packet sits at offset kHdr
   hipError_t e = row.suite == MQ_SUITE_CHACHA20
-                     ? mq_launch_chacha(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, st, pn, sc.stream)
-                     : mq_launch_aes(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, st, pn, sc.stream);
+                     ? mq_launch_chacha(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, st, pn, nullptr, sc.stream)
+                     : mq_launch_aes(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, st, pn, nullptr, sc.stream);
   if (e != hipSuccess) return MQ_ERR_HIP;
   if (hipMemcpyAsync(sc.host + Scratch::kStatus, st, 16, hipMemcpyDeviceToHost, sc.stream) != hipSuccess)
     return MQ_ERR_HIP;
@@ -617,7 +617,9 @@ void mq_keytable_free(mq_keytable* kt) {
   delete kt;
 }
 
-size_t mq_batch_workspace_size(uint32_t n) { return mq_partition_workspace(n); }
+// workspace: [open pre-pass HP masks, 8 B per packet][partition lists (mixed batches)]
+static size_t ws_align(size_t b) { return (b + 255) & ~(size_t)255; }
+size_t mq_batch_workspace_size(uint32_t n) { return ws_align(8 * (size_t)n) + mq_partition_workspace(n); }
 
 static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t arena_len,
                  const mq_pkt_desc* desc, uint32_t n, uint8_t* status, uint64_t* pn_out,
@@ -629,24 +631,26 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
   if (n == 0) return MQ_OK;
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
+  uint8_t* ws = (uint8_t*)workspace;
+  // open with a workspace: header-protection masks come from the one-lane-per-packet pre-pass
+  uint2* hpm = (open && ws) ? (uint2*)ws : nullptr;
   if (suite_hint == MQ_SUITE_CHACHA20) {
-    e = mq_launch_chacha(open, kt->dev, kt->rows, arena, arena_len, desc, n, nullptr, nullptr, status, pn_out, s);
+    e = mq_launch_chacha(open, kt->dev, kt->rows, arena, arena_len, desc, n, nullptr, nullptr, status, pn_out, hpm, s);
   } else if (suite_hint == MQ_SUITE_AES128GCM) {
-    e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, n, nullptr, nullptr, status, pn_out, s);
+    e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, n, nullptr, nullptr, status, pn_out, hpm, s);
   } else if (suite_hint == MQ_SUITE_MIXED) {
-    if (!workspace) return MQ_ERR_INVALID_ARG;
-    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    uint8_t* ws = (uint8_t*)workspace;
-    uint32_t* list = (uint32_t*)ws;
+    if (!ws) return MQ_ERR_INVALID_ARG;
+    uint8_t* pw = ws + ws_align(8 * (size_t)n);
+    uint32_t* list = (uint32_t*)pw;
     const size_t nblocks = ((size_t)n + 1023) / 1024;
-    uint32_t* bc = (uint32_t*)(ws + al(sizeof(uint32_t) * 2 * (size_t)n));
-    uint32_t* counts = (uint32_t*)(ws + al(sizeof(uint32_t) * 2 * (size_t)n) + al(sizeof(uint32_t) * 2 * nblocks));
+    uint32_t* bc = (uint32_t*)(pw + ws_align(sizeof(uint32_t) * 2 * (size_t)n));
+    uint32_t* counts = (uint32_t*)(pw + ws_align(sizeof(uint32_t) * 2 * (size_t)n) + ws_align(sizeof(uint32_t) * 2 * nblocks));
     e = mq_launch_partition(kt->dev, kt->rows, desc, n, list, bc, counts, s);
     if (e == hipSuccess)
-      e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, n, list, counts, status, pn_out, s);
+      e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, n, list, counts, status, pn_out, hpm, s);
     if (e == hipSuccess)
       e = mq_launch_chacha(open, kt->dev, kt->rows, arena, arena_len, desc, n, list + n, counts + 1, status,
-                           pn_out, s);
+                           pn_out, hpm, s);
   } else {
     return MQ_ERR_INVALID_ARG;
   }

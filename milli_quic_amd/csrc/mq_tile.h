@@ -39,6 +39,8 @@ struct PktCtx {
   mq_pkt_desc d;
   uint64_t pn;       // full packet number (seal: from d; open: decoded)
   uint32_t tile;     // tile index (diagnostic stamps)
+  bool pre_hp;       // open: header-protection mask precomputed by the pre-pass (wave-uniform)
+  uint32_t hm0, hm1; // that mask: bytes 0..3, byte 4
 };
 
 // decode_pn, reference src/packet/number.rs:52-70 (RFC 9000 A.3)
@@ -109,6 +111,9 @@ struct DmaStager {
   uint32_t fix_g = 0;
 
   __device__ __forceinline__ void issue() {
+#if MQ_PROF_SKIP & 8
+    return;
+#endif
     const uint32_t nk = (total + kWave - 1) / kWave;
     for (uint32_t k = 0; k < nk; ++k) {
       const uint32_t g = k * kWave + lane;
@@ -142,6 +147,9 @@ struct NoStager {
 // of neighbouring packets (other tiles) are never touched.
 __device__ __forceinline__ void stage_out(const uint8_t* smem, const Layout& lay, uint32_t total,
                                           uint8_t* arena, int lane) {
+#if MQ_PROF_SKIP & 4
+  return;
+#endif
   for (uint32_t g0 = 0; g0 < total; g0 += 4 * kWave) {
     uint4 v[4];
     int jj[4];
@@ -176,13 +184,36 @@ __device__ __forceinline__ void stage_out(const uint8_t* smem, const Layout& lay
 //   template <class S, class G> static __device__ void open(const S&, S::off_t pkt, PktCtx&, const KeyRow*, int j, bool direct, G& stg);
 // calling stg.issue() once (after their own global loads have been consumed) and stg.complete()
 // before touching packet bytes. Both must execute every wave_sync() in wave-uniform control flow.
+// Open pre-pass (RFC 9001 §5.4.2 sampling, recv.rs:363-370): one packet per lane; picks the packets
+// whose mask the tile kernel will need. Packets failing these checks are skipped here and
+// reported by the tile kernel's own validation.
+__device__ __forceinline__ bool prepass_pick(uint32_t t, uint32_t suite, const KeyRow* __restrict__ kt,
+                                             uint32_t n_rows, uint64_t arena_len,
+                                             const mq_pkt_desc* __restrict__ desc, uint32_t n,
+                                             const uint32_t* __restrict__ index,
+                                             const uint32_t* __restrict__ n_dev, uint32_t& i,
+                                             const KeyRow*& row, uint64_t& sample_at) {
+  const uint32_t count = n_dev ? *n_dev : n;
+  if (t >= count) return false;
+  i = index ? index[t] : t;
+  const mq_pkt_desc d = desc[i];
+  if (d.key_id >= n_rows || d.offset + (uint64_t)d.len > arena_len || (d.flags & MQ_PKT_NO_HP) ||
+      (uint64_t)d.pn_offset + 20 > d.len)
+    return false;
+  row = kt + d.key_id;
+  if (row->suite != suite) return false;
+  sample_at = d.offset + d.pn_offset + 4;
+  return true;
+}
+
 template <class Policy, bool OPEN>
 __device__ __forceinline__ void run_tile(uint8_t* smem, uint32_t tile_id, const KeyRow* __restrict__ kt,
                                          uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
                                          const mq_pkt_desc* __restrict__ desc, uint32_t n,
                                          const uint32_t* __restrict__ index,
                                          const uint32_t* __restrict__ n_dev,
-                                         uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out) {
+                                         uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,
+                                         const uint2* __restrict__ hpm) {
   const int lane = threadIdx.x & (kWave - 1), p = lane / kLanesPerPkt, j = lane % kLanesPerPkt;
   const uint32_t count = n_dev ? *n_dev : n;
   const uint32_t tile0 = tile_id * kPktsPerTile;
@@ -198,6 +229,13 @@ __device__ __forceinline__ void run_tile(uint8_t* smem, uint32_t tile_id, const 
   } else {
     c.d.offset = 0; c.d.len = 0; c.d.key_id = 0; c.d.pn = 0; c.d.pn_offset = 0; c.d.pn_len = 0;
     c.d.flags = 0; c.d.reserved = 0;
+  }
+  c.pre_hp = OPEN && hpm != nullptr;
+  c.hm0 = c.hm1 = 0;
+  if (OPEN && hpm && c.valid) {
+    const uint2 m = hpm[c.i];
+    c.hm0 = m.x;
+    c.hm1 = m.y;
   }
   c.st = c.valid ? validate<Policy::kSuite, OPEN>(c.d, kt, n_rows, arena_len) : (int)MQ_ERR_INVALID_ARG;
   c.act = c.valid && c.st == MQ_OK;

@@ -29,13 +29,15 @@ def to_dev(a):
     return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).to(DEV)
 
 
-def gpu_run(keys, arena, desc, hint, open_=False):
+def gpu_run(keys, arena, desc, hint, open_=False, use_ws=True):
+    """One batch through the C ABI. use_ws=False (single-suite hints only) runs open without a
+    workspace, i.e. with header protection inside the packet kernel instead of the pre-pass."""
     kt = KeyTable(keys)
     n = len(desc)
     a, d = to_dev(arena), to_dev(desc)
     st = torch.full((max(n, 1),), 0xEE, dtype=torch.uint8, device=DEV)
     pn = torch.zeros(max(n, 1), dtype=torch.int64, device=DEV)
-    ws = torch.empty(max(batch.workspace_bytes(n), 256), dtype=torch.uint8, device=DEV)
+    ws = torch.full((max(batch.workspace_bytes(n), 256),), 0xA5, dtype=torch.uint8, device=DEV) if use_ws else None
     if open_:
         batch.open_(kt, a, d, st, pn, hint, ws)
     else:
@@ -242,13 +244,14 @@ def test_failures_match_oracle(orc, suite):
     od["len"][6] = 24                        # sample out of range -> Crypto
     od["offset"][7] = len(bad) - 10          # past the arena end
     od["pn"][8] = (1 << 62) - 2              # decode_pn lands above 2^62-1 -> ProtocolViolation
-    g_out, g_st, g_pn = gpu_run(w.keys, bad, od, suite, open_=True)
     o_out, o_st, o_pn = oracle_run(orc, w.keys, bad, od, suite, open_=True)
-    assert (g_st == o_st).all(), np.nonzero(g_st != o_st)
     assert (o_st != 0).sum() >= 150
-    assert g_out.tobytes() == o_out.tobytes()
-    ok = o_st == 0
-    assert (g_pn[ok] == o_pn[ok]).all()
+    for use_ws in (True, False):  # HP pre-pass and in-kernel HP
+        g_out, g_st, g_pn = gpu_run(w.keys, bad, od, suite, open_=True, use_ws=use_ws)
+        assert (g_st == o_st).all(), (use_ws, np.nonzero(g_st != o_st))
+        assert g_out.tobytes() == o_out.tobytes(), use_ws
+        ok = o_st == 0
+        assert (g_pn[ok] == o_pn[ok]).all(), use_ws
     sd = w.seal_desc.copy()
     sd["pn_len"][3] = 0                      # invalid pn_len
     sd["pn_len"][4] = 5
@@ -270,10 +273,11 @@ def test_direct_path_and_disorder(orc, suite):
         o_out, o_st, _ = oracle_run(orc, w.keys, w.arena, sd, suite)
         assert (g_st == 0).all() and (g_st == o_st).all()
         assert g_out.tobytes() == o_out.tobytes()
-        g_back, g_st, g_pn = gpu_run(w.keys, g_out, od, suite, open_=True)
-        assert (g_st == 0).all() and (g_pn == w.pns[order]).all()
-        keep = w.arena.reshape(w.n, 1500)[:, :1484].tobytes()
-        assert g_back.reshape(w.n, 1500)[:, :1484].tobytes() == keep
+        for use_ws in (True, False):
+            g_back, g_st, g_pn = gpu_run(w.keys, g_out, od, suite, open_=True, use_ws=use_ws)
+            assert (g_st == 0).all() and (g_pn == w.pns[order]).all()
+            keep = w.arena.reshape(w.n, 1500)[:, :1484].tobytes()
+            assert g_back.reshape(w.n, 1500)[:, :1484].tobytes() == keep
 
 
 @pytest.mark.parametrize("L", [21, 36, 63, 64, 65, 100, 1350])
@@ -283,6 +287,12 @@ def test_small_and_odd_sizes(orc, L):
         g_out, g_st, _ = gpu_run(w.keys, w.arena, w.seal_desc, suite)
         o_out, o_st, _ = oracle_run(orc, w.keys, w.arena, w.seal_desc, suite)
         assert (g_st == o_st).all() and g_out.tobytes() == o_out.tobytes(), (suite, L)
+        o_back, o_st, o_pn = oracle_run(orc, w.keys, o_out, w.open_desc, suite, open_=True)
+        for use_ws in (True, False):
+            g_back, g_st, g_pn = gpu_run(w.keys, g_out, w.open_desc, suite, open_=True, use_ws=use_ws)
+            assert (g_st == o_st).all() and g_back.tobytes() == o_back.tobytes(), (suite, L, use_ws)
+            ok = o_st == 0
+            assert (g_pn[ok] == o_pn[ok]).all() and (g_pn[ok] == w.pns[ok]).all(), (suite, L, use_ws)
 
 
 def test_full_size_roundtrip_config_b(orc):
