@@ -315,7 +315,7 @@ struct AesPolicy {
         const bool a = c.act && b < nblk;
         const bool is_hp = hp_on && !hp_post && it == hp_it && (uint32_t)j == hp_lane;
         uint32_t ks[4];
-        if (wave_max_u32(is_hp ? 1u : 0u)) {  // iteration carrying HP blocks: per-lane key/input
+        if (wave_any(is_hp)) {  // iteration carrying HP blocks: per-lane key/input
           AesRk hk;
           load_rk(row->hp_rk, hk);
           uint32_t smp[4];
@@ -348,7 +348,7 @@ struct AesPolicy {
     tag_words(y, ej0, tag);
     if (c.act && j == 0) store_words<4>(sp, pay + P, tag);
     wave_sync();
-    if (wave_max_u32(hp_post ? 1u : 0u)) {
+    if (wave_any(hp_post)) {
       uint32_t t0, t1;
       hp_mask(sp, pkt + (c.act ? d.pn_offset + 4u : 0u), row, rb, t0, t1);
       if (hp_post && j == 0) { m0 = t0; m1 = t1; have_mask = true; }

@@ -224,7 +224,7 @@ struct ChaChaPolicy {
     if (c.act && j == 0) store_words<4>(sp, pay + P, tag);
     wave_sync();
     MQ_STAMP(c.tile, 4);
-    if (wave_max_u32(hp_post ? 1u : 0u)) {  // rare: sample includes tag bytes
+    if (wave_any(hp_post)) {  // rare: sample includes tag bytes
       uint32_t t0, t1;
       hp_mask(sp, pkt + (c.act ? d.pn_offset + 4u : 0u), row, t0, t1);
       if (hp_post && j == 0) { m0 = t0; m1 = t1; have_mask = true; }

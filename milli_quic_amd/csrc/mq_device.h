@@ -230,14 +230,23 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+// Reductions over the wave for OCTET-UNIFORM values (every lane of an octet holds the same
+// value, as for per-packet quantities): DPP row_mirror folds the two octets of a row, then
+// row_bcast15 / row_bcast31 fold the rows; the result is read from lane 63 (wave-uniform).
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    uint32_t y = (uint32_t)__shfl_xor((int)x, d, 64);
-    x = x > y ? x : y;
-  }
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x140, 0xf, 0xf, false));  // row_mirror
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x142, 0xa, 0xf, false));  // row_bcast15
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x143, 0xc, 0xf, false));  // row_bcast31
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+// inclusive prefix sum over the octets (octet-uniform x): octet q gets x_0 + ... + x_q
+__device__ __forceinline__ uint32_t oct_incl_scan(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);   // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast31
   return x;
 }
+__device__ __forceinline__ bool wave_any(bool b) { return __builtin_amdgcn_ballot_w64(b) != 0; }
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t x) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) {
@@ -251,14 +260,6 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
   for (int d = 32; d >= 1; d >>= 1) {
     uint64_t y = __shfl_xor(x, d, 64);
     x = x > y ? x : y;
-  }
-  return x;
-}
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
-    if (lane >= d) x += y;
   }
   return x;
 }

@@ -2,33 +2,19 @@
 // descriptor validation, HBM<->LDS gather/scatter of whole packets, packet-number decoding.
 //
 // One wave = one tile = kPktsPerTile (8) packets, lane = 8*p + j. The tile's packets are copied
-// whole into a private kLdsBytes LDS region ("image"), processed there, and written back. Two
-// image layouts (wave-uniform choice):
-//   fixed    every packet gets S = max(chunks) 16-B chunks: chunk g belongs to packet g / S
-//            (a multiply-shift, no lookups) — the common case (1-RTT packets up to ~1.2 KB);
-//   variable packets packed back to back; chunk g -> packet by a 3-step search of the slot
-//            table (mixed batches whose largest packet does not fit the fixed layout).
-// Tiles that fit neither run the same policy code on HBM directly ("direct" path).
+// whole into a private kLdsBytes LDS region ("image"), processed there, and written back.
+// Packet p's image is the run of 16-B arena chunks covering it, placed at LDS chunk slot_p
+// (an octet prefix sum of the chunk counts). Staging moves one packet per LDS-DMA instruction
+// group (SGPR base address, lane = chunk), write-back likewise with plain 16-B stores; only the
+// partial first/last chunks of unaligned packets go byte-wise, in one 16-lane pass per tile.
+// Tiles whose images exceed the LDS budget run the same policy code on HBM directly ("direct").
 #pragma once
 #include "mq_device.h"
 
 namespace mq {
 
-constexpr uint32_t kSlotBytes = 32;
-constexpr uint32_t kTableOff = kLdsBytes - kPktsPerTile * kSlotBytes;  // 9984
-constexpr uint32_t kDataBudget = kTableOff - kSlack;                   // 9920 bytes of packets
-constexpr uint64_t kMaxPn = (1ull << 62) - 1;                           // varint::MAX_VARINT
-
-struct SlotEnt {  // one per packet of the tile, in LDS
-  uint32_t slot;      // first 16-B chunk of the packet's image
-  uint32_t nch;       // chunks the packet occupies
-  uint32_t delta_lo;  // (arena chunk index of the packet's first chunk) - slot
-  uint32_t delta_hi;
-  uint32_t off_lo;    // arena byte offset of the packet
-  uint32_t off_hi;
-  uint32_t len;       // packet bytes
-  uint32_t write;     // 1: store the packet back (status OK)
-};
+constexpr uint32_t kDataBudget = kLdsBytes - kSlack;  // bytes of packet images per tile
+constexpr uint64_t kMaxPn = (1ull << 62) - 1;         // varint::MAX_VARINT
 
 // Per-lane view of its octet's packet.
 struct PktCtx {
@@ -80,59 +66,61 @@ __device__ __forceinline__ uint4 load_chunk_guarded(const uint8_t* arena, uint64
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-// chunk g of the image -> packet index p (wave-uniform layout choice)
-struct Layout {
-  const SlotEnt* tab;
-  uint32_t S;      // fixed layout: chunks per packet slot (0 = variable layout)
-  uint32_t magic;  // ceil(2^20 / S): g / S == (g * magic) >> 20 for g < 1024
-  __device__ __forceinline__ int pkt_of(uint32_t g) const {
-    if (S) return (int)((g * magic) >> 20);
-    int j = 0;  // largest j with slot[j] <= g (slots are non-decreasing)
-#pragma unroll
-    for (int step = kPktsPerTile / 2; step >= 1; step >>= 1)
-      if (tab[j + step].slot <= g) j += step;
-    return j;
-  }
+// Per-lane copy of its octet's packet placement (octet-uniform values; the rest is derived so
+// that only these stay live across the policy code).
+struct Placement {
+  uint32_t slot;     // first LDS chunk of the packet's image
+  uint64_t off;      // arena byte offset of the packet
+  uint32_t len;      // packet bytes (0: packet inactive)
+  __device__ __forceinline__ uint64_t base() const { return off & ~15ull; }  // image start
+  __device__ __forceinline__ uint32_t head() const { return (uint32_t)off & 15u; }
+  __device__ __forceinline__ uint32_t nch() const { return len ? (head() + len + 15) >> 4 : 0u; }
 };
 
-// HBM -> LDS staging with LDS-DMA (global_load_lds_dwordx4): the image's `total` 16-B chunks
-// land at LDS byte 16*g; one wave instruction moves 64 consecutive chunks (1 KiB) whose LDS
-// destination is lane-linear, while each lane supplies its own HBM source address, so whole
-// packets are gathered with contiguous HBM reads (tools/ubench/ubench3.hip: 5.5 TB/s vs 2.7 TB/s
-// for one-packet-per-lane strides). issue() returns immediately; complete() waits.
+__device__ __forceinline__ uint32_t lane_u32(uint32_t x, int l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, l);
+}
+__device__ __forceinline__ uint64_t lane_u64(uint64_t x, int l) {
+  return (uint64_t)lane_u32((uint32_t)(x >> 32), l) << 32 | lane_u32((uint32_t)x, l);
+}
+
+// HBM -> LDS staging with LDS-DMA (global_load_lds_dwordx4): per packet, one instruction per 64
+// chunks (1 KiB) whose LDS destination is lane-linear from the packet's slot; the HBM source is
+// the packet's (SGPR) base + 16 * lane, so every instruction is one contiguous 1-KiB read
+// (tools/ubench/ubench3.hip: 5.5 TB/s). A chunk that would read past the arena end is loaded
+// byte-wise instead. issue() returns immediately; complete() waits.
 struct DmaStager {
   uint8_t* smem;
-  Layout lay;
-  uint32_t total;
   const uint8_t* arena;
   uint64_t arena_len;
-  int lane;
-  uint64_t fix_addr = ~0ull;  // owned chunk that straddles the arena end (loaded byte-wise)
-  uint32_t fix_g = 0;
+  int lane, j;
+  Placement pl;
 
+  __device__ __forceinline__ bool tail_fix() const {  // last chunk reaches past the arena end
+    return pl.len && pl.base() + 16ull * pl.nch() > arena_len;
+  }
   __device__ __forceinline__ void issue() {
 #if MQ_PROF_SKIP & 8
     return;
 #endif
-    const uint32_t nk = (total + kWave - 1) / kWave;
-    for (uint32_t k = 0; k < nk; ++k) {
-      const uint32_t g = k * kWave + lane;
-      if (g < total) {
-        const SlotEnt& e = lay.tab[lay.pkt_of(g)];
-        const uint64_t addr = (((uint64_t)e.delta_hi << 32 | e.delta_lo) + g) << 4;
-        uint64_t src = addr;
-        if (addr + 16 > arena_len) {  // tail of the arena (or an unowned pad chunk beyond it)
-          if (g - e.slot < e.nch) { fix_addr = addr; fix_g = g; }
-          src = 0;
-        }
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(arena + src),
-                                         (__attribute__((address_space(3))) void*)(smem + k * 1024u), 16, 0, 0);
-      }
+    const uint32_t ndma = pl.nch() - (tail_fix() ? 1u : 0u);
+#pragma unroll
+    for (int q = 0; q < kPktsPerTile; ++q) {
+      const uint32_t n = lane_u32(ndma, kLanesPerPkt * q);
+      if (n == 0) continue;
+      const uint8_t* src = arena + lane_u64(pl.base(), kLanesPerPkt * q);
+      uint8_t* dst = smem + 16u * lane_u32(pl.slot, kLanesPerPkt * q);
+      for (uint32_t k = 0; k < n; k += kWave)
+        if (k + lane < n)
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 16u * (k + lane)),
+                                           (__attribute__((address_space(3))) void*)(dst + 16u * k), 16, 0, 0);
     }
   }
   __device__ __forceinline__ void complete() {
     wave_sync();  // workgroup-scope fence: s_waitcnt vmcnt(0) covers the LDS-DMA writes
-    if (fix_addr != ~0ull) *(uint4*)(smem + 16 * fix_g) = load_chunk_guarded(arena, fix_addr, arena_len);
+    if (j == 0 && tail_fix())
+      *(uint4*)(smem + 16u * (pl.slot + pl.nch() - 1)) =
+          load_chunk_guarded(arena, pl.base() + 16ull * (pl.nch() - 1), arena_len);
     wave_sync();
   }
 };
@@ -143,37 +131,48 @@ struct NoStager {
   __device__ __forceinline__ void complete() { wave_sync(); }
 };
 
-// LDS -> HBM for packets with write=1; chunks at packet edges are written byte-wise so bytes
-// of neighbouring packets (other tiles) are never touched.
-__device__ __forceinline__ void stage_out(const uint8_t* smem, const Layout& lay, uint32_t total,
-                                          uint8_t* arena, int lane) {
+// LDS -> HBM for packets with write=1: whole chunks with 16-B stores, then the partial edge
+// chunks of unaligned packets byte-wise (lane 2q: packet q's first chunk, lane 2q+1: its last),
+// so bytes of neighbouring packets (other tiles) are never touched.
+__device__ __forceinline__ void stage_out(const uint8_t* smem, uint8_t* arena, int lane, bool write,
+                                          const Placement& pl) {
 #if MQ_PROF_SKIP & 4
   return;
 #endif
-  for (uint32_t g0 = 0; g0 < total; g0 += 4 * kWave) {
-    uint4 v[4];
-    int jj[4];
+  const uint32_t nw = write ? pl.nch() : 0u, head = pl.head();
+  const uint32_t tail = (head + pl.len) & 15;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const uint32_t g = g0 + u * kWave + lane;
-      jj[u] = g < total ? lay.pkt_of(g) : 0;
-      if (g < total) v[u] = *(const uint4*)(smem + 16 * g);
+  for (int q = 0; q < kPktsPerTile; ++q) {
+    const int l = kLanesPerPkt * q;
+    const uint32_t n = lane_u32(nw, l);
+    if (n == 0) continue;
+    uint8_t* dst = arena + lane_u64(pl.base(), l);
+    const uint8_t* src = smem + 16u * lane_u32(pl.slot, l);
+    const uint32_t c0 = lane_u32(head, l) ? 1u : 0u, c1 = n - (lane_u32(tail, l) ? 1u : 0u);
+    for (uint32_t k = 0; k < n; k += kWave) {
+      const uint32_t c = k + lane;
+      if (c >= c0 && c < c1) *(uint4*)(dst + 16u * c) = *(const uint4*)(src + 16u * c);
     }
+  }
+  // edge pass
+  const int q = (lane >> 1) & (kPktsPerTile - 1), e = lane & 1, l = kLanesPerPkt * q;
+  const uint32_t n = (uint32_t)__shfl((int)nw, l, kWave);
+  const uint32_t h = (uint32_t)__shfl((int)head, l, kWave), t = (uint32_t)__shfl((int)tail, l, kWave);
+  uint32_t c = 0, lo = 0, hi = 0;
+  if (e == 0 && h) { c = 0; lo = h; hi = (n == 1 && t) ? t : 16u; }
+  if (e == 1 && t && (n > 1 || !h)) { c = n - 1; lo = 0; hi = t; }
+  const bool edge = lane < 2 * kPktsPerTile && n && hi > lo;
+  if (wave_any(edge)) {
+    const uint32_t slot = (uint32_t)__shfl((int)pl.slot, l, kWave);
+    const uint64_t base = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(pl.off >> 32), l, kWave) << 32 |
+                           (uint32_t)__shfl((int)(uint32_t)pl.off, l, kWave)) & ~15ull;
+    if (edge) {
+      const uint4 v = *(const uint4*)(smem + 16u * (slot + c));
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      uint8_t* dst = arena + base + 16ull * c;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const uint32_t g = g0 + u * kWave + lane;
-      if (g >= total) continue;
-      const SlotEnt& e = lay.tab[jj[u]];
-      if (!e.write) continue;
-      const uint64_t addr = (((uint64_t)e.delta_hi << 32 | e.delta_lo) + g) << 4;
-      const uint64_t off = (uint64_t)e.off_hi << 32 | e.off_lo, end = off + e.len;
-      const uint64_t lo = off > addr ? off : addr, hi = end < addr + 16 ? end : addr + 16;
-      if (lo == addr && hi == addr + 16) {
-        *(uint4*)(arena + addr) = v[u];
-      } else {
-        const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-        for (uint64_t a = lo; a < hi; ++a) arena[a] = (uint8_t)(w[(a - addr) >> 2] >> (8 * ((a - addr) & 3)));
-      }
+      for (uint32_t b = 0; b < 16; ++b)
+        if (b >= lo && b < hi) dst[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
     }
   }
 }
@@ -242,38 +241,26 @@ __device__ __forceinline__ void run_tile(uint8_t* smem, uint32_t tile_id, const 
   c.pn = c.d.pn;
   const KeyRow* row = kt + (c.act ? c.d.key_id : 0u);
   const uint64_t off = c.act ? c.d.offset : 0;
-  // chunks of the packet's image, clamped so sums cannot overflow; a clamped (huge) packet always
+  // chunks of the packet image, clamped so sums cannot overflow; a clamped (huge) packet always
   // exceeds the budget and sends the tile down the direct path
-  const uint64_t nch64 = c.act ? ((off + c.d.len + 15) >> 4) - (off >> 4) : 0u;
+  Placement pl;
+  pl.off = off;
+  pl.len = c.act ? c.d.len : 0u;
+  const uint64_t nch64 = c.act ? ((off & 15) + (uint64_t)c.d.len + 15) >> 4 : 0u;
   const uint32_t nch = (uint32_t)(nch64 < 0xFFFFu ? nch64 : 0xFFFFu);
-  const uint32_t S = wave_max_u32(nch);
-  const uint32_t mine = (j == 0) ? nch : 0u;
-  const uint32_t incl = wave_incl_scan(mine, lane);
-  const uint32_t sum = (uint32_t)__shfl((int)incl, kWave - 1, kWave);
-  const bool fixed = S * 16u * kPktsPerTile <= kDataBudget;
-  const uint32_t total = fixed ? S * kPktsPerTile : sum;
-  if (fixed || total * 16u <= kDataBudget) {
-    SlotEnt* tab = (SlotEnt*)(smem + kTableOff);
-    const uint32_t slot = fixed ? S * (uint32_t)p : oct_bcast0(incl - mine);
-    if (j == 0) {
-      const uint64_t delta = (off >> 4) - slot;
-      tab[p].slot = slot; tab[p].nch = nch; tab[p].delta_lo = (uint32_t)delta;
-      tab[p].delta_hi = (uint32_t)(delta >> 32); tab[p].off_lo = (uint32_t)off;
-      tab[p].off_hi = (uint32_t)(off >> 32); tab[p].len = c.act ? c.d.len : 0u; tab[p].write = 0;
-    }
-    wave_sync();
-    const Layout lay{tab, fixed ? S : 0u, fixed && S ? ((1u << 20) + S - 1) / S : 0u};
-    DmaStager stg{smem, lay, total, arena, arena_len, lane};
+  const uint32_t incl = oct_incl_scan(nch);
+  const uint32_t total = lane_u32(incl, kWave - 1);
+  if (total * 16u <= kDataBudget) {
+    pl.slot = incl - nch;
+    DmaStager stg{smem, arena, arena_len, lane, j, pl};
     LdsSpace sp{smem};
     MQ_STAMP(tile_id, 1);
-    const uint32_t pkt = slot * 16u + (uint32_t)(off & 15);
+    const uint32_t pkt = pl.slot * 16u + pl.head();
     if (OPEN) Policy::template open<LdsSpace>(sp, pkt, c, row, j, false, stg);
     else Policy::template seal<LdsSpace>(sp, pkt, c, row, j, stg);
     MQ_STAMP(tile_id, 6);
     wave_sync();
-    if (j == 0) tab[p].write = c.act ? 1u : 0u;
-    wave_sync();
-    stage_out(smem, lay, total, arena, lane);
+    stage_out(smem, arena, lane, c.act, pl);
     MQ_STAMP(tile_id, 7);
   } else {
     GlobalSpace sp{arena, arena_len};
