@@ -8,8 +8,8 @@ one rank per GPU) every rank protects its own 2^20-packet shard (config D; packe
 independent, so there is no data-path collective: scaling "weak").
 
   value  = sum over ranks of wire bytes x 2 / (t_seal + t_open) / 2^30   [GiB/s]
-  roofline.achieved = algorithmic bytes of one launch (2 x L per packet: read + write) / the
-                      average duration of the dominant kernel, from events on the launch stream
+  roofline.achieved = algorithmic bytes of one seal launch (2 x L per packet: read + write) /
+                      its average duration, from HIP events on the launch stream
   cpu_baseline = the C oracle (oracle/, "port") on a bounded sample, host threads stated
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config b|c|e] [--packets P]
 """
@@ -35,7 +35,9 @@ def parse():
     ap.add_argument("--config", default="b", choices=["b", "c", "e"])
     ap.add_argument("--packets", type=int, default=1 << 20, help="packets per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=1 << 17, help="packets in the CPU baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=1 << 16, help="packets in the CPU baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="minimum timed CPU baseline work")
+    ap.add_argument("--e2e", action="store_true", help="also measure the host-resident (H2D+D2H) rate")
     return ap.parse_args()
 
 
@@ -49,8 +51,9 @@ def build_workload(cfg, n, rank):
     return workload.config_e(n, seed=seed)
 
 
-def cpu_baseline(w, sample, threads):
-    """Time the CPU oracle (seal + open) on the first `sample` packets of the same workload."""
+def cpu_baseline(w, sample, threads, min_seconds=10.0):
+    """Time the CPU oracle (seal + open) on the first `sample` packets of the same workload,
+    repeated until at least `min_seconds` of CPU work have been timed (bounded sample)."""
     from oracle import oracle
     oracle.load()
     n = min(sample, w.n)
@@ -58,27 +61,84 @@ def cpu_baseline(w, sample, threads):
     arena = w.arena[:end].copy()
     sd, od = w.seal_desc[:n].copy(), w.open_desc[:n].copy()
     oracle.batch_seal(w.keys, arena.copy(), sd[: min(n, 256)].copy(), w.suite_hint, threads)  # warm
-    t0 = time.perf_counter()
-    st = oracle.batch_seal(w.keys, arena, sd, w.suite_hint, threads)
-    t1 = time.perf_counter()
-    st2, _ = oracle.batch_open(w.keys, arena, od, w.suite_hint, threads)
-    t2 = time.perf_counter()
-    assert (st == 0).all() and (st2 == 0).all(), "CPU oracle failed on its sample"
+    reps, t_seal, t_open = 0, 0.0, 0.0
+    while t_seal + t_open < min_seconds:
+        t0 = time.perf_counter()
+        st = oracle.batch_seal(w.keys, arena, sd, w.suite_hint, threads)
+        t1 = time.perf_counter()
+        st2, _ = oracle.batch_open(w.keys, arena, od, w.suite_hint, threads)
+        t2 = time.perf_counter()
+        assert (st == 0).all() and (st2 == 0).all(), "CPU oracle failed on its sample"
+        reps, t_seal, t_open = reps + 1, t_seal + (t1 - t0), t_open + (t2 - t1)
     wire = int(sd["len"].astype(np.int64).sum())
-    gibs = wire * 2 / (t2 - t0) / 2 ** 30
+    gibs = wire * 2 * reps / (t_seal + t_open) / 2 ** 30
     return {"value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": f"{n} packets ({wire / 1e6:.1f} MB) of the same workload, seal {t1 - t0:.2f}s + "
-                      f"open {t2 - t1:.2f}s, oracle/mq_oracle.c with {threads} host threads"}
+            "sample": f"{n} packets ({wire / 1e6:.1f} MB) of the same workload, seal+open repeated {reps}x "
+                      f"(seal {t_seal:.1f}s + open {t_open:.1f}s), oracle/mq_oracle.c on {threads} host threads"}
+
+
+def end_to_end(torch, batch, kt, w, sd, od, dev, chunks=8, reps=3):
+    """Host-resident rate (the path starts and ends in a socket buffer): pinned host arena ->
+    H2D -> seal -> D2H, then H2D -> open -> D2H, pipelined over `chunks` descriptor ranges on
+    two streams so copies overlap kernels. Returns GiB/s of wire bytes per direction."""
+    n = w.n
+    host = torch.from_numpy(w.arena).pin_memory()
+    back = torch.empty_like(host).pin_memory()
+    arena = torch.empty(host.numel(), dtype=torch.uint8, device=dev)
+    st = torch.zeros(n, dtype=torch.uint8, device=dev)
+    pn = torch.zeros(n, dtype=torch.int64, device=dev)
+    per = (n + chunks - 1) // chunks
+    wsl = [torch.empty(max(batch.workspace_bytes(per), 256), dtype=torch.uint8, device=dev) for _ in range(2)]
+    offs = w.seal_desc["offset"].astype(np.int64)
+    ends = offs + w.seal_desc["len"].astype(np.int64)
+    bounds = [(n * k) // chunks for k in range(chunks + 1)]
+    streams = [torch.cuda.Stream(device=dev) for _ in range(2)]
+
+    def one_pass(desc, open_):
+        for k in range(chunks):
+            lo, hi = bounds[k], bounds[k + 1]
+            if hi == lo:
+                continue
+            a, b = int(offs[lo:hi].min()), int(ends[lo:hi].max())
+            s = streams[k % 2]
+            with torch.cuda.stream(s):
+                arena[a:b].copy_(host[a:b], non_blocking=True)
+                if open_:
+                    batch.open_(kt, arena, desc[32 * lo:32 * hi], st[lo:hi], pn[lo:hi], w.suite_hint,
+                                wsl[k % 2], s.cuda_stream)
+                else:
+                    batch.seal(kt, arena, desc[32 * lo:32 * hi], st[lo:hi], w.suite_hint, wsl[k % 2],
+                               s.cuda_stream)
+                back[a:b].copy_(arena[a:b], non_blocking=True)
+        torch.cuda.synchronize()
+
+    res = {}
+    for name, desc, open_ in (("seal", sd, False), ("open", od, True)):
+        one_pass(desc, open_)  # warm
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            one_pass(desc, open_)
+        dt = (time.perf_counter() - t0) / reps
+        res[name] = round(w.wire_bytes / dt / 2 ** 30, 2)
+        if not open_:
+            host.copy_(back)  # the open pass starts from the sealed bytes
+    return {"unit": "GiB/s of wire bytes, host-resident (pinned) in and out", "chunks": chunks,
+            "seal": res["seal"], "open": res["open"]}
+
+
+KERNELS = {"b": "mq_chacha_seal_kernel", "c": "mq_aes_seal_kernel", "e": None}
 
 
 def load_traffic(cfg):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic_<cfg>.json, written by tools/pmc_summary.py: FETCH_SIZE x 2 + WRITE_SIZE)."""
+    kern = KERNELS.get(cfg)
+    path = os.path.join(ROOT, "profiles", f"pmc_traffic_{cfg}.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get(cfg)
-    except (OSError, ValueError):
+        return int(d["kernels"][kern]["hbm_bytes_per_launch"]) if kern else None
+    except (OSError, ValueError, KeyError, TypeError):
         return None
 
 
@@ -147,30 +207,25 @@ def main():
     open_ms = float(np.mean([ev[3 * i + 1].elapsed_time(ev[3 * i + 2]) for i in range(args.steps)]))
 
     wire = w.wire_bytes
-    t = torch.tensor([elapsed, float(fails), float(wire)], dtype=torch.float64, device=dev)
-    if world > 1:
-        tmax = t[:1].clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tsum = t[1:].clone()
-        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
-        elapsed, fails, total_wire = float(tmax[0]), int(tsum[0]), float(tsum[1])
-    else:
-        total_wire = float(wire)
+    from milli_quic_amd.shard import reduce_totals
+    tot = reduce_totals(elapsed, wire, fails, dist if world > 1 else None, dev)
+    elapsed, fails, total_wire = tot.elapsed, tot.failures, float(tot.wire_bytes)
     ms_per_step = elapsed / args.steps * 1e3
     value = total_wire * 2 / (elapsed / args.steps) / 2 ** 30
 
     if rank == 0:
-        dom_ms = max(seal_ms, open_ms)
+        # roofline kernel: seal — for configs b/c a single launch (mq_chacha_seal_kernel /
+        # mq_aes_seal_kernel) timed by events on its stream; open = pre-pass + packet kernel
         algo_bytes = 2.0 * wire  # per launch: read + write of every wire byte
-        achieved = algo_bytes / (dom_ms * 1e-3) / 1e9
+        achieved = algo_bytes / (seal_ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config),
-                "kernel": "open" if open_ms >= seal_ms else "seal",
+                "kernel": KERNELS[args.config] or "seal batch (partition + AES + ChaCha kernels)",
                 "seal_ms": round(seal_ms, 4), "open_ms": round(open_ms, 4),
                 "algorithmic_bytes_per_launch": int(algo_bytes)}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(w, args.cpu_sample, min(16, os.cpu_count() or 1))
+            cpu = cpu_baseline(w, args.cpu_sample, min(16, os.cpu_count() or 1), args.cpu_seconds)
         names = {"b": "configs[1]: 1M x 1200B ChaCha20-Poly1305 seal+open, 1-RTT short header",
                  "c": "configs[2]: 1M x 1200B AES-128-GCM seal+open + header protection",
                  "e": "configs[4]: mixed 64-1350B batch, Initial + 1-RTT, ChaCha20/AES-GCM interleaved"}
@@ -184,6 +239,8 @@ def main():
                        "seal_failures_or_open_failures": fails},
             "roofline": roof, "cpu_baseline": cpu,
         }
+        if args.e2e and world == 1:
+            out["end_to_end"] = end_to_end(torch, batch, kt, w, sd, od, dev)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -13,7 +13,8 @@
  * plus a device-resident BATCH API (mq_batch_*), which the reference lacks: it runs the send
  * composite of src/connection/transmit.rs:499-755 (seal + header protection) and the receive
  * composite of src/connection/recv.rs:340-421,953-1025 (header-protection removal, decode_pn,
- * open) over a whole arena of packets in HBM, one packet per GPU lane, ordered on a HIP stream.
+ * open) over a whole arena of packets in HBM (8 packets per wave, 8 lanes per packet), ordered
+ * on a HIP stream.
  *
  * All entry points take plain pointers and sizes. Every compute path runs on the GPU (gfx950);
  * there is no CPU fallback: without a usable device the calls return MQ_ERR_NO_DEVICE.
