@@ -51,7 +51,7 @@ int g_dev = 0;
 int ensure_device() {
   std::lock_guard<std::mutex> lk(g_dev_mu);
   if (g_dev_state == 1) {
-    hipSetDevice(g_dev);
+    (void)hipSetDevice(g_dev);
     return MQ_OK;
   }
   if (g_dev_state == -1) return MQ_ERR_NO_DEVICE;
@@ -287,8 +287,8 @@ struct Scratch {
     const size_t need = kHdr + ((pkt_bytes + 255) & ~(size_t)255) + 256;
     if (!stream && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return MQ_ERR_HIP;
     if (need <= cap) return MQ_OK;
-    if (dev) hipFree(dev);
-    if (host) hipHostFree(host);
+    if (dev) (void)hipFree(dev);
+    if (host) (void)hipHostFree(host);
     dev = nullptr; host = nullptr; cap = 0;
     if (hipMalloc(&dev, need) != hipSuccess) return MQ_ERR_HIP;
     if (hipHostMalloc(&host, need, hipHostMallocDefault) != hipSuccess) return MQ_ERR_HIP;
@@ -296,9 +296,9 @@ struct Scratch {
     return MQ_OK;
   }
   ~Scratch() {
-    if (dev) hipFree(dev);
-    if (host) hipHostFree(host);
-    if (stream) hipStreamDestroy(stream);
+    if (dev) (void)hipFree(dev);
+    if (host) (void)hipHostFree(host);
+    if (stream) (void)hipStreamDestroy(stream);
   }
 };
 
@@ -613,7 +613,7 @@ uint32_t mq_keytable_rows(const mq_keytable* kt) { return kt ? kt->rows : 0; }
 
 void mq_keytable_free(mq_keytable* kt) {
   if (!kt) return;
-  if (kt->dev) hipFree(kt->dev);
+  if (kt->dev) (void)hipFree(kt->dev);
   delete kt;
 }
 
@@ -690,23 +690,23 @@ int mq_batch_time_seal_open(const mq_keytable* kt, uint8_t* arena, uint64_t aren
   std::vector<hipEvent_t> ev(2 * iters + 1);
   for (auto& x : ev)
     if (hipEventCreate(&x) != hipSuccess) return MQ_ERR_HIP;
-  hipEventRecord(ev[0], s);
+  (void)hipEventRecord(ev[0], s);
   for (int i = 0; i < iters && rc == MQ_OK; ++i) {
     rc = mq_batch_seal(kt, arena, arena_len, desc, n, status, suite_hint, workspace, stream);
-    hipEventRecord(ev[2 * i + 1], s);
+    (void)hipEventRecord(ev[2 * i + 1], s);
     if (rc == MQ_OK) rc = mq_batch_open(kt, arena, arena_len, desc, n, status, pn_out, suite_hint, workspace, stream);
-    hipEventRecord(ev[2 * i + 2], s);
+    (void)hipEventRecord(ev[2 * i + 2], s);
   }
-  hipEventSynchronize(ev[2 * iters]);
+  (void)hipEventSynchronize(ev[2 * iters]);
   double ts = 0, to = 0;
   for (int i = 0; i < iters; ++i) {
     float a = 0, b = 0;
-    hipEventElapsedTime(&a, ev[2 * i], ev[2 * i + 1]);
-    hipEventElapsedTime(&b, ev[2 * i + 1], ev[2 * i + 2]);
+    (void)hipEventElapsedTime(&a, ev[2 * i], ev[2 * i + 1]);
+    (void)hipEventElapsedTime(&b, ev[2 * i + 1], ev[2 * i + 2]);
     ts += a;
     to += b;
   }
-  for (auto& x : ev) hipEventDestroy(x);
+  for (auto& x : ev) (void)hipEventDestroy(x);
   *seal_ms = (float)(ts / iters);
   *open_ms = (float)(to / iters);
   return rc;
