@@ -22,37 +22,41 @@ namespace mq {
 template <class S>
 __device__ __forceinline__ void poly_tag(const S& sp, typename S::off_t pkt, typename S::off_t pay,
                                          uint32_t aad_len, uint32_t ct_len,
-                                         const uint32_t (&otk)[8], int j, bool act,
+                                         const uint32_t* otk_lds, int j, bool act,
                                          uint32_t (&tag)[4]) {
 #if MQ_PROF_SKIP & 2
-  for (int w = 0; w < 4; ++w) tag[w] = otk[4 + w] ^ aad_len ^ ct_len;
+  for (int w = 0; w < 4; ++w) tag[w] = otk_lds[4 + w] ^ aad_len ^ ct_len;
   return;
 #endif
-  const P26 r = p26_from_words(otk[0] & 0x0fffffffu, otk[1] & 0x0ffffffcu, otk[2] & 0x0ffffffcu,
-                               otk[3] & 0x0ffffffcu, 0);
-  const P26m m1 = p26_mult(r);
-  P26 r2 = r;
-  p26_mul(r2, m1);
-  const P26m m2 = p26_mult(r2);
-  P26 r4 = r2;
-  p26_mul(r4, m2);
-  const P26m m4p = p26_mult(r4);
-  P26 r8 = r4;
-  p26_mul(r8, m4p);
-  // r^(8-j) from the bits of e = 8 - j (e = 8 -> r^8)
-  const uint32_t e = 8u - (uint32_t)j;
-  P26 rj;
+  const uint4 rk = *(const uint4*)otk_lds;  // one-time key r || s, written by octet lane 0
+  const P26 r = p26_from_words(rk.x & 0x0fffffffu, rk.y & 0x0ffffffcu, rk.z & 0x0ffffffcu,
+                               rk.w & 0x0ffffffcu, 0);
+  // powers by an octet prefix: v = r^(j+1) after three multiplies (r^2, then x r^2 on lanes with
+  // bit 1 of j, then x r^4 — taken from octet lane 3 — on lanes with bit 2); r^8 is octet lane 7's
+  // v, and the final multiplier r^(8-j) is lane 7-j's v (DPP row_half_mirror)
+  P26 v = r, t = r;
+  p26_mul(t, p26_mult(r));  // r^2
 #pragma unroll
-  for (int l = 0; l < 5; ++l) rj.l[l] = (e & 1) ? r.l[l] : (l == 0 ? 1u : 0u);
+  for (int l = 0; l < 5; ++l) v.l[l] = (j & 1) ? t.l[l] : v.l[l];
   {
-    P26 t = rj;
-    p26_mul(t, m2);
+    P26 u = v;
+    p26_mul(u, p26_mult(t));
 #pragma unroll
-    for (int l = 0; l < 5; ++l) rj.l[l] = (e & 2) ? t.l[l] : rj.l[l];
-    t = rj;
-    p26_mul(t, m4p);
+    for (int l = 0; l < 5; ++l) v.l[l] = (j & 2) ? u.l[l] : v.l[l];
+  }
+  {
+    P26 r4, u = v;
 #pragma unroll
-    for (int l = 0; l < 5; ++l) rj.l[l] = (e & 4) ? t.l[l] : (e == 8 ? r8.l[l] : rj.l[l]);
+    for (int l = 0; l < 5; ++l) r4.l[l] = oct_lane3(v.l[l]);
+    p26_mul(u, p26_mult(r4));
+#pragma unroll
+    for (int l = 0; l < 5; ++l) v.l[l] = (j & 4) ? u.l[l] : v.l[l];
+  }
+  P26 r8, rj;
+#pragma unroll
+  for (int l = 0; l < 5; ++l) {
+    r8.l[l] = oct_lane7(v.l[l]);
+    rj.l[l] = half_mirror(v.l[l]);
   }
   const P26m m8 = p26_mult(r8), mlast = p26_mult(rj);
 
@@ -65,38 +69,38 @@ __device__ __forceinline__ void poly_tag(const S& sp, typename S::off_t pkt, typ
 #pragma unroll
   for (int l = 0; l < 5; ++l) acc.l[l] = 0;
 
-  // MAC block k of this lane: where it lives and how many of its bytes are real
-  struct Blk { typename S::off_t src; int rem; uint32_t hib; bool lens; };
-  auto where = [&](uint32_t k) {
-    const int i = (int)(kLanesPerPkt * k) + j - z;
-    Blk b{pkt, 0, 0u, false};
-    if (act && i >= 0) {
-      b.hib = 1;
-      if ((uint32_t)i < A) {
-        b.src = pkt + 16 * (uint32_t)i; b.rem = (int)aad_len - 16 * i;
-      } else if ((uint32_t)i < A + T) {
-        b.src = pay + 16 * ((uint32_t)i - A); b.rem = (int)ct_len - 16 * (i - (int)A);
-      } else {
-        b.lens = true;
-      }
-    }
+  // MAC block i = 8k + j - z of this lane: where it lives, how many of its bytes are real
+  struct Blk { typename S::off_t src; int rem; bool pre, lens; };
+  auto where = [&](int i) {
+    Blk b;
+    const bool aad = i < (int)A;
+    b.pre = i < 0;  // prepended zero block
+    b.lens = i == (int)(A + T);
+    b.src = aad ? pkt + 16 * (uint32_t)max(i, 0) : pay + 16 * (uint32_t)(i - (int)A);
+    b.rem = aad ? (int)aad_len - 16 * i : (int)ct_len - 16 * (i - (int)A);
+    if (b.pre || b.lens) b.src = pkt;
     return b;
   };
   auto absorb = [&](const Blk& b, uint32_t (&m)[4]) {
+    // wave-uniform fast path: every active lane holds a whole AAD / ciphertext block
+    if (wave_any(act && (b.pre || b.lens || b.rem < 16))) {
 #pragma unroll
-    for (int w = 0; w < 4; ++w) m[w] &= byte_mask(b.rem, w);
-    if (b.lens) { m[0] = aad_len; m[1] = 0; m[2] = ct_len; m[3] = 0; }
-    const P26 x = p26_from_words(m[0], m[1], m[2], m[3], b.hib);
+      for (int w = 0; w < 4; ++w) m[w] &= byte_mask(b.pre ? 0 : b.rem, w);
+      if (b.lens) { m[0] = aad_len; m[1] = 0; m[2] = ct_len; m[3] = 0; }
+    }
+    const P26 x = p26_from_words(m[0], m[1], m[2], m[3], b.pre ? 0u : 1u);
 #pragma unroll
     for (int l = 0; l < 5; ++l) acc.l[l] += x.l[l];
   };
   if (Kmax > 0) {
-    Blk b = where(0);
+    int i = j - z;
+    Blk b = where(i);
     uint32_t m[4];
     load_words<4>(sp, b.src, m);
     for (uint32_t k = 0; k + 1 < Kmax; ++k) {
       absorb(b, m);
-      b = where(k + 1);
+      i += kLanesPerPkt;
+      b = where(i);
       load_words<4>(sp, b.src, m);  // next block's LDS reads overlap this multiply
       p26_mul(acc, m8);
     }
@@ -105,7 +109,8 @@ __device__ __forceinline__ void poly_tag(const S& sp, typename S::off_t pkt, typ
   }
 #pragma unroll
   for (int l = 0; l < 5; ++l) acc.l[l] = oct_sum(acc.l[l]);
-  const uint32_t s[4] = {otk[4], otk[5], otk[6], otk[7]};
+  const uint4 sk = *(const uint4*)(otk_lds + 4);
+  const uint32_t s[4] = {sk.x, sk.y, sk.z, sk.w};
   p26_finish(acc, s, tag);
 }
 
@@ -141,6 +146,11 @@ struct ChaChaPolicy {
     xor_words<16>(sp, pay + o, ks, (int)min(64u, P - o), raw);
   }
 
+  static __device__ __forceinline__ void store_otk(uint32_t* otk, const uint32_t (&ks)[16]) {
+    *(uint4*)otk = make_uint4(ks[0], ks[1], ks[2], ks[3]);
+    *(uint4*)(otk + 4) = make_uint4(ks[4], ks[5], ks[6], ks[7]);
+  }
+
   // ChaChaHeaderProtection::mask (rustcrypto.rs:197-220): block(hp, ctr = sample[0..4] LE,
   // nonce = sample[4..16]); the mask is keystream bytes 0..4.
   template <class S>
@@ -162,17 +172,16 @@ struct ChaChaPolicy {
   template <class S, class G>
   static __device__ void seal(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j, G& stg) {
     const mq_pkt_desc& d = c.d;
-    uint32_t key[8], hk[8];
+    uint32_t key[8];
     load_key8(row->key, key);
-    load_key8(row->hp, hk);
     const uint32_t aad_len = c.act ? (uint32_t)d.pn_offset + d.pn_len : 0u;
     const uint32_t P = c.act ? d.len - aad_len - 16 : 0u;
     const typename S::off_t pay = pkt + aad_len;
     // DirectionalKeys::nonce (src/crypto/mod.rs:66-74): iv ^ (0^32 || BE64(pn))
-    uint32_t n0 = row->iv[0], n1 = row->iv[1] ^ bswap32((uint32_t)(c.pn >> 32)),
-             n2 = row->iv[2] ^ bswap32((uint32_t)c.pn);
+    const uint32_t pn_hi = bswap32((uint32_t)(c.pn >> 32)), pn_lo = bswap32((uint32_t)c.pn);
+    uint32_t n0 = row->iv[0], n1 = row->iv[1] ^ pn_hi, n2 = row->iv[2] ^ pn_lo;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) { pin(key[k]); pin(hk[k]); }
+    for (int k = 0; k < 8; ++k) pin(key[k]);
     pin(n0); pin(n1); pin(n2);
     stg.issue();  // packet bytes stream into LDS while the first keystream block is computed
     const uint32_t nblk = 1 + (P + 63) / 64;  // block 0 = Poly1305 key, 1.. = keystream
@@ -182,7 +191,6 @@ struct ChaChaPolicy {
     if (hp_it == 0) { hp_it = 1; hp_lane = 0; }
     const uint32_t iters = max((nblk + kLanesPerPkt - 1) / kLanesPerPkt, (hp_on && !hp_post) ? hp_it + 1 : 0u);
     const uint32_t Imax = wave_max_u32(c.act ? iters : 0u);
-    uint32_t otk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t m0 = 0, m1 = 0;
     bool have_mask = false;
     for (uint32_t it = 0; it < Imax; ++it) {
@@ -191,36 +199,42 @@ struct ChaChaPolicy {
       const bool is_hp = hp_on && !hp_post && it == hp_it && (uint32_t)j == hp_lane;
       uint32_t w[17];
       if (it > 0) load_block(sp, pay, a ? ctr : 0u, w);  // LDS reads in flight during the block function
-      uint32_t kk[8], cc = ctr, x0 = n0, x1 = n1, x2 = n2;
-      if (it > 0) {
-        uint32_t smp[4];
+      uint32_t cc = ctr;
+      const bool hp_iter = wave_any(is_hp);
+      if (hp_iter) {  // the HP lane runs block(hp_key, sample) in this slot: swap its inputs in place
+        uint32_t smp[4], hk[8];
         load_words<4>(sp, pkt + (c.act ? d.pn_offset + 4u : 0u), smp);
-        if (is_hp) { cc = smp[0]; x0 = smp[1]; x1 = smp[2]; x2 = smp[3]; }
-      }
+        load_key8(row->hp, hk);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) kk[k] = is_hp ? hk[k] : key[k];
+        for (int k = 0; k < 8; ++k) key[k] = is_hp ? hk[k] : key[k];
+        if (is_hp) { cc = smp[0]; n0 = smp[1]; n1 = smp[2]; n2 = smp[3]; }
+      }
       uint32_t ks[16];
-      chacha20_block(kk, cc, x0, x1, x2, ks);
+      chacha20_block(key, cc, n0, n1, n2, ks);
       if (it == 0) {
         stg.complete();
         MQ_STAMP(c.tile, 2);
         load_block(sp, pay, a ? ctr : 0u, w);
       }
       if (a && ctr == 0) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) otk[k] = ks[k];
+        store_otk(c.otk, ks);  // the Poly1305 key waits in LDS until the MAC
       } else if (a) {
         store_block(sp, pay, ctr, P, ks, w);
       }
       if (is_hp) { m0 = ks[0]; m1 = ks[1]; have_mask = true; }
+      if (hp_iter && it + 1 < Imax) {  // restore the HP lane's AEAD inputs
+        uint32_t kr[8];
+        load_key8(row->key, kr);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) key[k] = is_hp ? kr[k] : key[k];
+        if (is_hp) { n0 = row->iv[0]; n1 = row->iv[1] ^ pn_hi; n2 = row->iv[2] ^ pn_lo; }
+      }
       wave_sync();  // this iteration's ciphertext (the HP sample) is visible to the next
     }
     if (Imax == 0) stg.complete();
     MQ_STAMP(c.tile, 3);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) otk[k] = oct_bcast0(otk[k]);
     uint32_t tag[4];
-    poly_tag(sp, pkt, pay, aad_len, P, otk, j, c.act, tag);
+    poly_tag(sp, pkt, pay, aad_len, P, c.otk, j, c.act, tag);
     if (c.act && j == 0) store_words<4>(sp, pay + P, tag);
     wave_sync();
     MQ_STAMP(c.tile, 4);
@@ -287,11 +301,10 @@ struct ChaChaPolicy {
     const uint32_t ctr0 = (uint32_t)j;
     uint32_t ks0[16];
     chacha20_block(key, ctr0, n0, n1, n2, ks0);
-    uint32_t otk[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) otk[k] = oct_bcast0(ks0[k]);
+    if (c.act && j == 0) store_otk(c.otk, ks0);
+    wave_sync();
     uint32_t tag[4], got[4];
-    poly_tag(sp, pkt, pay, aad_len, P, otk, j, c.act, tag);
+    poly_tag(sp, pkt, pay, aad_len, P, c.otk, j, c.act, tag);
     load_words<4>(sp, pay + P, got);
     const uint32_t diff = (tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) | (tag[3] ^ got[3]);
     if (c.act && diff != 0) {  // Error::Crypto, buffer left as received
@@ -326,7 +339,7 @@ struct ChaChaPolicy {
 
 using namespace mq;
 
-extern "C" __global__ __launch_bounds__(64) void mq_chacha_seal_kernel(
+extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void mq_chacha_seal_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
     const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,
     const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status) {
@@ -334,7 +347,7 @@ extern "C" __global__ __launch_bounds__(64) void mq_chacha_seal_kernel(
   run_tile<ChaChaPolicy, false>(smem, blockIdx.x, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr, nullptr);
 }
 
-extern "C" __global__ __launch_bounds__(64) void mq_chacha_open_kernel(
+extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void mq_chacha_open_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
     const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,
     const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,

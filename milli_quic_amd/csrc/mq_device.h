@@ -210,6 +210,12 @@ __device__ __forceinline__ uint32_t half_mirror(uint32_t x) {  // lane i <- lane
 __device__ __forceinline__ uint32_t oct_bcast0(uint32_t x) {
   return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x18);
 }
+__device__ __forceinline__ uint32_t oct_lane3(uint32_t x) {  // lane 3 of the octet
+  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x78);
+}
+__device__ __forceinline__ uint32_t oct_lane7(uint32_t x) {  // lane 7 of the octet
+  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0xF8);
+}
 __device__ __forceinline__ uint32_t oct_sum(uint32_t x) {
   x += quad_swap1(x);
   x += quad_swap2(x);

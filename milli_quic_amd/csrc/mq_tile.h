@@ -13,7 +13,8 @@
 
 namespace mq {
 
-constexpr uint32_t kDataBudget = kLdsBytes - kSlack;  // bytes of packet images per tile
+constexpr uint32_t kScratchBytes = 32 * kPktsPerTile;              // per-packet 32-B scratch (MAC key)
+constexpr uint32_t kDataBudget = kLdsBytes - kScratchBytes - kSlack;  // bytes of packet images
 constexpr uint64_t kMaxPn = (1ull << 62) - 1;         // varint::MAX_VARINT
 
 // Per-lane view of its octet's packet.
@@ -27,6 +28,7 @@ struct PktCtx {
   uint32_t tile;     // tile index (diagnostic stamps)
   bool pre_hp;       // open: header-protection mask precomputed by the pre-pass (wave-uniform)
   uint32_t hm0, hm1; // that mask: bytes 0..3, byte 4
+  uint32_t* otk;     // this packet's 32-B LDS scratch (one-time MAC key / E_K(J0)), in both paths
 };
 
 // decode_pn, reference src/packet/number.rs:52-70 (RFC 9000 A.3)
@@ -230,6 +232,7 @@ __device__ __forceinline__ void run_tile(uint8_t* smem, uint32_t tile_id, const 
     c.d.flags = 0; c.d.reserved = 0;
   }
   c.pre_hp = OPEN && hpm != nullptr;
+  c.otk = (uint32_t*)(smem + kLdsBytes - kScratchBytes + 32u * (uint32_t)p);
   c.hm0 = c.hm1 = 0;
   if (OPEN && hpm && c.valid) {
     const uint2 m = hpm[c.i];
