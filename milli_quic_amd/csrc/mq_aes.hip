@@ -285,7 +285,7 @@ struct AesPolicy {
   // in the first free slot after the blocks holding the sample (b = 1, 2), or in a separate phase
   // when the sample reaches into the tag.
   template <class S, class G>
-  static __device__ void seal(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j, G& stg) {
+  static __device__ __forceinline__ void seal(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j, G& stg) {
     const mq_pkt_desc& d = c.d;
     const uint32_t rb = (threadIdx.x & (kTReplicas - 1)) * 4;
     const uint32_t aad_len = c.act ? (uint32_t)d.pn_offset + d.pn_len : 0u;
@@ -357,7 +357,7 @@ struct AesPolicy {
   }
 
   template <class S, class G>
-  static __device__ void open(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j,
+  static __device__ __forceinline__ void open(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j,
                               bool direct, G& stg) {
     const mq_pkt_desc& d = c.d;
     stg.issue();

@@ -20,7 +20,9 @@ from collections import defaultdict
 
 def load(d):
     acc = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> [per dispatch]
-    for f in sorted(glob.glob(os.path.join(d, "*", "run_counter_collection.csv"))):
+    files = sorted(glob.glob(os.path.join(d, "*", "run_counter_collection.csv")))
+    files += sorted(glob.glob(os.path.join(d, "run_counter_collection.csv")))
+    for f in files:
         with open(f) as fh:
             per = defaultdict(float)  # (dispatch, kernel, counter) -> sum
             for r in csv.DictReader(fh):
