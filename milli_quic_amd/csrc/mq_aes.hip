@@ -438,30 +438,34 @@ struct AesPolicy {
 
 using namespace mq;
 
-extern "C" __global__ __launch_bounds__(64 * kAesWaves) void mq_aes_seal_kernel(
-    const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
-    const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,
-    const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  build_t0(threadIdx.x, blockDim.x);
-  __syncthreads();
-  const uint32_t w = threadIdx.x >> 6;
-  run_tile<AesPolicy, false>(smem + w * kLdsBytes, blockIdx.x * kAesWaves + w, kt, n_rows, arena, arena_len,
-                             desc, n, index, n_dev, status, nullptr, nullptr);
-}
-
-extern "C" __global__ __launch_bounds__(64 * kAesWaves) void mq_aes_open_kernel(
-    const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
-    const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,
-    const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,
-    const uint2* __restrict__ hpm) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  build_t0(threadIdx.x, blockDim.x);
-  __syncthreads();
-  const uint32_t w = threadIdx.x >> 6;
-  run_tile<AesPolicy, true>(smem + w * kLdsBytes, blockIdx.x * kAesWaves + w, kt, n_rows, arena, arena_len,
-                            desc, n, index, n_dev, status, pn_out, hpm);
-}
+// Tile kernels: kAesWaves waves per workgroup share the T-table; one tile per wave. The "1"
+// variants run when the key table has a single row (round keys and H powers in SGPRs).
+#define MQ_AES_KERNELS(NAME_SEAL, NAME_OPEN, SINGLE)                                                      \
+  extern "C" __global__ __launch_bounds__(64 * kAesWaves) void NAME_SEAL(                                 \
+      const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
+      const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
+      const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status) {                                 \
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];                                        \
+    build_t0(threadIdx.x, blockDim.x);                                                                    \
+    __syncthreads();                                                                                      \
+    const uint32_t w = threadIdx.x >> 6;                                                                  \
+    run_tile<AesPolicy, false, SINGLE>(smem + w * kLdsBytes, blockIdx.x * kAesWaves + w, kt, n_rows, arena, \
+                                       arena_len, desc, n, index, n_dev, status, nullptr, nullptr);       \
+  }                                                                                                       \
+  extern "C" __global__ __launch_bounds__(64 * kAesWaves) void NAME_OPEN(                                 \
+      const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
+      const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
+      const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,    \
+      const uint2* __restrict__ hpm) {                                                                    \
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];                                        \
+    build_t0(threadIdx.x, blockDim.x);                                                                    \
+    __syncthreads();                                                                                      \
+    const uint32_t w = threadIdx.x >> 6;                                                                  \
+    run_tile<AesPolicy, true, SINGLE>(smem + w * kLdsBytes, blockIdx.x * kAesWaves + w, kt, n_rows, arena, \
+                                      arena_len, desc, n, index, n_dev, status, pn_out, hpm);             \
+  }
+MQ_AES_KERNELS(mq_aes_seal_kernel, mq_aes_open_kernel, false)
+MQ_AES_KERNELS(mq_aes_seal1_kernel, mq_aes_open1_kernel, true)
 
 extern "C" __global__ __launch_bounds__(256) void mq_aes_hp_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, const uint32_t* __restrict__ key_ids,
@@ -511,11 +515,12 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
     if (e != hipSuccess) return e;
   }
   if (open)
-    hipLaunchKernelGGL(mq_aes_open_kernel, dim3(blocks), dim3(64 * kAesWaves), kLdsBytes * kAesWaves, s, kt,
-                       n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm);
+    hipLaunchKernelGGL(n_rows == 1 ? mq_aes_open1_kernel : mq_aes_open_kernel, dim3(blocks), dim3(64 * kAesWaves),
+                       kLdsBytes * kAesWaves, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status,
+                       pn_out, hpm);
   else
-    hipLaunchKernelGGL(mq_aes_seal_kernel, dim3(blocks), dim3(64 * kAesWaves), kLdsBytes * kAesWaves, s, kt,
-                       n_rows, arena, arena_len, desc, n, index, n_dev, status);
+    hipLaunchKernelGGL(n_rows == 1 ? mq_aes_seal1_kernel : mq_aes_seal_kernel, dim3(blocks), dim3(64 * kAesWaves),
+                       kLdsBytes * kAesWaves, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status);
   return hipGetLastError();
 }
 

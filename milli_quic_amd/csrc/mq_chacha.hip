@@ -170,7 +170,7 @@ struct ChaChaPolicy {
   // Poly1305 key); the HP block runs in the first free slot after ctr 1 (whose ciphertext holds
   // the sample) unless the sample reaches into the tag (tiny payloads: a separate phase).
   template <class S, class G>
-  static __device__ void seal(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j, G& stg) {
+  static __device__ __forceinline__ void seal(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j, G& stg) {
     const mq_pkt_desc& d = c.d;
     uint32_t key[8];
     load_key8(row->key, key);
@@ -249,7 +249,7 @@ struct ChaChaPolicy {
 
   // receive composite (recv.rs:340-421 / 953-1025): HP removal, decode_pn, open.
   template <class S, class G>
-  static __device__ void open(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j,
+  static __device__ __forceinline__ void open(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j,
                               bool direct, G& stg) {
     const mq_pkt_desc& d = c.d;
     stg.issue();
@@ -339,24 +339,29 @@ struct ChaChaPolicy {
 
 using namespace mq;
 
-extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void mq_chacha_seal_kernel(
-    const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
-    const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,
-    const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  run_tile<ChaChaPolicy, false>(smem, blockIdx.x, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr, nullptr);
-}
+// Tile kernels: one wave per workgroup, one tile per wave. The "1" variants are launched when the
+// key table has a single row (every valid packet on row 0): key material then lives in SGPRs.
+#define MQ_CHACHA_KERNELS(NAME_SEAL, NAME_OPEN, SINGLE)                                                   \
+  extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void NAME_SEAL(     \
+      const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
+      const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
+      const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status) {                                 \
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];                                        \
+    run_tile<ChaChaPolicy, false, SINGLE>(smem, blockIdx.x, kt, n_rows, arena, arena_len, desc, n, index, \
+                                          n_dev, status, nullptr, nullptr);                               \
+  }                                                                                                       \
+  extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void NAME_OPEN(     \
+      const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
+      const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
+      const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,    \
+      const uint2* __restrict__ hpm) {                                                                    \
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];                                        \
+    run_tile<ChaChaPolicy, true, SINGLE>(smem, blockIdx.x, kt, n_rows, arena, arena_len, desc, n, index,  \
+                                         n_dev, status, pn_out, hpm);                                     \
+  }
+MQ_CHACHA_KERNELS(mq_chacha_seal_kernel, mq_chacha_open_kernel, false)
+MQ_CHACHA_KERNELS(mq_chacha_seal1_kernel, mq_chacha_open1_kernel, true)
 
-extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void mq_chacha_open_kernel(
-    const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
-    const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,
-    const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,
-    const uint2* __restrict__ hpm) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  run_tile<ChaChaPolicy, true>(smem, blockIdx.x, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm);
-}
-
-// Batched HeaderProtection::mask for ChaCha20 rows (one sample per lane).
 extern "C" __global__ __launch_bounds__(256) void mq_chacha_hp_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, const uint32_t* __restrict__ key_ids,
     const uint8_t* __restrict__ samples, uint8_t* __restrict__ masks, uint32_t n) {
@@ -403,11 +408,11 @@ hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_
     if (e != hipSuccess) return e;
   }
   if (open)
-    hipLaunchKernelGGL(mq_chacha_open_kernel, dim3(tiles), dim3(kWave), kLdsBytes, s, kt, n_rows, arena,
-                       arena_len, desc, n, index, n_dev, status, pn_out, hpm);
+    hipLaunchKernelGGL(n_rows == 1 ? mq_chacha_open1_kernel : mq_chacha_open_kernel, dim3(tiles), dim3(kWave),
+                       kLdsBytes, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm);
   else
-    hipLaunchKernelGGL(mq_chacha_seal_kernel, dim3(tiles), dim3(kWave), kLdsBytes, s, kt, n_rows, arena,
-                       arena_len, desc, n, index, n_dev, status);
+    hipLaunchKernelGGL(n_rows == 1 ? mq_chacha_seal1_kernel : mq_chacha_seal_kernel, dim3(tiles), dim3(kWave),
+                       kLdsBytes, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status);
   return hipGetLastError();
 }
 

@@ -207,7 +207,9 @@ __device__ __forceinline__ bool prepass_pick(uint32_t t, uint32_t suite, const K
   return true;
 }
 
-template <class Policy, bool OPEN>
+// SINGLE_KEY: the key table has one row, so every valid packet uses row 0; the policies then get
+// a wave-uniform row pointer and read key material with scalar loads into SGPRs.
+template <class Policy, bool OPEN, bool SINGLE_KEY = false>
 __device__ __forceinline__ void run_tile(uint8_t* smem, uint32_t tile_id, const KeyRow* __restrict__ kt,
                                          uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
                                          const mq_pkt_desc* __restrict__ desc, uint32_t n,
@@ -242,7 +244,7 @@ __device__ __forceinline__ void run_tile(uint8_t* smem, uint32_t tile_id, const 
   c.st = c.valid ? validate<Policy::kSuite, OPEN>(c.d, kt, n_rows, arena_len) : (int)MQ_ERR_INVALID_ARG;
   c.act = c.valid && c.st == MQ_OK;
   c.pn = c.d.pn;
-  const KeyRow* row = kt + (c.act ? c.d.key_id : 0u);
+  const KeyRow* row = SINGLE_KEY ? kt : kt + (c.act ? c.d.key_id : 0u);
   const uint64_t off = c.act ? c.d.offset : 0;
   // chunks of the packet image, clamped so sums cannot overflow; a clamped (huge) packet always
   // exceeds the budget and sends the tile down the direct path
