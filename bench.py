@@ -129,10 +129,16 @@ def end_to_end(torch, batch, kt, w, sd, od, dev, chunks=8, reps=3):
 KERNELS = {"b": "mq_chacha_seal_kernel", "c": "mq_aes_seal_kernel", "e": None}
 
 
-def load_traffic(cfg):
+def seal_kernel(cfg, n_rows):
+    """The seal kernel a single-suite batch launches: the "1" variant (key material in SGPRs)
+    when the key table has a single row (launchers in mq_chacha.hip / mq_aes.hip)."""
+    k = KERNELS.get(cfg)
+    return k.replace("_seal_kernel", "_seal1_kernel") if k and n_rows == 1 else k
+
+
+def load_traffic(cfg, kern):
     """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic_<cfg>.json, written by tools/pmc_summary.py: FETCH_SIZE x 2 + WRITE_SIZE)."""
-    kern = KERNELS.get(cfg)
     path = os.path.join(ROOT, "profiles", f"pmc_traffic_{cfg}.json")
     try:
         with open(path) as f:
@@ -218,9 +224,10 @@ def main():
         # mq_aes_seal_kernel) timed by events on its stream; open = pre-pass + packet kernel
         algo_bytes = 2.0 * wire  # per launch: read + write of every wire byte
         achieved = algo_bytes / (seal_ms * 1e-3) / 1e9
+        kern = seal_kernel(args.config, len(w.keys))
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config),
-                "kernel": KERNELS[args.config] or "seal batch (partition + AES + ChaCha kernels)",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config, kern),
+                "kernel": kern or "seal batch (partition + AES + ChaCha kernels)",
                 "seal_ms": round(seal_ms, 4), "open_ms": round(open_ms, 4),
                 "algorithmic_bytes_per_launch": int(algo_bytes)}
         cpu = None
