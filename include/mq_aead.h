@@ -41,6 +41,10 @@ extern "C" {
 #define MQ_ERR_SUITE             5  /* packet's key suite differs from the launched kernel's  */
 #define MQ_ERR_NO_DEVICE         6  /* no gfx950 device / HIP runtime failure                 */
 #define MQ_ERR_HIP               7  /* HIP runtime error during a call                        */
+#define MQ_ERR_TLS               8  /* Error::Tls: an opened TLS record whose plaintext has no
+                                       valid inner content type (tcp_tls/connection.rs:546-556,
+                                       record.rs:131-139); the plaintext IS in place, as in the
+                                       reference (open_in_place succeeded before the scan)     */
 
 /* ---- cipher suites (TLS_AES_128_GCM_SHA256 = 0x1301, TLS_CHACHA20_POLY1305_SHA256 = 0x1303;
  *      reference tls/handshake.rs:636-654 maps KEY_LEN 16 -> 0x1301, 32 -> 0x1303) ----------- */
@@ -67,6 +71,13 @@ typedef struct mq_key_material {
 #define MQ_PKT_LONG_HEADER  0x01  /* header protection masks byte 0 with 0x0f (else 0x1f)     */
 #define MQ_PKT_NO_HP        0x02  /* plain AEAD: no header protection, pn_len taken from the
                                      descriptor on open, AAD = bytes [0, pn_offset + pn_len)  */
+#define MQ_PKT_TLS_RECORD   0x06  /* TLS 1.3 record (includes MQ_PKT_NO_HP): offset = the 5-byte
+                                     record header, len = 5 + data + 1 + 16 (seal) or 5 + the
+                                     header's length field (open), pn = sequence number
+                                     (record.rs:70-78 nonce), pn_offset = 5, pn_len = 0, and on
+                                     seal `reserved` = the inner content type. Seal writes the
+                                     header (23, 0x0303, len - 5) and the inner content type
+                                     byte, then seals with AAD = header (connection.rs:561-600) */
 
 typedef struct mq_pkt_desc {
   uint64_t offset;     /* byte offset of the packet's first header byte in the arena            */
@@ -171,6 +182,31 @@ int mq_batch_open(const mq_keytable* kt, uint8_t* arena, uint64_t arena_len,
 /* Batched HeaderProtection::mask: masks[i*5..] = mask(key_table[key_ids[i]].hp, samples[i*16..]) */
 int mq_batch_hp_mask(const mq_keytable* kt, const uint32_t* key_ids, const uint8_t* samples,
                      uint8_t* masks, uint32_t n, void* stream);
+
+/* ---- TLS 1.3 record layer over the same AEAD (the reference's second caller of Aead:
+ *      src/tcp_tls/record.rs:70-143, src/tcp_tls/connection.rs:264,306,546-600) ------------ */
+/* seal_record (record.rs:88-113): buf[..payload_len] holds plaintext; writes the inner content
+ * type at buf[payload_len] and seals payload_len + 1 bytes with AAD = (23, 0x0303,
+ * payload_len + 17 as u16). *out_len = payload_len + 17. MQ_ERR_BUFFER_TOO_SMALL (+needed) if
+ * buf_len < payload_len + 17; nonce rules as mq_aead_seal_in_place. */
+int mq_record_seal(const mq_aead_ctx* ctx, const uint8_t* nonce, size_t nonce_len, uint8_t* buf,
+                   size_t buf_len, size_t payload_len, uint8_t inner_type, size_t* out_len,
+                   size_t* needed);
+/* open_record (record.rs:122-143): opens buf[..ct_len] with AAD = header (the 5 received bytes),
+ * then finds the inner content type (last non-zero byte): *data_len, *inner_type. MQ_ERR_TLS if
+ * there is none or it is not 20..23 (plaintext left in place, as in the reference). */
+int mq_record_open(const mq_aead_ctx* ctx, const uint8_t* nonce, size_t nonce_len, uint8_t* buf,
+                   size_t buf_len, size_t ct_len, const uint8_t header[5], size_t* data_len,
+                   uint8_t* inner_type);
+/* Batched records: descriptors flagged MQ_PKT_TLS_RECORD (see above), any mix with QUIC packets
+ * of the same suite hint. Open additionally runs find_inner_content_type (connection.rs:546-556)
+ * per record: info[i] = data_len | (uint64_t)inner_type << 32 (QUIC rows: the decoded PN). */
+int mq_batch_seal_records(const mq_keytable* kt, uint8_t* arena, uint64_t arena_len,
+                          const mq_pkt_desc* desc, uint32_t n, uint8_t* status, uint32_t suite_hint,
+                          void* workspace, void* stream);
+int mq_batch_open_records(const mq_keytable* kt, uint8_t* arena, uint64_t arena_len,
+                          const mq_pkt_desc* desc, uint32_t n, uint8_t* status, uint64_t* info,
+                          uint32_t suite_hint, void* workspace, void* stream);
 
 /* ---- timing hooks for bench.py (HIP events on the launch stream) ---------------------------- */
 /* Time `iters` back-to-back (seal, open) pairs on `stream`; returns per-kernel average ms. */

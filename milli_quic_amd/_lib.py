@@ -20,6 +20,7 @@ MQ_ERR_PROTOCOL = 4
 MQ_ERR_SUITE = 5
 MQ_ERR_NO_DEVICE = 6
 MQ_ERR_HIP = 7
+MQ_ERR_TLS = 8
 
 MQ_SUITE_AES128GCM = 1
 MQ_SUITE_CHACHA20 = 2
@@ -27,6 +28,7 @@ MQ_SUITE_MIXED = 0xFF
 
 MQ_PKT_LONG_HEADER = 0x01
 MQ_PKT_NO_HP = 0x02
+MQ_PKT_TLS_RECORD = 0x06  # implies MQ_PKT_NO_HP
 
 
 class KeyMaterial(ctypes.Structure):
@@ -96,6 +98,12 @@ SIGNATURES = {
     "mq_batch_seal": (ctypes.c_int, [_vp, _vp, _u64, _vp, _u32, _vp, _u32, _vp, _vp]),
     "mq_batch_open": (ctypes.c_int, [_vp, _vp, _u64, _vp, _u32, _vp, _vp, _u32, _vp, _vp]),
     "mq_batch_hp_mask": (ctypes.c_int, [_vp, _vp, _vp, _vp, _u32, _vp]),
+    "mq_record_seal": (ctypes.c_int, [_vp, _vp, _sz, _vp, _sz, _sz, ctypes.c_uint8, ctypes.POINTER(_sz),
+                                      ctypes.POINTER(_sz)]),
+    "mq_record_open": (ctypes.c_int, [_vp, _vp, _sz, _vp, _sz, _sz, _vp, ctypes.POINTER(_sz),
+                                      ctypes.POINTER(ctypes.c_uint8)]),
+    "mq_batch_seal_records": (ctypes.c_int, [_vp, _vp, _u64, _vp, _u32, _vp, _u32, _vp, _vp]),
+    "mq_batch_open_records": (ctypes.c_int, [_vp, _vp, _u64, _vp, _u32, _vp, _vp, _u32, _vp, _vp]),
     "mq_batch_time_seal_open": (ctypes.c_int, [_vp, _vp, _u64, _vp, _u32, _vp, _vp, _u32, _vp, _vp,
                                                ctypes.c_int, ctypes.POINTER(ctypes.c_float),
                                                ctypes.POINTER(ctypes.c_float)]),

@@ -110,6 +110,29 @@ def open_(kt, arena, desc, status, pn_out, suite_hint, workspace=None, stream=No
     _raise(rc)
 
 
+def seal_records(kt, arena, desc, status, suite_hint, workspace=None, stream=None):
+    """Seal every TLS record of `desc` (MQ_PKT_TLS_RECORD rows, tls_record.record_descs) in place:
+    writes each record header and inner content type, then seals (tcp_tls/record.rs:88-113)."""
+    n = desc.numel() // 32
+    _check_out(status, None, n)
+    rc = _lib.load().mq_batch_seal_records(kt.handle, ctypes.c_void_p(arena.data_ptr()), arena.numel(),
+                                           ctypes.c_void_p(desc.data_ptr()), n, ctypes.c_void_p(status.data_ptr()),
+                                           suite_hint, _ws_ptr(workspace, n), _stream_ptr(stream))
+    _raise(rc)
+
+
+def open_records(kt, arena, desc, status, info, suite_hint, workspace=None, stream=None):
+    """Open every record in place and find its inner content type (record.rs:122-143,
+    connection.rs:546-556); info[i] = data_len | inner_type << 32 (tls_record.unpack_info)."""
+    n = desc.numel() // 32
+    _check_out(status, info, n)
+    rc = _lib.load().mq_batch_open_records(kt.handle, ctypes.c_void_p(arena.data_ptr()), arena.numel(),
+                                           ctypes.c_void_p(desc.data_ptr()), n, ctypes.c_void_p(status.data_ptr()),
+                                           ctypes.c_void_p(info.data_ptr()), suite_hint, _ws_ptr(workspace, n),
+                                           _stream_ptr(stream))
+    _raise(rc)
+
+
 def hp_mask(kt, key_ids, samples, masks, stream=None):
     """Batched HeaderProtection::mask: masks[i] = mask(row key_ids[i], samples[i])."""
     n = key_ids.numel()

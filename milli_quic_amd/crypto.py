@@ -40,6 +40,10 @@ class ProtocolViolation(Error):
     """Error::Transport(TransportError::ProtocolViolation)"""
 
 
+class TlsError(Error):
+    """Error::Tls (a TLS record without a valid inner content type, tcp_tls/connection.rs:546-556)"""
+
+
 class InvalidArgument(Error):
     """Cases where the reference panics (index out of range) or a NULL argument."""
 
@@ -57,6 +61,8 @@ def _raise(rc, needed=None):
         raise BufferTooSmall(needed)
     if rc == _lib.MQ_ERR_PROTOCOL:
         raise ProtocolViolation("packet number exceeds 2^62-1")
+    if rc == _lib.MQ_ERR_TLS:
+        raise TlsError("no valid inner content type")
     if rc in (_lib.MQ_ERR_INVALID_ARG, _lib.MQ_ERR_SUITE):
         raise InvalidArgument(_lib.status_str(rc))
     raise DeviceError(_lib.status_str(rc))

@@ -214,6 +214,11 @@ struct ChaChaPolicy {
       if (it == 0) {
         stg.complete();
         MQ_STAMP(c.tile, 2);
+        const bool rec = c.act && is_record(d);
+        if (wave_any(rec)) {  // TLS record: header (AAD) and inner content type before any use
+          if (rec && j == 0) write_record_header(sp, pkt, d);
+          wave_sync();
+        }
         load_block(sp, pay, a ? ctr : 0u, w);
       }
       if (a && ctr == 0) {

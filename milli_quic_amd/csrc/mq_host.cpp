@@ -35,6 +35,8 @@ hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_d
                                uint32_t* list, uint32_t* block_counts, uint32_t* counts,
                                hipStream_t s);
 size_t mq_partition_workspace(uint32_t n);
+hipError_t mq_launch_record_inner(const uint8_t* arena, uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
+                                  uint8_t* status, uint64_t* info, hipStream_t s);
 #ifdef MQ_STAMPS
 void mq_stamps_set_chacha(uint64_t* p);
 void mq_stamps_set_aes(uint64_t* p);
@@ -386,6 +388,7 @@ const char* mq_status_str(int status) {
     case MQ_ERR_SUITE: return "suite mismatch";
     case MQ_ERR_NO_DEVICE: return "no gfx950 device";
     case MQ_ERR_HIP: return "hip runtime error";
+    case MQ_ERR_TLS: return "tls";
     default: return "unknown";
   }
 }
@@ -666,6 +669,52 @@ int mq_batch_open(const mq_keytable* kt, uint8_t* arena, uint64_t arena_len, con
                   uint32_t n, uint8_t* status, uint64_t* pn_out, uint32_t suite_hint, void* workspace,
                   void* stream) {
   return batch(true, kt, arena, arena_len, desc, n, status, pn_out, suite_hint, workspace, stream);
+}
+
+// ---- TLS 1.3 records (tcp_tls/record.rs:88-143, connection.rs:546-600) -----------------------
+int mq_record_seal(const mq_aead_ctx* ctx, const uint8_t* nonce, size_t nonce_len, uint8_t* buf,
+                   size_t buf_len, size_t payload_len, uint8_t inner_type, size_t* out_len,
+                   size_t* needed) {
+  if (!ctx || !buf) return MQ_ERR_INVALID_ARG;
+  const size_t inner_len = payload_len + 1;  // plaintext || inner content type
+  if (buf_len < inner_len + 16) {            // record.rs:97-99
+    if (needed) *needed = inner_len + 16;
+    return MQ_ERR_BUFFER_TOO_SMALL;
+  }
+  const uint16_t outer = (uint16_t)(inner_len + 16);  // `as u16`, record.rs:103
+  const uint8_t aad[5] = {23, 3, 3, (uint8_t)(outer >> 8), (uint8_t)outer};
+  buf[payload_len] = inner_type;  // record.rs:100, before the seal (kept on a seal error too)
+  return mq_aead_seal_in_place(ctx, nonce, nonce_len, aad, 5, buf, buf_len, inner_len, out_len, needed);
+}
+
+int mq_record_open(const mq_aead_ctx* ctx, const uint8_t* nonce, size_t nonce_len, uint8_t* buf,
+                   size_t buf_len, size_t ct_len, const uint8_t header[5], size_t* data_len,
+                   uint8_t* inner_type) {
+  if (!ctx || !buf || !header) return MQ_ERR_INVALID_ARG;
+  size_t pt_len = 0;
+  const int rc = mq_aead_open_in_place(ctx, nonce, nonce_len, header, 5, buf, buf_len, ct_len, &pt_len);
+  if (rc != MQ_OK) return rc;
+  size_t pos = pt_len;  // find_inner_content_type (connection.rs:546-556)
+  while (pos > 0 && buf[pos - 1] == 0) --pos;
+  if (pos == 0 || buf[pos - 1] < 20 || buf[pos - 1] > 23) return MQ_ERR_TLS;
+  if (data_len) *data_len = pos - 1;
+  if (inner_type) *inner_type = buf[pos - 1];
+  return MQ_OK;
+}
+
+int mq_batch_seal_records(const mq_keytable* kt, uint8_t* arena, uint64_t arena_len, const mq_pkt_desc* desc,
+                          uint32_t n, uint8_t* status, uint32_t suite_hint, void* workspace, void* stream) {
+  return batch(false, kt, arena, arena_len, desc, n, status, nullptr, suite_hint, workspace, stream);
+}
+
+int mq_batch_open_records(const mq_keytable* kt, uint8_t* arena, uint64_t arena_len, const mq_pkt_desc* desc,
+                          uint32_t n, uint8_t* status, uint64_t* info, uint32_t suite_hint, void* workspace,
+                          void* stream) {
+  int rc = batch(true, kt, arena, arena_len, desc, n, status, info, suite_hint, workspace, stream);
+  if (rc != MQ_OK || n == 0) return rc;
+  return mq_launch_record_inner(arena, arena_len, desc, n, status, info, (hipStream_t)stream) == hipSuccess
+             ? MQ_OK
+             : MQ_ERR_HIP;
 }
 
 int mq_batch_hp_mask(const mq_keytable* kt, const uint32_t* key_ids, const uint8_t* samples,

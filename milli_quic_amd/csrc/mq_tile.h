@@ -41,6 +41,23 @@ __device__ __forceinline__ uint64_t decode_pn(uint32_t truncated, uint32_t pn_le
   return cand;
 }
 
+__device__ __forceinline__ bool is_record(const mq_pkt_desc& d) { return (d.flags & 0x04) != 0; }
+
+// TLS record seal (encrypt_into, tcp_tls/connection.rs:561-600; seal_record, record.rs:88-113):
+// record header = ApplicationData, legacy version 0x0303, length = len - 5 (the AAD), and the
+// inner content type after the plaintext. Written by one lane before any keystream or MAC touches
+// the record.
+template <class S>
+__device__ __forceinline__ void write_record_header(const S& sp, typename S::off_t rec, const mq_pkt_desc& d) {
+  const uint32_t outer = d.len - 5u;
+  sp.st8(rec, 23);
+  sp.st8(rec + 1, 3);
+  sp.st8(rec + 2, 3);
+  sp.st8(rec + 3, (uint8_t)(outer >> 8));
+  sp.st8(rec + 4, (uint8_t)outer);
+  sp.st8(rec + (d.len - 17u), (uint8_t)d.reserved);
+}
+
 // Descriptor checks in the order of the oracle (oracle/mq_oracle.c orc_run / orc_protect_packet /
 // orc_unprotect_packet), which follows transmit.rs:593-597,721-725 and recv.rs:364-366,970-973.
 template <uint32_t SUITE, bool OPEN>
@@ -49,6 +66,10 @@ __device__ __forceinline__ int validate(const mq_pkt_desc& d, const KeyRow* kt, 
   if (d.key_id >= n_rows || d.offset + (uint64_t)d.len > arena_len) return MQ_ERR_INVALID_ARG;
   if (kt[d.key_id].suite != SUITE) return MQ_ERR_SUITE;
   const bool no_hp = (d.flags & MQ_PKT_NO_HP) != 0;
+  if (is_record(d)) {  // TLS record (record.rs): 5-byte header AAD, no PN, u16 length field
+    if (!no_hp || d.pn_offset != 5 || d.pn_len != 0 || d.len > 5u + 0xFFFFu) return MQ_ERR_INVALID_ARG;
+    if (!OPEN && d.len < 5u + 1u + 16u) return MQ_ERR_BUFFER_TOO_SMALL;  // seal_record :97-99
+  }
   if (!OPEN) {
     if (!no_hp && (d.pn_len < 1 || d.pn_len > 4)) return MQ_ERR_INVALID_ARG;
     if ((uint64_t)d.len < (uint64_t)d.pn_offset + d.pn_len + 16) return MQ_ERR_BUFFER_TOO_SMALL;

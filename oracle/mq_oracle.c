@@ -514,11 +514,67 @@ uint64_t orc_decode_pn(uint32_t truncated, size_t pn_len, uint64_t largest_pn) {
  * packet bytes unchanged (the batch contract).                                              */
 static const size_t MAX_VARINT = (1ull << 62) - 1;
 
+/* TLS 1.3 records over the same Aead (descriptor flag MQ_PKT_TLS_RECORD): a record is
+ * [5-byte header][data][inner content type][tag]. seal: ref src/tcp_tls/connection.rs:561-600
+ * (encrypt_into: header 23, 0x0303, u16 length; plaintext || inner type sealed with AAD = header)
+ * and record.rs:88-113 (seal_record); nonce = iv ^ (0^4 || BE64(seq)) = record.rs:70-78. */
+static int orc_record_checks(const mq_pkt_desc* d) {
+  if ((d->flags & MQ_PKT_TLS_RECORD) != MQ_PKT_TLS_RECORD || d->pn_offset != 5 || d->pn_len != 0 ||
+      d->len > 5u + 0xFFFFu)
+    return MQ_ERR_INVALID_ARG;
+  return MQ_OK;
+}
+
+static int orc_seal_record(const mq_key_material* km, uint8_t* rec, const mq_pkt_desc* d) {
+  size_t klen = suite_key_len(km->suite);
+  int rc = orc_record_checks(d);
+  if (rc) return rc;
+  if (d->len < 5 + 1 + 16) return MQ_ERR_BUFFER_TOO_SMALL; /* record.rs:97-99 */
+  size_t inner_len = d->len - 5 - 16, out_len;
+  uint8_t* tmp = (uint8_t*)malloc(d->len);
+  memcpy(tmp, rec, d->len);
+  uint16_t outer = (uint16_t)(d->len - 5);
+  tmp[0] = 23; tmp[1] = 3; tmp[2] = 3; tmp[3] = (uint8_t)(outer >> 8); tmp[4] = (uint8_t)outer;
+  tmp[5 + inner_len - 1] = (uint8_t)d->reserved;
+  uint8_t nonce[12];
+  orc_nonce(km->iv, d->pn, nonce);
+  rc = orc_aead_seal(km->suite, km->key, klen, nonce, 12, tmp, 5, tmp + 5, d->len - 5, inner_len, &out_len, NULL);
+  if (rc == MQ_OK) memcpy(rec, tmp, d->len);
+  free(tmp);
+  return rc;
+}
+
+/* open: ref record.rs:122-143 (open_record) and connection.rs:546-556 (find_inner_content_type:
+ * last non-zero byte, ContentType::from_byte accepts 20..23, else Error::Tls with the plaintext
+ * already decrypted in place). *info = data_len | inner_type << 32. */
+static int orc_open_record(const mq_key_material* km, uint8_t* rec, const mq_pkt_desc* d, uint64_t* info) {
+  size_t klen = suite_key_len(km->suite), pt_len;
+  int rc = orc_record_checks(d);
+  if (rc) return rc;
+  if (d->len < 5 + 16) return MQ_ERR_CRYPTO; /* open_in_place: ciphertext shorter than the tag */
+  uint8_t* tmp = (uint8_t*)malloc(d->len);
+  memcpy(tmp, rec, d->len);
+  uint8_t nonce[12];
+  orc_nonce(km->iv, d->pn, nonce);
+  rc = orc_aead_open(km->suite, km->key, klen, nonce, 12, tmp, 5, tmp + 5, d->len - 5, d->len - 5, &pt_len);
+  if (rc == MQ_OK) {
+    size_t pos = pt_len;
+    while (pos > 0 && tmp[5 + pos - 1] == 0) --pos;
+    uint8_t ct = pos ? tmp[5 + pos - 1] : 0;
+    if (ct < 20 || ct > 23) rc = MQ_ERR_TLS;
+    else if (info) *info = (uint64_t)(pos - 1) | ((uint64_t)ct << 32);
+    memcpy(rec, tmp, d->len); /* decrypted in place even when the content type is bad */
+  }
+  free(tmp);
+  return rc;
+}
+
 /* send: ref src/connection/transmit.rs:625-755 (build_and_encrypt_packet) and :499-622 */
 int orc_protect_packet(const mq_key_material* km, uint8_t* pkt, const mq_pkt_desc* d) {
   int no_hp = (d->flags & MQ_PKT_NO_HP) != 0;
   size_t klen = suite_key_len(km->suite);
   if (!klen) return MQ_ERR_SUITE;
+  if (d->flags & 0x04) return orc_seal_record(km, pkt, d);
   if (!no_hp && (d->pn_len < 1 || d->pn_len > 4)) return MQ_ERR_INVALID_ARG;
   size_t hdr = (size_t)d->pn_offset + d->pn_len;
   if ((size_t)d->len < hdr + 16) return MQ_ERR_BUFFER_TOO_SMALL;
@@ -551,6 +607,7 @@ int orc_unprotect_packet(const mq_key_material* km, uint8_t* pkt, const mq_pkt_d
   int no_hp = (d->flags & MQ_PKT_NO_HP) != 0;
   size_t klen = suite_key_len(km->suite);
   if (!klen) return MQ_ERR_SUITE;
+  if (d->flags & 0x04) return orc_open_record(km, pkt, d, pn_out);
   uint8_t* tmp = (uint8_t*)malloc(d->len ? d->len : 1);
   memcpy(tmp, pkt, d->len);
   size_t pn_len;
