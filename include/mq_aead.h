@@ -161,6 +161,18 @@ int mq_keytable_update(mq_keytable* kt, uint32_t first_row, const mq_key_materia
 uint32_t mq_keytable_rows(const mq_keytable* kt);
 void mq_keytable_free(mq_keytable* kt);
 
+/* Batched Initial key derivation on the GPU (server-side Initial floods): derive_initial
+ * (connection/keys.rs:181-212 = key_schedule.rs:60-72 + derive_directional_keys :123-151 +
+ * Aes128GcmProvider::aead / header_protection, rustcrypto.rs:232-252) for n client DCIDs.
+ * dcids: device, 20-byte stride; dcid_lens: device, n bytes. Writes key-table rows
+ * first_row + 2i (client keys) and first_row + 2i + 1 (server keys) directly on the device;
+ * km_out (device, 2n entries, may be NULL) receives the same key material; status (device, n
+ * bytes): MQ_OK, or MQ_ERR_INVALID_ARG for a DCID longer than 20 bytes (its rows get suite 0).
+ * MQ_ERR_INVALID_ARG (nothing launched) if first_row + 2n exceeds the table. */
+int mq_batch_derive_initial(mq_keytable* kt, uint32_t first_row, const uint8_t* dcids,
+                            const uint8_t* dcid_lens, uint32_t n, mq_key_material* km_out,
+                            uint8_t* status, void* stream);
+
 /* ---- batch API (device pointers, stream-ordered, asynchronous) ------------------------------ */
 /* `arena` is device memory of `arena_len` bytes holding the packets; `desc` (n entries) and
  * `status` (n bytes, written with MQ_* per packet) are device memory; `pn_out` (open only,

@@ -90,6 +90,7 @@ SIGNATURES = {
     "mq_derive_initial_secrets": (ctypes.c_int, [_vp, _sz, _vp, _vp]),
     "mq_derive_key_material": (ctypes.c_int, [_u32, _vp, _sz, ctypes.POINTER(KeyMaterial)]),
     "mq_derive_next_secret": (ctypes.c_int, [_vp, _sz, _vp]),
+    "mq_batch_derive_initial": (ctypes.c_int, [_vp, _u32, _vp, _vp, _u32, _vp, _vp, _vp]),
     "mq_keytable_create": (ctypes.c_int, [ctypes.POINTER(KeyMaterial), _u32, ctypes.POINTER(_vp)]),
     "mq_keytable_update": (ctypes.c_int, [_vp, _u32, ctypes.POINTER(KeyMaterial), _u32]),
     "mq_keytable_rows": (_u32, [_vp]),

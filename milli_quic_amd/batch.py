@@ -110,6 +110,22 @@ def open_(kt, arena, desc, status, pn_out, suite_hint, workspace=None, stream=No
     _raise(rc)
 
 
+def derive_initial(kt, first_row, dcids, dcid_lens, status, km_out=None, stream=None):
+    """Batched derive_initial (connection/keys.rs:181-212) on the GPU: for n client DCIDs
+    (device uint8 tensors: dcids n x 20, dcid_lens n) write key-table rows first_row + 2i (client
+    keys) and first_row + 2i + 1 (server keys); km_out (n x 2 x 88 bytes) gets the key material."""
+    n = dcid_lens.numel()
+    if dcids.numel() < 20 * n or status.numel() < n:
+        raise crypto.InvalidArgument("dcids needs 20 bytes and status 1 byte per connection")
+    if km_out is not None and km_out.numel() * km_out.element_size() < 2 * 88 * n:
+        raise crypto.InvalidArgument("km_out needs 2 x 88 bytes per connection")
+    rc = _lib.load().mq_batch_derive_initial(kt.handle, first_row, ctypes.c_void_p(dcids.data_ptr()),
+                                             ctypes.c_void_p(dcid_lens.data_ptr()), n,
+                                             ctypes.c_void_p(km_out.data_ptr()) if km_out is not None else None,
+                                             ctypes.c_void_p(status.data_ptr()), _stream_ptr(stream))
+    _raise(rc)
+
+
 def seal_records(kt, arena, desc, status, suite_hint, workspace=None, stream=None):
     """Seal every TLS record of `desc` (MQ_PKT_TLS_RECORD rows, tls_record.record_descs) in place:
     writes each record header and inner content type, then seals (tcp_tls/record.rs:88-113)."""

@@ -40,6 +40,17 @@ struct alignas(16) KeyRow {
 };
 static_assert(sizeof(KeyRow) == 576, "KeyRow layout");
 
+constexpr uint32_t kMaxCidLen = 20;  // RFC 9000 §17.2 (reference ConnectionId capacity)
+
+// Constants of the batched Initial key derivation (mq_derive.hip), computed once on the host:
+// the compressed HMAC pads of the QUIC v1 salt (key_schedule.rs:10-13) and the padded HMAC
+// message blocks of HKDF-Expand-Label(secret, label, "", L) || 0x01 for "client in" (32),
+// "server in" (32), "quic key" (16), "quic iv" (12), "quic hp" (16) (key_schedule.rs:23-55).
+struct MQDeriveConsts {
+  uint32_t salt_ist[8], salt_ost[8];
+  uint32_t lbl[5][16];
+};
+
 // ------------------------------------------------------------------------------------------
 // byte-address spaces: LDS (staged tile) or the HBM arena (direct path)
 struct LdsSpace {

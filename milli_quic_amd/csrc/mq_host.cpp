@@ -35,6 +35,9 @@ hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_d
                                uint32_t* list, uint32_t* block_counts, uint32_t* counts,
                                hipStream_t s);
 size_t mq_partition_workspace(uint32_t n);
+hipError_t mq_launch_derive_initial(const mq::MQDeriveConsts& k, const uint8_t* dcids, const uint8_t* dcid_lens,
+                                    uint32_t n, KeyRow* rows, mq_key_material* km_out, uint8_t* status,
+                                    hipStream_t s);
 hipError_t mq_launch_record_inner(const uint8_t* arena, uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
                                   uint8_t* status, uint64_t* info, hipStream_t s);
 #ifdef MQ_STAMPS
@@ -669,6 +672,68 @@ int mq_batch_open(const mq_keytable* kt, uint8_t* arena, uint64_t arena_len, con
                   uint32_t n, uint8_t* status, uint64_t* pn_out, uint32_t suite_hint, void* workspace,
                   void* stream) {
   return batch(true, kt, arena, arena_len, desc, n, status, pn_out, suite_hint, workspace, stream);
+}
+
+}  // extern "C"
+
+// ---- batched Initial key derivation (keys.rs:181-212 per new client DCID) ---------------------
+namespace {
+// The padded second block of HMAC(secret, HkdfLabel(label, "", L) || 0x01) (key_schedule.rs:23-55;
+// one HKDF-Expand block since L <= 32), as 16 big-endian words.
+void label_block(const char* label, uint16_t out_len, uint32_t w[16]) {
+  uint8_t b[64] = {0};
+  const size_t ll = std::strlen(label);
+  size_t n = 0;
+  b[n++] = (uint8_t)(out_len >> 8);
+  b[n++] = (uint8_t)out_len;
+  b[n++] = (uint8_t)(6 + ll);
+  std::memcpy(b + n, "tls13 ", 6);
+  n += 6;
+  std::memcpy(b + n, label, ll);
+  n += ll;
+  b[n++] = 0;     // empty context
+  b[n++] = 0x01;  // HKDF-Expand block counter
+  b[n] = 0x80;
+  const uint64_t bits = (64 + n) * 8;
+  for (int i = 0; i < 8; ++i) b[56 + i] = (uint8_t)(bits >> (56 - 8 * i));
+  for (int i = 0; i < 16; ++i) w[i] = be32(b + 4 * i);
+}
+
+const mq::MQDeriveConsts& derive_consts() {
+  static mq::MQDeriveConsts k;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    static const uint8_t salt[20] = {0x38, 0x76, 0x2c, 0xf7, 0xf5, 0x59, 0x34, 0xb3, 0x4d, 0x17,
+                                     0x9a, 0xe6, 0xa4, 0xc8, 0x0c, 0xad, 0xcc, 0xbb, 0x7f, 0x0a};
+    uint8_t pad[64];
+    Sha256 si, so;
+    for (int i = 0; i < 64; ++i) pad[i] = (i < 20 ? salt[i] : 0) ^ 0x36;
+    si.block(pad);
+    for (int i = 0; i < 64; ++i) pad[i] = (i < 20 ? salt[i] : 0) ^ 0x5c;
+    so.block(pad);
+    for (int i = 0; i < 8; ++i) { k.salt_ist[i] = si.h[i]; k.salt_ost[i] = so.h[i]; }
+    label_block("client in", 32, k.lbl[0]);
+    label_block("server in", 32, k.lbl[1]);
+    label_block("quic key", 16, k.lbl[2]);
+    label_block("quic iv", 12, k.lbl[3]);
+    label_block("quic hp", 16, k.lbl[4]);
+  });
+  return k;
+}
+}  // namespace
+
+extern "C" {
+
+int mq_batch_derive_initial(mq_keytable* kt, uint32_t first_row, const uint8_t* dcids, const uint8_t* dcid_lens,
+                            uint32_t n, mq_key_material* km_out, uint8_t* status, void* stream) {
+  if (!kt || (n && (!dcids || !dcid_lens || !status))) return MQ_ERR_INVALID_ARG;
+  if ((uint64_t)first_row + 2ull * n > kt->rows) return MQ_ERR_INVALID_ARG;
+  const int rc = ensure_device();
+  if (rc) return rc;
+  return mq_launch_derive_initial(derive_consts(), dcids, dcid_lens, n, kt->dev + first_row, km_out, status,
+                                  (hipStream_t)stream) == hipSuccess
+             ? MQ_OK
+             : MQ_ERR_HIP;
 }
 
 // ---- TLS 1.3 records (tcp_tls/record.rs:88-143, connection.rs:546-600) -----------------------
