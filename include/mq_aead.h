@@ -93,6 +93,39 @@ typedef struct mq_pkt_desc {
   uint32_t reserved;
 } mq_pkt_desc;
 
+/* ---- send composite from frames (mq_batch_protect; transmit.rs:499-755) ------------------- */
+#define MQ_LEVEL_INITIAL      0
+#define MQ_LEVEL_HANDSHAKE    1
+#define MQ_LEVEL_APPLICATION  2
+#define MQ_SEND_PAD_TO_MIN    0x01  /* Initial: pad to MIN_INITIAL_PACKET_SIZE = 1200
+                                       (build_and_encrypt_initial_packet's pad_to_min)          */
+
+typedef struct mq_conn_send {       /* what the send path reads from a Connection             */
+  uint8_t  dcid_len;                /* remote_cid (transmit.rs:513, 653), <= 20                */
+  uint8_t  scid_len;                /* local_cids[0] or empty (:514-518, 654-658), <= 20       */
+  uint8_t  key_phase;               /* keys.key_phase() for 1-RTT (:677-678)                   */
+  uint8_t  reserved0;
+  uint8_t  dcid[20];
+  uint8_t  scid[20];
+  uint32_t key_row[3];              /* key-table row of the send keys per level (Initial rows
+                                       must be AES-128-GCM, keys.rs:131-136)                   */
+  uint32_t reserved1[2];
+} mq_conn_send;                     /* 64 bytes */
+
+typedef struct mq_send_req {        /* one packet to build and protect                         */
+  uint64_t frames_offset;           /* payload_frames in the frames arena                      */
+  uint64_t out_offset;              /* where the packet is written in the output arena         */
+  uint64_t pn;                      /* next_pn[level]                                          */
+  uint64_t largest_acked;           /* largest_recv_pn[level].unwrap_or(0) (:509, 635): picks
+                                       the PN length (number.rs:9-26)                          */
+  uint32_t frame_len;
+  uint32_t out_cap;                 /* bytes available at out_offset (the reference's out.len()) */
+  uint32_t conn;                    /* row of the connection table                             */
+  uint8_t  level;                   /* MQ_LEVEL_*                                               */
+  uint8_t  flags;                   /* MQ_SEND_*                                                */
+  uint16_t reserved;
+} mq_send_req;                      /* 48 bytes */
+
 /* ---- opaque handles ---------------------------------------------------------------------- */
 typedef struct mq_aead_ctx mq_aead_ctx;     /* one Aead instance (immutable after creation)      */
 typedef struct mq_hp_ctx mq_hp_ctx;         /* one HeaderProtection instance                     */
@@ -191,6 +224,23 @@ int mq_batch_seal(const mq_keytable* kt, uint8_t* arena, uint64_t arena_len,
 int mq_batch_open(const mq_keytable* kt, uint8_t* arena, uint64_t arena_len,
                   const mq_pkt_desc* desc, uint32_t n, uint8_t* status, uint64_t* pn_out,
                   uint32_t suite_hint, void* workspace, void* stream);
+/* Send composite from plaintext frames: per request, what
+ * build_and_encrypt_initial_packet (transmit.rs:499-622) and build_and_encrypt_packet
+ * (:625-755) do after frame assembly — PN length (number.rs:9-26), Initial / Handshake / short
+ * header with the Length varint (long_header.rs:214-314, short_header.rs:33-47, first byte
+ * 0x40 | key_phase << 2 | pn_len - 1), encode_pn, PADDING (Initial to 1200 with pad_to_min,
+ * else pn_len + payload + tag >= 20), seal with AAD = header || PN, header protection — writing
+ * the protected packet at out + req.out_offset. pkt_len[i] = packet length (MQ_OK), or the
+ * reference's `needed` for MQ_ERR_BUFFER_TOO_SMALL. Packets that fail leave `out` untouched.
+ * MQ_ERR_INVALID_ARG per packet for a bad conn / level / key row / range. `frames`, `out`,
+ * `conns`, `req`, `status`, `pkt_len` and `workspace` (mq_batch_protect_workspace_size(n)
+ * bytes) are device memory; frames and out must not overlap. */
+size_t mq_batch_protect_workspace_size(uint32_t n);
+int mq_batch_protect(const mq_keytable* kt, const mq_conn_send* conns, uint32_t n_conns,
+                     const uint8_t* frames, uint64_t frames_len, uint8_t* out, uint64_t out_len,
+                     const mq_send_req* req, uint32_t n, uint8_t* status, uint32_t* pkt_len,
+                     uint32_t suite_hint, void* workspace, void* stream);
+
 /* Batched HeaderProtection::mask: masks[i*5..] = mask(key_table[key_ids[i]].hp, samples[i*16..]) */
 int mq_batch_hp_mask(const mq_keytable* kt, const uint32_t* key_ids, const uint8_t* samples,
                      uint8_t* masks, uint32_t n, void* stream);

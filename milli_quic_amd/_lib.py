@@ -30,6 +30,9 @@ MQ_PKT_LONG_HEADER = 0x01
 MQ_PKT_NO_HP = 0x02
 MQ_PKT_TLS_RECORD = 0x06  # implies MQ_PKT_NO_HP
 
+MQ_LEVEL_INITIAL, MQ_LEVEL_HANDSHAKE, MQ_LEVEL_APPLICATION = 0, 1, 2
+MQ_SEND_PAD_TO_MIN = 0x01
+
 
 class KeyMaterial(ctypes.Structure):
     """mq_key_material: what CryptoProvider::aead + ::header_protection consume."""
@@ -91,6 +94,8 @@ SIGNATURES = {
     "mq_derive_key_material": (ctypes.c_int, [_u32, _vp, _sz, ctypes.POINTER(KeyMaterial)]),
     "mq_derive_next_secret": (ctypes.c_int, [_vp, _sz, _vp]),
     "mq_batch_derive_initial": (ctypes.c_int, [_vp, _u32, _vp, _vp, _u32, _vp, _vp, _vp]),
+    "mq_batch_protect_workspace_size": (_sz, [_u32]),
+    "mq_batch_protect": (ctypes.c_int, [_vp, _vp, _u32, _vp, _u64, _vp, _u64, _vp, _u32, _vp, _vp, _u32, _vp, _vp]),
     "mq_keytable_create": (ctypes.c_int, [ctypes.POINTER(KeyMaterial), _u32, ctypes.POINTER(_vp)]),
     "mq_keytable_update": (ctypes.c_int, [_vp, _u32, ctypes.POINTER(KeyMaterial), _u32]),
     "mq_keytable_rows": (_u32, [_vp]),

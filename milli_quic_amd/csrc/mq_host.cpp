@@ -38,6 +38,11 @@ size_t mq_partition_workspace(uint32_t n);
 hipError_t mq_launch_derive_initial(const mq::MQDeriveConsts& k, const uint8_t* dcids, const uint8_t* dcid_lens,
                                     uint32_t n, KeyRow* rows, mq_key_material* km_out, uint8_t* status,
                                     hipStream_t s);
+hipError_t mq_launch_build(const KeyRow* kt, uint32_t n_rows, const mq_conn_send* conns, uint32_t n_conns,
+                           const uint8_t* frames, uint64_t frames_len, uint8_t* out, uint64_t out_len,
+                           const mq_send_req* req, uint32_t n, mq_pkt_desc* desc, uint8_t* bstatus,
+                           uint32_t* pkt_len, hipStream_t s);
+hipError_t mq_launch_send_status(const uint8_t* bstatus, uint8_t* status, uint32_t n, hipStream_t s);
 hipError_t mq_launch_record_inner(const uint8_t* arena, uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
                                   uint8_t* status, uint64_t* info, hipStream_t s);
 #ifdef MQ_STAMPS
@@ -734,6 +739,34 @@ int mq_batch_derive_initial(mq_keytable* kt, uint32_t first_row, const uint8_t* 
                                   (hipStream_t)stream) == hipSuccess
              ? MQ_OK
              : MQ_ERR_HIP;
+}
+
+// ---- send composite from frames (transmit.rs:499-755) -----------------------------------------
+// workspace: [descriptors 32 B x n][build status n][seal workspace]
+size_t mq_batch_protect_workspace_size(uint32_t n) {
+  return ws_align(sizeof(mq_pkt_desc) * (size_t)n) + ws_align(n) + mq_batch_workspace_size(n);
+}
+
+int mq_batch_protect(const mq_keytable* kt, const mq_conn_send* conns, uint32_t n_conns, const uint8_t* frames,
+                     uint64_t frames_len, uint8_t* out, uint64_t out_len, const mq_send_req* req, uint32_t n,
+                     uint8_t* status, uint32_t* pkt_len, uint32_t suite_hint, void* workspace, void* stream) {
+  if (!kt || (n && (!conns || !frames || !out || !req || !status || !pkt_len || !workspace)))
+    return MQ_ERR_INVALID_ARG;
+  if (((uintptr_t)out & 15) != 0) return MQ_ERR_INVALID_ARG;
+  const int rc = ensure_device();
+  if (rc) return rc;
+  if (n == 0) return MQ_OK;
+  hipStream_t s = (hipStream_t)stream;
+  uint8_t* ws = (uint8_t*)workspace;
+  mq_pkt_desc* desc = (mq_pkt_desc*)ws;
+  uint8_t* bstatus = ws + ws_align(sizeof(mq_pkt_desc) * (size_t)n);
+  void* seal_ws = bstatus + ws_align(n);
+  if (mq_launch_build(kt->dev, kt->rows, conns, n_conns, frames, frames_len, out, out_len, req, n, desc, bstatus,
+                      pkt_len, s) != hipSuccess)
+    return MQ_ERR_HIP;
+  const int sr = batch(false, kt, out, out_len, desc, n, status, nullptr, suite_hint, seal_ws, stream);
+  if (sr != MQ_OK) return sr;
+  return mq_launch_send_status(bstatus, status, n, s) == hipSuccess ? MQ_OK : MQ_ERR_HIP;
 }
 
 // ---- TLS 1.3 records (tcp_tls/record.rs:88-143, connection.rs:546-600) -----------------------

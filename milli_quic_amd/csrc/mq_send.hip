@@ -1,0 +1,164 @@
+// mq_send.hip — the send composite from plaintext frames on gfx950.
+//
+// The reference builds each packet in build_and_encrypt_initial_packet (src/connection/
+// transmit.rs:499-622) and build_and_encrypt_packet (:625-755): PN length from largest_acked
+// (src/packet/number.rs:9-26), the Initial / Handshake long header with its Length varint
+// (src/packet/long_header.rs:214-314) or the 1-RTT short header (short_header.rs:33-47, first
+// byte 0x40 | key_phase << 2 | pn_len - 1), encode_pn (number.rs:32-43), the frames, PADDING
+// (Initial up to 1200 bytes when pad_to_min; otherwise pn_len + payload + tag >= 20), then seal
+// and header protection. Here mq_build_kernel does everything up to the seal for a whole batch —
+// one wave per packet: the request and connection rows are wave-uniform (scalar loads), the
+// header is computed once, and the frames move with aligned dword stores — and emits an
+// mq_pkt_desc per packet; the ChaCha20-Poly1305 / AES-128-GCM tile kernels then seal and
+// header-protect those descriptors, and mq_send_status_kernel folds the build statuses in.
+#include "mq_device.h"
+
+using namespace mq;
+
+namespace {
+
+__device__ __forceinline__ uint32_t varint_len(uint64_t v) {
+  return v < 64 ? 1u : v < 16384 ? 2u : v < (1u << 30) ? 4u : 8u;
+}
+
+// encode_initial_header / encode_handshake_header length (long_header.rs:222-225, 279-280)
+__device__ __forceinline__ uint32_t long_header_len(const mq_conn_send& c, bool initial, uint64_t payload_length) {
+  return 1 + 4 + 1 + c.dcid_len + 1 + c.scid_len + (initial ? 1u : 0u) + varint_len(payload_length);
+}
+
+// byte b of the header (b < hdr_len); wave-uniform inputs
+__device__ __forceinline__ uint8_t header_byte(const mq_conn_send& c, uint32_t level, uint32_t pn_len,
+                                              uint64_t payload_length, uint32_t b) {
+  if (level == MQ_LEVEL_APPLICATION) {
+    if (b == 0) return (uint8_t)(0x40 | ((c.key_phase & 1) << 2) | (pn_len - 1));
+    return c.dcid[b - 1];
+  }
+  const bool initial = level == MQ_LEVEL_INITIAL;
+  if (b == 0) return (uint8_t)((initial ? 0xC0 : 0xE0) | ((pn_len - 1) & 3));
+  if (b < 5) return b == 4 ? 1 : 0;  // QUIC_VERSION_1
+  uint32_t p = 5;
+  if (b == p) return c.dcid_len;
+  if (b < p + 1 + c.dcid_len) return c.dcid[b - p - 1];
+  p += 1 + c.dcid_len;
+  if (b == p) return c.scid_len;
+  if (b < p + 1 + c.scid_len) return c.scid[b - p - 1];
+  p += 1 + c.scid_len;
+  if (initial) {
+    if (b == p) return 0;  // token length (the reference sends no token, transmit.rs:519)
+    ++p;
+  }
+  const uint32_t n = varint_len(payload_length), k = b - p;  // varint.rs:72-110
+  uint8_t v = (uint8_t)(payload_length >> (8 * (n - 1 - k)));
+  if (k == 0) v |= n == 1 ? 0 : n == 2 ? 0x40 : n == 4 ? 0x80 : 0xc0;
+  return v;
+}
+
+}  // namespace
+
+extern "C" __global__ __launch_bounds__(64) void mq_build_kernel(
+    const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_conn_send* __restrict__ conns, uint32_t n_conns,
+    const uint8_t* __restrict__ frames, uint64_t frames_len, uint8_t* __restrict__ out, uint64_t out_len,
+    const mq_send_req* __restrict__ req, uint32_t n, mq_pkt_desc* __restrict__ desc, uint8_t* __restrict__ bstatus,
+    uint32_t* __restrict__ pkt_len) {
+  const uint32_t i = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (i >= n) return;
+  const mq_send_req r = req[i];
+  mq_pkt_desc d;
+  d.offset = r.out_offset; d.len = 0; d.key_id = 0xFFFFFFFFu; d.pn = r.pn; d.pn_offset = 0; d.pn_len = 0;
+  d.flags = 0; d.reserved = 0;
+  int st = MQ_OK;
+  uint32_t len = 0;
+  const mq_conn_send* cp = r.conn < n_conns ? conns + r.conn : nullptr;
+  if (!cp || r.level > MQ_LEVEL_APPLICATION || r.frames_offset + (uint64_t)r.frame_len > frames_len ||
+      r.out_offset + (uint64_t)r.out_cap > out_len || cp->key_row[r.level] >= n_rows || cp->dcid_len > 20 ||
+      cp->scid_len > 20) {
+    st = MQ_ERR_INVALID_ARG;
+  } else if (r.level == MQ_LEVEL_INITIAL && kt[cp->key_row[0]].suite != MQ_SUITE_AES128GCM) {
+    st = MQ_ERR_SUITE;  // Initial packets are AES-128-GCM (keys.rs:131-136)
+  }
+  if (st != MQ_OK) {
+    if (lane == 0) { desc[i] = d; bstatus[i] = (uint8_t)st; pkt_len[i] = 0; }
+    return;
+  }
+  const mq_conn_send c = *cp;
+  // pn_length (number.rs:9-26)
+  const uint64_t unacked = r.pn > r.largest_acked ? r.pn - r.largest_acked : 1;
+  const uint32_t pn_len = unacked < (1u << 7) ? 1u : unacked < (1u << 15) ? 2u : unacked < (1u << 23) ? 3u : 4u;
+  uint32_t pad = 0, hdr;
+  uint64_t payload_length = 0;
+  if (r.level == MQ_LEVEL_INITIAL) {  // transmit.rs:521-558
+    const uint64_t pl = pn_len + (uint64_t)r.frame_len + 16;
+    const uint64_t total = long_header_len(c, true, pl) + pl;
+    if ((r.flags & MQ_SEND_PAD_TO_MIN) && total < 1200) pad = (uint32_t)(1200 - total);
+    payload_length = pl + pad;
+    hdr = long_header_len(c, true, payload_length);
+  } else {  // :641-686
+    const uint32_t min_enc = pn_len >= 20 ? 0u : 20u - pn_len;
+    if (r.frame_len + 16u < min_enc) pad = min_enc - r.frame_len - 16u;
+    payload_length = pn_len + (uint64_t)r.frame_len + pad + 16;
+    hdr = r.level == MQ_LEVEL_HANDSHAKE ? long_header_len(c, false, payload_length) : 1u + c.dcid_len;
+  }
+  const uint64_t total = (uint64_t)hdr + pn_len + r.frame_len + pad + 16;
+  if (r.out_cap < hdr) { st = MQ_ERR_BUFFER_TOO_SMALL; len = hdr; }
+  else if (r.out_cap < hdr + pn_len) { st = MQ_ERR_BUFFER_TOO_SMALL; len = pn_len; }
+  else if (total > r.out_cap) { st = MQ_ERR_BUFFER_TOO_SMALL; len = (uint32_t)total; }
+  if (st != MQ_OK) {
+    if (lane == 0) { desc[i] = d; bstatus[i] = (uint8_t)st; pkt_len[i] = len; }
+    return;
+  }
+  uint8_t* dst = out + r.out_offset;
+  // header and PN bytes
+  for (uint32_t b = lane; b < hdr + pn_len; b += kWave)
+    dst[b] = b < hdr ? header_byte(c, r.level, pn_len, payload_length, b)
+                     : (uint8_t)(r.pn >> (8 * (pn_len - 1 - (b - hdr))));
+  // frames (aligned dword stores, realigned source), then PADDING (0x00) and the tag room
+  uint8_t* pd = dst + hdr + pn_len;
+  const uint8_t* ps = frames + r.frames_offset;
+  const uint32_t m = r.frame_len;
+  const uint32_t head = min((uint32_t)((4u - ((uintptr_t)pd & 3u)) & 3u), m);
+  if ((uint32_t)lane < head) pd[lane] = ps[lane];
+  const uint32_t words = (m - head) >> 2;
+  const uintptr_t sa = (uintptr_t)(ps + head);
+  const uint32_t sh = (uint32_t)(sa & 3u) * 8u;
+  const uint32_t* s4 = (const uint32_t*)(sa & ~(uintptr_t)3);
+  uint32_t* d4 = (uint32_t*)(pd + head);
+  for (uint32_t q = lane; q < words; q += kWave) {
+    const uint32_t lo = s4[q];
+    d4[q] = sh ? __builtin_amdgcn_alignbit(s4[q + 1], lo, sh) : lo;  // same aligned dword as a used byte
+  }
+  for (uint32_t b = head + 4 * words + lane; b < m + pad + 16; b += kWave) pd[b] = b < m ? ps[b] : 0;
+  if (lane == 0) {
+    d.len = (uint32_t)total;
+    d.key_id = c.key_row[r.level];
+    d.pn_offset = (uint16_t)hdr;
+    d.pn_len = (uint8_t)pn_len;
+    d.flags = r.level != MQ_LEVEL_APPLICATION ? MQ_PKT_LONG_HEADER : 0;
+    desc[i] = d;
+    bstatus[i] = MQ_OK;
+    pkt_len[i] = (uint32_t)total;
+  }
+}
+
+// build failures keep their status (the seal kernel saw an invalid key id for them)
+extern "C" __global__ __launch_bounds__(256) void mq_send_status_kernel(const uint8_t* __restrict__ bstatus,
+                                                                        uint8_t* __restrict__ status, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && bstatus[i] != MQ_OK) status[i] = bstatus[i];
+}
+
+hipError_t mq_launch_build(const KeyRow* kt, uint32_t n_rows, const mq_conn_send* conns, uint32_t n_conns,
+                           const uint8_t* frames, uint64_t frames_len, uint8_t* out, uint64_t out_len,
+                           const mq_send_req* req, uint32_t n, mq_pkt_desc* desc, uint8_t* bstatus,
+                           uint32_t* pkt_len, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(mq_build_kernel, dim3(n), dim3(kWave), 0, s, kt, n_rows, conns, n_conns, frames, frames_len,
+                     out, out_len, req, n, desc, bstatus, pkt_len);
+  return hipGetLastError();
+}
+
+hipError_t mq_launch_send_status(const uint8_t* bstatus, uint8_t* status, uint32_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(mq_send_status_kernel, dim3((n + 255) / 256), dim3(256), 0, s, bstatus, status, n);
+  return hipGetLastError();
+}

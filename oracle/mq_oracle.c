@@ -650,6 +650,98 @@ int orc_unprotect_packet(const mq_key_material* km, uint8_t* pkt, const mq_pkt_d
 }
 
 /* ---------------------------------------------------------------------------------------- */
+/* Send composite from frames: ref src/connection/transmit.rs:499-622 (Initial, pad_to_min) and
+ * :625-755 (Handshake / 1-RTT), with the header codecs of src/packet/long_header.rs:214-314,
+ * short_header.rs:33-47, number.rs:32-43 and varint.rs:72-110. Writes the protected packet to
+ * out[0..] only on success; *len = its length, or `needed` of a BufferTooSmall.             */
+static size_t orc_varint_len(uint64_t v) { return v < 64 ? 1 : v < 16384 ? 2 : v < (1u << 30) ? 4 : 8; }
+static size_t orc_put_varint(uint8_t* p, uint64_t v) {
+  size_t n = orc_varint_len(v);
+  for (size_t i = 0; i < n; ++i) p[i] = (uint8_t)(v >> (8 * (n - 1 - i)));
+  p[0] |= (uint8_t)(n == 1 ? 0 : n == 2 ? 0x40 : n == 4 ? 0x80 : 0xc0);
+  return n;
+}
+/* encode_initial_header (long_header.rs:214-265; token always empty, transmit.rs:519) /
+ * encode_handshake_header (:272-314) */
+static size_t orc_long_header(uint8_t* h, const mq_conn_send* c, int initial, size_t pn_len,
+                              uint64_t payload_length) {
+  size_t p = 0;
+  h[p++] = (uint8_t)((initial ? 0xC0 : 0xE0) | ((pn_len - 1) & 3));
+  h[p++] = 0; h[p++] = 0; h[p++] = 0; h[p++] = 1; /* QUIC_VERSION_1 */
+  h[p++] = c->dcid_len; memcpy(h + p, c->dcid, c->dcid_len); p += c->dcid_len;
+  h[p++] = c->scid_len; memcpy(h + p, c->scid, c->scid_len); p += c->scid_len;
+  if (initial) h[p++] = 0; /* token length 0 */
+  p += orc_put_varint(h + p, payload_length);
+  return p;
+}
+
+int orc_protect_frames(const mq_key_material* km, const mq_conn_send* c, const mq_send_req* r,
+                       const uint8_t* frames, uint8_t* out, uint64_t out_cap, uint32_t* len) {
+  size_t pn_len = orc_pn_length(r->pn, r->largest_acked), frame_len = r->frame_len, pad = 0, hdr;
+  uint8_t h[128];
+  int is_long = r->level != MQ_LEVEL_APPLICATION;
+  if (r->level > MQ_LEVEL_APPLICATION || c->dcid_len > 20 || c->scid_len > 20) return MQ_ERR_INVALID_ARG;
+  if (r->level == MQ_LEVEL_INITIAL) {
+    uint64_t payload_length = pn_len + frame_len + 16;
+    hdr = orc_long_header(h, c, 1, pn_len, payload_length);
+    if ((r->flags & MQ_SEND_PAD_TO_MIN) && hdr + payload_length < 1200) pad = 1200 - (hdr + payload_length);
+    hdr = orc_long_header(h, c, 1, pn_len, pn_len + frame_len + pad + 16); /* :551-558 */
+  } else {
+    size_t min_enc = pn_len >= 20 ? 0 : 20 - pn_len; /* :644-649 */
+    if (frame_len + 16 < min_enc) pad = min_enc - frame_len - 16;
+    if (r->level == MQ_LEVEL_HANDSHAKE) {
+      hdr = orc_long_header(h, c, 0, pn_len, pn_len + frame_len + pad + 16);
+    } else {
+      h[0] = (uint8_t)(0x40 | ((c->key_phase & 1) << 2) | (pn_len - 1)); /* :677-679 */
+      memcpy(h + 1, c->dcid, c->dcid_len);
+      hdr = 1 + (size_t)c->dcid_len;
+    }
+  }
+  if (out_cap < hdr) { *len = (uint32_t)hdr; return MQ_ERR_BUFFER_TOO_SMALL; }             /* encode_*_header */
+  if (out_cap < hdr + pn_len) { *len = (uint32_t)pn_len; return MQ_ERR_BUFFER_TOO_SMALL; } /* encode_pn */
+  size_t total = hdr + pn_len + frame_len + pad + 16;
+  if (total > out_cap) { *len = (uint32_t)total; return MQ_ERR_BUFFER_TOO_SMALL; }         /* :566-570, :693-697 */
+  uint8_t* pkt = (uint8_t*)calloc(total, 1);
+  memcpy(pkt, h, hdr);
+  for (size_t i = 0; i < pn_len; ++i) pkt[hdr + i] = (uint8_t)(r->pn >> (8 * (pn_len - 1 - i)));
+  memcpy(pkt + hdr + pn_len, frames, frame_len); /* then PADDING frames (0x00) and the tag room */
+  mq_pkt_desc d;
+  memset(&d, 0, sizeof d);
+  d.len = (uint32_t)total; d.pn = r->pn; d.pn_offset = (uint16_t)hdr; d.pn_len = (uint8_t)pn_len;
+  d.flags = is_long ? MQ_PKT_LONG_HEADER : 0;
+  int rc = orc_protect_packet(km, pkt, &d);
+  if (rc == MQ_OK) { memcpy(out, pkt, total); *len = (uint32_t)total; }
+  free(pkt);
+  return rc;
+}
+
+void orc_batch_protect(const mq_key_material* rows, uint32_t n_rows, const mq_conn_send* conns,
+                       uint32_t n_conns, const uint8_t* frames, uint64_t frames_len, uint8_t* out,
+                       uint64_t out_len, const mq_send_req* req, uint32_t n, uint8_t* status,
+                       uint32_t* pkt_len, uint32_t suite_hint) {
+  for (uint32_t i = 0; i < n; ++i) {
+    const mq_send_req* r = &req[i];
+    int st;
+    uint32_t len = 0;
+    if (r->conn >= n_conns || r->level > MQ_LEVEL_APPLICATION ||
+        r->frames_offset + (uint64_t)r->frame_len > frames_len ||
+        r->out_offset + (uint64_t)r->out_cap > out_len || conns[r->conn].key_row[r->level] >= n_rows) {
+      st = MQ_ERR_INVALID_ARG;
+    } else {
+      const mq_key_material* km = &rows[conns[r->conn].key_row[r->level]];
+      if ((suite_hint != MQ_SUITE_MIXED && km->suite != suite_hint) ||
+          (r->level == MQ_LEVEL_INITIAL && km->suite != MQ_SUITE_AES128GCM))
+        st = MQ_ERR_SUITE;
+      else
+        st = orc_protect_frames(km, &conns[r->conn], r, frames + r->frames_offset, out + r->out_offset,
+                                r->out_cap, &len);
+    }
+    status[i] = (uint8_t)st;
+    pkt_len[i] = len;
+  }
+}
+
+/* ---------------------------------------------------------------------------------------- */
 typedef struct {
   const mq_key_material* rows; uint32_t n_rows; uint8_t* arena; uint64_t arena_len;
   const mq_pkt_desc* desc; uint8_t* status; uint64_t* pn_out; uint32_t suite_hint;

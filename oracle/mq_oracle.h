@@ -76,6 +76,14 @@ int orc_protect_packet(const mq_key_material* km, uint8_t* pkt, const mq_pkt_des
 int orc_unprotect_packet(const mq_key_material* km, uint8_t* pkt, const mq_pkt_desc* d,
                          uint64_t* pn_out);
 
+/* send composite from frames (transmit.rs:499-755): header / PN encode, padding, seal, HP */
+int orc_protect_frames(const mq_key_material* km, const mq_conn_send* c, const mq_send_req* r,
+                       const uint8_t* frames, uint8_t* out, uint64_t out_cap, uint32_t* len);
+void orc_batch_protect(const mq_key_material* rows, uint32_t n_rows, const mq_conn_send* conns,
+                       uint32_t n_conns, const uint8_t* frames, uint64_t frames_len, uint8_t* out,
+                       uint64_t out_len, const mq_send_req* req, uint32_t n, uint8_t* status,
+                       uint32_t* pkt_len, uint32_t suite_hint);
+
 /* batch drivers with the product's descriptor semantics; `threads` <= 1 runs serially */
 void orc_batch_seal(const mq_key_material* rows, uint32_t n_rows, uint8_t* arena,
                     uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n, uint8_t* status,

@@ -152,3 +152,16 @@ def batch_open(rows, arena, desc, suite_hint, threads=1):
                           ctypes.c_uint32(n), _p(status), _p(pn), ctypes.c_uint32(suite_hint),
                           ctypes.c_int(threads))
     return status, pn
+
+
+def batch_protect(rows, conns, frames, out, req, suite_hint):
+    """Send composite from frames (transmit.rs:499-755) into the host copy `out` (np.uint8);
+    conns / req are numpy arrays of milli_quic_amd.send CONN_DTYPE / REQ_DTYPE."""
+    arr, nr = _rows(rows)
+    n = len(req)
+    status = np.zeros(n, dtype=np.uint8)
+    pkt_len = np.zeros(n, dtype=np.uint32)
+    load().orc_batch_protect(arr, ctypes.c_uint32(nr), _p(conns), ctypes.c_uint32(len(conns)), _p(frames),
+                             ctypes.c_uint64(frames.size), _p(out), ctypes.c_uint64(out.size), _p(req),
+                             ctypes.c_uint32(n), _p(status), _p(pkt_len), ctypes.c_uint32(suite_hint))
+    return status, pkt_len
