@@ -126,6 +126,50 @@ typedef struct mq_send_req {        /* one packet to build and protect          
   uint16_t reserved;
 } mq_send_req;                      /* 48 bytes */
 
+/* ---- receive composite over raw datagrams (mq_batch_recv; recv.rs:189-510, 953-1025) ----- */
+#define MQ_ERR_DEFERRED          9  /* mq_batch_recv: not processed because an earlier packet of
+                                       its connection changed state differently than the batch
+                                       speculated (or a second key update in one batch) — bytes
+                                       untouched; resubmit after the batch                      */
+#define MQ_RECV_HAS_INITIAL   0x01  /* mq_conn_recv.flags: which recv keys are installed         */
+#define MQ_RECV_HAS_HANDSHAKE 0x02
+#define MQ_RECV_HAS_APP       0x04  /* current 1-RTT keys (app_row[1])                           */
+#define MQ_RECV_HAS_PREV      0x08  /* previous generation (app_row[0], keys.rs:585-589)          */
+#define MQ_RECV_HAS_NEXT      0x10  /* next generation, derived ahead with "quic ku"
+                                       (app_row[2]; keys.rs:498-522)                            */
+
+typedef struct mq_dgram {           /* one received UDP datagram, in arrival order              */
+  uint64_t offset;                  /* in the arena                                             */
+  uint32_t len;
+  uint32_t conn;                    /* row of the connection table (the caller's DCID lookup)    */
+} mq_dgram;                         /* 16 bytes */
+
+typedef struct mq_conn_recv {       /* receive-side connection state, updated in place           */
+  uint32_t initial_row;             /* key-table rows of the recv keys (HP keys are shared by   */
+  uint32_t handshake_row;           /* all 1-RTT generations, keys.rs:386-414)                  */
+  uint32_t app_row[3];              /* 1-RTT: previous, current, next generation                */
+  uint8_t  dcid_len;                /* local CID length for short headers (recv.rs:341-345)     */
+  uint8_t  key_phase;               /* keys.key_phase() (keys.rs:364-366)                        */
+  uint8_t  flags;                   /* MQ_RECV_HAS_*                                             */
+  uint8_t  key_updates;             /* out: peer key updates confirmed by this batch             */
+  uint64_t largest_pn[3];           /* largest_recv_pn per level; None == 0 (unwrap_or(0))       */
+  uint64_t reserved[2];
+} mq_conn_recv;                     /* 64 bytes */
+
+typedef struct mq_recv_pkt {        /* one packet found in the datagrams, in arrival order       */
+  uint64_t offset;                  /* packet start in the arena                                 */
+  uint64_t pn;                      /* decoded packet number (MQ_OK)                             */
+  uint32_t len;                     /* long: pn_offset + Length; short: rest of the datagram     */
+  uint32_t dgram;                   /* datagram index                                            */
+  uint16_t payload_offset;          /* MQ_OK: plaintext at offset + payload_offset, length
+                                       len - payload_offset - 16                                 */
+  uint8_t  level;                   /* MQ_LEVEL_*                                                 */
+  uint8_t  status;                  /* MQ_* (the Result of recv_initial / _handshake / _short)   */
+  uint8_t  key_gen;                 /* opened 1-RTT packets: keys of the 0 previous, 1 current,
+                                       2 next generation (0 otherwise)                           */
+  uint8_t  reserved[3];
+} mq_recv_pkt;                      /* 32 bytes */
+
 /* ---- opaque handles ---------------------------------------------------------------------- */
 typedef struct mq_aead_ctx mq_aead_ctx;     /* one Aead instance (immutable after creation)      */
 typedef struct mq_hp_ctx mq_hp_ctx;         /* one HeaderProtection instance                     */
@@ -240,6 +284,24 @@ int mq_batch_protect(const mq_keytable* kt, const mq_conn_send* conns, uint32_t 
                      const uint8_t* frames, uint64_t frames_len, uint8_t* out, uint64_t out_len,
                      const mq_send_req* req, uint32_t n, uint8_t* status, uint32_t* pkt_len,
                      uint32_t suite_hint, void* workspace, void* stream);
+
+/* Receive composite over raw datagrams: Connection::recv's datagram loop
+ * (recv.rs:189-265) without frame dispatch — CoalescedPackets splitting (packet/coalesce.rs:26-133),
+ * long-header parsing (long_header.rs:92-206), header-protection removal, decode_pn against the
+ * connection's running largest_recv_pn, the 1-RTT key-phase logic (current keys, previous keys
+ * on failure, next keys + rotation on a phase flip; recv.rs:410-509) and open. Datagrams of one
+ * connection are processed in arrival order (one sequential pass per connection on the device,
+ * speculating that packets open; MQ_ERR_DEFERRED marks the rare packets whose inputs the
+ * speculation got wrong). 0-RTT, Retry and Version Negotiation packets are skipped, as in the
+ * reference (:221-226). Opened packets are decrypted in place (header unmasked); others keep
+ * their bytes. pkts receives up to max_pkts records in arrival order, *n_pkts (device) their
+ * count; conns is updated (largest_recv_pn, key phase / rotation). Initial keys must already be
+ * installed (mq_batch_derive_initial). All pointers are device memory; workspace has
+ * mq_batch_recv_workspace_size(n_dgrams, max_pkts, n_conns) bytes. */
+size_t mq_batch_recv_workspace_size(uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_conns);
+int mq_batch_recv(const mq_keytable* kt, mq_conn_recv* conns, uint32_t n_conns, uint8_t* arena,
+                  uint64_t arena_len, const mq_dgram* dgrams, uint32_t n_dgrams, mq_recv_pkt* pkts,
+                  uint32_t max_pkts, uint32_t* n_pkts, void* workspace, void* stream);
 
 /* Batched HeaderProtection::mask: masks[i*5..] = mask(key_table[key_ids[i]].hp, samples[i*16..]) */
 int mq_batch_hp_mask(const mq_keytable* kt, const uint32_t* key_ids, const uint8_t* samples,

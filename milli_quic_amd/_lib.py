@@ -21,6 +21,7 @@ MQ_ERR_SUITE = 5
 MQ_ERR_NO_DEVICE = 6
 MQ_ERR_HIP = 7
 MQ_ERR_TLS = 8
+MQ_ERR_DEFERRED = 9
 
 MQ_SUITE_AES128GCM = 1
 MQ_SUITE_CHACHA20 = 2
@@ -96,6 +97,8 @@ SIGNATURES = {
     "mq_batch_derive_initial": (ctypes.c_int, [_vp, _u32, _vp, _vp, _u32, _vp, _vp, _vp]),
     "mq_batch_protect_workspace_size": (_sz, [_u32]),
     "mq_batch_protect": (ctypes.c_int, [_vp, _vp, _u32, _vp, _u64, _vp, _u64, _vp, _u32, _vp, _vp, _u32, _vp, _vp]),
+    "mq_batch_recv_workspace_size": (_sz, [_u32, _u32, _u32]),
+    "mq_batch_recv": (ctypes.c_int, [_vp, _vp, _u32, _vp, _u64, _vp, _u32, _vp, _u32, _vp, _vp, _vp]),
     "mq_keytable_create": (ctypes.c_int, [ctypes.POINTER(KeyMaterial), _u32, ctypes.POINTER(_vp)]),
     "mq_keytable_update": (ctypes.c_int, [_vp, _u32, ctypes.POINTER(KeyMaterial), _u32]),
     "mq_keytable_rows": (_u32, [_vp]),

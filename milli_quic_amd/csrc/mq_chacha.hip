@@ -421,6 +421,15 @@ hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_
   return hipGetLastError();
 }
 
+// header-protection masks of the ChaCha20 rows of `desc` only (mq_recv.hip plans with them)
+hipError_t mq_launch_chacha_prepass(const KeyRow* kt, uint32_t n_rows, const uint8_t* arena, uint64_t arena_len,
+                                    const mq_pkt_desc* desc, uint32_t n, uint2* hpm, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(mq_chacha_open_hp_kernel, dim3((n + 255) / 256), dim3(256), 0, s, kt, n_rows, arena, arena_len,
+                     desc, n, (const uint32_t*)nullptr, (const uint32_t*)nullptr, hpm);
+  return hipGetLastError();
+}
+
 hipError_t mq_launch_chacha_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t* key_ids,
                                const uint8_t* samples, uint8_t* masks, uint32_t n, hipStream_t s) {
   if (n == 0) return hipSuccess;

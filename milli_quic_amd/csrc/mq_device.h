@@ -51,6 +51,14 @@ struct MQDeriveConsts {
   uint32_t lbl[5][16];
 };
 
+// The AEAD passes of the datagram receive composite (mq_recv.hip), run by mq_host.cpp's batch
+// driver: primary descriptors / statuses, retry (previous-generation keys) descriptors / statuses.
+struct MQRecvPass {
+  mq_pkt_desc *d1, *d2;
+  uint8_t *st1, *st2;
+  void* open_ws;
+};
+
 // ------------------------------------------------------------------------------------------
 // byte-address spaces: LDS (staged tile) or the HBM arena (direct path)
 struct LdsSpace {

@@ -43,6 +43,18 @@ hipError_t mq_launch_build(const KeyRow* kt, uint32_t n_rows, const mq_conn_send
                            const mq_send_req* req, uint32_t n, mq_pkt_desc* desc, uint8_t* bstatus,
                            uint32_t* pkt_len, hipStream_t s);
 hipError_t mq_launch_send_status(const uint8_t* bstatus, uint8_t* status, uint32_t n, hipStream_t s);
+size_t mq_recv_workspace(uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_conns, size_t open_ws_bytes);
+hipError_t mq_recv_front(const KeyRow* kt, uint32_t n_rows, mq_conn_recv* conns, uint32_t n_conns, uint8_t* arena,
+                         uint64_t arena_len, const mq_dgram* dg, uint32_t n_dgrams, uint32_t max_pkts,
+                         uint32_t* n_pkts, mq_recv_pkt* out, void* ws_ptr, size_t open_ws_bytes, mq::MQRecvPass* pass,
+                         hipStream_t s);
+hipError_t mq_recv_walk(const KeyRow* kt, uint32_t n_rows, mq_conn_recv* conns, uint32_t n_conns,
+                        uint32_t n_dgrams, uint32_t max_pkts, mq_recv_pkt* out, void* ws_ptr, size_t open_ws_bytes,
+                        bool final_walk, hipStream_t s);
+hipError_t mq_recv_retry(uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_conns, void* ws_ptr, size_t open_ws_bytes,
+                         hipStream_t s);
+hipError_t mq_recv_outcomes(uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_conns, void* ws_ptr,
+                            size_t open_ws_bytes, hipStream_t s);
 hipError_t mq_launch_record_inner(const uint8_t* arena, uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
                                   uint8_t* status, uint64_t* info, hipStream_t s);
 #ifdef MQ_STAMPS
@@ -767,6 +779,45 @@ int mq_batch_protect(const mq_keytable* kt, const mq_conn_send* conns, uint32_t 
   const int sr = batch(false, kt, out, out_len, desc, n, status, nullptr, suite_hint, seal_ws, stream);
   if (sr != MQ_OK) return sr;
   return mq_launch_send_status(bstatus, status, n, s) == hipSuccess ? MQ_OK : MQ_ERR_HIP;
+}
+
+// ---- receive composite over raw datagrams (recv.rs:189-510, 953-1025) --------------------------
+size_t mq_batch_recv_workspace_size(uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_conns) {
+  return mq_recv_workspace(n_dgrams, max_pkts, n_conns, mq_batch_workspace_size(max_pkts));
+}
+
+int mq_batch_recv(const mq_keytable* kt, mq_conn_recv* conns, uint32_t n_conns, uint8_t* arena, uint64_t arena_len,
+                  const mq_dgram* dgrams, uint32_t n_dgrams, mq_recv_pkt* pkts, uint32_t max_pkts, uint32_t* n_pkts,
+                  void* workspace, void* stream) {
+  if (!kt || !n_pkts || !workspace || (n_conns && !conns) || (n_dgrams && (!arena || !dgrams)) ||
+      (max_pkts && !pkts))
+    return MQ_ERR_INVALID_ARG;
+  if (((uintptr_t)arena & 15) != 0) return MQ_ERR_INVALID_ARG;
+  const int rc = ensure_device();
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t open_ws = mq_batch_workspace_size(max_pkts);
+  mq::MQRecvPass p;
+  if (mq_recv_front(kt->dev, kt->rows, conns, n_conns, arena, arena_len, dgrams, n_dgrams, max_pkts, n_pkts, pkts,
+                    workspace, open_ws, &p, s) != hipSuccess)
+    return MQ_ERR_HIP;
+  if (!max_pkts) return MQ_OK;
+  // walk -> AEAD passes -> walk ...: the first walk speculates that every packet opens, later walks
+  // re-attempt what the real outcomes changed (rare: after a failed packet); the last walk defers
+  // anything still unresolved. Fixed rounds keep the call asynchronous (no host read-back).
+  constexpr int kRounds = 2;
+  for (int round = 0; round < kRounds; ++round) {
+    int r = batch(true, kt, arena, arena_len, p.d1, max_pkts, p.st1, nullptr, MQ_SUITE_MIXED, p.open_ws, stream);
+    if (r != MQ_OK) return r;
+    if (mq_recv_retry(n_dgrams, max_pkts, n_conns, workspace, open_ws, s) != hipSuccess) return MQ_ERR_HIP;
+    r = batch(true, kt, arena, arena_len, p.d2, max_pkts, p.st2, nullptr, MQ_SUITE_MIXED, p.open_ws, stream);
+    if (r != MQ_OK) return r;
+    if (mq_recv_outcomes(n_dgrams, max_pkts, n_conns, workspace, open_ws, s) != hipSuccess) return MQ_ERR_HIP;
+    if (mq_recv_walk(kt->dev, kt->rows, conns, n_conns, n_dgrams, max_pkts, pkts, workspace, open_ws,
+                     round + 1 == kRounds, s) != hipSuccess)
+      return MQ_ERR_HIP;
+  }
+  return MQ_OK;
 }
 
 // ---- TLS 1.3 records (tcp_tls/record.rs:88-143, connection.rs:546-600) -----------------------

@@ -1,0 +1,533 @@
+// mq_recv.hip — the receive composite over raw UDP datagrams on gfx950.
+//
+// The reference's Connection::recv (src/connection/recv.rs:189-265) walks the coalesced packets
+// of each datagram (src/packet/coalesce.rs:26-133), parses long headers (long_header.rs:92-206),
+// removes header protection, decodes the packet number against the connection's running
+// largest_recv_pn, picks 1-RTT keys by the key-phase bit (current, previous on failure, next +
+// rotation on a flip; recv.rs:410-509) and opens the payload. Per connection this is a sequential
+// state machine; across connections it is independent. On the device:
+//
+//   split   one lane per datagram: CoalescedPackets -> packet records (count, scan, emit, so
+//           records stay in arrival order)
+//   masks   the header-protection pre-pass kernels of the suites (one lane per packet)
+//   sort    stable radix sort of record indices by connection (hipCUB) -> per-connection runs
+//   plan    one lane per connection walks its run in arrival order: unmasks the first byte,
+//           decodes the PN against the running largest PN, chooses the key generation, and
+//           SPECULATES that every packet opens (largest PN / rotation advance) -> descriptors
+//   open    the ChaCha20-Poly1305 / AES-128-GCM tile kernels, then a retry pass with the
+//           previous-generation keys for 1-RTT packets that failed with the current ones
+//   commit  one lane per connection replays its run with the real outcomes: statuses, PNs and
+//           the connection state; a packet whose inputs the speculation got wrong (only possible
+//           after an earlier packet of the connection failed) and that did not open is
+//           MQ_ERR_DEFERRED (untouched, to be resubmitted)
+#include <hipcub/hipcub.hpp>
+
+#include "mq_device.h"
+
+using namespace mq;
+
+namespace {
+
+constexpr uint8_t kPending = 0xFF;
+constexpr uint32_t kNoRow = 0xFFFFFFFFu;
+
+// working record of one packet (workspace)
+struct RecvWork {
+  uint64_t offset;    // packet start in the arena
+  uint32_t len;       // long: pn_offset + Length; short: rest of the datagram
+  uint32_t dgram;
+  uint32_t conn;
+  uint16_t pn_off;    // long: from the header; short: 1 + dcid_len (set by plan)
+  uint8_t level;
+  uint8_t pre;        // kPending, or a status found before any crypto
+};
+
+// speculative plan of one packet (workspace)
+struct RecvPlan {
+  uint64_t pn;        // decoded PN
+  uint64_t lbefore;   // largest PN of its level before it
+  uint32_t row;       // key row opened with (primary)
+  uint32_t retry;     // previous-generation row for the retry pass, or kNoRow
+  uint32_t trunc;     // truncated PN (header protection removed; state independent)
+  uint8_t status;     // kPending (to open) or a final status
+  uint8_t gen;        // key generation of `row`
+  uint8_t phase;      // key-phase bit of the unmasked first byte
+  uint8_t pn_len;
+};
+
+__device__ __forceinline__ bool get_varint(const uint8_t* p, uint64_t avail, uint64_t& v, uint32_t& used) {
+  if (avail < 1) return false;
+  const uint32_t n = 1u << (p[0] >> 6);
+  if (avail < n) return false;
+  uint64_t x = p[0] & 0x3f;
+  for (uint32_t i = 1; i < n; ++i) x = (x << 8) | p[i];
+  v = x;
+  used = n;
+  return true;
+}
+
+// CoalescedPackets::next (coalesce.rs:29-132). kind: 0 Initial, 1 0-RTT, 2 Handshake, 3 Retry,
+// 4 short, 5 version negotiation. false = the datagram's iteration stops here.
+__device__ __forceinline__ bool next_packet(const uint8_t* r, uint64_t avail, uint64_t& plen, int& kind,
+                                            uint32_t& pn_off) {
+  if (!(r[0] & 0x80)) { plen = avail; kind = 4; return true; }
+  if (avail < 6) return false;
+  const uint32_t version = ((uint32_t)r[1] << 24) | ((uint32_t)r[2] << 16) | ((uint32_t)r[3] << 8) | r[4];
+  if (version == 0) { plen = avail; kind = 5; return true; }
+  uint64_t pos = 6 + (uint64_t)r[5];
+  if (pos >= avail) return false;
+  const uint64_t scid = r[pos++];
+  if (pos + scid > avail) return false;
+  pos += scid;
+  const int type = (r[0] & 0x30) >> 4;
+  uint64_t v;
+  uint32_t used;
+  if (type == 0) {
+    if (!get_varint(r + pos, avail - pos, v, used)) return false;
+    pos += used;
+    if (v > avail - pos) return false;
+    pos += v;
+  }
+  if (type == 3) { plen = avail; kind = 3; return true; }
+  if (!get_varint(r + pos, avail - pos, v, used)) return false;
+  pos += used;
+  if (v > avail - pos) return false;
+  plen = pos + v;
+  kind = type;
+  pn_off = (uint32_t)pos;
+  return true;
+}
+
+__device__ __forceinline__ uint64_t decode_pn(uint32_t truncated, uint32_t pn_len, uint64_t largest) {
+  const uint64_t win = 1ull << (8 * pn_len), hwin = win >> 1, mask = win - 1;
+  const uint64_t expected = largest + 1;
+  const uint64_t cand = (expected & ~mask) | truncated;
+  if (cand + hwin <= expected && cand + win <= (1ull << 62)) return cand + win;
+  if (cand > expected + hwin && cand >= win) return cand - win;
+  return cand;
+}
+
+}  // namespace
+
+// ---- split ------------------------------------------------------------------------------------
+extern "C" __global__ __launch_bounds__(256) void mq_recv_split_kernel(
+    const uint8_t* __restrict__ arena, uint64_t arena_len, const mq_dgram* __restrict__ dg, uint32_t n_dgrams,
+    uint32_t n_conns, uint32_t* __restrict__ counts, const uint32_t* __restrict__ base, RecvWork* __restrict__ work,
+    uint32_t max_pkts) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_dgrams) return;
+  const mq_dgram d = dg[g];
+  uint32_t k = 0;
+  if (d.conn < n_conns && d.offset + (uint64_t)d.len <= arena_len) {
+    const uint8_t* b = arena + d.offset;
+    uint64_t off = 0;
+    while (off < d.len) {
+      uint64_t plen = 0;
+      int kind = 0;
+      uint32_t pn_off = 0;
+      if (!next_packet(b + off, d.len - off, plen, kind, pn_off)) break;
+      if (kind != 1 && kind != 3 && kind != 5) {  // 0-RTT, Retry, VN are skipped (recv.rs:221-226)
+        if (base) {
+          const uint32_t at = base[g] + k;
+          if (at < max_pkts) {
+            RecvWork w;
+            w.offset = d.offset + off;
+            w.len = (uint32_t)plen;
+            w.dgram = g;
+            w.conn = d.conn;
+            w.pn_off = (uint16_t)pn_off;
+            w.level = kind == 0 ? MQ_LEVEL_INITIAL : kind == 2 ? MQ_LEVEL_HANDSHAKE : MQ_LEVEL_APPLICATION;
+            w.pre = kPending;
+            work[at] = w;
+          }
+        }
+        ++k;
+      }
+      off += plen;
+    }
+  }
+  if (!base) counts[g] = k;
+}
+
+// sort keys / values and the provisional descriptors the header-protection pre-pass reads
+extern "C" __global__ __launch_bounds__(256) void mq_recv_prep_kernel(
+    const mq_conn_recv* __restrict__ conns, const uint32_t* __restrict__ total, RecvWork* __restrict__ work,
+    uint32_t max_pkts, uint32_t n_rows, uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
+    mq_pkt_desc* __restrict__ desc) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= max_pkts) return;
+  const uint32_t n = min(*total, max_pkts);
+  vals[i] = i;
+  mq_pkt_desc d;
+  d.offset = 0; d.len = 0; d.key_id = kNoRow; d.pn = 0; d.pn_offset = 0; d.pn_len = 0; d.flags = 0; d.reserved = 0;
+  if (i >= n) {
+    keys[i] = 0xFFFFFFFFu;
+    desc[i] = d;
+    return;
+  }
+  RecvWork w = work[i];
+  const mq_conn_recv c = conns[w.conn];
+  keys[i] = w.conn;
+  if (w.level == MQ_LEVEL_APPLICATION) w.pn_off = (uint16_t)(1 + c.dcid_len);
+  // checks of recv_initial / recv_handshake / recv_short before the sample is read
+  uint8_t pre = kPending;
+  uint32_t row = kNoRow;
+  if (w.level == MQ_LEVEL_APPLICATION) {
+    if (w.len < 1u + c.dcid_len) pre = MQ_ERR_BUFFER_TOO_SMALL;  // parse_short_header
+    else if (!(c.flags & MQ_RECV_HAS_APP) || c.app_row[1] >= n_rows) pre = MQ_ERR_CRYPTO;
+    else if (w.len > 2048) pre = MQ_ERR_BUFFER_TOO_SMALL;          // recv.rs:356-360
+    else row = c.app_row[1];                                          // HP keys of every generation
+  } else {
+    const bool ini = w.level == MQ_LEVEL_INITIAL;
+    const uint32_t r = ini ? c.initial_row : c.handshake_row;
+    if (!(c.flags & (ini ? MQ_RECV_HAS_INITIAL : MQ_RECV_HAS_HANDSHAKE)) || r >= n_rows) pre = MQ_ERR_CRYPTO;
+    else if (w.len > 2048) pre = MQ_ERR_BUFFER_TOO_SMALL;          // decrypt_long_packet :963-965
+    else row = r;
+  }
+  if (pre == kPending && (uint32_t)w.pn_off + 20 > w.len) pre = MQ_ERR_CRYPTO;  // sample (:364-366, :970-973)
+  w.pre = pre;
+  work[i] = w;
+  if (pre == kPending) {
+    d.offset = w.offset; d.len = w.len; d.key_id = row; d.pn_offset = w.pn_off;
+    d.flags = w.level != MQ_LEVEL_APPLICATION ? MQ_PKT_LONG_HEADER : 0;
+  }
+  desc[i] = d;
+}
+
+// per-connection run boundaries in the sorted order
+extern "C" __global__ __launch_bounds__(256) void mq_recv_seg_kernel(const uint32_t* __restrict__ skeys,
+                                                                     uint32_t max_pkts, uint32_t n_conns,
+                                                                     uint32_t* __restrict__ seg_lo,
+                                                                     uint32_t* __restrict__ seg_hi) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= max_pkts) return;
+  const uint32_t k = skeys[s];
+  if (k >= n_conns) return;
+  if (s == 0 || skeys[s - 1] != k) seg_lo[k] = s;
+  if (s + 1 == max_pkts || skeys[s + 1] != k) seg_hi[k] = s + 1;
+}
+
+// ---- plan: one lane per connection, speculating that every packet opens -----------------------
+struct ConnState {
+  uint64_t largest[3];
+  uint32_t row[3];
+  uint8_t phase, flags, updates;
+};
+
+__device__ __forceinline__ ConnState load_state(const mq_conn_recv& c) {
+  ConnState s;
+  for (int l = 0; l < 3; ++l) { s.largest[l] = c.largest_pn[l]; s.row[l] = c.app_row[l]; }
+  s.phase = c.key_phase;
+  s.flags = c.flags;
+  s.updates = c.key_updates;
+  return s;
+}
+
+// header-protection removal of one packet from the arena as received: truncated PN, PN length and
+// key-phase bit (recv.rs:363-391, :968-992); independent of the connection state
+__device__ __forceinline__ void unmask(const RecvWork& w, const uint8_t* arena, uint2 m, RecvPlan& p) {
+  const bool lng = w.level != MQ_LEVEL_APPLICATION;
+  const uint8_t* pk = arena + w.offset;
+  const uint8_t b0 = pk[0] ^ ((uint8_t)m.x & (lng ? 0x0f : 0x1f));
+  const uint32_t pn_len = (b0 & 3u) + 1;
+  const uint32_t mk = (m.x >> 8) | (m.y << 24);
+  uint32_t trunc = 0;
+  for (uint32_t b = 0; b < pn_len; ++b) trunc = (trunc << 8) | (uint8_t)(pk[w.pn_off + b] ^ (uint8_t)(mk >> (8 * b)));
+  p.trunc = trunc;
+  p.pn_len = (uint8_t)pn_len;
+  p.phase = (b0 >> 2) & 1;
+}
+
+// what the sequential reference decides for one packet in state s: decoded PN and key choice
+// (status kPending = goes to the AEAD); p.trunc / pn_len / phase from unmask()
+__device__ __forceinline__ void decide(const ConnState& s, const RecvWork& w, const mq_conn_recv& c, uint32_t n_rows,
+                                       RecvPlan& p) {
+  p.retry = kNoRow;
+  p.gen = 1;
+  p.row = kNoRow;
+  p.pn = 0;
+  p.lbefore = 0;
+  p.status = w.pre;
+  if (w.pre != kPending) return;
+  p.lbefore = s.largest[w.level];
+  p.pn = decode_pn(p.trunc, p.pn_len, p.lbefore);
+  if (p.pn > (1ull << 62) - 1) { p.status = MQ_ERR_PROTOCOL; return; }  // recv.rs:393-395, 994-997
+  if (w.level != MQ_LEVEL_APPLICATION) {
+    p.row = w.level == MQ_LEVEL_INITIAL ? c.initial_row : c.handshake_row;
+  } else if (p.phase == s.phase) {
+    p.row = s.row[1];
+    if ((s.flags & MQ_RECV_HAS_PREV) && s.row[0] < n_rows) p.retry = s.row[0];
+  } else if (!(s.flags & MQ_RECV_HAS_NEXT) || s.row[2] >= n_rows) {
+    // no next-generation keys: derive_next_recv_keys fails (Crypto) when none were installed;
+    // after a rotation in this batch the next-next keys need the host (DEFERRED)
+    p.status = s.updates != c.key_updates ? (uint8_t)MQ_ERR_DEFERRED : (uint8_t)MQ_ERR_CRYPTO;
+  } else {
+    p.row = s.row[2];
+    p.gen = 2;
+  }
+}
+
+__device__ __forceinline__ void advance(ConnState& s, const RecvWork& w, const RecvPlan& p, uint8_t gen) {
+  if (p.pn > s.largest[w.level]) s.largest[w.level] = p.pn;  // recv.rs:239-247
+  if (w.level == MQ_LEVEL_APPLICATION && gen == 2) {          // confirm_peer_key_update (keys.rs:532-583)
+    s.row[0] = s.row[1];
+    s.row[1] = s.row[2];
+    s.flags = (uint8_t)((s.flags | MQ_RECV_HAS_PREV) & ~MQ_RECV_HAS_NEXT);
+    s.phase ^= 1;
+    s.updates++;
+  }
+}
+
+// header-protection removal of every packet from the arena as received (state independent)
+extern "C" __global__ __launch_bounds__(256) void mq_recv_unmask_kernel(const uint8_t* __restrict__ arena,
+                                                                        const RecvWork* __restrict__ work,
+                                                                        const uint2* __restrict__ hpm,
+                                                                        const uint32_t* __restrict__ total,
+                                                                        uint32_t max_pkts, RecvPlan* __restrict__ hdr,
+                                                                        uint8_t* __restrict__ outcome) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= max_pkts) return;
+  outcome[i] = 0;
+  if (i >= min(*total, max_pkts)) return;
+  const RecvWork w = work[i];
+  RecvPlan p;
+  p.trunc = 0; p.pn_len = 0; p.phase = 0;
+  if (w.pre == kPending) unmask(w, arena, hpm[i], p);
+  hdr[i] = p;
+}
+
+// ---- walk: one lane per connection replays its packets in arrival order ---------------------------
+// With every outcome known so far it decides each packet exactly as the sequential reference does;
+// a packet whose AEAD attempt is missing or was made with other inputs gets a new attempt (d1 / d2)
+// and is SPECULATED to open, so the walk can go on. Repeated after each pair of AEAD passes until
+// nothing new is attempted; the last walk (`final`) marks what is still unresolved DEFERRED.
+enum : uint8_t { kNone = 0, kOk1 = 1, kOk0 = 2, kFail = 3 };
+
+extern "C" __global__ __launch_bounds__(64) void mq_recv_walk_kernel(
+    const mq_conn_recv* __restrict__ conn0, mq_conn_recv* __restrict__ conns, uint32_t n_conns,
+    const RecvWork* __restrict__ work, const uint32_t* __restrict__ svals, const uint32_t* __restrict__ seg_lo,
+    const uint32_t* __restrict__ seg_hi, const RecvPlan* __restrict__ hdr, uint32_t n_rows,
+    RecvPlan* __restrict__ tried, const uint8_t* __restrict__ outcome, mq_pkt_desc* __restrict__ d1,
+    mq_pkt_desc* __restrict__ d2, mq_recv_pkt* __restrict__ out, uint32_t* __restrict__ attempts, int final_walk) {
+  const uint32_t ci = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ci >= n_conns) return;
+  const mq_conn_recv c = conn0[ci];
+  ConnState s = load_state(c);
+  uint32_t new_attempts = 0;
+  for (uint32_t k = seg_lo[ci]; k < seg_hi[ci]; ++k) {
+    const uint32_t i = svals[k];
+    const RecvWork w = work[i];
+    RecvPlan p = hdr[i];
+    decide(s, w, c, n_rows, p);
+    mq_pkt_desc a;
+    a.offset = w.offset; a.len = w.len; a.key_id = kNoRow; a.pn = p.lbefore; a.pn_offset = w.pn_off;
+    a.pn_len = 0; a.flags = w.level != MQ_LEVEL_APPLICATION ? MQ_PKT_LONG_HEADER : 0; a.reserved = 0;
+    mq_pkt_desc b = a;
+    uint8_t st = p.status, gen = p.gen;
+    RecvPlan used = p;
+    if (p.status == kPending) {
+      const uint8_t o = outcome[i];
+      const RecvPlan t = tried[i];
+      const bool same = o != kNone && t.pn == p.pn && t.row == p.row && t.retry == p.retry && t.gen == p.gen;
+      if (same || o == kOk1 || o == kOk0) {  // known outcome (an opened packet keeps its inputs)
+        used = same ? p : t;
+        st = (o == kOk1 || o == kOk0) ? (uint8_t)MQ_OK : (uint8_t)MQ_ERR_CRYPTO;
+        gen = o == kOk0 ? 0 : used.gen;
+      } else if (final_walk) {
+        st = MQ_ERR_DEFERRED;
+      } else {  // (re)attempt with the inputs the reference would use; speculate it opens
+        tried[i] = p;
+        a.key_id = p.row;
+        b.key_id = p.retry;
+        ++new_attempts;
+        st = MQ_OK;
+      }
+    }
+    d1[i] = a;
+    d2[i] = b;
+    mq_recv_pkt r;
+    r.offset = w.offset; r.len = w.len; r.dgram = w.dgram; r.level = w.level; r.status = st;
+    r.pn = st == MQ_OK ? used.pn : 0;
+    r.payload_offset = st == MQ_OK ? (uint16_t)(w.pn_off + used.pn_len) : 0;
+    r.key_gen = (w.level == MQ_LEVEL_APPLICATION && st == MQ_OK) ? gen : 0;
+    r.reserved[0] = r.reserved[1] = r.reserved[2] = 0;
+    out[i] = r;
+    if (st == MQ_OK) advance(s, w, used, gen);
+  }
+  if (new_attempts) atomicAdd(attempts, new_attempts);
+  mq_conn_recv o = c;
+  for (int l = 0; l < 3; ++l) { o.largest_pn[l] = s.largest[l]; o.app_row[l] = s.row[l]; }
+  o.key_phase = s.phase;
+  o.flags = s.flags;
+  o.key_updates = s.updates;
+  conns[ci] = o;
+}
+
+// retry pass descriptors: only 1-RTT packets whose current keys failed (recv.rs:441-474)
+extern "C" __global__ __launch_bounds__(256) void mq_recv_retry_kernel(const uint8_t* __restrict__ st1,
+                                                                       mq_pkt_desc* __restrict__ d2, uint32_t max_pkts) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= max_pkts) return;
+  if (!(d2[i].key_id != kNoRow && st1[i] == MQ_ERR_CRYPTO)) d2[i].key_id = kNoRow;
+}
+
+// outcomes of this round's attempts
+extern "C" __global__ __launch_bounds__(256) void mq_recv_outcome_kernel(const mq_pkt_desc* __restrict__ d1,
+                                                                         const mq_pkt_desc* __restrict__ d2,
+                                                                         const uint8_t* __restrict__ st1,
+                                                                         const uint8_t* __restrict__ st2,
+                                                                         uint8_t* __restrict__ outcome,
+                                                                         uint32_t max_pkts) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= max_pkts || d1[i].key_id == kNoRow) return;
+  outcome[i] = st1[i] == MQ_OK ? kOk1 : (d2[i].key_id != kNoRow && st2[i] == MQ_OK) ? kOk0 : kFail;
+}
+
+// ---- launch helpers ------------------------------------------------------------------------------
+namespace {
+size_t al(size_t b) { return (b + 255) & ~(size_t)255; }
+
+struct RecvWs {
+  uint32_t *counts, *base, *total, *keys, *vals, *skeys, *svals, *seg_lo, *seg_hi, *attempts;
+  RecvWork* work;
+  RecvPlan *hdr, *tried;
+  mq_conn_recv* conn0;
+  uint2* hpm;
+  mq_pkt_desc *d1, *d2;
+  uint8_t *st1, *st2, *outcome;
+  void* cub;
+  size_t cub_bytes;
+  uint8_t* open_ws;
+  size_t bytes;
+};
+
+size_t cub_bytes(uint32_t n_dgrams, uint32_t max_pkts) {
+  size_t a = 0, b = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, a, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n_dgrams + 1);
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                           (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)max_pkts, 0, 32);
+  return a > b ? a : b;
+}
+
+RecvWs layout(uint8_t* p, uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_conns, size_t open_ws_bytes) {
+  RecvWs w;
+  size_t o = 0;
+  auto take = [&](size_t bytes) { uint8_t* q = p ? p + o : nullptr; o += al(bytes); return q; };
+  w.counts = (uint32_t*)take(4ull * n_dgrams + 4);
+  w.base = (uint32_t*)take(4ull * n_dgrams + 4);
+  w.total = (uint32_t*)take(8);
+  w.attempts = (uint32_t*)take(8);
+  w.keys = (uint32_t*)take(4ull * max_pkts);
+  w.vals = (uint32_t*)take(4ull * max_pkts);
+  w.skeys = (uint32_t*)take(4ull * max_pkts);
+  w.svals = (uint32_t*)take(4ull * max_pkts);
+  w.seg_lo = (uint32_t*)take(4ull * n_conns);
+  w.seg_hi = (uint32_t*)take(4ull * n_conns);
+  w.conn0 = (mq_conn_recv*)take(sizeof(mq_conn_recv) * (size_t)n_conns);
+  w.work = (RecvWork*)take(sizeof(RecvWork) * (size_t)max_pkts);
+  w.hdr = (RecvPlan*)take(sizeof(RecvPlan) * (size_t)max_pkts);
+  w.tried = (RecvPlan*)take(sizeof(RecvPlan) * (size_t)max_pkts);
+  w.hpm = (uint2*)take(8ull * max_pkts);
+  w.d1 = (mq_pkt_desc*)take(sizeof(mq_pkt_desc) * (size_t)max_pkts);
+  w.d2 = (mq_pkt_desc*)take(sizeof(mq_pkt_desc) * (size_t)max_pkts);
+  w.st1 = take(max_pkts);
+  w.st2 = take(max_pkts);
+  w.outcome = take(max_pkts);
+  w.cub_bytes = cub_bytes(n_dgrams, max_pkts);
+  w.cub = take(w.cub_bytes);
+  w.open_ws = take(open_ws_bytes);
+  w.bytes = o;
+  return w;
+}
+}  // namespace
+
+size_t mq_recv_workspace(uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_conns, size_t open_ws_bytes) {
+  return layout(nullptr, n_dgrams, max_pkts, n_conns, open_ws_bytes).bytes;
+}
+
+hipError_t mq_launch_chacha_prepass(const KeyRow* kt, uint32_t n_rows, const uint8_t* arena, uint64_t arena_len,
+                                    const mq_pkt_desc* desc, uint32_t n, uint2* hpm, hipStream_t s);
+hipError_t mq_launch_aes_prepass(const KeyRow* kt, uint32_t n_rows, const uint8_t* arena, uint64_t arena_len,
+                                 const mq_pkt_desc* desc, uint32_t n, uint2* hpm, hipStream_t s);
+
+hipError_t mq_recv_walk(const KeyRow* kt, uint32_t n_rows, mq_conn_recv* conns, uint32_t n_conns,
+                        uint32_t n_dgrams, uint32_t max_pkts, mq_recv_pkt* out, void* ws_ptr, size_t open_ws_bytes,
+                        bool final_walk, hipStream_t s);
+
+// split, header-protection masks, sort, first walk (mq_host.cpp then runs the AEAD passes)
+hipError_t mq_recv_front(const KeyRow* kt, uint32_t n_rows, mq_conn_recv* conns, uint32_t n_conns, uint8_t* arena,
+                         uint64_t arena_len, const mq_dgram* dg, uint32_t n_dgrams, uint32_t max_pkts,
+                         uint32_t* n_pkts, mq_recv_pkt* out, void* ws_ptr, size_t open_ws_bytes, MQRecvPass* pass,
+                         hipStream_t s) {
+  RecvWs w = layout((uint8_t*)ws_ptr, n_dgrams, max_pkts, n_conns, open_ws_bytes);
+  pass->d1 = w.d1; pass->d2 = w.d2; pass->st1 = w.st1; pass->st2 = w.st2; pass->open_ws = w.open_ws;
+  const dim3 b256(256);
+  hipError_t e = hipSuccess;
+  if (n_dgrams) {
+    hipLaunchKernelGGL(mq_recv_split_kernel, dim3((n_dgrams + 255) / 256), b256, 0, s, arena, arena_len, dg, n_dgrams,
+                       n_conns, w.counts, (const uint32_t*)nullptr, w.work, max_pkts);
+    if ((e = hipMemsetAsync(w.counts + n_dgrams, 0, 4, s)) != hipSuccess) return e;  // total lands in base[n]
+    size_t cb = w.cub_bytes;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(w.cub, cb, w.counts, w.base, (int)n_dgrams + 1, s)) != hipSuccess)
+      return e;
+    if ((e = hipMemcpyAsync(w.total, w.base + n_dgrams, 4, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(mq_recv_split_kernel, dim3((n_dgrams + 255) / 256), b256, 0, s, arena, arena_len, dg, n_dgrams,
+                       n_conns, w.counts, (const uint32_t*)w.base, w.work, max_pkts);
+  } else if ((e = hipMemsetAsync(w.total, 0, 4, s)) != hipSuccess) {
+    return e;
+  }
+  if ((e = hipMemcpyAsync(n_pkts, w.total, 4, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+  if (n_conns && (e = hipMemcpyAsync(w.conn0, conns, sizeof(mq_conn_recv) * (size_t)n_conns,
+                                     hipMemcpyDeviceToDevice, s)) != hipSuccess)
+    return e;
+  if (max_pkts == 0) return hipGetLastError();
+  hipLaunchKernelGGL(mq_recv_prep_kernel, dim3((max_pkts + 255) / 256), b256, 0, s, w.conn0, w.total, w.work, max_pkts,
+                     n_rows, w.keys, w.vals, w.d1);
+  if ((e = mq_launch_chacha_prepass(kt, n_rows, arena, arena_len, w.d1, max_pkts, w.hpm, s)) != hipSuccess) return e;
+  if ((e = mq_launch_aes_prepass(kt, n_rows, arena, arena_len, w.d1, max_pkts, w.hpm, s)) != hipSuccess) return e;
+  hipLaunchKernelGGL(mq_recv_unmask_kernel, dim3((max_pkts + 255) / 256), b256, 0, s, arena, w.work, w.hpm, w.total,
+                     max_pkts, w.hdr, w.outcome);
+  size_t cb = w.cub_bytes;
+  if ((e = hipcub::DeviceRadixSort::SortPairs(w.cub, cb, w.keys, w.skeys, w.vals, w.svals, (int)max_pkts, 0, 32, s)) !=
+      hipSuccess)
+    return e;
+  if (n_conns) {
+    if ((e = hipMemsetAsync(w.seg_lo, 0, 4ull * n_conns, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(w.seg_hi, 0, 4ull * n_conns, s)) != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(mq_recv_seg_kernel, dim3((max_pkts + 255) / 256), b256, 0, s, w.skeys, max_pkts, n_conns, w.seg_lo,
+                     w.seg_hi);
+  return mq_recv_walk(kt, n_rows, conns, n_conns, n_dgrams, max_pkts, out, ws_ptr, open_ws_bytes, false, s);
+}
+
+// one walk (after the first, the previous round's AEAD outcomes are folded in first)
+hipError_t mq_recv_walk(const KeyRow* /*kt*/, uint32_t n_rows, mq_conn_recv* conns, uint32_t n_conns,
+                        uint32_t n_dgrams, uint32_t max_pkts, mq_recv_pkt* out, void* ws_ptr, size_t open_ws_bytes,
+                        bool final_walk, hipStream_t s) {
+  RecvWs w = layout((uint8_t*)ws_ptr, n_dgrams, max_pkts, n_conns, open_ws_bytes);
+  hipError_t e;
+  if ((e = hipMemsetAsync(w.attempts, 0, 4, s)) != hipSuccess) return e;
+  if (n_conns)
+    hipLaunchKernelGGL(mq_recv_walk_kernel, dim3((n_conns + 63) / 64), dim3(64), 0, s, w.conn0, conns, n_conns, w.work,
+                       w.svals, w.seg_lo, w.seg_hi, w.hdr, n_rows, w.tried, w.outcome, w.d1, w.d2, out, w.attempts,
+                       (int)final_walk);
+  return hipGetLastError();
+}
+
+// between the primary and the retry AEAD pass / after both
+hipError_t mq_recv_retry(uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_conns, void* ws_ptr, size_t open_ws_bytes,
+                         hipStream_t s) {
+  RecvWs w = layout((uint8_t*)ws_ptr, n_dgrams, max_pkts, n_conns, open_ws_bytes);
+  if (max_pkts)
+    hipLaunchKernelGGL(mq_recv_retry_kernel, dim3((max_pkts + 255) / 256), dim3(256), 0, s, w.st1, w.d2, max_pkts);
+  return hipGetLastError();
+}
+
+hipError_t mq_recv_outcomes(uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_conns, void* ws_ptr,
+                            size_t open_ws_bytes, hipStream_t s) {
+  RecvWs w = layout((uint8_t*)ws_ptr, n_dgrams, max_pkts, n_conns, open_ws_bytes);
+  if (max_pkts)
+    hipLaunchKernelGGL(mq_recv_outcome_kernel, dim3((max_pkts + 255) / 256), dim3(256), 0, s, w.d1, w.d2, w.st1, w.st2,
+                       w.outcome, max_pkts);
+  return hipGetLastError();
+}

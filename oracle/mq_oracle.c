@@ -742,6 +742,169 @@ void orc_batch_protect(const mq_key_material* rows, uint32_t n_rows, const mq_co
 }
 
 /* ---------------------------------------------------------------------------------------- */
+/* Receive composite over raw datagrams: ref src/connection/recv.rs:189-265 (datagram loop,
+ * errors drop the packet), :268-337 + :953-1025 (Initial / Handshake), :340-510 (1-RTT with key
+ * phase), src/packet/coalesce.rs:26-133 and long_header.rs:92-206 (parsing), varint.rs (decode).
+ * Frame dispatch is out of scope: a packet that opens counts as processed (largest_recv_pn).   */
+static int orc_get_varint(const uint8_t* p, size_t avail, uint64_t* v, size_t* used) {
+  if (avail < 1) return MQ_ERR_BUFFER_TOO_SMALL;
+  size_t n = (size_t)1 << (p[0] >> 6);
+  if (avail < n) return MQ_ERR_BUFFER_TOO_SMALL;
+  uint64_t x = p[0] & 0x3f;
+  for (size_t i = 1; i < n; ++i) x = (x << 8) | p[i];
+  *v = x; *used = n;
+  return MQ_OK;
+}
+
+/* CoalescedPackets::next (coalesce.rs:29-132): *plen = packet length; *kind = 0 Initial,
+ * 1 0-RTT, 2 Handshake, 3 Retry, 4 short, 5 version negotiation; *pn_off / *length for Initial /
+ * Handshake (parse_*_header). Returns non-zero when the datagram's iteration stops (error). */
+static int orc_next_packet(const uint8_t* rem, size_t avail, size_t* plen, int* kind, size_t* pn_off,
+                           uint64_t* length) {
+  if (!(rem[0] & 0x80)) { *plen = avail; *kind = 4; return 0; }
+  if (avail < 6) return 1;
+  uint32_t version = ((uint32_t)rem[1] << 24) | ((uint32_t)rem[2] << 16) | ((uint32_t)rem[3] << 8) | rem[4];
+  if (version == 0) { *plen = avail; *kind = 5; return 0; }
+  size_t pos = 6 + rem[5];
+  if (pos >= avail) return 1; /* pos + dcid_len >= len (:62) */
+  size_t scid = rem[pos++];
+  if (pos + scid > avail) return 1;
+  pos += scid;
+  int type = (rem[0] & 0x30) >> 4;
+  uint64_t v;
+  size_t used;
+  if (type == 0) {
+    if (orc_get_varint(rem + pos, avail - pos, &v, &used)) return 1;
+    pos += used;
+    if (v > avail - pos) return 1;
+    pos += (size_t)v;
+  }
+  if (type == 3) { *plen = avail; *kind = 3; return 0; }
+  if (orc_get_varint(rem + pos, avail - pos, &v, &used)) return 1;
+  pos += used;
+  if (v > avail - pos) return 1;
+  *plen = pos + (size_t)v; *kind = type; *pn_off = pos; *length = v;
+  return 0;
+}
+
+/* HP removal + decode_pn + open of one packet at pkt[0..len) with keys `km` (recv.rs:363-421 /
+ * 968-1018); the packet is only written on success. *pn_out / *poff on success. */
+static int orc_recv_open(const mq_key_material* km, uint8_t* pkt, size_t len, size_t pn_off, int long_hdr,
+                         uint64_t largest, uint64_t* pn_out, size_t* poff, int* phase_out) {
+  if (pn_off + 4 + 16 > len) return MQ_ERR_CRYPTO;
+  uint8_t mask[5], b0;
+  size_t klen = suite_key_len(km->suite);
+  if (!klen) return MQ_ERR_CRYPTO;
+  orc_hp_mask(km->suite, km->hp, klen > 16 ? klen : 16, pkt + pn_off + 4, 16, mask);
+  b0 = pkt[0] ^ (mask[0] & (long_hdr ? 0x0f : 0x1f));
+  size_t pn_len = (size_t)(b0 & 3) + 1;
+  uint32_t trunc = 0;
+  for (size_t i = 0; i < pn_len; ++i) trunc = (trunc << 8) | (uint8_t)(pkt[pn_off + i] ^ mask[1 + i]);
+  uint64_t pn = orc_decode_pn(trunc, pn_len, largest);
+  if (pn > (1ull << 62) - 1) return MQ_ERR_PROTOCOL;
+  if (phase_out) *phase_out = (b0 >> 2) & 1;
+  *pn_out = pn;
+  *poff = pn_off + pn_len;
+  return MQ_OK;
+}
+
+static int orc_recv_aead(const mq_key_material* km, uint8_t* pkt, size_t len, size_t pn_off, int long_hdr,
+                         uint64_t pn) {
+  mq_pkt_desc d;
+  memset(&d, 0, sizeof d);
+  d.len = (uint32_t)len; d.pn = pn - 1; d.pn_offset = (uint16_t)pn_off;
+  d.flags = long_hdr ? MQ_PKT_LONG_HEADER : 0;
+  /* largest = pn - 1 decodes back to pn for any encoding; the composite redoes HP removal */
+  uint64_t got;
+  if (pn == 0) { d.pn = 0; }
+  int rc = orc_unprotect_packet(km, pkt, &d, &got);
+  return rc;
+}
+
+void orc_batch_recv(const mq_key_material* rows, uint32_t n_rows, mq_conn_recv* conns, uint32_t n_conns,
+                    uint8_t* arena, uint64_t arena_len, const mq_dgram* dg, uint32_t n_dgrams,
+                    mq_recv_pkt* out, uint32_t max_pkts, uint32_t* n_pkts) {
+  uint32_t np = 0;
+  uint8_t* upd0 = (uint8_t*)malloc(n_conns ? n_conns : 1);
+  for (uint32_t k = 0; k < n_conns; ++k) upd0[k] = conns[k].key_updates;
+  for (uint32_t g = 0; g < n_dgrams; ++g) {
+    if (dg[g].conn >= n_conns || dg[g].offset + (uint64_t)dg[g].len > arena_len) continue;
+    mq_conn_recv* c = &conns[dg[g].conn];
+    uint8_t* base = arena + dg[g].offset;
+    size_t off = 0;
+    while (off < dg[g].len) {
+      size_t plen = 0, pn_off = 0;
+      uint64_t length = 0;
+      int kind;
+      if (orc_next_packet(base + off, dg[g].len - off, &plen, &kind, &pn_off, &length)) break;
+      uint8_t* pkt = base + off;
+      off += plen;
+      if (kind == 1 || kind == 3 || kind == 5) continue; /* 0-RTT, Retry, VN skipped (:221-226) */
+      mq_recv_pkt r;
+      memset(&r, 0, sizeof r);
+      r.offset = (uint64_t)(pkt - arena); r.len = (uint32_t)plen; r.dgram = g;
+      int st = MQ_OK, lvl = kind == 0 ? MQ_LEVEL_INITIAL : kind == 2 ? MQ_LEVEL_HANDSHAKE : MQ_LEVEL_APPLICATION;
+      r.level = (uint8_t)lvl;
+      uint64_t pn = 0;
+      size_t poff = 0;
+      if (lvl != MQ_LEVEL_APPLICATION) { /* recv_initial / recv_handshake -> decrypt_long_packet */
+        uint32_t row = lvl == MQ_LEVEL_INITIAL ? c->initial_row : c->handshake_row;
+        int has = c->flags & (lvl == MQ_LEVEL_INITIAL ? MQ_RECV_HAS_INITIAL : MQ_RECV_HAS_HANDSHAKE);
+        size_t total = pn_off + (size_t)length;
+        if (!has || row >= n_rows) st = MQ_ERR_CRYPTO;
+        else if (total > 2048) st = MQ_ERR_BUFFER_TOO_SMALL; /* :963-965 */
+        else st = orc_recv_open(&rows[row], pkt, total, pn_off, 1, c->largest_pn[lvl], &pn, &poff, NULL);
+        if (st == MQ_OK) st = orc_recv_aead(&rows[row], pkt, total, pn_off, 1, pn);
+        r.len = (uint32_t)total;
+      } else { /* recv_short (:340-510) */
+        size_t dl = c->dcid_len;
+        int phase = 0;
+        if (plen < 1 + dl) st = MQ_ERR_BUFFER_TOO_SMALL;                       /* parse_short_header */
+        else if (!(c->flags & MQ_RECV_HAS_APP) || c->app_row[1] >= n_rows) st = MQ_ERR_CRYPTO;
+        else if (plen > 2048) st = MQ_ERR_BUFFER_TOO_SMALL;                    /* :356-360 */
+        else st = orc_recv_open(&rows[c->app_row[1]], pkt, plen, 1 + dl, 0, c->largest_pn[2], &pn, &poff, &phase);
+        if (st == MQ_OK) {
+          if (phase == c->key_phase) {
+            st = orc_recv_aead(&rows[c->app_row[1]], pkt, plen, 1 + dl, 0, pn);
+            r.key_gen = 1;
+            if (st != MQ_OK) { /* :441-474: previous keys, else Error::Crypto */
+              st = MQ_ERR_CRYPTO;
+              if ((c->flags & MQ_RECV_HAS_PREV) && c->app_row[0] < n_rows) {
+                st = orc_recv_aead(&rows[c->app_row[0]], pkt, plen, 1 + dl, 0, pn);
+                r.key_gen = 0;
+              }
+            }
+          } else { /* :476-509: next generation, rotate on success */
+            /* no next-generation keys installed: Crypto (derive_next_recv_keys without a secret);
+             * after a rotation inside this batch the next-next keys need the host: Deferred */
+            st = c->key_updates != upd0[dg[g].conn] ? MQ_ERR_DEFERRED : MQ_ERR_CRYPTO;
+            if ((c->flags & MQ_RECV_HAS_NEXT) && c->app_row[2] < n_rows) {
+              st = orc_recv_aead(&rows[c->app_row[2]], pkt, plen, 1 + dl, 0, pn);
+              r.key_gen = 2;
+              if (st == MQ_OK) {
+                c->app_row[0] = c->app_row[1]; c->app_row[1] = c->app_row[2];
+                c->flags = (uint8_t)((c->flags | MQ_RECV_HAS_PREV) & ~MQ_RECV_HAS_NEXT);
+                c->key_phase ^= 1; c->key_updates++;
+              }
+            }
+          }
+        }
+      }
+      if (st != MQ_OK) r.key_gen = 0; /* only meaningful for opened 1-RTT packets */
+      if (st == MQ_OK) {
+        r.pn = pn; r.payload_offset = (uint16_t)poff;
+        if (pn > c->largest_pn[lvl]) c->largest_pn[lvl] = pn; /* :239-247 */
+      }
+      r.status = (uint8_t)st;
+      if (np < max_pkts) out[np] = r;
+      ++np;
+    }
+  }
+  free(upd0);
+  *n_pkts = np;
+}
+
+/* ---------------------------------------------------------------------------------------- */
 typedef struct {
   const mq_key_material* rows; uint32_t n_rows; uint8_t* arena; uint64_t arena_len;
   const mq_pkt_desc* desc; uint8_t* status; uint64_t* pn_out; uint32_t suite_hint;

@@ -84,6 +84,11 @@ void orc_batch_protect(const mq_key_material* rows, uint32_t n_rows, const mq_co
                        uint64_t out_len, const mq_send_req* req, uint32_t n, uint8_t* status,
                        uint32_t* pkt_len, uint32_t suite_hint);
 
+/* receive composite over raw datagrams (recv.rs:189-510, 953-1025), conns updated in place */
+void orc_batch_recv(const mq_key_material* rows, uint32_t n_rows, mq_conn_recv* conns, uint32_t n_conns,
+                    uint8_t* arena, uint64_t arena_len, const mq_dgram* dg, uint32_t n_dgrams,
+                    mq_recv_pkt* out, uint32_t max_pkts, uint32_t* n_pkts);
+
 /* batch drivers with the product's descriptor semantics; `threads` <= 1 runs serially */
 void orc_batch_seal(const mq_key_material* rows, uint32_t n_rows, uint8_t* arena,
                     uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n, uint8_t* status,

@@ -1,0 +1,114 @@
+"""Synthetic receive-side traffic for the datagram composite tests (test_recv.py, test_gpu_recv.py).
+
+Packets are built and protected by the oracle's send composite (pinned to RFC 9001 A.5), with
+PN lengths chosen from what the receiver has seen (number.rs:9-26), so the receive composite
+must recover them (decode_pn against the running largest PN). Per connection: Initial and
+Handshake packets coalesced into one datagram (Initial padded to 1200), then 1-RTT packets
+with a peer key update (key phase flip to the next generation) part-way; across connections the
+datagrams interleave. Extra cases: tampered packets, a Version Negotiation / Retry / 0-RTT
+packet (skipped), a truncated long header (iteration stops), a short packet shorter than the
+CID, a connection without 1-RTT keys, a phase flip without next-generation keys.
+"""
+import numpy as np
+
+from milli_quic_amd import _lib, packet, recv, send
+from milli_quic_amd.key_schedule import derive_initial_secrets, key_material
+
+
+def build_traffic(orc, seed=1, n_conns=12, n_app=30):
+    rng = np.random.default_rng(seed)
+    keys = [_lib.KeyMaterial()]  # row 0: unused
+    conns = np.zeros(n_conns, dtype=recv.CONN_DTYPE)
+    scripts = []  # per connection: list of (datagram parts), each part = (level, row, phase, pn, frames, tamper)
+    for c in range(n_conns):
+        dcid = rng.bytes(int(rng.choice([0, 4, 8, 20])))
+        client, _ = derive_initial_secrets(rng.bytes(8))
+        suite = int(rng.choice([_lib.MQ_SUITE_AES128GCM, _lib.MQ_SUITE_CHACHA20]))
+        rows = {}
+        rows["init"] = len(keys); keys.append(key_material(_lib.MQ_SUITE_AES128GCM, client))
+        rows["hs"] = len(keys); keys.append(key_material(suite, rng.bytes(32)))
+        g0 = key_material(suite, rng.bytes(32))
+        g1 = key_material(suite, rng.bytes(32))
+        g1.hp[:] = g0.hp[:]  # HP keys survive key updates (keys.rs:386-414)
+        rows["g0"] = len(keys); keys.append(g0)
+        rows["g1"] = len(keys); keys.append(g1)
+        conns[c]["initial_row"], conns[c]["handshake_row"] = rows["init"], rows["hs"]
+        conns[c]["app_row"] = [0, rows["g0"], rows["g1"]]
+        conns[c]["dcid_len"] = len(dcid)
+        conns[c]["flags"] = recv.HAS_INITIAL | recv.HAS_HANDSHAKE | recv.HAS_APP | recv.HAS_NEXT
+        dg = [[("init", 0, 0, 0, rng.bytes(int(rng.integers(30, 300))), False),
+               ("hs", 1, 0, 0, rng.bytes(int(rng.integers(20, 200))), False)],
+              [("init", 0, 0, 1, rng.bytes(40), False)],
+              [("hs", 1, 0, 1, rng.bytes(int(rng.integers(5, 100))), False),
+               ("g0", 2, 0, 0, rng.bytes(int(rng.integers(1, 50))), False)]]
+        flip = int(rng.integers(5, n_app - 5))
+        pn = 0
+        for k in range(n_app):
+            pn += int(rng.choice([1, 1, 1, 2, 3, 200, 40000]))
+            gen = "g1" if k >= flip else "g0"
+            tamper = bool(rng.random() < 0.08) and k not in (flip, flip - 1)
+            dg.append([(gen, 2, 1 if gen == "g1" else 0, pn, rng.bytes(int(rng.integers(0, 1300))), tamper)])
+        scripts.append((dcid, rows, dg))
+    return keys, conns, scripts
+
+
+def protect_one(orc, keys, dcid, level, row, phase, pn, largest, frames, pad):
+    cs = send.make_conns([dcid], [b"\x01\x02\x03\x04"], [[row, row, row]], phase)
+    req = np.zeros(1, dtype=send.REQ_DTYPE)
+    req["pn"], req["largest_acked"], req["frame_len"] = pn, largest, len(frames)
+    req["out_cap"], req["level"] = 4096, level
+    req["flags"] = send.PAD_TO_MIN if pad else 0
+    out = np.zeros(4096, dtype=np.uint8)
+    st, ln = orc.batch_protect(keys, cs, np.frombuffer(frames + b"\0", dtype=np.uint8), out, req, _lib.MQ_SUITE_MIXED)
+    assert st[0] == 0
+    return out[:ln[0]].tobytes()
+
+
+def assemble(orc, keys, conns, scripts, seed=1, extras=True):
+    """Interleave the connections' datagrams (per-connection order kept) into one arena."""
+    rng = np.random.default_rng(seed + 100)
+    largest = np.zeros((len(scripts), 3), dtype=np.int64)  # what the receiver will have seen
+    queues = []
+    for c, (dcid, rows, dgs) in enumerate(scripts):
+        q = []
+        for parts in dgs:
+            blob = b""
+            for (name, level, phase, pn, frames, tamper) in parts:
+                la = int(largest[c, level])
+                p = protect_one(orc, keys, dcid, level, rows[name], phase, pn, la, frames,
+                                pad=(level == 0 and len(parts) > 1))
+                if tamper:
+                    b = bytearray(p)
+                    b[-20] ^= 0x10
+                    p = bytes(b)
+                else:
+                    largest[c, level] = max(la, pn)
+                blob += p
+            q.append((c, blob))
+        queues.append(q)
+    order = []
+    idx = [0] * len(queues)
+    while any(idx[c] < len(queues[c]) for c in range(len(queues))):
+        c = int(rng.choice([k for k in range(len(queues)) if idx[k] < len(queues[k])]))
+        order.append(queues[c][idx[c]])
+        idx[c] += 1
+    if extras:
+        c0 = 0
+        vn = bytes([0x80]) + bytes(4) + bytes([0]) + bytes([0]) + b"\x00\x00\x00\x01"
+        retry = bytes([0xF0]) + (1).to_bytes(4, "big") + bytes([0, 0]) + rng.bytes(20)
+        zrtt = bytes([0xD0]) + (1).to_bytes(4, "big") + bytes([0, 0]) + packet.encode_varint(10) + rng.bytes(10)
+        trunc = bytes([0xC0]) + (1).to_bytes(4, "big") + bytes([30]) + rng.bytes(5)  # DCID runs past the end
+        order += [(c0, vn), (c0, retry), (c0, zrtt + bytes([0x40]) + rng.bytes(30)), (c0, trunc)]
+        order.append((c0, bytes([0x40])))                      # shorter than 1 + dcid_len -> BTS
+        order.append((1, bytes([0x45]) + rng.bytes(60)))       # phase flip garbage
+    dgrams = np.zeros(len(order), dtype=recv.DGRAM_DTYPE)
+    pos, blobs = 0, []
+    for i, (c, blob) in enumerate(order):
+        pos = (pos + 7) // 8 * 8 if i % 3 else pos  # some unaligned datagrams
+        dgrams[i]["offset"], dgrams[i]["len"], dgrams[i]["conn"] = pos, len(blob), c
+        blobs.append((pos, blob))
+        pos += len(blob)
+    arena = np.zeros(pos + 64, dtype=np.uint8)
+    for o, b in blobs:
+        arena[o:o + len(b)] = np.frombuffer(b, dtype=np.uint8)
+    return arena, dgrams
