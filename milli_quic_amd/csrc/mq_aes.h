@@ -1,8 +1,14 @@
 // mq_aes.h — AES-128 and GF(2^128) building blocks for gfx950 without AES / carry-less-multiply
 // instructions, shared by the AES-128-GCM packet kernels (mq_aes.hip) and the batched Initial key
 // derivation (mq_derive.hip):
-//   * AES-128 rounds from one T-table (T0, 1 KiB) in LDS replicated kTReplicas x per workgroup
-//     (entry x, replica lane & 7 -> fewer bank conflicts), T1..T3 by rotation (FIPS-197 §5.1);
+//   * AES-128 rounds from T-tables in LDS (FIPS-197 §5.1). The packet tile kernels use a wide
+//     table (T0 and T2 = ror(T0, 16), 32 replicas each, 64 KiB): one v_perm_b32 forms each
+//     lookup address, every ds_read_b32 is bank-conflict-free, and a round column needs one
+//     rotation. The one-block-per-lane kernels (HP pre-pass, key derivation) keep a small table
+//     (T0 only, 8 replicas, 8 KiB) because they run too few rounds per workgroup to pay for more;
+//   * GHASH multiplies by H^8 in the single-key tile kernels go through an LDS table of
+//     (v x^(4p)) * H^8 for every nibble position p and value v (8 KiB): 32 conflict-free
+//     ds_read_b128 and XORs per multiply, no reduction;
 //   * GHASH multiplies in the bit-reflected polynomial basis with 32x32 carry-less products built
 //     from integer v_mad_u64_u32 on bit-holed operands (4-bit spacing, <= 8 terms per output
 //     position, so no carry reaches the next kept bit), Karatsuba 128 -> 64 -> 32 (9 products per
@@ -32,7 +38,6 @@ __constant__ uint8_t kSbox[256] = {
     0x8c, 0xa1, 0x89, 0x0d, 0xbf, 0xe6, 0x42, 0x68, 0x41, 0x99, 0x2d, 0x0f, 0xb0, 0x54, 0xbb, 0x16};
 
 constexpr int kTReplicas = 8;
-constexpr int kAesWaves = 4;  // waves (tiles) per workgroup sharing one T-table
 __shared__ uint32_t g_t0[256 * kTReplicas];
 
 __device__ __forceinline__ void build_t0(int tid, int nthreads) {
@@ -120,6 +125,17 @@ __device__ __forceinline__ uint64_t bmul32(uint32_t x, const uint32_t (&y)[4]) {
          (z3 & 0x8888888888888888ull);
 }
 
+// 256-bit product p7..p0 -> a = p mod (x^128 + x^7 + x^2 + x + 1): x^(128+j) -> x^j + x^(j+1) +
+// x^(j+2) + x^(j+7)
+__device__ __forceinline__ void gf_fold(uint32_t p0, uint32_t p1, uint32_t p2, uint32_t p3, uint32_t p4,
+                                        uint32_t p5, uint32_t p6, uint32_t p7, uint32_t (&a)[4]) {
+  const uint32_t t = (p7 >> 31) ^ (p7 >> 30) ^ (p7 >> 25);
+  a[0] = p0 ^ p4 ^ (p4 << 1) ^ (p4 << 2) ^ (p4 << 7) ^ t ^ (t << 1) ^ (t << 2) ^ (t << 7);
+  a[1] = p1 ^ p5 ^ ((p5 << 1) | (p4 >> 31)) ^ ((p5 << 2) | (p4 >> 30)) ^ ((p5 << 7) | (p4 >> 25));
+  a[2] = p2 ^ p6 ^ ((p6 << 1) | (p5 >> 31)) ^ ((p6 << 2) | (p5 >> 30)) ^ ((p6 << 7) | (p5 >> 25));
+  a[3] = p3 ^ p7 ^ ((p7 << 1) | (p6 >> 31)) ^ ((p7 << 2) | (p6 >> 30)) ^ ((p7 << 7) | (p6 >> 25));
+}
+
 // a = a * b mod (x^128 + x^7 + x^2 + x + 1), b prepared
 __device__ __forceinline__ void gf_mul(uint32_t (&a)[4], const GfOp& b) {
   const uint32_t c0 = a[0] ^ a[2], c1 = a[1] ^ a[3];
@@ -138,12 +154,175 @@ __device__ __forceinline__ void gf_mul(uint32_t (&a)[4], const GfOp& b) {
   // P = L + M x^64 + H x^128  (8 words)
   const uint32_t p0 = L[0], p1 = L[1], p2 = L[2] ^ M[0], p3 = L[3] ^ M[1];
   const uint32_t p4 = H[0] ^ M[2], p5 = H[1] ^ M[3], p6 = H[2], p7 = H[3];
-  // fold x^(128+j) -> x^j + x^(j+1) + x^(j+2) + x^(j+7)
-  const uint32_t t = (p7 >> 31) ^ (p7 >> 30) ^ (p7 >> 25);
-  a[0] = p0 ^ p4 ^ (p4 << 1) ^ (p4 << 2) ^ (p4 << 7) ^ t ^ (t << 1) ^ (t << 2) ^ (t << 7);
-  a[1] = p1 ^ p5 ^ ((p5 << 1) | (p4 >> 31)) ^ ((p5 << 2) | (p4 >> 30)) ^ ((p5 << 7) | (p4 >> 25));
-  a[2] = p2 ^ p6 ^ ((p6 << 1) | (p5 >> 31)) ^ ((p6 << 2) | (p5 >> 30)) ^ ((p6 << 7) | (p5 >> 25));
-  a[3] = p3 ^ p7 ^ ((p7 << 1) | (p6 >> 31)) ^ ((p7 << 2) | (p6 >> 30)) ^ ((p7 << 7) | (p6 >> 25));
+  gf_fold(p0, p1, p2, p3, p4, p5, p6, p7, a);
+}
+
+// ---- tables of the packet tile kernels (mq_aes.hip): one static LDS block per workgroup --------
+//  [0, 8 KiB)       GHASH table (single-key kernels): entry (p, v) at byte 256 p + 16 v holds
+//                   (v x^(4p)) * H^8 as 4 reflected words, p = nibble position 0..31 of the
+//                   operand (nibble p = bits 4p..4p+3 of the reflected value), v = its value.
+//                   a * H^8 = XOR over p of entry (p, nibble p of a). The 16 entries of one
+//                   position cover the 64 banks once, so any lane mix reads conflict-free.
+//  [8 KiB, 72 KiB)  wide T-table: row x (256 B) = 32 replicas of T0[x], then 32 replicas of
+//                   T2[x] = ror(T0[x], 16). Lane l reads replica l & 31, so the 32 lanes of each
+//                   ds_read_b32 lane group hit 32 distinct banks. The byte address of
+//                   "row = byte k of s" is perm(s, 4 (l & 31) [+ 128 for T2]) — one v_perm_b32.
+constexpr uint32_t kGhBytes = 8192, kTwBytes = 65536;
+constexpr int kAesWaves = 8;  // tile waves per workgroup: 72 KiB tables + 8 x 10 KiB images = 152 KiB
+__shared__ __attribute__((aligned(16))) uint32_t g_aes_lds[(kGhBytes + kTwBytes) / 4];
+
+__device__ __forceinline__ uint32_t xtime8(uint32_t s) { return ((s << 1) ^ ((s & 0x80) ? 0x11bu : 0u)) & 0xffu; }
+
+__device__ __forceinline__ void build_tw(int tid, int nthreads) {
+  uint4* tw = (uint4*)((uint8_t*)g_aes_lds + kGhBytes);
+  for (int e = tid; e < 256 * 16; e += nthreads) {  // 16-B group e: row e >> 4, quarter e & 15
+    const uint32_t s = kSbox[e >> 4], s2 = xtime8(s);
+    const uint32_t t0 = (s2 << 24) | (s << 16) | (s << 8) | (s2 ^ s);
+    const uint32_t v = (e & 8) ? ror(t0, 16) : t0;
+    tw[e] = make_uint4(v, v, v, v);
+  }
+}
+
+// this lane's replica byte offsets into a T-table row: T0 (r0) and T2 (r2)
+struct TwLane { uint32_t r0, r2; };
+__device__ __forceinline__ TwLane tw_lane() {
+  const uint32_t r = (threadIdx.x & 31u) * 4u;
+  return TwLane{r, r + 128u};
+}
+// T-table entry of row "byte k of s" from the half selected by rsel (L.r0: T0, L.r2: T2)
+__device__ __forceinline__ uint32_t twl(uint32_t s, int k, uint32_t rsel) {
+  const uint32_t addr = __builtin_amdgcn_perm(s, rsel, 0x0c0c0000u | ((4u + (uint32_t)k) << 8));
+  return *(const uint32_t*)((const uint8_t*)g_aes_lds + kGhBytes + addr);
+}
+
+// AES-128 encryption of a block of big-endian column words with the wide table:
+// T1[x] = ror(T0[x], 8) and T3[x] = ror(T2[x], 8), so each output column is
+// T0[a] ^ T2[c] ^ ror(T0[b] ^ T2[d], 8) ^ k; the final round takes S[x] from T2 byte 3,
+// T0 byte 2, T0 byte 1 and T2 byte 0.
+__device__ __forceinline__ void aes128_block(const AesRk& rk, const TwLane& L, uint32_t& s0, uint32_t& s1,
+                                             uint32_t& s2, uint32_t& s3) {
+#if MQ_PROF_SKIP & 16
+  s0 ^= rk.w[0]; s1 ^= rk.w[41]; s2 ^= rk.w[42] ^ L.r0; s3 ^= rk.w[43];
+  return;
+#endif
+  s0 ^= rk.w[0]; s1 ^= rk.w[1]; s2 ^= rk.w[2]; s3 ^= rk.w[3];
+#pragma unroll
+  for (int r = 1; r < 10; ++r) {
+    const uint32_t t0 = twl(s0, 3, L.r0) ^ twl(s2, 1, L.r2) ^ ror(twl(s1, 2, L.r0) ^ twl(s3, 0, L.r2), 8) ^ rk.w[4 * r];
+    const uint32_t t1 = twl(s1, 3, L.r0) ^ twl(s3, 1, L.r2) ^ ror(twl(s2, 2, L.r0) ^ twl(s0, 0, L.r2), 8) ^ rk.w[4 * r + 1];
+    const uint32_t t2 = twl(s2, 3, L.r0) ^ twl(s0, 1, L.r2) ^ ror(twl(s3, 2, L.r0) ^ twl(s1, 0, L.r2), 8) ^ rk.w[4 * r + 2];
+    const uint32_t t3 = twl(s3, 3, L.r0) ^ twl(s1, 1, L.r2) ^ ror(twl(s0, 2, L.r0) ^ twl(s2, 0, L.r2), 8) ^ rk.w[4 * r + 3];
+    s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+  }
+  auto fin = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
+    return (__builtin_amdgcn_perm(twl(a, 3, L.r2), twl(b, 2, L.r0), 0x07020c0cu) |
+            __builtin_amdgcn_perm(twl(c, 1, L.r0), twl(d, 0, L.r2), 0x0c0c0500u)) ^ k;
+  };
+  const uint32_t o0 = fin(s0, s1, s2, s3, rk.w[40]), o1 = fin(s1, s2, s3, s0, rk.w[41]),
+                 o2 = fin(s2, s3, s0, s1, rk.w[42]), o3 = fin(s3, s0, s1, s2, rk.w[43]);
+  s0 = o0; s1 = o1; s2 = o2; s3 = o3;
+}
+
+// Two independent blocks a, b through the wide table with their rounds interleaved: twice the
+// independent LDS reads per round, so the lookup latency of one block hides behind the other's.
+__device__ __forceinline__ void aes128_block2(const AesRk& rk, const TwLane& L, uint32_t (&a)[4], uint32_t (&b)[4]) {
+#if MQ_PROF_SKIP & 16
+  a[0] ^= rk.w[0]; a[1] ^= rk.w[41]; a[2] ^= L.r0; b[0] ^= rk.w[1]; b[1] ^= rk.w[42]; b[3] ^= L.r2;
+  return;
+#endif
+#pragma unroll
+  for (int q = 0; q < 4; ++q) { a[q] ^= rk.w[q]; b[q] ^= rk.w[q]; }
+#pragma unroll
+  for (int r = 1; r < 10; ++r) {
+    uint32_t ta[4], tb[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int q1 = (q + 1) & 3, q2 = (q + 2) & 3, q3 = (q + 3) & 3;
+      ta[q] = twl(a[q], 3, L.r0) ^ twl(a[q2], 1, L.r2) ^ ror(twl(a[q1], 2, L.r0) ^ twl(a[q3], 0, L.r2), 8) ^ rk.w[4 * r + q];
+      tb[q] = twl(b[q], 3, L.r0) ^ twl(b[q2], 1, L.r2) ^ ror(twl(b[q1], 2, L.r0) ^ twl(b[q3], 0, L.r2), 8) ^ rk.w[4 * r + q];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { a[q] = ta[q]; b[q] = tb[q]; }
+  }
+  uint32_t oa[4], ob[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int q1 = (q + 1) & 3, q2 = (q + 2) & 3, q3 = (q + 3) & 3;
+    oa[q] = (__builtin_amdgcn_perm(twl(a[q], 3, L.r2), twl(a[q1], 2, L.r0), 0x07020c0cu) |
+             __builtin_amdgcn_perm(twl(a[q2], 1, L.r0), twl(a[q3], 0, L.r2), 0x0c0c0500u)) ^ rk.w[40 + q];
+    ob[q] = (__builtin_amdgcn_perm(twl(b[q], 3, L.r2), twl(b[q1], 2, L.r0), 0x07020c0cu) |
+             __builtin_amdgcn_perm(twl(b[q2], 1, L.r0), twl(b[q3], 0, L.r2), 0x0c0c0500u)) ^ rk.w[40 + q];
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) { a[q] = oa[q]; b[q] = ob[q]; }
+}
+
+// a = x^i * h (reflected basis), 0 <= i < 128: shift into 8 words, then fold
+__device__ __forceinline__ void gf_mul_xi(const uint32_t (&h)[4], uint32_t i, uint32_t (&a)[4]) {
+  const uint32_t r = i & 31u, q = i >> 5;
+  uint32_t sh[5];
+  sh[0] = h[0] << r;
+#pragma unroll
+  for (int k = 1; k < 4; ++k) sh[k] = r ? ((h[k] << r) | (h[k - 1] >> (32u - r))) : h[k];
+  sh[4] = r ? h[3] >> (32u - r) : 0u;
+  uint32_t p[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      if (k - t >= 0 && k - t <= 4) v = (q == (uint32_t)t) ? sh[k - t] : v;
+    p[k] = v;
+  }
+  gf_fold(p[0], p[1], p[2], p[3], p[4], p[5], p[6], p[7], a);
+}
+
+// GHASH table for multiplier h (reflected words), built by the whole workgroup: basis entries
+// (p, 1 << b) = x^(4p+b) h first, then every other entry as the XOR of its bits' basis entries.
+// Ends with a workgroup barrier.
+__device__ __forceinline__ void build_gh(const uint32_t (&h)[4], int tid, int nthreads) {
+  uint4* gh = (uint4*)g_aes_lds;
+  for (int i = tid; i < 128; i += nthreads) {
+    uint32_t a[4];
+    gf_mul_xi(h, (uint32_t)i, a);
+    gh[(i >> 2) * 16 + (1 << (i & 3))] = make_uint4(a[0], a[1], a[2], a[3]);
+  }
+  __syncthreads();
+  for (int e = tid; e < 512; e += nthreads) {
+    const int p = e >> 4, v = e & 15;
+    if (v != 0 && (v & (v - 1)) == 0) continue;  // basis entry
+    uint4 acc = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      if ((v >> b) & 1) {
+        const uint4 x = gh[p * 16 + (1 << b)];
+        acc.x ^= x.x; acc.y ^= x.y; acc.z ^= x.z; acc.w ^= x.w;
+      }
+    gh[e] = acc;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t byte_of(uint32_t x, int m) {
+  return m == 0 ? (x & 0xffu) : (m == 3 ? (x >> 24) : __builtin_amdgcn_ubfe(x, 8 * m, 8));
+}
+
+// a = a * H^8 through the GHASH table: nibble 2m of word w sits (times 16) in byte m of
+// (a[w] << 4) & 0xf0f0f0f0, nibble 2m+1 in byte m of a[w] & 0xf0f0f0f0 — each a ready byte offset
+// of its entry within its position's 256-B row.
+__device__ __forceinline__ void gh_mul_tab(uint32_t (&a)[4]) {
+  uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const uint32_t lo = (a[w] << 4) & 0xf0f0f0f0u, hi = a[w] & 0xf0f0f0f0u;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const uint4 e0 = *(const uint4*)((const uint8_t*)g_aes_lds + 256u * (8 * w + 2 * m) + byte_of(lo, m));
+      const uint4 e1 = *(const uint4*)((const uint8_t*)g_aes_lds + 256u * (8 * w + 2 * m + 1) + byte_of(hi, m));
+      r0 ^= e0.x ^ e1.x; r1 ^= e0.y ^ e1.y; r2 ^= e0.z ^ e1.z; r3 ^= e0.w ^ e1.w;
+    }
+  }
+  a[0] = r0; a[1] = r1; a[2] = r2; a[3] = r3;
 }
 
 }  // namespace mq

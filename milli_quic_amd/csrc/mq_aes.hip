@@ -5,12 +5,14 @@
 // composed as in src/connection/transmit.rs:499-755 and src/connection/recv.rs:340-421,953-1025.
 //
 // gfx950 has no AES or carry-less-multiply instructions, so:
-//   * AES-128 rounds use one T-table (T0, 1 KiB) in LDS replicated 8x per workgroup (entry x,
-//     replica lane&7 -> fewer bank conflicts), T1..T3 by rotation, round keys in VGPRs;
-//   * GHASH multiplies in the bit-reflected polynomial basis with 32x32 carry-less products
-//     built from integer v_mad_u64_u32 on bit-holed operands (4-bit spacing, <= 8 terms per
-//     output position, so no carry ever reaches the next kept bit), Karatsuba 128 -> 64 -> 32
-//     (9 products per multiply), then the x^128 + x^7 + x^2 + x + 1 fold.
+//   * AES-128 rounds use the wide T-table (T0 and T2, 32 replicas each, 64 KiB per workgroup,
+//     mq_aes.h): one v_perm_b32 per lookup address, conflict-free ds_read_b32, one rotation per
+//     round column; round keys in SGPRs (single-key kernels) or VGPRs;
+//   * GHASH: in the single-key kernels every Horner step's multiply by H^8 is 32 table reads
+//     (mq_aes.h gh_mul_tab, built per workgroup from H^8); the final multiply by H^(8-j) and all
+//     multiplies of the multi-key kernels use the bit-holed integer product (gf_mul).
+// Workgroups of kAesWaves waves are persistent (one per CU, LDS-bound), so the 72 KiB of tables
+// are built once per CU and each wave walks tiles w, w + stride, ...
 // Work split per tile (mq_tile.h): keystream block b of a packet (b = 0: E_K(J0), b >= 1:
 // counter b+1) on lane b % 8; GHASH interleaved over the octet with H^8 (precomputed on the
 // host per key) and a final multiply by H^(8-j).
@@ -23,7 +25,7 @@ namespace mq {
 // blocks 8k + j with multiplier H^8, then one final multiply by H^(8-j) (row->H[7-j], computed on
 // the host per key), then the octet XOR. Every lane of the octet returns the same value
 // (reflected basis).
-template <class S>
+template <bool TAB, class S>
 __device__ __forceinline__ void ghash(const S& sp, typename S::off_t pkt, typename S::off_t pay,
                                       uint32_t aad_len, uint32_t ct_len, const KeyRow* row, int j,
                                       bool act, uint32_t (&y)[4]) {
@@ -34,9 +36,11 @@ __device__ __forceinline__ void ghash(const S& sp, typename S::off_t pkt, typena
   uint32_t hp[4];
   GfOp m8, mlast;
   {
+    if (!TAB) {
 #pragma unroll
-    for (int w = 0; w < 4; ++w) hp[w] = brev(row->H[7][w]);
-    m8 = gf_prepare(hp);
+      for (int w = 0; w < 4; ++w) hp[w] = brev(row->H[7][w]);
+      m8 = gf_prepare(hp);
+    }
     const int e = 7 - j;  // H^(8-j)
 #pragma unroll
     for (int w = 0; w < 4; ++w) hp[w] = brev(row->H[e][w]);
@@ -81,7 +85,8 @@ __device__ __forceinline__ void ghash(const S& sp, typename S::off_t pkt, typena
       absorb(b, m);
       b = where(k + 1);
       load_words<4>(sp, b.src, m);
-      gf_mul(acc, m8);
+      if (TAB) gh_mul_tab(acc);
+      else gf_mul(acc, m8);
     }
     absorb(b, m);
     gf_mul(acc, mlast);
@@ -90,15 +95,27 @@ __device__ __forceinline__ void ghash(const S& sp, typename S::off_t pkt, typena
   for (int w = 0; w < 4; ++w) y[w] = oct_xor(acc[w]);
 }
 
-struct AesPolicy {
+// TAB: single-key kernel with the GHASH table of H^8 in LDS
+template <bool TAB>
+struct AesPolicyT {
   static constexpr uint32_t kSuite = MQ_SUITE_AES128GCM;
 
   // keystream of block index b (0: E(J0), b >= 1: counter b + 1) as little-endian data words
-  static __device__ __forceinline__ void ctr_block(const AesRk& rk, uint32_t rb, const uint32_t (&nb)[3],
+  static __device__ __forceinline__ void ctr_block(const AesRk& rk, const TwLane& rb, const uint32_t (&nb)[3],
                                                    uint32_t b, uint32_t (&ks)[4]) {
     uint32_t s0 = nb[0], s1 = nb[1], s2 = nb[2], s3 = b == 0 ? 1u : b + 1;
     aes128_block(rk, rb, s0, s1, s2, s3);
     ks[0] = bswap32(s0); ks[1] = bswap32(s1); ks[2] = bswap32(s2); ks[3] = bswap32(s3);
+  }
+
+  // blocks b and b + 8 (the lane's next iteration) at once
+  static __device__ __forceinline__ void ctr_block2(const AesRk& rk, const TwLane& rb, const uint32_t (&nb)[3],
+                                                    uint32_t b, uint32_t (&ks)[4], uint32_t (&ks2)[4]) {
+    uint32_t x[4] = {nb[0], nb[1], nb[2], b == 0 ? 1u : b + 1};
+    uint32_t y[4] = {nb[0], nb[1], nb[2], b + kLanesPerPkt + 1};
+    aes128_block2(rk, rb, x, y);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { ks[q] = bswap32(x[q]); ks2[q] = bswap32(y[q]); }
   }
 
   template <class S>
@@ -112,9 +129,10 @@ struct AesPolicy {
   }
 
   // AesHeaderProtection::mask (rustcrypto.rs:175-186): AES-ECB(hp, sample)[0..5]
-  template <class S>
+  // (rb: TwLane in the tile kernels, the small table's replica offset in the per-lane kernels)
+  template <class S, class T>
   static __device__ __forceinline__ void hp_mask(const S& sp, typename S::off_t sample_at,
-                                                 const KeyRow* row, uint32_t rb, uint32_t& m0, uint32_t& m1) {
+                                                 const KeyRow* row, const T& rb, uint32_t& m0, uint32_t& m1) {
     uint32_t smp[4];
     load_words<4>(sp, sample_at, smp);
     AesRk hk;
@@ -154,7 +172,7 @@ struct AesPolicy {
   template <class S, class G>
   static __device__ __forceinline__ void seal(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j, G& stg) {
     const mq_pkt_desc& d = c.d;
-    const uint32_t rb = (threadIdx.x & (kTReplicas - 1)) * 4;
+    const TwLane rb = tw_lane();
     const uint32_t aad_len = c.act ? (uint32_t)d.pn_offset + d.pn_len : 0u;
     const uint32_t P = c.act ? d.len - aad_len - 16 : 0u;
     const typename S::off_t pay = pkt + aad_len;
@@ -177,10 +195,41 @@ struct AesPolicy {
       for (int k = 0; k < 44; ++k) pin(rk.w[k]);
       pin(nb[0]); pin(nb[1]); pin(nb[2]);
       stg.issue();
-      for (uint32_t it = 0; it < Imax; ++it) {
+      auto first_iter = [&]() {  // before any packet byte is touched
+        stg.complete();
+        const bool rec = c.act && is_record(d);
+        if (wave_any(rec)) {  // TLS record: header (AAD) and inner content type before any use
+          if (rec && j == 0) write_record_header(sp, pkt, d);
+          wave_sync();
+        }
+      };
+      auto use_block = [&](uint32_t b, const uint32_t (&ks)[4]) {
+        if (c.act && b < nblk) {
+          if (b == 0) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) ej0[k] = ks[k];
+          } else {
+            xor_block(sp, pay, b, P, ks);
+          }
+        }
+      };
+      uint32_t it = 0;
+      while (it < Imax) {
         const uint32_t b = (uint32_t)j + kLanesPerPkt * it;
-        const bool a = c.act && b < nblk;
         const bool is_hp = hp_on && !hp_post && it == hp_it && (uint32_t)j == hp_lane;
+        const bool hp_next = hp_on && !hp_post && it + 1 == hp_it && (uint32_t)j == hp_lane;
+        // iterations it and it + 1 together unless either carries an HP block (its sample is
+        // ciphertext of iteration 0, and its lane needs the HP key)
+        if (it + 1 < Imax && !wave_any(is_hp || hp_next)) {
+          uint32_t ks[4], ks2[4];
+          ctr_block2(rk, rb, nb, b, ks, ks2);
+          if (it == 0) first_iter();
+          use_block(b, ks);
+          use_block(b + kLanesPerPkt, ks2);
+          wave_sync();
+          it += 2;
+          continue;
+        }
         uint32_t ks[4];
         if (wave_any(is_hp)) {  // iteration carrying HP blocks: per-lane key/input
           AesRk hk;
@@ -197,28 +246,17 @@ struct AesPolicy {
         } else {
           ctr_block(rk, rb, nb, b, ks);
         }
-        if (it == 0) {
-          stg.complete();
-          const bool rec = c.act && is_record(d);
-          if (wave_any(rec)) {  // TLS record: header (AAD) and inner content type before any use
-            if (rec && j == 0) write_record_header(sp, pkt, d);
-            wave_sync();
-          }
-        }
-        if (a && b == 0) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) ej0[k] = ks[k];
-        } else if (a) {
-          xor_block(sp, pay, b, P, ks);
-        }
-        wave_sync();
+        if (it == 0) first_iter();
+        if (!is_hp) use_block(b, ks);
+        wave_sync();  // this iteration's ciphertext (the HP sample) is visible to the next
+        it += 1;
       }
       if (Imax == 0) stg.complete();
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) ej0[k] = oct_bcast0(ej0[k]);
     uint32_t y[4], tag[4];
-    ghash(sp, pkt, pay, aad_len, P, row, j, c.act, y);
+    ghash<TAB>(sp, pkt, pay, aad_len, P, row, j, c.act, y);
     tag_words(y, ej0, tag);
     if (c.act && j == 0) store_words<4>(sp, pay + P, tag);
     wave_sync();
@@ -236,7 +274,7 @@ struct AesPolicy {
     const mq_pkt_desc& d = c.d;
     stg.issue();
     stg.complete();
-    const uint32_t rb = (threadIdx.x & (kTReplicas - 1)) * 4;
+    const TwLane rb = tw_lane();
     uint32_t pn_len = d.pn_len;
     uint8_t orig_b0 = 0;
     uint32_t orig_pn = 0;
@@ -276,7 +314,7 @@ struct AesPolicy {
     const uint32_t C = (nblk + kLanesPerPkt - 1) / kLanesPerPkt;
     const uint32_t Cmax = wave_max_u32(c.act ? C : 0u);
     uint32_t y[4];
-    ghash(sp, pkt, pay, aad_len, P, row, j, c.act, y);
+    ghash<TAB>(sp, pkt, pay, aad_len, P, row, j, c.act, y);
     AesRk rk;
     load_rk(row->aes_rk, rk);
     uint32_t ks0[4];  // block j: E(J0) on lane 0, keystream elsewhere
@@ -294,12 +332,19 @@ struct AesPolicy {
     }
     wave_sync();
     if (c.act && j >= 1 && (uint32_t)j < nblk) xor_block(sp, pay, (uint32_t)j, P, ks0);
-    for (uint32_t it = 1; it < Cmax; ++it) {
+    uint32_t it = 1;
+    for (; it + 1 < Cmax; it += 2) {  // two iterations per pass (interleaved AES rounds)
       const uint32_t b = (uint32_t)j + kLanesPerPkt * it;
-      const bool a = c.act && b < nblk;
+      uint32_t ks[4], ks2[4];
+      ctr_block2(rk, rb, nb, b, ks, ks2);
+      if (c.act && b < nblk) xor_block(sp, pay, b, P, ks);
+      if (c.act && b + kLanesPerPkt < nblk) xor_block(sp, pay, b + kLanesPerPkt, P, ks2);
+    }
+    if (it < Cmax) {
+      const uint32_t b = (uint32_t)j + kLanesPerPkt * it;
       uint32_t ks[4];
       ctr_block(rk, rb, nb, b, ks);
-      if (a) xor_block(sp, pay, b, P, ks);
+      if (c.act && b < nblk) xor_block(sp, pay, b, P, ks);
     }
     if (direct && hdr_written && !c.act) {
       sp.st8(pkt, orig_b0);
@@ -312,19 +357,34 @@ struct AesPolicy {
 
 using namespace mq;
 
-// Tile kernels: kAesWaves waves per workgroup share the T-table; one tile per wave. The "1"
-// variants run when the key table has a single row (round keys and H powers in SGPRs).
+// Tile kernels: persistent workgroups of kAesWaves waves share the LDS tables (built once per
+// workgroup); wave w walks tiles blockIdx.x * kAesWaves + w + k * gridDim.x * kAesWaves. The "1"
+// variants run when the key table has a single row: round keys and H powers in SGPRs, and the
+// GHASH table of that row's H^8.
+template <bool SINGLE>
+__device__ __forceinline__ void aes_tables(const KeyRow* __restrict__ kt) {
+  build_tw(threadIdx.x, blockDim.x);
+  if (SINGLE) {
+    uint32_t h8[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) h8[w] = brev(kt[0].H[7][w]);
+    build_gh(h8, threadIdx.x, blockDim.x);  // ends with a barrier
+  } else {
+    __syncthreads();
+  }
+}
+
 #define MQ_AES_KERNELS(NAME_SEAL, NAME_OPEN, SINGLE)                                                      \
   extern "C" __global__ __launch_bounds__(64 * kAesWaves) void NAME_SEAL(                                 \
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
       const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status) {                                 \
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];                                        \
-    build_t0(threadIdx.x, blockDim.x);                                                                    \
-    __syncthreads();                                                                                      \
-    const uint32_t w = threadIdx.x >> 6;                                                                  \
-    run_tile<AesPolicy, false, SINGLE>(smem + w * kLdsBytes, blockIdx.x * kAesWaves + w, kt, n_rows, arena, \
-                                       arena_len, desc, n, index, n_dev, status, nullptr, nullptr);       \
+    aes_tables<SINGLE>(kt);                                                                               \
+    const uint32_t w = threadIdx.x >> 6, tiles = (n + kPktsPerTile - 1) / kPktsPerTile;                  \
+    for (uint32_t t = blockIdx.x * kAesWaves + w; t < tiles; t += gridDim.x * kAesWaves)                  \
+      run_tile<AesPolicyT<SINGLE>, false, SINGLE>(smem + w * kLdsBytes, t, kt, n_rows, arena, arena_len,  \
+                                                  desc, n, index, n_dev, status, nullptr, nullptr);       \
   }                                                                                                       \
   extern "C" __global__ __launch_bounds__(64 * kAesWaves) void NAME_OPEN(                                 \
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
@@ -332,11 +392,11 @@ using namespace mq;
       const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,    \
       const uint2* __restrict__ hpm) {                                                                    \
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];                                        \
-    build_t0(threadIdx.x, blockDim.x);                                                                    \
-    __syncthreads();                                                                                      \
-    const uint32_t w = threadIdx.x >> 6;                                                                  \
-    run_tile<AesPolicy, true, SINGLE>(smem + w * kLdsBytes, blockIdx.x * kAesWaves + w, kt, n_rows, arena, \
-                                      arena_len, desc, n, index, n_dev, status, pn_out, hpm);             \
+    aes_tables<SINGLE>(kt);                                                                               \
+    const uint32_t w = threadIdx.x >> 6, tiles = (n + kPktsPerTile - 1) / kPktsPerTile;                  \
+    for (uint32_t t = blockIdx.x * kAesWaves + w; t < tiles; t += gridDim.x * kAesWaves)                  \
+      run_tile<AesPolicyT<SINGLE>, true, SINGLE>(smem + w * kLdsBytes, t, kt, n_rows, arena, arena_len,   \
+                                                 desc, n, index, n_dev, status, pn_out, hpm);             \
   }
 MQ_AES_KERNELS(mq_aes_seal_kernel, mq_aes_open_kernel, false)
 MQ_AES_KERNELS(mq_aes_seal1_kernel, mq_aes_open1_kernel, true)
@@ -352,7 +412,7 @@ extern "C" __global__ __launch_bounds__(256) void mq_aes_hp_kernel(
   if (kid >= n_rows || kt[kid].suite != MQ_SUITE_AES128GCM) return;
   GlobalSpace sp{const_cast<uint8_t*>(samples), (uint64_t)n * 16};
   uint32_t m0, m1;
-  AesPolicy::hp_mask(sp, (uint64_t)i * 16, kt + kid, (threadIdx.x & (kTReplicas - 1)) * 4, m0, m1);
+  AesPolicyT<false>::hp_mask(sp, (uint64_t)i * 16, kt + kid, (threadIdx.x & (kTReplicas - 1)) * 4, m0, m1);
   for (int b = 0; b < 4; ++b) masks[5 * (size_t)i + b] = (uint8_t)(m0 >> (8 * b));
   masks[5 * (size_t)i + 4] = (uint8_t)m1;
 }
@@ -372,8 +432,20 @@ extern "C" __global__ __launch_bounds__(256) void mq_aes_open_hp_kernel(
     return;
   GlobalSpace sp{const_cast<uint8_t*>(arena), arena_len};
   uint32_t m0, m1;
-  AesPolicy::hp_mask(sp, at, row, (threadIdx.x & (kTReplicas - 1)) * 4, m0, m1);
+  AesPolicyT<false>::hp_mask(sp, at, row, (threadIdx.x & (kTReplicas - 1)) * 4, m0, m1);
   hpm[i] = make_uint2(m0, m1);
+}
+
+// Persistent grid: one workgroup per CU (152 KiB of LDS each), capped by the tile count.
+static uint32_t aes_grid(uint32_t tiles) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, v = 0;
+    (void)hipGetDevice(&dev);
+    cus = hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0 ? v : 256;
+  }
+  const uint32_t wgs = (tiles + kAesWaves - 1) / kAesWaves;
+  return wgs < (uint32_t)cus ? wgs : (uint32_t)cus;
 }
 
 hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena, uint64_t arena_len,
@@ -381,7 +453,8 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
                          uint8_t* status, uint64_t* pn_out, uint2* hpm, hipStream_t s) {
   const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
   if (tiles == 0) return hipSuccess;
-  const uint32_t blocks = (tiles + kAesWaves - 1) / kAesWaves;
+  const uint32_t blocks = aes_grid(tiles);
+  const size_t dyn = (size_t)kLdsBytes * kAesWaves;
   if (open && hpm) {
     hipLaunchKernelGGL(mq_aes_open_hp_kernel, dim3((n + 255) / 256), dim3(256), 0, s, kt, n_rows, arena,
                        arena_len, desc, n, index, n_dev, hpm);
@@ -390,11 +463,10 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
   }
   if (open)
     hipLaunchKernelGGL(n_rows == 1 ? mq_aes_open1_kernel : mq_aes_open_kernel, dim3(blocks), dim3(64 * kAesWaves),
-                       kLdsBytes * kAesWaves, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status,
-                       pn_out, hpm);
+                       dyn, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm);
   else
     hipLaunchKernelGGL(n_rows == 1 ? mq_aes_seal1_kernel : mq_aes_seal_kernel, dim3(blocks), dim3(64 * kAesWaves),
-                       kLdsBytes * kAesWaves, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status);
+                       dyn, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status);
   return hipGetLastError();
 }
 
