@@ -19,6 +19,8 @@
 #include "mq_aes.h"
 #include "mq_tile.h"
 
+#include <cstdlib>
+
 namespace mq {
 
 // Interleaved GHASH over AAD||pad||CT||pad||[len(A)]64||[len(C)]64 (bit lengths): lane j takes
@@ -381,10 +383,10 @@ __device__ __forceinline__ void aes_tables(const KeyRow* __restrict__ kt) {
       const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status) {                                 \
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];                                        \
     aes_tables<SINGLE>(kt);                                                                               \
-    const uint32_t w = threadIdx.x >> 6, tiles = (n + kPktsPerTile - 1) / kPktsPerTile;                  \
-    for (uint32_t t = blockIdx.x * kAesWaves + w; t < tiles; t += gridDim.x * kAesWaves)                  \
-      run_tile<AesPolicyT<SINGLE>, false, SINGLE>(smem + w * kLdsBytes, t, kt, n_rows, arena, arena_len,  \
-                                                  desc, n, index, n_dev, status, nullptr, nullptr);       \
+    const uint32_t w = threadIdx.x >> 6;                                                                  \
+    run_tiles<AesPolicyT<SINGLE>, false, SINGLE>(smem + w * kLdsBytes, blockIdx.x * kAesWaves + w,        \
+                                                 gridDim.x * kAesWaves, kt, n_rows, arena, arena_len, desc,\
+                                                 n, index, n_dev, status, nullptr, nullptr);              \
   }                                                                                                       \
   extern "C" __global__ __launch_bounds__(64 * kAesWaves) void NAME_OPEN(                                 \
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
@@ -393,10 +395,10 @@ __device__ __forceinline__ void aes_tables(const KeyRow* __restrict__ kt) {
       const uint2* __restrict__ hpm) {                                                                    \
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];                                        \
     aes_tables<SINGLE>(kt);                                                                               \
-    const uint32_t w = threadIdx.x >> 6, tiles = (n + kPktsPerTile - 1) / kPktsPerTile;                  \
-    for (uint32_t t = blockIdx.x * kAesWaves + w; t < tiles; t += gridDim.x * kAesWaves)                  \
-      run_tile<AesPolicyT<SINGLE>, true, SINGLE>(smem + w * kLdsBytes, t, kt, n_rows, arena, arena_len,   \
-                                                 desc, n, index, n_dev, status, pn_out, hpm);             \
+    const uint32_t w = threadIdx.x >> 6;                                                                  \
+    run_tiles<AesPolicyT<SINGLE>, true, SINGLE>(smem + w * kLdsBytes, blockIdx.x * kAesWaves + w,         \
+                                                gridDim.x * kAesWaves, kt, n_rows, arena, arena_len, desc, \
+                                                n, index, n_dev, status, pn_out, hpm);                    \
   }
 MQ_AES_KERNELS(mq_aes_seal_kernel, mq_aes_open_kernel, false)
 MQ_AES_KERNELS(mq_aes_seal1_kernel, mq_aes_open1_kernel, true)
@@ -444,8 +446,14 @@ static uint32_t aes_grid(uint32_t tiles) {
     (void)hipGetDevice(&dev);
     cus = hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0 ? v : 256;
   }
+  static int per_cu = -1;
+  if (per_cu < 0) {  // diagnostic override: workgroups per CU of the grid (0 = one tile per wave)
+    const char* e = getenv("MQ_AES_WGS_PER_CU");
+    per_cu = e ? max(atoi(e), 0) : 1;
+  }
   const uint32_t wgs = (tiles + kAesWaves - 1) / kAesWaves;
-  return wgs < (uint32_t)cus ? wgs : (uint32_t)cus;
+  if (per_cu == 0) return wgs;
+  return wgs < (uint32_t)(cus * per_cu) ? wgs : (uint32_t)(cus * per_cu);
 }
 
 hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena, uint64_t arena_len,

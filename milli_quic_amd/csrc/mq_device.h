@@ -24,6 +24,7 @@ constexpr int kWave = 64;
 constexpr int kPktsPerTile = 8;
 constexpr int kLanesPerPkt = kWave / kPktsPerTile;  // 8: one octet of lanes per packet
 constexpr uint32_t kLdsBytes = 10240;                // LDS per tile (wave) -> 16 waves/CU
+constexpr uint32_t kCuLdsBytes = 160 * 1024;         // LDS per CU (gfx950)
 constexpr uint32_t kSlack = 64;                      // over-read room after the last slot
 
 // Device key-table row (576 B). Filled on the host by mq_keytable_create (mq_host.cpp).

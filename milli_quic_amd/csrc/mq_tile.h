@@ -60,11 +60,13 @@ __device__ __forceinline__ void write_record_header(const S& sp, typename S::off
 
 // Descriptor checks in the order of the oracle (oracle/mq_oracle.c orc_run / orc_protect_packet /
 // orc_unprotect_packet), which follows transmit.rs:593-597,721-725 and recv.rs:364-366,970-973.
-template <uint32_t SUITE, bool OPEN>
+// SINGLE: one-row key table, so the suite check reads row 0 (a scalar load that does not wait
+// for the descriptor).
+template <uint32_t SUITE, bool OPEN, bool SINGLE = false>
 __device__ __forceinline__ int validate(const mq_pkt_desc& d, const KeyRow* kt, uint32_t n_rows,
                                         uint64_t arena_len) {
   if (d.key_id >= n_rows || d.offset + (uint64_t)d.len > arena_len) return MQ_ERR_INVALID_ARG;
-  if (kt[d.key_id].suite != SUITE) return MQ_ERR_SUITE;
+  if ((SINGLE ? kt[0].suite : kt[d.key_id].suite) != SUITE) return MQ_ERR_SUITE;
   const bool no_hp = (d.flags & MQ_PKT_NO_HP) != 0;
   if (is_record(d)) {  // TLS record (record.rs): 5-byte header AAD, no PN, u16 length field
     if (!no_hp || d.pn_offset != 5 || d.pn_len != 0 || d.len > 5u + 0xFFFFu) return MQ_ERR_INVALID_ARG;
@@ -230,6 +232,19 @@ __device__ __forceinline__ bool prepass_pick(uint32_t t, uint32_t suite, const K
 
 // SINGLE_KEY: the key table has one row, so every valid packet uses row 0; the policies then get
 // a wave-uniform row pointer and read key material with scalar loads into SGPRs.
+// Descriptor words of a tile fetched ahead of time (flat batches, run_tiles): lane 8p + j holds
+// dword j of packet p's descriptor (dw) and, for open, dword j < 2 of its HP mask (hm); octet
+// swizzles rebuild the descriptor, so a prefetch costs two VGPRs.
+struct TilePrefetch {
+  bool on;  // wave-uniform
+  uint32_t dw, hm;
+};
+
+template <int K>
+__device__ __forceinline__ uint32_t oct_lane(uint32_t x) {  // lane K of the octet
+  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x18 | (K << 5));
+}
+
 template <class Policy, bool OPEN, bool SINGLE_KEY = false>
 __device__ __forceinline__ void run_tile(uint8_t* smem, uint32_t tile_id, const KeyRow* __restrict__ kt,
                                          uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
@@ -237,7 +252,8 @@ __device__ __forceinline__ void run_tile(uint8_t* smem, uint32_t tile_id, const 
                                          const uint32_t* __restrict__ index,
                                          const uint32_t* __restrict__ n_dev,
                                          uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,
-                                         const uint2* __restrict__ hpm) {
+                                         const uint2* __restrict__ hpm,
+                                         TilePrefetch pf = TilePrefetch{false, 0u, 0u}) {
   const int lane = threadIdx.x & (kWave - 1), p = lane / kLanesPerPkt, j = lane % kLanesPerPkt;
   const uint32_t count = n_dev ? *n_dev : n;
   const uint32_t tile0 = tile_id * kPktsPerTile;
@@ -247,22 +263,35 @@ __device__ __forceinline__ void run_tile(uint8_t* smem, uint32_t tile_id, const 
   c.tile = tile_id;
   const uint32_t t = tile0 + p;
   c.valid = t < count;
-  c.i = c.valid ? (index ? index[t] : t) : 0u;
-  if (c.valid) {
-    c.d = desc[c.i];
-  } else {
-    c.d.offset = 0; c.d.len = 0; c.d.key_id = 0; c.d.pn = 0; c.d.pn_offset = 0; c.d.pn_len = 0;
-    c.d.flags = 0; c.d.reserved = 0;
-  }
   c.pre_hp = OPEN && hpm != nullptr;
   c.otk = (uint32_t*)(smem + kLdsBytes - kScratchBytes + 32u * (uint32_t)p);
   c.hm0 = c.hm1 = 0;
-  if (OPEN && hpm && c.valid) {
-    const uint2 m = hpm[c.i];
-    c.hm0 = m.x;
-    c.hm1 = m.y;
+  if (pf.on) {  // flat batch, words already in registers
+    c.i = t;
+    const uint32_t w0 = oct_lane<0>(pf.dw), w1 = oct_lane<1>(pf.dw), w2 = oct_lane<2>(pf.dw),
+                   w3 = oct_lane<3>(pf.dw), w4 = oct_lane<4>(pf.dw), w5 = oct_lane<5>(pf.dw),
+                   w6 = oct_lane<6>(pf.dw), w7 = oct_lane<7>(pf.dw);
+    c.d.offset = (uint64_t)w1 << 32 | w0;
+    c.d.len = w2; c.d.key_id = w3;
+    c.d.pn = (uint64_t)w5 << 32 | w4;
+    c.d.pn_offset = (uint16_t)w6; c.d.pn_len = (uint8_t)(w6 >> 16); c.d.flags = (uint8_t)(w6 >> 24);
+    c.d.reserved = w7;
+    if (OPEN && hpm) { c.hm0 = oct_lane<0>(pf.hm); c.hm1 = oct_lane<1>(pf.hm); }
+  } else {
+    c.i = c.valid ? (index ? index[t] : t) : 0u;
+    if (c.valid) {
+      c.d = desc[c.i];
+    } else {
+      c.d.offset = 0; c.d.len = 0; c.d.key_id = 0; c.d.pn = 0; c.d.pn_offset = 0; c.d.pn_len = 0;
+      c.d.flags = 0; c.d.reserved = 0;
+    }
+    if (OPEN && hpm && c.valid) {
+      const uint2 m = hpm[c.i];
+      c.hm0 = m.x;
+      c.hm1 = m.y;
+    }
   }
-  c.st = c.valid ? validate<Policy::kSuite, OPEN>(c.d, kt, n_rows, arena_len) : (int)MQ_ERR_INVALID_ARG;
+  c.st = c.valid ? validate<Policy::kSuite, OPEN, SINGLE_KEY>(c.d, kt, n_rows, arena_len) : (int)MQ_ERR_INVALID_ARG;
   c.act = c.valid && c.st == MQ_OK;
   c.pn = c.d.pn;
   const KeyRow* row = SINGLE_KEY ? kt : kt + (c.act ? c.d.key_id : 0u);
@@ -297,6 +326,40 @@ __device__ __forceinline__ void run_tile(uint8_t* smem, uint32_t tile_id, const 
   if (c.valid && j == 0) {
     status[c.i] = (uint8_t)c.st;
     if (OPEN && pn_out && c.st == MQ_OK) pn_out[c.i] = c.pn;
+  }
+}
+
+// Persistent tile loop: this wave runs tiles first, first + stride, ... For flat batches (no
+// index list) the next tile's descriptor words (and HP masks) are loaded while the current tile
+// is processed, so a tile starts without waiting on a descriptor fetch.
+template <class Policy, bool OPEN, bool SINGLE_KEY = false>
+__device__ __forceinline__ void run_tiles(uint8_t* smem, uint32_t first, uint32_t stride, const KeyRow* __restrict__ kt,
+                                          uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
+                                          const mq_pkt_desc* __restrict__ desc, uint32_t n,
+                                          const uint32_t* __restrict__ index, const uint32_t* __restrict__ n_dev,
+                                          uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,
+                                          const uint2* __restrict__ hpm) {
+  const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
+  if (index || n_dev) {
+    for (uint32_t t = first; t < tiles; t += stride)
+      run_tile<Policy, OPEN, SINGLE_KEY>(smem, t, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status,
+                                         pn_out, hpm);
+    return;
+  }
+  const uint32_t lane = threadIdx.x & (kWave - 1), p = lane / kLanesPerPkt, j = lane % kLanesPerPkt;
+  auto fetch = [&](uint32_t t, uint32_t& dw, uint32_t& hm) {
+    const uint32_t i = t * kPktsPerTile + p;
+    const bool ok = t < tiles && i < n;
+    dw = ok ? reinterpret_cast<const uint32_t*>(desc)[(size_t)i * 8 + j] : 0u;
+    hm = (OPEN && hpm && ok && j < 2) ? reinterpret_cast<const uint32_t*>(hpm)[(size_t)i * 2 + j] : 0u;
+  };
+  uint32_t dw, hm;
+  fetch(first, dw, hm);
+  for (uint32_t t = first; t < tiles; t += stride) {
+    const TilePrefetch pf{true, dw, hm};
+    fetch(t + stride, dw, hm);
+    run_tile<Policy, OPEN, SINGLE_KEY>(smem, t, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status,
+                                       pn_out, hpm, pf);
   }
 }
 
