@@ -10,7 +10,8 @@ independent, so there is no data-path collective: scaling "weak").
   value  = sum over ranks of wire bytes x 2 / (t_seal + t_open) / 2^30   [GiB/s]
   roofline.achieved = algorithmic bytes of one seal launch (2 x L per packet: read + write) /
                       its average duration, from HIP events on the launch stream
-  cpu_baseline = the C oracle (oracle/, "port") on a bounded sample, host threads stated
+  cpu_baseline = the C oracle (oracle/, "port") on a bounded sample, host threads stated;
+  cpu_openssl  = OpenSSL EVP running the same composites on that sample (16 threads and 1)
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config b|c|e] [--packets P]
 """
 import argparse
@@ -75,6 +76,35 @@ def cpu_baseline(w, sample, threads, min_seconds=10.0):
     return {"value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
             "sample": f"{n} packets ({wire / 1e6:.1f} MB) of the same workload, seal+open repeated {reps}x "
                       f"(seal {t_seal:.1f}s + open {t_open:.1f}s), oracle/mq_oracle.c on {threads} host threads"}
+
+
+def cpu_openssl(w, sample, threads, min_seconds=3.0):
+    """OpenSSL 3 EVP (libcrypto.so.3, dlopen'ed; its AVX2/AVX-512/AES-NI code paths) running the
+    same seal + open composites (oracle/ossl_baseline.c) on the same bounded sample, on `threads`
+    host threads and on one: the like-for-like stand-in for the reference's RustCrypto backends
+    (SURVEY §8d). None when libcrypto.so.3 is absent."""
+    from oracle import oracle
+    if not oracle.ossl_available():
+        return None
+    n = min(sample, w.n)
+    end = int(w.seal_desc["offset"][n - 1]) + int(w.seal_desc["len"][n - 1])
+    sd, od = w.seal_desc[:n].copy(), w.open_desc[:n].copy()
+    wire = int(sd["len"].astype(np.int64).sum())
+    out = {"unit": "GiB/s", "kind": "openssl-evp"}
+    for key, thr in (("value", threads), ("value_1core", 1)):
+        arena = w.arena[:end].copy()
+        reps, t = 0, 0.0
+        while t < min_seconds:
+            t0 = time.perf_counter()
+            st = oracle.ossl_batch(w.keys, arena, sd, False, thr)
+            st2 = oracle.ossl_batch(w.keys, arena, od, True, thr)
+            t += time.perf_counter() - t0
+            assert (st == 0).all() and (st2 == 0).all(), "OpenSSL leg failed on its sample"
+            reps += 1
+        out[key] = round(wire * 2 * reps / t / 2 ** 30, 3)
+    out["cores"] = threads
+    out["sample"] = f"{n} packets ({wire / 1e6:.1f} MB) of the same workload, seal+open, {threads} threads and 1"
+    return out
 
 
 def end_to_end(torch, batch, kt, w, sd, od, dev, chunks=8, reps=3):
@@ -230,9 +260,11 @@ def main():
                 "kernel": kern or "seal batch (partition + AES + ChaCha kernels)",
                 "seal_ms": round(seal_ms, 4), "open_ms": round(open_ms, 4),
                 "algorithmic_bytes_per_launch": int(algo_bytes)}
-        cpu = None
+        cpu = ossl = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(w, args.cpu_sample, min(16, os.cpu_count() or 1), args.cpu_seconds)
+            thr = min(16, os.cpu_count() or 1)
+            cpu = cpu_baseline(w, args.cpu_sample, thr, args.cpu_seconds)
+            ossl = cpu_openssl(w, args.cpu_sample, thr)
         names = {"b": "configs[1]: 1M x 1200B ChaCha20-Poly1305 seal+open, 1-RTT short header",
                  "c": "configs[2]: 1M x 1200B AES-128-GCM seal+open + header protection",
                  "e": "configs[4]: mixed 64-1350B batch, Initial + 1-RTT, ChaCha20/AES-GCM interleaved"}
@@ -246,6 +278,8 @@ def main():
                        "seal_failures_or_open_failures": fails},
             "roofline": roof, "cpu_baseline": cpu,
         }
+        if ossl is not None:
+            out["cpu_openssl"] = ossl
         if args.e2e and world == 1:
             out["end_to_end"] = end_to_end(torch, batch, kt, w, sd, od, dev)
         print(json.dumps(out), flush=True)

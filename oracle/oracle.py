@@ -12,8 +12,10 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "build", "liborc.so")
+OSSL_LIB = os.path.join(HERE, "build", "libossl.so")
 
 _lib = None
+_ossl = None
 
 
 def build():
@@ -178,3 +180,29 @@ def batch_recv(rows, conns, arena, dgrams, max_pkts):
                           ctypes.c_uint64(arena.size), _p(dgrams), ctypes.c_uint32(len(dgrams)), _p(out),
                           ctypes.c_uint32(max_pkts), ctypes.byref(n))
     return out[:min(n.value, max_pkts)], n.value
+
+
+def _load_ossl():
+    global _ossl
+    if _ossl is None:
+        if not os.path.exists(OSSL_LIB):
+            build()
+        _ossl = ctypes.CDLL(OSSL_LIB)
+    return _ossl
+
+
+def ossl_available():
+    """True when libcrypto.so.3 can be dlopen'ed (OpenSSL EVP leg of the CPU baseline)."""
+    return bool(_load_ossl().ossl_available())
+
+
+def ossl_batch(rows, arena, desc, open_, threads=1):
+    """OpenSSL EVP seal (open_=False) or open of `desc` in place on the host copy `arena`, with
+    the same composites as the batch API (ossl_baseline.c); returns per-packet status or None when
+    libcrypto.so.3 is absent."""
+    arr, nr = _rows(rows)
+    n = len(desc)
+    status = np.zeros(n, dtype=np.uint8)
+    rc = _load_ossl().ossl_batch(arr, ctypes.c_uint32(nr), _p(arena), ctypes.c_uint64(arena.size), _p(desc),
+                                 ctypes.c_uint32(n), _p(status), ctypes.c_int(threads), ctypes.c_int(1 if open_ else 0))
+    return None if rc != 0 else status
