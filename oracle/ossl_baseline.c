@@ -38,12 +38,12 @@ static struct {
   int (*dec_update)(EVP_CIPHER_CTX*, uint8_t*, int*, const uint8_t*, int);
   int (*dec_final)(EVP_CIPHER_CTX*, uint8_t*, int*);
   int (*ctrl)(EVP_CIPHER_CTX*, int, int, void*);
+  void (*cipher_free)(EVP_CIPHER*);
 } E;
 
 enum { CTRL_SET_IVLEN = 0x9, CTRL_GET_TAG = 0x10, CTRL_SET_TAG = 0x11 };
 
 static pthread_once_t g_once = PTHREAD_ONCE_INIT;
-static EVP_CIPHER* g_ciphers[4];
 
 static void load_libcrypto(void) {
   void* h = dlopen("libcrypto.so.3", RTLD_NOW | RTLD_LOCAL);
@@ -54,14 +54,18 @@ static void load_libcrypto(void) {
   SYM(enc_init, "EVP_EncryptInit_ex") SYM(enc_update, "EVP_EncryptUpdate") SYM(enc_final, "EVP_EncryptFinal_ex")
   SYM(dec_init, "EVP_DecryptInit_ex") SYM(dec_update, "EVP_DecryptUpdate") SYM(dec_final, "EVP_DecryptFinal_ex")
   SYM(ctrl, "EVP_CIPHER_CTX_ctrl")
+  SYM(cipher_free, "EVP_CIPHER_free")
 #undef SYM
-  /* explicitly fetched ciphers: the legacy EVP_chacha20_poly1305() objects re-fetch from the
-     provider (under a global lock) on every init */
-  static const char* names[4] = {"ChaCha20-Poly1305", "ChaCha20", "AES-128-GCM", "AES-128-ECB"};
-  for (int i = 0; i < 4; ++i)
-    if (!(g_ciphers[i] = E.fetch(NULL, names[i], NULL))) return;
+  EVP_CIPHER* c = E.fetch(NULL, "ChaCha20-Poly1305", NULL);
+  if (!c) return;
+  E.cipher_free(c);
   E.ok = 1;
 }
+
+/* Explicitly fetched ciphers, one set per thread: the legacy EVP_chacha20_poly1305() objects
+ * re-fetch from the provider (under a global lock) on every init, and a cipher object shared by
+ * all threads has its reference count bounced between cores on every init. */
+static const char* const kCipherNames[4] = {"ChaCha20-Poly1305", "ChaCha20", "AES-128-GCM", "AES-128-ECB"};
 
 int ossl_available(void) {
   pthread_once(&g_once, load_libcrypto);
@@ -159,15 +163,17 @@ static void* worker(void* p) {
   Job* j = (Job*)p;
   Ctx c[2];
   const uint32_t suites[2] = {MQ_SUITE_CHACHA20, MQ_SUITE_AES128GCM};
+  EVP_CIPHER* ciph[4];
+  for (int i = 0; i < 4; ++i) ciph[i] = E.fetch(NULL, kCipherNames[i], NULL);
   for (int s = 0; s < 2; ++s) {
     c[s].suite = suites[s];
     c[s].row = 0xffffffffu;
     c[s].aead_e = E.ctx_new();
     c[s].aead_d = E.ctx_new();
     c[s].hp = E.ctx_new();
-    E.enc_init(c[s].aead_e, g_ciphers[2 * s], NULL, NULL, NULL);
-    E.dec_init(c[s].aead_d, g_ciphers[2 * s], NULL, NULL, NULL);
-    E.enc_init(c[s].hp, g_ciphers[2 * s + 1], NULL, NULL, NULL);
+    E.enc_init(c[s].aead_e, ciph[2 * s], NULL, NULL, NULL);
+    E.dec_init(c[s].aead_d, ciph[2 * s], NULL, NULL, NULL);
+    E.enc_init(c[s].hp, ciph[2 * s + 1], NULL, NULL, NULL);
   }
   for (uint32_t i = j->lo; i < j->hi; ++i) {
     const mq_pkt_desc* d = j->desc + i;
@@ -175,6 +181,7 @@ static void* worker(void* p) {
     j->status[i] = (uint8_t)one(cx, j->rows, j->arena, d, j->open);
   }
   for (int s = 0; s < 2; ++s) { E.ctx_free(c[s].aead_e); E.ctx_free(c[s].aead_d); E.ctx_free(c[s].hp); }
+  for (int i = 0; i < 4; ++i) E.cipher_free(ciph[i]);
   return NULL;
 }
 

@@ -18,6 +18,8 @@ for c in c e; do
 done
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_b -o run -- python3 bench.py --no-cpu-baseline > $O/prof_b.json 2> $O/prof_b.err || { tail $O/prof_b.err; exit 1; }
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c -o run -- python3 bench.py --config c --no-cpu-baseline > $O/prof_c.json 2> $O/prof_c.err || { tail $O/prof_c.err; exit 1; }
-bash tools/gpu_pmc.sh b 1048576 && python3 tools/pmc_summary.py gpurun_out/pmc_b --json $O/pmc_traffic_b.json > $O/pmc_b.txt || exit 1
-bash tools/gpu_pmc.sh c 1048576 && python3 tools/pmc_summary.py gpurun_out/pmc_c --json $O/pmc_traffic_c.json > $O/pmc_c.txt || exit 1
+timeout -k 10 300 python tools/bench_aux.py > $O/aux.json 2> $O/aux.err || { tail $O/aux.err; exit 1; }
+cat $O/aux.json
+bash tools/gpu_pmc.sh b 1048576 && python3 tools/pmc_summary.py gpurun_out/pmc_b --tiles 131072 --json $O/pmc_traffic_b.json > $O/pmc_b.txt || exit 1
+bash tools/gpu_pmc.sh c 1048576 && python3 tools/pmc_summary.py gpurun_out/pmc_c --tiles 131072 --json $O/pmc_traffic_c.json > $O/pmc_c.txt || exit 1
 echo ROUND_OK

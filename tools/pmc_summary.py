@@ -38,6 +38,9 @@ def load(d):
 def main():
     d = sys.argv[1]
     out_json = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
+    # --tiles T: per-tile counts for the tile kernels (the AES kernels are persistent: one wave
+    # walks many tiles, so per-wave counts are not per-tile there)
+    tiles = int(sys.argv[sys.argv.index("--tiles") + 1]) if "--tiles" in sys.argv else None
     res = load(d)
     summary = {}
     for k in sorted(res):
@@ -52,6 +55,11 @@ def main():
             print(f"   -> VALU instr / wave       {s['valu_per_wave']:.0f}")
         if w and "SQ_INSTS_LDS" in c:
             print(f"   -> LDS instr / wave        {c['SQ_INSTS_LDS'] / w:.0f}")
+        if tiles and "hp_kernel" not in k and "partition" not in k:
+            for x in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU"):
+                if x in c:
+                    s[x.lower() + "_per_tile"] = c[x] / tiles
+                    print(f"   -> {x} / tile {c[x] / tiles:10.0f}")
         if "SQ_WAVE_CYCLES" in c and "SQ_ACTIVE_INST_VALU" in c:
             s["valu_active_frac_of_wave_cycles"] = c["SQ_ACTIVE_INST_VALU"] / c["SQ_WAVE_CYCLES"]
             print(f"   -> VALU active / wave cyc  {s['valu_active_frac_of_wave_cycles']:.3f}")

@@ -22,6 +22,8 @@ from milli_quic_amd.batch import KeyTable  # noqa: E402
 
 NAMES = {"seal": ["setup", "dma+blk0", "chacha", "poly+tag", "hp", "-", "store"],
          "open": ["setup", "dma", "hp+unmask", "blk0+poly+verify", "xor", "-", "store"]}
+AES_NAMES = {"seal": ["setup", "dma+ctr0", "ctr", "ghash+tag", "hp", "-", "store"],
+             "open": ["setup", "dma", "hp+unmask", "ghash", "ej0+blk0+verify", "ctr", "store"]}
 
 
 def main():
@@ -31,6 +33,7 @@ def main():
     lib.mq_debug_set_stamps.argtypes = [ctypes.c_void_p]
     assert lib.mq_device_init(0) == 0
     w = {"b": workload.config_b, "c": workload.config_c, "e": workload.config_e}[cfg](n)
+    names = AES_NAMES if cfg == "c" else NAMES
     dev = torch.device("cuda", 0)
     kt = KeyTable(w.keys)
     arena = torch.from_numpy(w.arena).to(dev)
@@ -62,7 +65,7 @@ def main():
                 ok = s[:, k] > 0
                 if ok.sum() == 0:
                     continue
-                print(f"   {k}:{NAMES[which][k - 1]:18s} median={int(np.median(d[ok])):7d} mean={int(d[ok].mean()):7d}"
+                print(f"   {k}:{names[which][k - 1]:18s} median={int(np.median(d[ok])):7d} mean={int(d[ok].mean()):7d}"
                       f"  ({100 * d[ok].mean() / life.mean():.1f}%)")
                 prev = np.where(ok, s[:, k], prev)
             # concurrency: tiles alive at the midpoint of the kernel
