@@ -208,11 +208,15 @@ __device__ __forceinline__ void aes128_block(const AesRk& rk, const TwLane& L, u
   s0 ^= rk.w[0]; s1 ^= rk.w[1]; s2 ^= rk.w[2]; s3 ^= rk.w[3];
 #pragma unroll
   for (int r = 1; r < 10; ++r) {
-    const uint32_t t0 = twl(s0, 3, L.r0) ^ twl(s2, 1, L.r2) ^ ror(twl(s1, 2, L.r0) ^ twl(s3, 0, L.r2), 8) ^ rk.w[4 * r];
-    const uint32_t t1 = twl(s1, 3, L.r0) ^ twl(s3, 1, L.r2) ^ ror(twl(s2, 2, L.r0) ^ twl(s0, 0, L.r2), 8) ^ rk.w[4 * r + 1];
-    const uint32_t t2 = twl(s2, 3, L.r0) ^ twl(s0, 1, L.r2) ^ ror(twl(s3, 2, L.r0) ^ twl(s1, 0, L.r2), 8) ^ rk.w[4 * r + 2];
-    const uint32_t t3 = twl(s3, 3, L.r0) ^ twl(s1, 1, L.r2) ^ ror(twl(s0, 2, L.r0) ^ twl(s2, 0, L.r2), 8) ^ rk.w[4 * r + 3];
-    s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+    const uint32_t l0 = twl(s0, 3, L.r0), l1 = twl(s2, 1, L.r2), l2 = twl(s1, 2, L.r0), l3 = twl(s3, 0, L.r2);
+    const uint32_t l4 = twl(s1, 3, L.r0), l5 = twl(s3, 1, L.r2), l6 = twl(s2, 2, L.r0), l7 = twl(s0, 0, L.r2);
+    const uint32_t l8 = twl(s2, 3, L.r0), l9 = twl(s0, 1, L.r2), l10 = twl(s3, 2, L.r0), l11 = twl(s1, 0, L.r2);
+    const uint32_t l12 = twl(s3, 3, L.r0), l13 = twl(s1, 1, L.r2), l14 = twl(s0, 2, L.r0), l15 = twl(s2, 0, L.r2);
+    __builtin_amdgcn_sched_barrier(0);  // all 16 lookups in flight before the first is consumed
+    s0 = l0 ^ l1 ^ ror(l2 ^ l3, 8) ^ rk.w[4 * r];
+    s1 = l4 ^ l5 ^ ror(l6 ^ l7, 8) ^ rk.w[4 * r + 1];
+    s2 = l8 ^ l9 ^ ror(l10 ^ l11, 8) ^ rk.w[4 * r + 2];
+    s3 = l12 ^ l13 ^ ror(l14 ^ l15, 8) ^ rk.w[4 * r + 3];
   }
   auto fin = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
     return (__builtin_amdgcn_perm(twl(a, 3, L.r2), twl(b, 2, L.r0), 0x07020c0cu) |
@@ -234,27 +238,41 @@ __device__ __forceinline__ void aes128_block2(const AesRk& rk, const TwLane& L, 
   for (int q = 0; q < 4; ++q) { a[q] ^= rk.w[q]; b[q] ^= rk.w[q]; }
 #pragma unroll
   for (int r = 1; r < 10; ++r) {
-    uint32_t ta[4], tb[4];
+    // all 32 lookups of the round are issued before any is consumed (sched_barrier), so the LDS
+    // queue streams them with up to 15 in flight instead of draining after every column
+    uint32_t la[16], lb[16];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int q1 = (q + 1) & 3, q2 = (q + 2) & 3, q3 = (q + 3) & 3;
-      ta[q] = twl(a[q], 3, L.r0) ^ twl(a[q2], 1, L.r2) ^ ror(twl(a[q1], 2, L.r0) ^ twl(a[q3], 0, L.r2), 8) ^ rk.w[4 * r + q];
-      tb[q] = twl(b[q], 3, L.r0) ^ twl(b[q2], 1, L.r2) ^ ror(twl(b[q1], 2, L.r0) ^ twl(b[q3], 0, L.r2), 8) ^ rk.w[4 * r + q];
+      la[4 * q] = twl(a[q], 3, L.r0); la[4 * q + 1] = twl(a[q2], 1, L.r2);
+      la[4 * q + 2] = twl(a[q1], 2, L.r0); la[4 * q + 3] = twl(a[q3], 0, L.r2);
+      lb[4 * q] = twl(b[q], 3, L.r0); lb[4 * q + 1] = twl(b[q2], 1, L.r2);
+      lb[4 * q + 2] = twl(b[q1], 2, L.r0); lb[4 * q + 3] = twl(b[q3], 0, L.r2);
     }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) { a[q] = ta[q]; b[q] = tb[q]; }
+    for (int q = 0; q < 4; ++q) {
+      a[q] = la[4 * q] ^ la[4 * q + 1] ^ ror(la[4 * q + 2] ^ la[4 * q + 3], 8) ^ rk.w[4 * r + q];
+      b[q] = lb[4 * q] ^ lb[4 * q + 1] ^ ror(lb[4 * q + 2] ^ lb[4 * q + 3], 8) ^ rk.w[4 * r + q];
+    }
   }
-  uint32_t oa[4], ob[4];
+  uint32_t la[16], lb[16];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int q1 = (q + 1) & 3, q2 = (q + 2) & 3, q3 = (q + 3) & 3;
-    oa[q] = (__builtin_amdgcn_perm(twl(a[q], 3, L.r2), twl(a[q1], 2, L.r0), 0x07020c0cu) |
-             __builtin_amdgcn_perm(twl(a[q2], 1, L.r0), twl(a[q3], 0, L.r2), 0x0c0c0500u)) ^ rk.w[40 + q];
-    ob[q] = (__builtin_amdgcn_perm(twl(b[q], 3, L.r2), twl(b[q1], 2, L.r0), 0x07020c0cu) |
-             __builtin_amdgcn_perm(twl(b[q2], 1, L.r0), twl(b[q3], 0, L.r2), 0x0c0c0500u)) ^ rk.w[40 + q];
+    la[4 * q] = twl(a[q], 3, L.r2); la[4 * q + 1] = twl(a[q1], 2, L.r0);
+    la[4 * q + 2] = twl(a[q2], 1, L.r0); la[4 * q + 3] = twl(a[q3], 0, L.r2);
+    lb[4 * q] = twl(b[q], 3, L.r2); lb[4 * q + 1] = twl(b[q1], 2, L.r0);
+    lb[4 * q + 2] = twl(b[q2], 1, L.r0); lb[4 * q + 3] = twl(b[q3], 0, L.r2);
   }
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) { a[q] = oa[q]; b[q] = ob[q]; }
+  for (int q = 0; q < 4; ++q) {
+    a[q] = (__builtin_amdgcn_perm(la[4 * q], la[4 * q + 1], 0x07020c0cu) |
+            __builtin_amdgcn_perm(la[4 * q + 2], la[4 * q + 3], 0x0c0c0500u)) ^ rk.w[40 + q];
+    b[q] = (__builtin_amdgcn_perm(lb[4 * q], lb[4 * q + 1], 0x07020c0cu) |
+            __builtin_amdgcn_perm(lb[4 * q + 2], lb[4 * q + 3], 0x0c0c0500u)) ^ rk.w[40 + q];
+  }
 }
 
 // a = x^i * h (reflected basis), 0 <= i < 128: shift into 8 words, then fold

@@ -199,6 +199,7 @@ struct AesPolicyT {
       stg.issue();
       auto first_iter = [&]() {  // before any packet byte is touched
         stg.complete();
+        MQ_STAMP(c.tile, 2);
         const bool rec = c.act && is_record(d);
         if (wave_any(rec)) {  // TLS record: header (AAD) and inner content type before any use
           if (rec && j == 0) write_record_header(sp, pkt, d);
@@ -255,6 +256,7 @@ struct AesPolicyT {
       }
       if (Imax == 0) stg.complete();
     }
+    MQ_STAMP(c.tile, 3);
 #pragma unroll
     for (int k = 0; k < 4; ++k) ej0[k] = oct_bcast0(ej0[k]);
     uint32_t y[4], tag[4];
@@ -262,12 +264,14 @@ struct AesPolicyT {
     tag_words(y, ej0, tag);
     if (c.act && j == 0) store_words<4>(sp, pay + P, tag);
     wave_sync();
+    MQ_STAMP(c.tile, 4);
     if (wave_any(hp_post)) {
       uint32_t t0, t1;
       hp_mask(sp, pkt + (c.act ? d.pn_offset + 4u : 0u), row, rb, t0, t1);
       if (hp_post && j == 0) { m0 = t0; m1 = t1; have_mask = true; }
     }
     if (have_mask) apply_hp(sp, pkt, d, m0, m1);
+    MQ_STAMP(c.tile, 5);
   }
 
   template <class S, class G>
@@ -276,6 +280,7 @@ struct AesPolicyT {
     const mq_pkt_desc& d = c.d;
     stg.issue();
     stg.complete();
+    MQ_STAMP(c.tile, 2);
     const TwLane rb = tw_lane();
     uint32_t pn_len = d.pn_len;
     uint8_t orig_b0 = 0;
@@ -316,7 +321,9 @@ struct AesPolicyT {
     const uint32_t C = (nblk + kLanesPerPkt - 1) / kLanesPerPkt;
     const uint32_t Cmax = wave_max_u32(c.act ? C : 0u);
     uint32_t y[4];
+    MQ_STAMP(c.tile, 3);
     ghash<TAB>(sp, pkt, pay, aad_len, P, row, j, c.act, y);
+    MQ_STAMP(c.tile, 4);
     AesRk rk;
     load_rk(row->aes_rk, rk);
     uint32_t ks0[4];  // block j: E(J0) on lane 0, keystream elsewhere
@@ -333,6 +340,7 @@ struct AesPolicyT {
       c.act = false;
     }
     wave_sync();
+    MQ_STAMP(c.tile, 5);
     if (c.act && j >= 1 && (uint32_t)j < nblk) xor_block(sp, pay, (uint32_t)j, P, ks0);
     uint32_t it = 1;
     for (; it + 1 < Cmax; it += 2) {  // two iterations per pass (interleaved AES rounds)
