@@ -97,11 +97,23 @@ __device__ __forceinline__ void poly_tag(const S& sp, typename S::off_t pkt, typ
     Blk b = where(i);
     uint32_t m[4];
     load_words<4>(sp, b.src, m);
+    // steady state: every active lane moves from one whole ciphertext block to the next one 8
+    // blocks on (src + 128, payload alignment fixed), so the address and realignment selector
+    // need no per-step recomputation
+    const uint32_t sel_pay = sel_load((uint32_t)(pay & 3));
+    const int ct_full_end = (int)A + (int)(ct_len >> 4);  // first index past the whole CT blocks
     for (uint32_t k = 0; k + 1 < Kmax; ++k) {
       absorb(b, m);
+      const bool steady = !act || (i >= (int)A && i + kLanesPerPkt < ct_full_end);
       i += kLanesPerPkt;
-      b = where(i);
-      load_words<4>(sp, b.src, m);  // next block's LDS reads overlap this multiply
+      if (!wave_any(!steady)) {
+        b.src += 128;
+        b.rem -= 128;
+        load_words_sel<4>(sp, b.src & ~(typename S::off_t)3, sel_pay, m);
+      } else {
+        b = where(i);
+        load_words<4>(sp, b.src, m);  // next block's LDS reads overlap this multiply
+      }
       p26_mul(acc, m8);
     }
     absorb(b, m);

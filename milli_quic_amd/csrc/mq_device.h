@@ -98,16 +98,21 @@ __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
   return __builtin_amdgcn_perm(hi, lo, sel);
 }
 
-// Read N payload-aligned words starting at byte address `a` (any alignment).
+// Read N payload-aligned words starting at dword-aligned address b + (alignment encoded in the
+// v_perm selector `sel` = sel_load(a & 3)), for loops that step a fixed stride.
 template <int N, class S>
-__device__ __forceinline__ void load_words(const S& sp, typename S::off_t a, uint32_t (&w)[N]) {
-  typename S::off_t b = a & ~(typename S::off_t)3;
-  uint32_t sel = sel_load((uint32_t)(a & 3));
+__device__ __forceinline__ void load_words_sel(const S& sp, typename S::off_t b, uint32_t sel, uint32_t (&w)[N]) {
   uint32_t m[N + 1];
 #pragma unroll
   for (int k = 0; k <= N; ++k) m[k] = sp.ld32(b + 4 * k);
 #pragma unroll
   for (int k = 0; k < N; ++k) w[k] = perm(m[k + 1], m[k], sel);
+}
+
+// Read N payload-aligned words starting at byte address `a` (any alignment).
+template <int N, class S>
+__device__ __forceinline__ void load_words(const S& sp, typename S::off_t a, uint32_t (&w)[N]) {
+  load_words_sel<N>(sp, a & ~(typename S::off_t)3, sel_load((uint32_t)(a & 3)), w);
 }
 
 // bytes [lo, hi) of a dword
