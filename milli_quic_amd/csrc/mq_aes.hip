@@ -279,39 +279,24 @@ struct AesPolicyT {
                               bool direct, G& stg) {
     const mq_pkt_desc& d = c.d;
     stg.issue();
-    stg.complete();
-    MQ_STAMP(c.tile, 2);
     const TwLane rb = tw_lane();
-    uint32_t pn_len = d.pn_len;
-    uint8_t orig_b0 = 0;
+    uint32_t pn_len = d.pn_len, trunc = 0;
+    uint8_t orig_b0 = 0, b0 = 0;
     uint32_t orig_pn = 0;
-    bool hdr_written = false;
-    if (c.act && !(d.flags & MQ_PKT_NO_HP)) {
-      uint32_t m0 = c.hm0, m1 = c.hm1;
-      if (!c.pre_hp) hp_mask(sp, pkt + d.pn_offset + 4, row, rb, m0, m1);
-      const uint8_t fb = (d.flags & MQ_PKT_LONG_HEADER) ? 0x0f : 0x1f;
-      orig_b0 = sp.ld8(pkt);
-      const uint8_t b0 = orig_b0 ^ ((uint8_t)m0 & fb);
-      pn_len = (b0 & 3u) + 1;
-      const uint32_t mk = (m0 >> 8) | (m1 << 24);
-      uint32_t trunc = 0;
-      for (uint32_t b = 0; b < pn_len; ++b) {
-        const uint8_t e = sp.ld8(pkt + d.pn_offset + b);
-        orig_pn |= (uint32_t)e << (8 * b);
-        trunc = (trunc << 8) | (uint8_t)(e ^ (uint8_t)(mk >> (8 * b)));
-      }
-      c.pn = decode_pn(trunc, pn_len, d.pn);
-      if (c.pn > kMaxPn) {
-        c.st = MQ_ERR_PROTOCOL;
-        c.act = false;
-      } else if (j == 0) {
-        sp.st8(pkt, b0);
-        for (uint32_t b = 0; b < pn_len; ++b)
-          sp.st8(pkt + d.pn_offset + b, (uint8_t)(trunc >> (8 * (pn_len - 1 - b))));
-        hdr_written = true;
+    const bool hp = c.act && !(d.flags & MQ_PKT_NO_HP);
+    // header (recv.rs:363-395): from the pre-pass values when present (wave-uniform), so that
+    // in the single-key kernels the nonce and the first CTR block are computed while the packet
+    // is still landing in LDS
+    if (c.pre_hp) {
+      if (hp) b0 = header_from_prepass(c, pn_len, trunc);
+    } else {
+      stg.complete();
+      if (hp) {
+        uint32_t m0, m1;
+        hp_mask(sp, pkt + d.pn_offset + 4, row, rb, m0, m1);
+        b0 = header_from_mask(sp, pkt, c, m0, m1, pn_len, trunc);
       }
     }
-    wave_sync();
     const uint32_t aad_len = c.act ? (uint32_t)d.pn_offset + pn_len : 0u;
     const uint32_t P = c.act ? d.len - aad_len - 16 : 0u;
     const typename S::off_t pay = pkt + aad_len;
@@ -320,14 +305,24 @@ struct AesPolicyT {
     const uint32_t nblk = 1 + (P + 15) / 16;
     const uint32_t C = (nblk + kLanesPerPkt - 1) / kLanesPerPkt;
     const uint32_t Cmax = wave_max_u32(c.act ? C : 0u);
+    AesRk rk;
+    uint32_t ks0[4];  // block j: E(J0) on lane 0, keystream elsewhere
+    if (TAB) {  // round keys in SGPRs: cheap to keep across the GHASH
+      load_rk(row->aes_rk, rk);
+      ctr_block(rk, rb, nb, (uint32_t)j, ks0);
+    }
+    if (c.pre_hp) stg.complete();
+    MQ_STAMP(c.tile, 2);
+    const bool hdr_written = hp && write_unmasked_header(sp, pkt, c, j, b0, pn_len, trunc, orig_b0, orig_pn);
+    wave_sync();
     uint32_t y[4];
     MQ_STAMP(c.tile, 3);
     ghash<TAB>(sp, pkt, pay, aad_len, P, row, j, c.act, y);
     MQ_STAMP(c.tile, 4);
-    AesRk rk;
-    load_rk(row->aes_rk, rk);
-    uint32_t ks0[4];  // block j: E(J0) on lane 0, keystream elsewhere
-    ctr_block(rk, rb, nb, (uint32_t)j, ks0);
+    if (!TAB) {
+      load_rk(row->aes_rk, rk);
+      ctr_block(rk, rb, nb, (uint32_t)j, ks0);
+    }
     uint32_t ej0[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) ej0[k] = oct_bcast0(ks0[k]);
@@ -428,7 +423,10 @@ extern "C" __global__ __launch_bounds__(256) void mq_aes_hp_kernel(
 }
 
 // Open pre-pass: AesHeaderProtection::mask of every packet's sample, one packet per lane.
-extern "C" __global__ __launch_bounds__(256) void mq_aes_open_hp_kernel(
+// DECODE (the batch open path): store the unmasked first byte and truncated PN (prepass_decode)
+// instead of the raw mask (which mq_recv.hip's planner consumes).
+template <bool DECODE>
+__global__ __launch_bounds__(256) void mq_aes_open_hp_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, const uint8_t* __restrict__ arena, uint64_t arena_len,
     const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,
     const uint32_t* __restrict__ n_dev, uint2* __restrict__ hpm) {
@@ -437,13 +435,14 @@ extern "C" __global__ __launch_bounds__(256) void mq_aes_open_hp_kernel(
   uint32_t i;
   const KeyRow* row;
   uint64_t at;
+  mq_pkt_desc d;
   if (!prepass_pick(blockIdx.x * blockDim.x + threadIdx.x, MQ_SUITE_AES128GCM, kt, n_rows, arena_len, desc, n,
-                    index, n_dev, i, row, at))
+                    index, n_dev, i, row, at, d))
     return;
   GlobalSpace sp{const_cast<uint8_t*>(arena), arena_len};
   uint32_t m0, m1;
   AesPolicyT<false>::hp_mask(sp, at, row, (threadIdx.x & (kTReplicas - 1)) * 4, m0, m1);
-  hpm[i] = make_uint2(m0, m1);
+  hpm[i] = DECODE ? prepass_decode(arena, d, m0, m1) : make_uint2(m0, m1);
 }
 
 // Persistent grid: one workgroup per CU (152 KiB of LDS each), capped by the tile count.
@@ -472,7 +471,7 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
   const uint32_t blocks = aes_grid(tiles);
   const size_t dyn = (size_t)kLdsBytes * kAesWaves;
   if (open && hpm) {
-    hipLaunchKernelGGL(mq_aes_open_hp_kernel, dim3((n + 255) / 256), dim3(256), 0, s, kt, n_rows, arena,
+    hipLaunchKernelGGL(mq_aes_open_hp_kernel<true>, dim3((n + 255) / 256), dim3(256), 0, s, kt, n_rows, arena,
                        arena_len, desc, n, index, n_dev, hpm);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -490,7 +489,7 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
 hipError_t mq_launch_aes_prepass(const KeyRow* kt, uint32_t n_rows, const uint8_t* arena, uint64_t arena_len,
                                  const mq_pkt_desc* desc, uint32_t n, uint2* hpm, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(mq_aes_open_hp_kernel, dim3((n + 255) / 256), dim3(256), 0, s, kt, n_rows, arena, arena_len,
+  hipLaunchKernelGGL(mq_aes_open_hp_kernel<false>, dim3((n + 255) / 256), dim3(256), 0, s, kt, n_rows, arena, arena_len,
                      desc, n, (const uint32_t*)nullptr, (const uint32_t*)nullptr, hpm);
   return hipGetLastError();
 }

@@ -270,40 +270,23 @@ struct ChaChaPolicy {
                               bool direct, G& stg) {
     const mq_pkt_desc& d = c.d;
     stg.issue();
-    stg.complete();
-    MQ_STAMP(c.tile, 2);
-    uint32_t pn_len = d.pn_len;
-    uint8_t orig_b0 = 0;
+    uint32_t pn_len = d.pn_len, trunc = 0;
+    uint8_t orig_b0 = 0, b0 = 0;
     uint32_t orig_pn = 0;
-    bool hdr_written = false;
-    if (c.act && !(d.flags & MQ_PKT_NO_HP)) {
-      // recv.rs:363-391 / :968-992: mask, unmask byte 0, pn_len, unmask PN, decode_pn
-      uint32_t m0 = c.hm0, m1 = c.hm1;
-      if (!c.pre_hp) hp_mask(sp, pkt + d.pn_offset + 4, row, m0, m1);
-      const uint8_t fb = (d.flags & MQ_PKT_LONG_HEADER) ? 0x0f : 0x1f;
-      orig_b0 = sp.ld8(pkt);
-      const uint8_t b0 = orig_b0 ^ ((uint8_t)m0 & fb);
-      pn_len = (b0 & 3u) + 1;
-      const uint32_t mk = (m0 >> 8) | (m1 << 24);
-      uint32_t trunc = 0;
-      for (uint32_t b = 0; b < pn_len; ++b) {
-        const uint8_t e = sp.ld8(pkt + d.pn_offset + b);
-        orig_pn |= (uint32_t)e << (8 * b);
-        trunc = (trunc << 8) | (uint8_t)(e ^ (uint8_t)(mk >> (8 * b)));
-      }
-      c.pn = decode_pn(trunc, pn_len, d.pn);
-      if (c.pn > kMaxPn) {  // recv.rs:393-395
-        c.st = MQ_ERR_PROTOCOL;
-        c.act = false;
-      } else if (j == 0) {
-        sp.st8(pkt, b0);
-        for (uint32_t b = 0; b < pn_len; ++b)
-          sp.st8(pkt + d.pn_offset + b, (uint8_t)(trunc >> (8 * (pn_len - 1 - b))));
-        hdr_written = true;
+    const bool hp = c.act && !(d.flags & MQ_PKT_NO_HP);
+    // recv.rs:363-395 / :968-997: mask, unmask byte 0, pn_len, unmask PN, decode_pn. With the
+    // pre-pass (wave-uniform) those values arrive with the descriptor, so the nonce and the first
+    // keystream block are computed while the packet is still landing in LDS.
+    if (c.pre_hp) {
+      if (hp) b0 = header_from_prepass(c, pn_len, trunc);
+    } else {
+      stg.complete();
+      if (hp) {
+        uint32_t m0, m1;
+        hp_mask(sp, pkt + d.pn_offset + 4, row, m0, m1);
+        b0 = header_from_mask(sp, pkt, c, m0, m1, pn_len, trunc);
       }
     }
-    wave_sync();
-    MQ_STAMP(c.tile, 3);
     uint32_t key[8];
     load_key8(row->key, key);
     const uint32_t aad_len = c.act ? (uint32_t)d.pn_offset + pn_len : 0u;
@@ -318,6 +301,10 @@ struct ChaChaPolicy {
     const uint32_t ctr0 = (uint32_t)j;
     uint32_t ks0[16];
     chacha20_block(key, ctr0, n0, n1, n2, ks0);
+    if (c.pre_hp) stg.complete();
+    MQ_STAMP(c.tile, 2);
+    const bool hdr_written = hp && write_unmasked_header(sp, pkt, c, j, b0, pn_len, trunc, orig_b0, orig_pn);
+    MQ_STAMP(c.tile, 3);
     if (c.act && j == 0) store_otk(c.otk, ks0);
     wave_sync();
     uint32_t tag[4], got[4];
@@ -397,21 +384,25 @@ extern "C" __global__ __launch_bounds__(256) void mq_chacha_hp_kernel(
 }
 
 // Open pre-pass: ChaChaHeaderProtection::mask of every packet's sample, one packet per lane, so
-// the tile kernel spends no keystream slot of its octet on it.
-extern "C" __global__ __launch_bounds__(256) void mq_chacha_open_hp_kernel(
+// the tile kernel spends no keystream slot of its octet on it. DECODE (the batch open path):
+// store the unmasked first byte and truncated PN (prepass_decode) instead of the raw mask
+// (which mq_recv.hip's planner consumes).
+template <bool DECODE>
+__global__ __launch_bounds__(256) void mq_chacha_open_hp_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, const uint8_t* __restrict__ arena, uint64_t arena_len,
     const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,
     const uint32_t* __restrict__ n_dev, uint2* __restrict__ hpm) {
   uint32_t i;
   const KeyRow* row;
   uint64_t at;
+  mq_pkt_desc d;
   if (!prepass_pick(blockIdx.x * blockDim.x + threadIdx.x, MQ_SUITE_CHACHA20, kt, n_rows, arena_len, desc, n,
-                    index, n_dev, i, row, at))
+                    index, n_dev, i, row, at, d))
     return;
   GlobalSpace sp{const_cast<uint8_t*>(arena), arena_len};
   uint32_t m0, m1;
   ChaChaPolicy::hp_mask(sp, at, row, m0, m1);
-  hpm[i] = make_uint2(m0, m1);
+  hpm[i] = DECODE ? prepass_decode(arena, d, m0, m1) : make_uint2(m0, m1);
 }
 
 // ---- host-side launchers (called from mq_host.cpp) -------------------------------------------
@@ -422,7 +413,7 @@ hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_
   const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
   if (tiles == 0) return hipSuccess;
   if (open && hpm) {
-    hipLaunchKernelGGL(mq_chacha_open_hp_kernel, dim3((n + 255) / 256), dim3(256), 0, s, kt, n_rows, arena,
+    hipLaunchKernelGGL(mq_chacha_open_hp_kernel<true>, dim3((n + 255) / 256), dim3(256), 0, s, kt, n_rows, arena,
                        arena_len, desc, n, index, n_dev, hpm);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -440,7 +431,7 @@ hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_
 hipError_t mq_launch_chacha_prepass(const KeyRow* kt, uint32_t n_rows, const uint8_t* arena, uint64_t arena_len,
                                     const mq_pkt_desc* desc, uint32_t n, uint2* hpm, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(mq_chacha_open_hp_kernel, dim3((n + 255) / 256), dim3(256), 0, s, kt, n_rows, arena, arena_len,
+  hipLaunchKernelGGL(mq_chacha_open_hp_kernel<false>, dim3((n + 255) / 256), dim3(256), 0, s, kt, n_rows, arena, arena_len,
                      desc, n, (const uint32_t*)nullptr, (const uint32_t*)nullptr, hpm);
   return hipGetLastError();
 }

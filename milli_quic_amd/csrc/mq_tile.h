@@ -216,17 +216,81 @@ __device__ __forceinline__ bool prepass_pick(uint32_t t, uint32_t suite, const K
                                              const mq_pkt_desc* __restrict__ desc, uint32_t n,
                                              const uint32_t* __restrict__ index,
                                              const uint32_t* __restrict__ n_dev, uint32_t& i,
-                                             const KeyRow*& row, uint64_t& sample_at) {
+                                             const KeyRow*& row, uint64_t& sample_at, mq_pkt_desc& d) {
   const uint32_t count = n_dev ? *n_dev : n;
   if (t >= count) return false;
   i = index ? index[t] : t;
-  const mq_pkt_desc d = desc[i];
+  d = desc[i];
   if (d.key_id >= n_rows || d.offset + (uint64_t)d.len > arena_len || (d.flags & MQ_PKT_NO_HP) ||
       (uint64_t)d.pn_offset + 20 > d.len)
     return false;
   row = kt + d.key_id;
   if (row->suite != suite) return false;
   sample_at = d.offset + d.pn_offset + 4;
+  return true;
+}
+
+// Batch-open pre-pass output: instead of the raw mask, what the tile kernel derives from it —
+// the unmasked first byte (| 0x100) and the unmasked truncated packet number (recv.rs:371-391) —
+// so the tile kernel knows pn_len and the nonce before its packet has landed in LDS.
+__device__ __forceinline__ uint2 prepass_decode(const uint8_t* __restrict__ arena, const mq_pkt_desc& d,
+                                                uint32_t m0, uint32_t m1) {
+  const uint8_t fb = (d.flags & MQ_PKT_LONG_HEADER) ? 0x0f : 0x1f;
+  const uint8_t b0 = arena[d.offset] ^ ((uint8_t)m0 & fb);
+  const uint32_t pn_len = (b0 & 3u) + 1, mk = (m0 >> 8) | (m1 << 24);
+  uint32_t trunc = 0;
+  for (uint32_t b = 0; b < pn_len; ++b)
+    trunc = (trunc << 8) | (uint8_t)(arena[d.offset + d.pn_offset + b] ^ (uint8_t)(mk >> (8 * b)));
+  return make_uint2(trunc, 0x100u | b0);
+}
+
+// Open, header part (recv.rs:363-395 / :968-997) with the pre-pass values: pn_len, truncated PN,
+// decode_pn and the PN range check. Returns the unmasked first byte.
+__device__ __forceinline__ uint8_t header_from_prepass(PktCtx& c, uint32_t& pn_len, uint32_t& trunc) {
+  const uint8_t b0 = (uint8_t)c.hm1;
+  pn_len = (b0 & 3u) + 1;
+  trunc = c.hm0;
+  c.pn = decode_pn(trunc, pn_len, c.d.pn);
+  if (c.pn > kMaxPn) {
+    c.st = MQ_ERR_PROTOCOL;
+    c.act = false;
+  }
+  return b0;
+}
+
+// Open, header part without the pre-pass: mask (from the policy), unmask byte 0 and the PN in
+// the packet bytes, decode_pn, range check. Returns the unmasked first byte.
+template <class S>
+__device__ __forceinline__ uint8_t header_from_mask(const S& sp, typename S::off_t pkt, PktCtx& c, uint32_t m0,
+                                                    uint32_t m1, uint32_t& pn_len, uint32_t& trunc) {
+  const mq_pkt_desc& d = c.d;
+  const uint8_t fb = (d.flags & MQ_PKT_LONG_HEADER) ? 0x0f : 0x1f;
+  const uint8_t b0 = sp.ld8(pkt) ^ ((uint8_t)m0 & fb);
+  pn_len = (b0 & 3u) + 1;
+  const uint32_t mk = (m0 >> 8) | (m1 << 24);
+  trunc = 0;
+  for (uint32_t b = 0; b < pn_len; ++b)
+    trunc = (trunc << 8) | (uint8_t)(sp.ld8(pkt + d.pn_offset + b) ^ (uint8_t)(mk >> (8 * b)));
+  c.pn = decode_pn(trunc, pn_len, d.pn);
+  if (c.pn > kMaxPn) {
+    c.st = MQ_ERR_PROTOCOL;
+    c.act = false;
+  }
+  return b0;
+}
+
+// Writes the unmasked header of an opened packet (octet lane 0), keeping the received bytes for
+// the direct path's undo on failure.
+template <class S>
+__device__ __forceinline__ bool write_unmasked_header(const S& sp, typename S::off_t pkt, const PktCtx& c, int j,
+                                                      uint8_t b0, uint32_t pn_len, uint32_t trunc,
+                                                      uint8_t& orig_b0, uint32_t& orig_pn) {
+  if (!c.act || j != 0) return false;
+  orig_b0 = sp.ld8(pkt);
+  orig_pn = 0;
+  for (uint32_t b = 0; b < pn_len; ++b) orig_pn |= (uint32_t)sp.ld8(pkt + c.d.pn_offset + b) << (8 * b);
+  sp.st8(pkt, b0);
+  for (uint32_t b = 0; b < pn_len; ++b) sp.st8(pkt + c.d.pn_offset + b, (uint8_t)(trunc >> (8 * (pn_len - 1 - b))));
   return true;
 }
 
