@@ -312,7 +312,7 @@ def test_full_size_roundtrip_config_b(orc):
     idx = np.sort(rng.choice(w.n, size=512, replace=False))
     sub_desc = w.seal_desc[idx].copy()
     o_arena = w.arena.copy()
-    o_st = orc.batch_seal(w.keys, o_arena, sub_desc, w.suite_hint, threads=8)
+    o_st = orc.batch_seal(w.keys, o_arena, sub_desc, w.suite_hint)
     assert (o_st == 0).all()
     for i in idx:
         lo = int(w.seal_desc["offset"][i])
@@ -324,3 +324,31 @@ def test_full_size_roundtrip_config_b(orc):
     back = a.cpu().numpy()
     v = back.reshape(w.n, 1200)[:, :1184]
     assert v.tobytes() == w.arena.reshape(w.n, 1200)[:, :1184].tobytes()
+
+
+# ---------------------------------------------------------------------------------------------
+# batches big enough that every wave of the persistent AES-GCM kernels (one 8-wave workgroup per
+# CU) walks several tiles, with the next tile's descriptors prefetched (flat batches) or read
+# through the partition lists (mixed batches); bit-exact against the oracle on every byte.
+@pytest.mark.parametrize("cfg,n", [("c", 1 << 17), ("e", 1 << 17), ("b", 1 << 15)])
+def test_multi_tile_waves_vs_oracle(orc, cfg, n):
+    w = {"b": workload.config_b, "c": workload.config_c, "e": workload.config_e}[cfg](n)
+    g_out, g_st, _ = gpu_run(w.keys, w.arena, w.seal_desc, w.suite_hint)
+    o_out, o_st, _ = oracle_run(orc, w.keys, w.arena, w.seal_desc, w.suite_hint)
+    assert (o_st == 0).all() and (g_st == o_st).all()
+    assert g_out.tobytes() == o_out.tobytes()
+    for use_ws in ((True, False) if w.suite_hint != _lib.MQ_SUITE_MIXED else (True,)):
+        g_back, g_st, g_pn = gpu_run(w.keys, g_out, w.open_desc, w.suite_hint, open_=True, use_ws=use_ws)
+        assert (g_st == 0).all() and (g_pn == w.pns).all()
+        o_back, _, _ = oracle_run(orc, w.keys, o_out, w.open_desc, w.suite_hint, open_=True)
+        assert g_back.tobytes() == o_back.tobytes()
+
+
+def test_tile_count_edges_aes(orc):
+    # tile counts just below / at / above one tile per wave of the persistent grid (256 CUs x 8
+    # waves = 2048 tiles) and a ragged last tile
+    for n in (2047 * 8 + 3, 2048 * 8, 2049 * 8 + 5):
+        w = workload.config_c(n)
+        g_out, g_st, _ = gpu_run(w.keys, w.arena, w.seal_desc, w.suite_hint)
+        o_out, o_st, _ = oracle_run(orc, w.keys, w.arena, w.seal_desc, w.suite_hint)
+        assert (g_st == 0).all() and g_out.tobytes() == o_out.tobytes()
