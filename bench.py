@@ -168,7 +168,8 @@ def seal_kernel(cfg, n_rows):
 
 def load_traffic(cfg, kern):
     """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC summary
-    (profiles/pmc_traffic_<cfg>.json, written by tools/pmc_summary.py: FETCH_SIZE x 2 + WRITE_SIZE)."""
+    (profiles/pmc_traffic_<cfg>.json, written by tools/pmc_summary.py: FETCH_SIZE x 2 + WRITE_SIZE),
+    measured at the default 2^20 packets per GPU (reported only for that size)."""
     path = os.path.join(ROOT, "profiles", f"pmc_traffic_{cfg}.json")
     try:
         with open(path) as f:
@@ -186,10 +187,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # MQ_BENCH_BACKEND=gloo with more ranks than GPUs rehearses the N-rank path on one GPU
+    # (ranks then share devices: local % device_count); the driver's runs use RCCL, one GPU per rank
+    backend = os.environ.get("MQ_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(local)
 
@@ -256,7 +265,7 @@ def main():
         achieved = algo_bytes / (seal_ms * 1e-3) / 1e9
         kern = seal_kernel(args.config, len(w.keys))
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config, kern),
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config, kern) if w.n == 1 << 20 else None,
                 "kernel": kern or "seal batch (partition + AES + ChaCha kernels)",
                 "seal_ms": round(seal_ms, 4), "open_ms": round(open_ms, 4),
                 "algorithmic_bytes_per_launch": int(algo_bytes)}

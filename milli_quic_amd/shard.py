@@ -49,6 +49,8 @@ def reduce_totals(elapsed, wire_bytes, failures, dist=None, device=None):
     if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
         return Totals(float(elapsed), int(wire_bytes), int(failures))
     import torch
+    if dist.get_backend() != "nccl":
+        device = "cpu"  # gloo reduces host tensors
     t_max = torch.tensor([float(elapsed)], dtype=torch.float64, device=device)
     t_sum = torch.tensor([float(wire_bytes), float(failures)], dtype=torch.float64, device=device)
     dist.all_reduce(t_max, op=dist.ReduceOp.MAX)

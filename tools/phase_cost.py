@@ -10,7 +10,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-BUILD = os.path.join(ROOT, "milli_quic_amd", "csrc", "build")
+BUILD = os.path.join(ROOT, "milli_quic_amd", "prof")
 
 
 def child(lib, cfg, n):
