@@ -160,8 +160,8 @@ __device__ __forceinline__ void xor_words(const S& sp, typename S::off_t a, cons
 }
 
 // Write N payload-aligned words at byte address `a` (any alignment), preserving the bytes of
-// the two edge dwords outside the range by read-modify-write. Only for a single writer per
-// packet (e.g. the tag, written by lane j == 0 after every keystream update of its packet).
+// the two edge dwords outside the range. Only for a single writer per packet (e.g. the tag,
+// written by lane j == 0 after every keystream update of its packet).
 template <int N, class S>
 __device__ __forceinline__ void store_words(const S& sp, typename S::off_t a, const uint32_t (&w)[N]) {
   const typename S::off_t b = a & ~(typename S::off_t)3;
@@ -176,8 +176,10 @@ __device__ __forceinline__ void store_words(const S& sp, typename S::off_t a, co
   const uint32_t e0 = sp.ld32(b), eN = sp.ld32(b + 4 * N);
 #pragma unroll
   for (int m = 1; m < N; ++m) sp.st32(b + 4 * m, perm(w[m], w[m - 1], sel));
-  sp.st32(b, (e0 & keep) | (perm(w[0], 0u, sel) & ~keep));
-  sp.st32(b + 4 * N, (eN & ~keep) | (perm(0u, w[N - 1], sel) & keep));
+  // edge dwords: XOR the change of this packet's own bytes in, never rewrite the neighbour's
+  // (on the direct path another wave may be updating them at the same time)
+  sp.xor32(b, (e0 ^ perm(w[0], 0u, sel)) & ~keep);
+  sp.xor32(b + 4 * N, (eN ^ perm(0u, w[N - 1], sel)) & keep);
 }
 
 // Keep the compiler from sinking the wait for `x`'s load past this point (used to retire the

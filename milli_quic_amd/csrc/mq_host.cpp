@@ -32,9 +32,10 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
 hipError_t mq_launch_aes_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t* key_ids,
                             const uint8_t* samples, uint8_t* masks, uint32_t n, hipStream_t s);
 hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_desc* desc, uint32_t n,
-                               uint32_t* list, uint32_t* block_counts, uint32_t* counts,
-                               hipStream_t s);
+                               uint32_t* list, uint32_t* hist, uint32_t* counts, hipStream_t s);
 size_t mq_partition_workspace(uint32_t n);
+void mq_partition_layout(uint32_t n, size_t* hist_off, size_t* counts_off);
+uint32_t mq_partition_list_cap(uint32_t n);
 hipError_t mq_launch_derive_initial(const mq::MQDeriveConsts& k, const uint8_t* dcids, const uint8_t* dcid_lens,
                                     uint32_t n, KeyRow* rows, mq_key_material* km_out, uint8_t* status,
                                     hipStream_t s);
@@ -665,14 +666,17 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
     if (!ws) return MQ_ERR_INVALID_ARG;
     uint8_t* pw = ws + ws_align(8 * (size_t)n);
     uint32_t* list = (uint32_t*)pw;
-    const size_t nblocks = ((size_t)n + 1023) / 1024;
-    uint32_t* bc = (uint32_t*)(pw + ws_align(sizeof(uint32_t) * 2 * (size_t)n));
-    uint32_t* counts = (uint32_t*)(pw + ws_align(sizeof(uint32_t) * 2 * (size_t)n) + ws_align(sizeof(uint32_t) * 2 * nblocks));
-    e = mq_launch_partition(kt->dev, kt->rows, desc, n, list, bc, counts, s);
+    size_t hist_off, counts_off;
+    mq_partition_layout(n, &hist_off, &counts_off);
+    uint32_t* hist = (uint32_t*)(pw + hist_off);
+    uint32_t* counts = (uint32_t*)(pw + counts_off);
+    // list mode: the grids cover the list capacity; the kernels read the real lengths from counts
+    const uint32_t cap = mq_partition_list_cap(n);
+    e = mq_launch_partition(kt->dev, kt->rows, desc, n, list, hist, counts, s);
     if (e == hipSuccess)
-      e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, n, list, counts, status, pn_out, hpm, s);
+      e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list, counts, status, pn_out, hpm, s);
     if (e == hipSuccess)
-      e = mq_launch_chacha(open, kt->dev, kt->rows, arena, arena_len, desc, n, list + n, counts + 1, status,
+      e = mq_launch_chacha(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list + cap, counts + 1, status,
                            pn_out, hpm, s);
   } else {
     return MQ_ERR_INVALID_ARG;

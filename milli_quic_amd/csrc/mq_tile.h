@@ -16,6 +16,7 @@ namespace mq {
 constexpr uint32_t kScratchBytes = 32 * kPktsPerTile;              // per-packet 32-B scratch (MAC key)
 constexpr uint32_t kDataBudget = kLdsBytes - kScratchBytes - kSlack;  // bytes of packet images
 constexpr uint64_t kMaxPn = (1ull << 62) - 1;         // varint::MAX_VARINT
+constexpr uint32_t kListHole = 0xFFFFFFFFu;            // index-list entry without a packet (mq_partition.hip)
 
 // Per-lane view of its octet's packet.
 struct PktCtx {
@@ -220,6 +221,7 @@ __device__ __forceinline__ bool prepass_pick(uint32_t t, uint32_t suite, const K
   const uint32_t count = n_dev ? *n_dev : n;
   if (t >= count) return false;
   i = index ? index[t] : t;
+  if (i == kListHole) return false;
   d = desc[i];
   if (d.key_id >= n_rows || d.offset + (uint64_t)d.len > arena_len || (d.flags & MQ_PKT_NO_HP) ||
       (uint64_t)d.pn_offset + 20 > d.len)
@@ -343,6 +345,7 @@ __device__ __forceinline__ void run_tile(uint8_t* smem, uint32_t tile_id, const 
     if (OPEN && hpm) { c.hm0 = oct_lane<0>(pf.hm); c.hm1 = oct_lane<1>(pf.hm); }
   } else {
     c.i = c.valid ? (index ? index[t] : t) : 0u;
+    if (c.i == kListHole) { c.valid = false; c.i = 0; }
     if (c.valid) {
       c.d = desc[c.i];
     } else {

@@ -215,8 +215,12 @@ def oracle_run(orc, keys, arena, desc, hint, open_=False):
     return a, orc.batch_seal(keys, a, desc, hint, threads=8), None
 
 
-def test_mixed_batch_vs_oracle(orc):
-    w = workload.config_e(20000, seed=0x1234)
+@pytest.mark.parametrize("n,lmin,lmax", [(20000, 64, 1350), (6000, 64, 4000), (3000, 1200, 1500)])
+def test_mixed_batch_vs_oracle(orc, n, lmin, lmax):
+    # the partition groups packets by suite and 64-B length class; long classes get tiles with
+    # holes (fewer packets per tile), the longest class tiles overflow LDS and run the direct
+    # path next to staged neighbours
+    w = workload.config_e(n, seed=0x1234 + lmax, lmin=lmin, lmax=lmax)
     g_out, g_st, _ = gpu_run(w.keys, w.arena, w.seal_desc, w.suite_hint)
     o_out, o_st, _ = oracle_run(orc, w.keys, w.arena, w.seal_desc, w.suite_hint)
     assert (o_st == 0).all()
