@@ -24,14 +24,21 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, n, out_dir):
+def _span(w, rank, world, balance):
+    if balance == "bytes":
+        return shard.shard_range_bytes(w.seal_desc["len"], rank, world)
+    return shard.shard_range(w.n, rank, world)
+
+
+def _worker(rank, world, port, n, out_dir, balance):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle import oracle
     w = workload.config_e(n, seed=0xABCD)  # every rank builds the same global batch
-    arena, desc = shard.shard_batch(w.arena, w.seal_desc, rank, world)
+    arena, desc = shard.shard_batch(w.arena, w.seal_desc, rank, world, balance=balance)
     st = oracle.batch_seal(w.keys, arena, desc, w.suite_hint, threads=2)
-    lo, hi = shard.shard_range(w.n, rank, world)
+    csum = shard.reduce_checksum(shard.tag_checksum(arena, desc), dist)
+    lo, hi = _span(w, rank, world, balance)
     odesc = w.open_desc[lo:hi].copy()
     odesc["offset"] = desc["offset"]
     sealed = arena.copy()
@@ -39,7 +46,8 @@ def _worker(rank, world, port, n, out_dir):
     tot = shard.reduce_totals(0.5 + rank, int(desc["len"].astype(np.int64).sum()),
                               int((st != 0).sum() + (st2 != 0).sum()), dist)
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), sealed=sealed, desc=desc, st=st, st2=st2, pn=pn,
-             tot=np.array([tot.elapsed, tot.wire_bytes, tot.failures], dtype=np.float64))
+             tot=np.array([tot.elapsed, tot.wire_bytes, tot.failures], dtype=np.float64),
+             csum=np.array([csum], dtype=np.int64))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -59,18 +67,35 @@ def test_reduce_totals_single_process():
     assert (t.elapsed, t.wire_bytes, t.failures) == (1.5, 100, 2)
 
 
-def test_two_rank_gloo_shards_match_single_process(tmp_path):
+def test_shard_range_bytes_balances_bytes():
+    rng = np.random.default_rng(7)
+    for n in (0, 1, 5, 1000, 20000):
+        L = rng.integers(64, 1351, size=n)
+        for world in (1, 2, 3, 8):
+            spans = [shard.shard_range_bytes(L, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            if n >= world * 10:
+                share = L.sum() / world
+                for lo, hi in spans:  # within one packet of the ideal share at either end
+                    assert abs(int(L[lo:hi].sum()) - share) <= 2 * L.max()
+
+
+@pytest.mark.parametrize("balance", ["count", "bytes"])
+def test_two_rank_gloo_shards_match_single_process(tmp_path, balance):
     n, world = 3000, 2
-    mp.spawn(_worker, args=(world, _free_port(), n, str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), n, str(tmp_path), balance), nprocs=world, join=True)
     from oracle import oracle
     w = workload.config_e(n, seed=0xABCD)
     whole = w.arena.copy()
     st_all = oracle.batch_seal(w.keys, whole, w.seal_desc.copy(), w.suite_hint, threads=2)
     assert (st_all == 0).all()
+    whole_csum = shard.tag_checksum(whole, w.seal_desc)
     total_wire = 0
     for r in range(world):
         z = np.load(tmp_path / f"r{r}.npz")
-        lo, hi = shard.shard_range(n, r, world)
+        assert int(z["csum"][0]) == whole_csum  # checksum of the shards' checksums
+        lo, hi = _span(w, r, world, balance)
         assert (z["st"] == 0).all() and (z["st2"] == 0).all()
         assert (z["pn"] == w.pns[lo:hi]).all()
         for k in range(hi - lo):  # every sealed packet of the shard equals the whole-batch seal
