@@ -70,6 +70,10 @@ struct LdsSpace {
   __device__ __forceinline__ uint8_t ld8(uint32_t a) const { return base[a]; }
   __device__ __forceinline__ void st8(uint32_t a, uint8_t v) const { base[a] = v; }
   __device__ __forceinline__ void xor32(uint32_t a, uint32_t v) const { atomicXor((uint32_t*)(base + a), v); }
+  // dword at a: bytes under `mask` become those of v (the wave's private image: no other writer)
+  __device__ __forceinline__ void merge32(uint32_t a, uint32_t old, uint32_t v, uint32_t mask) const {
+    st32(a, (old & ~mask) | (v & mask));
+  }
 };
 
 struct GlobalSpace {
@@ -87,6 +91,11 @@ struct GlobalSpace {
   __device__ __forceinline__ uint8_t ld8(uint64_t a) const { return a < len ? base[a] : (uint8_t)0; }
   __device__ __forceinline__ void st8(uint64_t a, uint8_t v) const { base[a] = v; }
   __device__ __forceinline__ void xor32(uint64_t a, uint32_t v) const { atomicXor((uint32_t*)(base + a), v); }
+  // dword at a: bytes under `mask` become those of v. Another wave may be updating the other
+  // bytes (a neighbouring packet on the direct path), so only the change of ours is XORed in.
+  __device__ __forceinline__ void merge32(uint64_t a, uint32_t old, uint32_t v, uint32_t mask) const {
+    xor32(a, (old ^ v) & mask);
+  }
 };
 
 // v_perm_b32 selectors: loads realign memory dwords to a payload that starts `v` bytes into a
@@ -176,10 +185,9 @@ __device__ __forceinline__ void store_words(const S& sp, typename S::off_t a, co
   const uint32_t e0 = sp.ld32(b), eN = sp.ld32(b + 4 * N);
 #pragma unroll
   for (int m = 1; m < N; ++m) sp.st32(b + 4 * m, perm(w[m], w[m - 1], sel));
-  // edge dwords: XOR the change of this packet's own bytes in, never rewrite the neighbour's
-  // (on the direct path another wave may be updating them at the same time)
-  sp.xor32(b, (e0 ^ perm(w[0], 0u, sel)) & ~keep);
-  sp.xor32(b + 4 * N, (eN ^ perm(0u, w[N - 1], sel)) & keep);
+  // edge dwords: only this packet's bytes change (merge32: race-free on the direct path)
+  sp.merge32(b, e0, perm(w[0], 0u, sel), ~keep);
+  sp.merge32(b + 4 * N, eN, perm(0u, w[N - 1], sel), keep);
 }
 
 // Keep the compiler from sinking the wait for `x`'s load past this point (used to retire the
