@@ -170,6 +170,9 @@ __device__ __forceinline__ void gf_mul(uint32_t (&a)[4], const GfOp& b) {
 constexpr uint32_t kGhBytes = 8192, kTwBytes = 65536;
 constexpr int kAesWaves = 8;  // tile waves per workgroup: 72 KiB tables + 8 x 10 KiB images = 152 KiB
 __shared__ __attribute__((aligned(16))) uint32_t g_aes_lds[(kGhBytes + kTwBytes) / 4];
+// multi-key tile kernels: the key row whose H^8 the GHASH table holds (the batch's most frequent
+// AES key, found by the mixed-batch partition), or nullptr when the table is not built
+__shared__ const KeyRow* g_aes_hot_row;
 
 __device__ __forceinline__ uint32_t xtime8(uint32_t s) { return ((s << 1) ^ ((s & 0x80) ? 0x11bu : 0u)) & 0xffu; }
 

@@ -26,11 +26,13 @@ namespace mq {
 // Interleaved GHASH over AAD||pad||CT||pad||[len(A)]64||[len(C)]64 (bit lengths): lane j takes
 // blocks 8k + j with multiplier H^8, then one final multiply by H^(8-j) (row->H[7-j], computed on
 // the host per key), then the octet XOR. Every lane of the octet returns the same value
-// (reflected basis).
+// (reflected basis). The H^8 multiplies go through the LDS table in the single-key kernels (TAB)
+// and, in the multi-key kernels, in waves whose active packets all use the table's row
+// (g_aes_hot_row); otherwise through the bit-holed integer product.
 template <bool TAB, class S>
-__device__ __forceinline__ void ghash(const S& sp, typename S::off_t pkt, typename S::off_t pay,
-                                      uint32_t aad_len, uint32_t ct_len, const KeyRow* row, int j,
-                                      bool act, uint32_t (&y)[4]) {
+__device__ __forceinline__ void ghash_impl(const S& sp, typename S::off_t pkt, typename S::off_t pay,
+                                           uint32_t aad_len, uint32_t ct_len, const KeyRow* row, int j,
+                                           bool act, uint32_t (&y)[4]) {
 #if MQ_PROF_SKIP & 2
   for (int w = 0; w < 4; ++w) y[w] = row->H[0][w] ^ aad_len ^ ct_len;
   return;
@@ -95,6 +97,17 @@ __device__ __forceinline__ void ghash(const S& sp, typename S::off_t pkt, typena
   }
 #pragma unroll
   for (int w = 0; w < 4; ++w) y[w] = oct_xor(acc[w]);
+}
+
+// Two instantiations, so that a wave holds the registers of one multiply method only.
+template <bool TAB, class S>
+__device__ __forceinline__ void ghash(const S& sp, typename S::off_t pkt, typename S::off_t pay,
+                                      uint32_t aad_len, uint32_t ct_len, const KeyRow* row, int j,
+                                      bool act, uint32_t (&y)[4]) {
+  if (TAB || (g_aes_hot_row != nullptr && !wave_any(act && row != g_aes_hot_row)))
+    ghash_impl<true>(sp, pkt, pay, aad_len, ct_len, row, j, act, y);
+  else
+    ghash_impl<false>(sp, pkt, pay, aad_len, ct_len, row, j, act, y);
 }
 
 // TAB: single-key kernel with the GHASH table of H^8 in LDS
@@ -367,14 +380,20 @@ using namespace mq;
 // variants run when the key table has a single row: round keys and H powers in SGPRs, and the
 // GHASH table of that row's H^8.
 template <bool SINGLE>
-__device__ __forceinline__ void aes_tables(const KeyRow* __restrict__ kt) {
+__device__ __forceinline__ void aes_tables(const KeyRow* __restrict__ kt, uint32_t n_rows,
+                                           const uint32_t* __restrict__ hot) {
   build_tw(threadIdx.x, blockDim.x);
-  if (SINGLE) {
+  // multi-key kernels: a GHASH table for the hot row when the partition found one (`hot` points
+  // at its index in the workspace; an out-of-range index means none)
+  const uint32_t r = SINGLE ? 0u : (hot ? *hot : 0xFFFFFFFFu);
+  if (SINGLE || r < n_rows) {
+    if (!SINGLE && threadIdx.x == 0) g_aes_hot_row = kt + r;
     uint32_t h8[4];
 #pragma unroll
-    for (int w = 0; w < 4; ++w) h8[w] = brev(kt[0].H[7][w]);
+    for (int w = 0; w < 4; ++w) h8[w] = brev(kt[r].H[7][w]);
     build_gh(h8, threadIdx.x, blockDim.x);  // ends with a barrier
   } else {
+    if (threadIdx.x == 0) g_aes_hot_row = nullptr;
     __syncthreads();
   }
 }
@@ -383,9 +402,9 @@ __device__ __forceinline__ void aes_tables(const KeyRow* __restrict__ kt) {
   extern "C" __global__ __launch_bounds__(64 * kAesWaves) void NAME_SEAL(                                 \
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
-      const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status) {                                 \
+      const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, const uint32_t* __restrict__ hot) { \
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];                                        \
-    aes_tables<SINGLE>(kt);                                                                               \
+    aes_tables<SINGLE>(kt, n_rows, hot);                                                                  \
     const uint32_t w = threadIdx.x >> 6;                                                                  \
     run_tiles<AesPolicyT<SINGLE>, false, SINGLE>(smem + w * kLdsBytes, blockIdx.x * kAesWaves + w,        \
                                                  gridDim.x * kAesWaves, kt, n_rows, arena, arena_len, desc,\
@@ -395,9 +414,9 @@ __device__ __forceinline__ void aes_tables(const KeyRow* __restrict__ kt) {
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
       const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,    \
-      const uint2* __restrict__ hpm) {                                                                    \
+      const uint2* __restrict__ hpm, const uint32_t* __restrict__ hot) {                                  \
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];                                        \
-    aes_tables<SINGLE>(kt);                                                                               \
+    aes_tables<SINGLE>(kt, n_rows, hot);                                                                  \
     const uint32_t w = threadIdx.x >> 6;                                                                  \
     run_tiles<AesPolicyT<SINGLE>, true, SINGLE>(smem + w * kLdsBytes, blockIdx.x * kAesWaves + w,         \
                                                 gridDim.x * kAesWaves, kt, n_rows, arena, arena_len, desc, \
@@ -465,7 +484,7 @@ static uint32_t aes_grid(uint32_t tiles) {
 
 hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena, uint64_t arena_len,
                          const mq_pkt_desc* desc, uint32_t n, const uint32_t* index, const uint32_t* n_dev,
-                         uint8_t* status, uint64_t* pn_out, uint2* hpm, hipStream_t s) {
+                         uint8_t* status, uint64_t* pn_out, uint2* hpm, hipStream_t s, const uint32_t* hot) {
   const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
   if (tiles == 0) return hipSuccess;
   const uint32_t blocks = aes_grid(tiles);
@@ -478,10 +497,10 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
   }
   if (open)
     hipLaunchKernelGGL(n_rows == 1 ? mq_aes_open1_kernel : mq_aes_open_kernel, dim3(blocks), dim3(64 * kAesWaves),
-                       dyn, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm);
+                       dyn, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm, hot);
   else
     hipLaunchKernelGGL(n_rows == 1 ? mq_aes_seal1_kernel : mq_aes_seal_kernel, dim3(blocks), dim3(64 * kAesWaves),
-                       dyn, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status);
+                       dyn, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, hot);
   return hipGetLastError();
 }
 

@@ -28,7 +28,7 @@ hipError_t mq_launch_chacha_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t
 hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena,
                          uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
                          const uint32_t* index, const uint32_t* n_dev, uint8_t* status,
-                         uint64_t* pn_out, uint2* hpm, hipStream_t s);
+                         uint64_t* pn_out, uint2* hpm, hipStream_t s, const uint32_t* hot = nullptr);
 hipError_t mq_launch_aes_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t* key_ids,
                             const uint8_t* samples, uint8_t* masks, uint32_t n, hipStream_t s);
 hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_desc* desc, uint32_t n,
@@ -674,7 +674,8 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
     const uint32_t cap = mq_partition_list_cap(n);
     e = mq_launch_partition(kt->dev, kt->rows, desc, n, list, hist, counts, s);
     if (e == hipSuccess)
-      e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list, counts, status, pn_out, hpm, s);
+      e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list, counts, status, pn_out, hpm, s,
+                        counts + 2 /* the partition's hot AES key row */);
     if (e == hipSuccess)
       e = mq_launch_chacha(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list + cap, counts + 1, status,
                            pn_out, hpm, s);

@@ -13,8 +13,14 @@
 // the order changes nothing but the tile composition: a tile runs as long as its longest packet,
 // and a uniformly mixed 64-1350-B batch otherwise pays for 8 x its maximum in nearly every tile.
 //
-// Counting sort in three launches: per-block class histograms (class-major), one exclusive scan of
-// the histograms, scatter.
+// AES packets are further split by key: the batch's majority AES key (Boyer-Moore vote; in a
+// server's mix the 1-RTT key of the busiest path) goes first in the AES list, so its tiles are
+// key-uniform and the multi-key AES kernels run their GHASH through the LDS table of that key's
+// H^8 (counts[2] = its row, or 0xFFFFFFFF). With no majority the vote's candidate is just some
+// key: results are the same, only fewer tiles use the table.
+//
+// Launches: per-block votes, one vote reduction, per-block class histograms (class-major), one
+// exclusive scan of the histograms, scatter.
 #include "mq_tile.h"
 
 using namespace mq;
@@ -23,15 +29,40 @@ namespace {
 constexpr int kPartThreads = 256;
 constexpr int kPartItems = 16;  // descriptors per thread
 constexpr int kPartBlock = kPartThreads * kPartItems;
-constexpr uint32_t kLenClasses = 32;  // per suite: min(len / 64, 31), longest first
-constexpr uint32_t kClasses = 2 * kLenClasses;
+constexpr uint32_t kLenClasses = 32;  // per group: min(len / 64, 31), longest first
+constexpr uint32_t kGroups = 3;       // AES with the hot key, other AES (both: list 0), the rest (list 1)
+constexpr uint32_t kClasses = kGroups * kLenClasses;
 constexpr uint32_t kBudgetChunks = kDataBudget / 16;
+constexpr uint32_t kNoKey = 0xFFFFFFFFu;
 
-// class = suite * kLenClasses + (31 - length bucket); suite 0 = AES-128-GCM, 1 = the rest
-__device__ __forceinline__ uint32_t part_class(const KeyRow* kt, uint32_t n_rows, const mq_pkt_desc& d) {
-  const bool aes = d.key_id < n_rows && kt[d.key_id].suite == MQ_SUITE_AES128GCM;
+__device__ __forceinline__ bool is_aes(const KeyRow* kt, uint32_t n_rows, const mq_pkt_desc& d) {
+  return d.key_id < n_rows && kt[d.key_id].suite == MQ_SUITE_AES128GCM;
+}
+
+// class = group * kLenClasses + (31 - length bucket)
+__device__ __forceinline__ uint32_t part_class(const KeyRow* kt, uint32_t n_rows, uint32_t hot,
+                                               const mq_pkt_desc& d) {
+  const uint32_t g = is_aes(kt, n_rows, d) ? (d.key_id == hot ? 0u : 1u) : 2u;
   const uint32_t b = min(d.len >> 6, kLenClasses - 1);
-  return (aes ? 0u : kLenClasses) + (kLenClasses - 1 - b);
+  return g * kLenClasses + (kLenClasses - 1 - b);
+}
+
+// Boyer-Moore majority pairs (candidate, count); combining any partition of the input in any
+// order keeps the majority element if there is one
+__device__ __forceinline__ uint2 vote_join(uint2 a, uint2 b) {
+  if (a.x == b.x) return make_uint2(a.x, a.y + b.y);
+  return a.y >= b.y ? make_uint2(a.x, a.y - b.y) : make_uint2(b.x, b.y - a.y);
+}
+
+__device__ __forceinline__ uint2 block_vote(uint2 v) {  // 256 threads
+  __shared__ uint2 s_v[kPartThreads];
+  s_v[threadIdx.x] = v;
+  __syncthreads();
+  for (int d = kPartThreads / 2; d > 0; d >>= 1) {
+    if ((int)threadIdx.x < d) s_v[threadIdx.x] = vote_join(s_v[threadIdx.x], s_v[threadIdx.x + d]);
+    __syncthreads();
+  }
+  return s_v[0];
 }
 
 // Packets per tile of a class: as many as fit the LDS image budget at the class's longest
@@ -53,15 +84,40 @@ uint32_t mq_partition_list_cap(uint32_t n) {
   return (uint32_t)((c + kPktsPerTile - 1) & ~(uint64_t)(kPktsPerTile - 1));
 }
 
+extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_vote_kernel(
+    const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_pkt_desc* __restrict__ desc, uint32_t n,
+    uint2* __restrict__ votes) {
+  uint2 v = make_uint2(kNoKey, 0u);
+  for (int k = 0; k < kPartItems; ++k) {
+    const uint32_t i = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
+    if (i < n) {
+      const mq_pkt_desc d = desc[i];
+      if (is_aes(kt, n_rows, d)) v = vote_join(v, make_uint2(d.key_id, 1u));
+    }
+  }
+  v = block_vote(v);
+  if (threadIdx.x == 0) votes[blockIdx.x] = v;
+}
+
+// Single workgroup: the batch's vote; meta[0] = the hot key row (kNoKey if no AES packet)
+extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_vote_reduce_kernel(
+    const uint2* __restrict__ votes, uint32_t nblocks, uint32_t* __restrict__ meta) {
+  uint2 v = make_uint2(kNoKey, 0u);
+  for (uint32_t k = threadIdx.x; k < nblocks; k += kPartThreads) v = vote_join(v, votes[k]);
+  v = block_vote(v);
+  if (threadIdx.x == 0) meta[0] = v.y ? v.x : kNoKey;
+}
+
 extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_count_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_pkt_desc* __restrict__ desc, uint32_t n,
-    uint32_t nblocks, uint32_t* __restrict__ hist) {
+    uint32_t nblocks, const uint32_t* __restrict__ hot_p, uint32_t* __restrict__ hist) {
   __shared__ uint32_t s_cnt[kClasses];
   if (threadIdx.x < kClasses) s_cnt[threadIdx.x] = 0;
   __syncthreads();
+  const uint32_t hot = *hot_p;
   for (int k = 0; k < kPartItems; ++k) {
     const uint32_t i = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
-    if (i < n) atomicAdd(&s_cnt[part_class(kt, n_rows, desc[i])], 1u);
+    if (i < n) atomicAdd(&s_cnt[part_class(kt, n_rows, hot, desc[i])], 1u);
   }
   __syncthreads();
   if (threadIdx.x < kClasses) hist[(size_t)threadIdx.x * nblocks + blockIdx.x] = s_cnt[threadIdx.x];
@@ -69,8 +125,8 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_count_kernel(
 
 // Single workgroup: per class, the exclusive scan of its per-block counts (in place: the rank of
 // the block's first packet inside the class); then the class segments (whole tiles) are laid out
-// suite by suite: seg[c] = first list entry of class c (suite 1 starts at `cap`), counts[s] =
-// entries of suite s's list, holes included.
+// list by list (groups 0 and 1: list 0, group 2: list 1 at `cap`): seg[c] = first list entry of
+// class c, counts[s] = entries of list s, holes included.
 extern "C" __global__ __launch_bounds__(1024) void mq_part_scan_kernel(uint32_t* __restrict__ hist,
                                                                         uint32_t nblocks, uint32_t cap,
                                                                         uint32_t* __restrict__ counts,
@@ -97,8 +153,9 @@ extern "C" __global__ __launch_bounds__(1024) void mq_part_scan_kernel(uint32_t*
   __syncthreads();
   if (threadIdx.x < 2) {
     const uint32_t s = threadIdx.x;
+    const uint32_t c0 = s == 0 ? 0u : 2 * kLenClasses, c1 = s == 0 ? 2 * kLenClasses : kClasses;
     uint32_t e = 0;
-    for (uint32_t c = s * kLenClasses; c < (s + 1) * kLenClasses; ++c) {
+    for (uint32_t c = c0; c < c1; ++c) {
       seg[c] = s * cap + e;
       const uint32_t ppt = class_ppt(c);
       e += kPktsPerTile * ((s_tot[c] + ppt - 1) / ppt);
@@ -109,9 +166,10 @@ extern "C" __global__ __launch_bounds__(1024) void mq_part_scan_kernel(uint32_t*
 
 extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_scatter_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_pkt_desc* __restrict__ desc, uint32_t n,
-    uint32_t nblocks, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ seg,
-    uint32_t* __restrict__ list) {
+    uint32_t nblocks, const uint32_t* __restrict__ hot_p, const uint32_t* __restrict__ hist,
+    const uint32_t* __restrict__ seg, uint32_t* __restrict__ list) {
   __shared__ uint32_t s_rank[kClasses];
+  const uint32_t hot = *hot_p;
   const int lane = threadIdx.x & 63;
   if (threadIdx.x < kClasses) s_rank[threadIdx.x] = hist[(size_t)threadIdx.x * nblocks + blockIdx.x];
   __syncthreads();
@@ -119,11 +177,11 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_scatter_kerne
   for (int k = 0; k < kPartItems; ++k) {
     const uint32_t i = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
     const bool in = i < n;
-    const uint32_t c = in ? part_class(kt, n_rows, desc[i]) : 0u;
-    // lanes of this wave with the same class (6 ballots), rank among them = peers below
+    const uint32_t c = in ? part_class(kt, n_rows, hot, desc[i]) : 0u;
+    // lanes of this wave with the same class (7 ballots), rank among them = peers below
     uint64_t peers = __ballot(in);
 #pragma unroll
-    for (int bit = 0; bit < 6; ++bit) {
+    for (int bit = 0; bit < 7; ++bit) {
       const uint64_t b = __ballot((c >> bit) & 1u);
       peers &= ((c >> bit) & 1u) ? b : ~b;
     }
@@ -145,30 +203,34 @@ hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_d
   const uint32_t nblocks = (n + kPartBlock - 1) / kPartBlock;
   if (nblocks == 0) return hipMemsetAsync(counts, 0, 2 * sizeof(uint32_t), s);
   const uint32_t cap = mq_partition_list_cap(n);
-  uint32_t* seg = counts + 2;
+  uint32_t* hot = counts + 2;  // meta: counts[0..1] | hot row | pad | seg[kClasses]
+  uint32_t* seg = counts + 4;
+  uint2* votes = (uint2*)(hist + (size_t)kClasses * nblocks);
   hipError_t e = hipMemsetAsync(list, 0xff, sizeof(uint32_t) * 2 * (size_t)cap, s);  // holes
   if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(mq_part_vote_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, kt, n_rows, desc, n, votes);
+  hipLaunchKernelGGL(mq_part_vote_reduce_kernel, dim3(1), dim3(kPartThreads), 0, s, votes, nblocks, hot);
   hipLaunchKernelGGL(mq_part_count_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, kt, n_rows, desc, n,
-                     nblocks, hist);
+                     nblocks, hot, hist);
   hipLaunchKernelGGL(mq_part_scan_kernel, dim3(1), dim3(1024), 0, s, hist, nblocks, cap, counts, seg);
   hipLaunchKernelGGL(mq_part_scatter_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, kt, n_rows, desc, n,
-                     nblocks, hist, seg, list);
+                     nblocks, hot, hist, seg, list);
   return hipGetLastError();
 }
 
-// list (2 x cap entries) | class histograms (kClasses per block) | 2 totals + kClasses segment
-// starts, 256-B aligned pieces
+// list (2 x cap entries) | class histograms (kClasses per block) + votes (2 words per block) |
+// meta (2 totals, hot row, pad, kClasses segment starts), 256-B aligned pieces
 static size_t part_align(size_t b) { return (b + 255) & ~(size_t)255; }
 
 size_t mq_partition_workspace(uint32_t n) {
   const size_t nblocks = (n + kPartBlock - 1) / kPartBlock;
   return part_align(sizeof(uint32_t) * 2 * (size_t)mq_partition_list_cap(n)) +
-         part_align(sizeof(uint32_t) * kClasses * nblocks) + part_align(sizeof(uint32_t) * (2 + kClasses));
+         part_align(sizeof(uint32_t) * (kClasses + 2) * nblocks) + part_align(sizeof(uint32_t) * (4 + kClasses));
 }
 
 // offsets of the pieces inside the partition workspace
 void mq_partition_layout(uint32_t n, size_t* hist_off, size_t* counts_off) {
   const size_t nblocks = (n + kPartBlock - 1) / kPartBlock;
   *hist_off = part_align(sizeof(uint32_t) * 2 * (size_t)mq_partition_list_cap(n));
-  *counts_off = *hist_off + part_align(sizeof(uint32_t) * kClasses * nblocks);
+  *counts_off = *hist_off + part_align(sizeof(uint32_t) * (kClasses + 2) * nblocks);
 }

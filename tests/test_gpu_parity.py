@@ -215,6 +215,35 @@ def oracle_run(orc, keys, arena, desc, hint, open_=False):
     return a, orc.batch_seal(keys, a, desc, hint, threads=8), None
 
 
+@pytest.mark.parametrize("n_keys,majority", [(97, False), (5, False), (2, True)])
+def test_mixed_hint_aes_keys_vs_oracle(orc, n_keys, majority):
+    # MQ_SUITE_MIXED over an all-AES batch: the partition's majority vote picks a hot key whose
+    # tiles run GHASH through the workgroup table; without a majority (97 or 5 keys round-robin)
+    # its candidate is one key among many, with a majority (2 keys, 3/4 of packets on key 0) it
+    # is key 0. Results equal the oracle either way.
+    w = workload.uniform(4000, _lib.MQ_SUITE_AES128GCM, L=700, n_keys=n_keys)
+    seal, opn = w.seal_desc.copy(), w.open_desc.copy()
+    if majority:
+        k = (np.arange(w.n) % 4 == 3).astype(np.uint32)
+        seal["key_id"] = k
+        opn["key_id"] = k
+    g_out, g_st, _ = gpu_run(w.keys, w.arena, seal, _lib.MQ_SUITE_MIXED)
+    o_out, o_st, _ = oracle_run(orc, w.keys, w.arena, seal, _lib.MQ_SUITE_MIXED)
+    assert (o_st == 0).all() and (g_st == o_st).all()
+    assert g_out.tobytes() == o_out.tobytes()
+    g_back, g_st, g_pn = gpu_run(w.keys, g_out, opn, _lib.MQ_SUITE_MIXED, open_=True)
+    o_back, o_st, o_pn = oracle_run(orc, w.keys, o_out, opn, _lib.MQ_SUITE_MIXED, open_=True)
+    assert (g_st == 0).all() and (g_st == o_st).all() and (g_pn == o_pn).all()
+    assert g_back.tobytes() == o_back.tobytes()
+    # open restores every plaintext byte; the 16 tag bytes of each packet stay as sealed (the
+    # workload's plaintext has zeros there, seal wrote the tag, open leaves it in place)
+    L = 700
+    tag = np.zeros(len(w.arena), dtype=bool)
+    tag.reshape(-1, L)[:, L - 16:] = True
+    assert g_back[~tag].tobytes() == w.arena[~tag].tobytes()
+    assert g_back[tag].tobytes() == g_out[tag].tobytes()
+
+
 @pytest.mark.parametrize("n,lmin,lmax", [(20000, 64, 1350), (6000, 64, 4000), (3000, 1200, 1500)])
 def test_mixed_batch_vs_oracle(orc, n, lmin, lmax):
     # the partition groups packets by suite and 64-B length class; long classes get tiles with
