@@ -50,6 +50,23 @@ __global__ __launch_bounds__(256) void k_rate(uint32_t* out, uint32_t seed) {
       P4(x0) P4(x1) P4(x2) P4(x3)
       f0 = x0.x; f1 = x0.y; f2 = x1.x; f3 = x1.y; f4 = x2.x; f5 = x2.y; f6 = x3.x; f7 = x3.y;
     }
+    if (K == 23) {  // grouped by type across 8 chains: 8 add, 8 xor, 8 alignbit
+#define GA(I) asm volatile("v_add_u32 %0, %0, %1" : "+v"(a##I) : "v"(b));
+#define GX(I) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a##I) : "v"(b));
+#define GR(I) asm volatile("v_alignbit_b32 %0, %0, %0, 16" : "+v"(a##I));
+#define G8(M) M(0) M(1) M(2) M(3) M(4) M(5) M(6) M(7)
+      G8(GA) G8(GX) G8(GR)
+    }
+    if (K == 24) {  // add/xor only, grouped
+      G8(GA) G8(GX)
+    }
+    if (K == 25) {  // grouped by 4: 4 add, 4 xor, 4 align (the compiled ChaCha round shape)
+      GA(0) GA(1) GA(2) GA(3) GX(0) GX(1) GX(2) GX(3) GR(0) GR(1) GR(2) GR(3)
+      GA(4) GA(5) GA(6) GA(7) GX(4) GX(5) GX(6) GX(7) GR(4) GR(5) GR(6) GR(7)
+    }
+    if (K == 26) {  // fast ops in runs of 16, then 8 slow
+      G8(GA) G8(GA) G8(GX) G8(GX) G8(GR) G8(GR)
+    }
     if (K == 11) {  // mixed ChaCha-like: add, xor, alignbit
 #define Q(I) asm volatile("v_add_u32 %0, %0, %1\n v_xor_b32 %0, %0, %1\n v_alignbit_b32 %0, %0, %0, 16" : "+v"(a##I) : "v"(b));
       Q(0) Q(1) Q(2) Q(3) Q(4) Q(5) Q(6) Q(7)
@@ -96,6 +113,16 @@ int run(const char* name, int instr_per_iter, int waves_per_simd) {
 }
 
 int main() {
+  for (int w : {2, 4, 8}) {
+    run<23>("grp8 add/xor/align", 24, w);
+    run<24>("grp8 add/xor", 16, w);
+    run<25>("grp4 add/xor/align", 24, w);
+    run<26>("grp8 x2", 48, w);
+    run<11>("add/xor/align", 24, w);
+    run<0>("v_add_u32", 16, w);
+    run<2>("v_alignbit_b32", 16, w);
+  }
+  return 0;
   for (int w : {2, 4}) {
     run<14>("v_xor_b32_sdwa", 16, w);
     run<15>("v_add_u32_e64", 16, w);
