@@ -1,3 +1,6 @@
+"""Debugging aid for the receive composite (test infrastructure): runs one seeded traffic batch
+through mq_batch_recv and the oracle and prints the first differing packets.
+Usage (GPU box): python tests/debug_recv_diff.py"""
 import sys, numpy as np
 sys.path.insert(0, "tests"); sys.path.insert(0, ".")
 import torch

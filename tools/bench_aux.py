@@ -6,6 +6,8 @@ stream; median of `reps`). Prints one JSON object; the round's copy lives in pro
   recv     mq_batch_recv: the same 2^20 packets as one-packet datagrams of 4096 connections
   records  mq_batch_seal_records / open_records: 2^20 x 1200-B and 2^16 x 16 KiB TLS records
            (AES-128-GCM)
+  hp_mask  mq_batch_hp_mask (SURVEY §8d "mask-only timing"): 2^20 16-B samples -> 5-B masks,
+           AES-128 (config C keys) and ChaCha20 (config B keys)
 Usage: python tools/bench_aux.py [reps]
 """
 import json
@@ -116,6 +118,18 @@ def bench_records(reps, n, L):
             "GiB_per_s_seal_open": round(2 * wire / (ms_s + ms_o) * 1e3 / 2 ** 30, 1)}
 
 
+def bench_hp_mask(reps, suite, n=1 << 20):
+    secret = workload.A1_SERVER_SECRET if suite == _lib.MQ_SUITE_AES128GCM else workload.A5_SECRET
+    km = workload.key_material(suite, secret)
+    kt = KeyTable([km])
+    smp = workload.splitmix_bytes(16 * n, seed=11)
+    s_d = t(smp)
+    kid = torch.zeros(n, dtype=torch.int32, device=DEV)
+    masks = torch.zeros(5 * n, dtype=torch.uint8, device=DEV)
+    ms = timed(lambda: batch.hp_mask(kt, kid, s_d, masks), reps)  # parity: tests/test_gpu_parity.py
+    return {"samples": n, "ms": round(ms, 4), "masks_per_s": round(n / ms * 1e3)}
+
+
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
     assert _lib.load().mq_device_init(0) == 0
@@ -123,6 +137,8 @@ def main():
     res["protect"], res["recv"] = bench_protect_recv(reps)
     res["records_1200"] = bench_records(reps, 1 << 20, 1200)
     res["records_16k"] = bench_records(reps, 1 << 16, 16384 + 5 + 17)
+    res["hp_mask_aes"] = bench_hp_mask(reps, _lib.MQ_SUITE_AES128GCM)
+    res["hp_mask_chacha"] = bench_hp_mask(reps, _lib.MQ_SUITE_CHACHA20)
     print(json.dumps(res), flush=True)
 
 
