@@ -7,8 +7,9 @@
 // byte 0x40 | key_phase << 2 | pn_len - 1), encode_pn (number.rs:32-43), the frames, PADDING
 // (Initial up to 1200 bytes when pad_to_min; otherwise pn_len + payload + tag >= 20), then seal
 // and header protection. Here mq_build_kernel does everything up to the seal for a whole batch —
-// one wave per packet: the request and connection rows are wave-uniform (scalar loads), the
-// header is computed once, and the frames move with aligned dword stores — and emits an
+// each wave builds packets one after another (grid-stride over the batch): the request and
+// connection rows are wave-uniform (scalar loads), the header is computed once, and the frames
+// move 16 B per lane with dword-aligned stores (realigned source) — and emits an
 // mq_pkt_desc per packet; the ChaCha20-Poly1305 / AES-128-GCM tile kernels then seal and
 // header-protect those descriptors, and mq_send_status_kernel folds the build statuses in.
 #include "mq_device.h"
@@ -55,14 +56,14 @@ __device__ __forceinline__ uint8_t header_byte(const mq_conn_send& c, uint32_t l
 
 }  // namespace
 
-extern "C" __global__ __launch_bounds__(64) void mq_build_kernel(
-    const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_conn_send* __restrict__ conns, uint32_t n_conns,
-    const uint8_t* __restrict__ frames, uint64_t frames_len, uint8_t* __restrict__ out, uint64_t out_len,
-    const mq_send_req* __restrict__ req, uint32_t n, mq_pkt_desc* __restrict__ desc, uint8_t* __restrict__ bstatus,
-    uint32_t* __restrict__ pkt_len) {
-  const uint32_t i = blockIdx.x;
-  const int lane = threadIdx.x;
-  if (i >= n) return;
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+// packet i (wave-uniform) built by one wave
+__device__ __forceinline__ void build_one(
+    uint32_t i, int lane, const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_conn_send* __restrict__ conns,
+    uint32_t n_conns, const uint8_t* __restrict__ frames, uint64_t frames_len, uint8_t* __restrict__ out,
+    uint64_t out_len, const mq_send_req* __restrict__ req, mq_pkt_desc* __restrict__ desc,
+    uint8_t* __restrict__ bstatus, uint32_t* __restrict__ pkt_len) {
   const mq_send_req r = req[i];
   mq_pkt_desc d;
   d.offset = r.out_offset; d.len = 0; d.key_id = 0xFFFFFFFFu; d.pn = r.pn; d.pn_offset = 0; d.pn_len = 0;
@@ -81,7 +82,7 @@ extern "C" __global__ __launch_bounds__(64) void mq_build_kernel(
     if (lane == 0) { desc[i] = d; bstatus[i] = (uint8_t)st; pkt_len[i] = 0; }
     return;
   }
-  const mq_conn_send c = *cp;
+  const mq_conn_send& c = *cp;  // read in place: a copy indexed per lane would live in scratch
   // pn_length (number.rs:9-26)
   const uint64_t unacked = r.pn > r.largest_acked ? r.pn - r.largest_acked : 1;
   const uint32_t pn_len = unacked < (1u << 7) ? 1u : unacked < (1u << 15) ? 2u : unacked < (1u << 23) ? 3u : 4u;
@@ -123,7 +124,22 @@ extern "C" __global__ __launch_bounds__(64) void mq_build_kernel(
   const uint32_t sh = (uint32_t)(sa & 3u) * 8u;
   const uint32_t* s4 = (const uint32_t*)(sa & ~(uintptr_t)3);
   uint32_t* d4 = (uint32_t*)(pd + head);
-  for (uint32_t q = lane; q < words; q += kWave) {
+  // 4 words per lane: 16-B stores at dword alignment; every source dword read holds a used byte
+  const uint32_t quads = words >> 2;
+  for (uint32_t q = lane; q < quads; q += kWave) {
+    const uint32_t* sq = s4 + 4 * q;
+    const uint32_t a0 = sq[0], a1 = sq[1], a2 = sq[2], a3 = sq[3];
+    u32x4_a4 v;
+    if (sh) {
+      const uint32_t a4 = sq[4];
+      v = u32x4_a4{__builtin_amdgcn_alignbit(a1, a0, sh), __builtin_amdgcn_alignbit(a2, a1, sh),
+                   __builtin_amdgcn_alignbit(a3, a2, sh), __builtin_amdgcn_alignbit(a4, a3, sh)};
+    } else {
+      v = u32x4_a4{a0, a1, a2, a3};
+    }
+    *(u32x4_a4*)(d4 + 4 * q) = v;
+  }
+  for (uint32_t q = 4 * quads + lane; q < words; q += kWave) {
     const uint32_t lo = s4[q];
     d4[q] = sh ? __builtin_amdgcn_alignbit(s4[q + 1], lo, sh) : lo;  // same aligned dword as a used byte
   }
@@ -140,6 +156,19 @@ extern "C" __global__ __launch_bounds__(64) void mq_build_kernel(
   }
 }
 
+constexpr int kBuildWaves = 4;  // waves per workgroup
+
+extern "C" __global__ __launch_bounds__(64 * kBuildWaves) void mq_build_kernel(
+    const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_conn_send* __restrict__ conns, uint32_t n_conns,
+    const uint8_t* __restrict__ frames, uint64_t frames_len, uint8_t* __restrict__ out, uint64_t out_len,
+    const mq_send_req* __restrict__ req, uint32_t n, mq_pkt_desc* __restrict__ desc, uint8_t* __restrict__ bstatus,
+    uint32_t* __restrict__ pkt_len) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * kBuildWaves + (threadIdx.x >> 6)));
+  for (uint32_t i = w; i < n; i += gridDim.x * kBuildWaves)
+    build_one(i, lane, kt, n_rows, conns, n_conns, frames, frames_len, out, out_len, req, desc, bstatus, pkt_len);
+}
+
 // build failures keep their status (the seal kernel saw an invalid key id for them)
 extern "C" __global__ __launch_bounds__(256) void mq_send_status_kernel(const uint8_t* __restrict__ bstatus,
                                                                         uint8_t* __restrict__ status, uint32_t n) {
@@ -152,8 +181,11 @@ hipError_t mq_launch_build(const KeyRow* kt, uint32_t n_rows, const mq_conn_send
                            const mq_send_req* req, uint32_t n, mq_pkt_desc* desc, uint8_t* bstatus,
                            uint32_t* pkt_len, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(mq_build_kernel, dim3(n), dim3(kWave), 0, s, kt, n_rows, conns, n_conns, frames, frames_len,
-                     out, out_len, req, n, desc, bstatus, pkt_len);
+  // grid-stride: up to 4096 workgroups (16 waves per CU on 256 CUs), each wave then builds
+  // n / 16384 packets in turn
+  const uint32_t wgs = (n + kBuildWaves - 1) / kBuildWaves;
+  hipLaunchKernelGGL(mq_build_kernel, dim3(wgs < 4096u ? wgs : 4096u), dim3(64 * kBuildWaves), 0, s, kt, n_rows,
+                     conns, n_conns, frames, frames_len, out, out_len, req, n, desc, bstatus, pkt_len);
   return hipGetLastError();
 }
 
