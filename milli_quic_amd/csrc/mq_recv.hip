@@ -314,10 +314,30 @@ extern "C" __global__ __launch_bounds__(64) void mq_recv_walk_kernel(
   const mq_conn_recv c = conn0[ci];
   ConnState s = load_state(c);
   uint32_t new_attempts = 0;
-  for (uint32_t k = seg_lo[ci]; k < seg_hi[ci]; ++k) {
-    const uint32_t i = svals[k];
-    const RecvWork w = work[i];
-    RecvPlan p = hdr[i];
+  // software-pipelined walk: the inputs of packet k + 1 (and the index of k + 2) are loaded
+  // before packet k is processed, so the lane waits on memory once per packet at most instead of
+  // three dependent times (the loads never alias this iteration's stores: indices are distinct)
+  const uint32_t lo = seg_lo[ci], hi = seg_hi[ci];
+  uint32_t i_n = 0, i_nn = 0;
+  RecvWork w_n{};
+  RecvPlan p_n{}, t_n{};
+  uint8_t o_n = kNone;
+  if (lo < hi) {
+    i_n = svals[lo];
+    w_n = work[i_n]; p_n = hdr[i_n]; o_n = outcome[i_n]; t_n = tried[i_n];
+  }
+  if (lo + 1 < hi) i_nn = svals[lo + 1];
+  for (uint32_t k = lo; k < hi; ++k) {
+    const uint32_t i = i_n;
+    const RecvWork w = w_n;
+    RecvPlan p = p_n;
+    const uint8_t o_cur = o_n;
+    const RecvPlan t_cur = t_n;
+    if (k + 1 < hi) {
+      i_n = i_nn;
+      w_n = work[i_n]; p_n = hdr[i_n]; o_n = outcome[i_n]; t_n = tried[i_n];
+    }
+    if (k + 2 < hi) i_nn = svals[k + 2];
     decide(s, w, c, n_rows, p);
     mq_pkt_desc a;
     a.offset = w.offset; a.len = w.len; a.key_id = kNoRow; a.pn = p.lbefore; a.pn_offset = w.pn_off;
@@ -326,8 +346,8 @@ extern "C" __global__ __launch_bounds__(64) void mq_recv_walk_kernel(
     uint8_t st = p.status, gen = p.gen;
     RecvPlan used = p;
     if (p.status == kPending) {
-      const uint8_t o = outcome[i];
-      const RecvPlan t = tried[i];
+      const uint8_t o = o_cur;
+      const RecvPlan t = t_cur;
       const bool same = o != kNone && t.pn == p.pn && t.row == p.row && t.retry == p.retry && t.gen == p.gen;
       if (same || o == kOk1 || o == kOk0) {  // known outcome (an opened packet keeps its inputs)
         used = same ? p : t;
