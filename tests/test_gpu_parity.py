@@ -262,9 +262,12 @@ def test_mixed_batch_vs_oracle(orc, n, lmin, lmax):
     assert g_back.tobytes() == o_back.tobytes()
 
 
-@pytest.mark.parametrize("suite", [1, 2])
-def test_failures_match_oracle(orc, suite):
+@pytest.mark.parametrize("suite,mixed", [(1, False), (2, False), (1, True), (2, True)])
+def test_failures_match_oracle(orc, suite, mixed):
+    # mixed: the same failures through MQ_SUITE_MIXED (partition; invalid key ids land in the
+    # ChaCha list and are rejected there)
     w = workload.uniform(2048, suite, L=300)
+    hint = _lib.MQ_SUITE_MIXED if mixed else suite
     sealed, st, _ = oracle_run(orc, w.keys, w.arena, w.seal_desc, suite)
     rng = np.random.default_rng(suite)
     bad = sealed.copy()
@@ -277,10 +280,10 @@ def test_failures_match_oracle(orc, suite):
     od["len"][6] = 24                        # sample out of range -> Crypto
     od["offset"][7] = len(bad) - 10          # past the arena end
     od["pn"][8] = (1 << 62) - 2              # decode_pn lands above 2^62-1 -> ProtocolViolation
-    o_out, o_st, o_pn = oracle_run(orc, w.keys, bad, od, suite, open_=True)
+    o_out, o_st, o_pn = oracle_run(orc, w.keys, bad, od, hint, open_=True)
     assert (o_st != 0).sum() >= 150
-    for use_ws in (True, False):  # HP pre-pass and in-kernel HP
-        g_out, g_st, g_pn = gpu_run(w.keys, bad, od, suite, open_=True, use_ws=use_ws)
+    for use_ws in ((True,) if mixed else (True, False)):  # HP pre-pass and in-kernel HP
+        g_out, g_st, g_pn = gpu_run(w.keys, bad, od, hint, open_=True, use_ws=use_ws)
         assert (g_st == o_st).all(), (use_ws, np.nonzero(g_st != o_st))
         assert g_out.tobytes() == o_out.tobytes(), use_ws
         ok = o_st == 0
@@ -290,9 +293,23 @@ def test_failures_match_oracle(orc, suite):
     sd["pn_len"][4] = 5
     sd["len"][9] = 20                        # len < pn_offset + pn_len + 16
     sd["key_id"][10] = 1 << 20
-    g_out, g_st, _ = gpu_run(w.keys, w.arena, sd, suite)
-    o_out, o_st, _ = oracle_run(orc, w.keys, w.arena, sd, suite)
+    g_out, g_st, _ = gpu_run(w.keys, w.arena, sd, hint)
+    o_out, o_st, _ = oracle_run(orc, w.keys, w.arena, sd, hint)
     assert (g_st == o_st).all() and g_out.tobytes() == o_out.tobytes()
+
+
+@pytest.mark.parametrize("n", [1, 5, 63, 4097])
+def test_mixed_batch_small_counts(orc, n):
+    # partition edges: fewer packets than a tile, one partial partition block, class segments
+    # with a single packet (hole-padded tiles)
+    w = workload.config_e(n, seed=0x77 + n)
+    g_out, g_st, _ = gpu_run(w.keys, w.arena, w.seal_desc, w.suite_hint)
+    o_out, o_st, _ = oracle_run(orc, w.keys, w.arena, w.seal_desc, w.suite_hint)
+    assert (o_st == 0).all() and (g_st == o_st).all() and g_out.tobytes() == o_out.tobytes()
+    g_back, g_st, g_pn = gpu_run(w.keys, g_out, w.open_desc, w.suite_hint, open_=True)
+    o_back, o_st, o_pn = oracle_run(orc, w.keys, o_out, w.open_desc, w.suite_hint, open_=True)
+    assert (g_st == 0).all() and (g_st == o_st).all() and (g_pn == o_pn).all()
+    assert g_back.tobytes() == o_back.tobytes()
 
 
 @pytest.mark.parametrize("suite", [1, 2])
