@@ -257,7 +257,8 @@ int mq_batch_derive_initial(mq_keytable* kt, uint32_t first_row, const uint8_t* 
  * MQ_SUITE_CHACHA20 / MQ_SUITE_AES128GCM for a single-suite batch (one launch; rows of the
  * other suite get MQ_ERR_SUITE) or MQ_SUITE_MIXED (packets are partitioned on the device first
  * by suite and 64-B length class, so that a tile's packets need similar work; results do not
- * depend on the order; needs `workspace` of mq_batch_workspace_size(n) bytes of device memory).
+ * depend on the order; needs `workspace` of mq_batch_workspace_size(n) bytes of device memory;
+ * at most 2^30 packets per mixed batch, else MQ_ERR_INVALID_ARG).
  * `workspace` is optional for single-suite batches; given to mq_batch_open it also enables the
  * header-protection pre-pass (one lane per packet computes the mask, so the packet kernel spends
  * no keystream slot on it) — same results, faster. Workspace contents need not be initialised.

@@ -663,7 +663,9 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
   } else if (suite_hint == MQ_SUITE_AES128GCM) {
     e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, n, nullptr, nullptr, status, pn_out, hpm, s);
   } else if (suite_hint == MQ_SUITE_MIXED) {
-    if (!ws) return MQ_ERR_INVALID_ARG;
+    // the two index lists (2 x mq_partition_list_cap(n) entries, holes included) are addressed
+    // with 32-bit positions: up to 2^30 packets per mixed batch
+    if (!ws || n > (1u << 30)) return MQ_ERR_INVALID_ARG;
     uint8_t* pw = ws + ws_align(8 * (size_t)n);
     uint32_t* list = (uint32_t*)pw;
     size_t hist_off, counts_off;
