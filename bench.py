@@ -266,6 +266,8 @@ def main():
         kern = seal_kernel(args.config, len(w.keys))
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config, kern) if w.n == 1 << 20 else None,
+                # north_star's "HBM-read roofline" fraction: wire bytes read per seal ÷ 8 TB/s
+                "read_frac": round(wire / (seal_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "kernel": kern or "seal batch (partition + AES + ChaCha kernels)",
                 "seal_ms": round(seal_ms, 4), "open_ms": round(open_ms, 4),
                 "algorithmic_bytes_per_launch": int(algo_bytes)}
