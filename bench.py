@@ -3,20 +3,30 @@
 
 One "step" = seal (AEAD + header protection) then open (HP removal + decode_pn + AEAD open) of
 the whole per-GPU batch, in place in HBM. Default workload = BASELINE configs[1]: 2^20 x 1200-B
-1-RTT packets, ChaCha20-Poly1305. With --gpus N (torch.distributed.run,
-one rank per GPU) every rank protects its own 2^20-packet shard (config D; packets are
-independent, so there is no data-path collective: scaling "weak").
+1-RTT packets, ChaCha20-Poly1305.
 
-  value  = sum over ranks of wire bytes x 2 / (t_seal + t_open) / 2^30   [GiB/s]
+N GPUs (config D): one process per GPU. `python bench.py --gpus N` launches the N
+ranks itself (torch.distributed.run as a child process, started before anything touches the GPU);
+under the driver's own `torch.distributed.run ... bench.py --gpus N` each rank just runs. The N
+ranks hold ONE global batch of N x 2^20 packets: rank s owns packets [s 2^20, (s+1) 2^20) (global
+index g -> pn 0x10000000 + g, key row g mod K, payload bytes [1200 g, 1200 (g+1)) of the SplitMix64
+stream). Rank 0 derives the keys and broadcasts them (RCCL); packets are independent, so there is
+no data-path collective ("weak" scaling). After the timed region the ranks all-reduce their
+failure counts and tag checksums; rank 0 checks the checksum of a fixed sample of global indices
+against the CPU oracle (the checker, outside the timed region).
+
+  value  = sum over ranks of wire bytes x 2 / max-over-ranks(t_seal + t_open) / 2^30   [GiB/s]
   roofline.achieved = algorithmic bytes of one seal launch (2 x L per packet: read + write) /
                       its average duration, from HIP events on the launch stream
-  cpu_baseline = the C oracle (oracle/, "port") on a bounded sample, host threads stated;
-  cpu_openssl  = OpenSSL EVP running the same composites on that sample (16 threads and 1)
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config b|c|e] [--packets P]
+  cpu_baseline = the C oracle (oracle/, "port") on a bounded sample (1 core, the box's CPU share,
+                 all cores); cpu_openssl = OpenSSL EVP running the same composites
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config b|c|e] [--packets P] [--keys K]
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -28,70 +38,175 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="b", choices=["b", "c", "e"])
     ap.add_argument("--packets", type=int, default=1 << 20, help="packets per GPU")
+    ap.add_argument("--keys", type=int, default=1, help="configs b/c: key rows, key_id = g mod K (SURVEY §8d)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1 << 16, help="packets in the CPU baseline sample")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="minimum timed CPU baseline work")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="minimum timed CPU work per thread count")
     ap.add_argument("--e2e", action="store_true", help="also measure the host-resident (H2D+D2H) rate")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-def build_workload(cfg, n, rank):
-    from milli_quic_amd import workload
-    seed = workload.SEED ^ (rank * 0x9E3779B97F4A7C15 & 0xFFFFFFFFFFFFFFFF)
-    if cfg == "b":
-        return workload.config_b(n, seed=seed)
-    if cfg == "c":
-        return workload.config_c(n, seed=seed)
-    return workload.config_e(n, seed=seed)
+# ---- launcher -------------------------------------------------------------------------------
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
-def cpu_baseline(w, sample, threads, min_seconds=10.0):
-    """Time the CPU oracle (seal + open) on the first `sample` packets of the same workload,
-    repeated until at least `min_seconds` of CPU work have been timed (bounded sample)."""
+def launch_ranks(n, argv, script=None):
+    """Run `script` (this file) as n ranks under torch.distributed.run, one process per GPU, in a
+    child process (this process never initialises the GPU; no exec). Returns the exit code."""
+    script = script or os.path.abspath(__file__)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", script, *argv]
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    return subprocess.call(cmd, env=env)
+
+
+def init_dist(backend):
+    """One rank per GPU: (rank, world, local device index). backend "nccl" is RCCL on ROCm;
+    "gloo" rehearses the N-rank path (on one GPU: ranks share device local % device_count)."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if backend == "gloo" and torch.cuda.device_count() > 0:
+        local = local % torch.cuda.device_count()
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+    return rank, world, local
+
+
+# ---- workload ---------------------------------------------------------------------------------
+def rank_keys(cfg, n_keys, dist, device):
+    """Key rows: derived by rank 0 (HKDF from the RFC 9001 secrets), broadcast to every rank."""
+    from milli_quic_amd import _lib, shard, workload
+    if cfg == "e":
+        return None  # config E derives its own per-connection keys on every rank
+    rows = None
+    if dist is None or not dist.is_initialized() or dist.get_rank() == 0:
+        suite = _lib.MQ_SUITE_CHACHA20 if cfg == "b" else _lib.MQ_SUITE_AES128GCM
+        rows = workload.uniform_keys(suite, n_keys)
+    return shard.broadcast_keys(rows, dist, device)
+
+
+def build_shard(cfg, n, rank, world, keys):
+    """This rank's shard. Configs b/c: global indices [rank n, (rank+1) n) of one global batch.
+    Config e (mixed, generated per rank): an independent batch per rank (seeded by rank)."""
+    from milli_quic_amd import _lib, workload
+    if cfg == "e":
+        seed = workload.SEED ^ (rank * 0x9E3779B97F4A7C15 & 0xFFFFFFFFFFFFFFFF)
+        return workload.config_e(n, seed=seed)
+    suite = _lib.MQ_SUITE_CHACHA20 if cfg == "b" else _lib.MQ_SUITE_AES128GCM
+    return workload.uniform(n, suite, start=rank * n, keys=keys)
+
+
+def sample_for_rank(cfg, n, rank, world):
+    """(global sample indices, local positions of those in this rank's shard)."""
+    from milli_quic_amd import shard
+    if cfg == "e":
+        g = shard.sample_indices(n)
+        return g, g
+    g = shard.sample_indices(n * world)
+    mine = g[(g >= rank * n) & (g < (rank + 1) * n)]
+    return g, mine - rank * n
+
+
+def oracle_sample_checksum(cfg, w, g, keys):
+    """CPU oracle (the checker) on the sampled global indices: the tag checksum the GPU run must
+    reproduce. Config e: rank 0's own batch."""
+    from milli_quic_amd import _lib, shard, workload
     from oracle import oracle
     oracle.load()
+    if cfg == "e":
+        sd = w.seal_desc[g].copy()
+        arena = w.arena.copy()
+        st = oracle.batch_seal(w.keys, arena, sd, w.suite_hint, threads=min(16, os.cpu_count() or 1))
+        return int((st != 0).sum()), shard.tag_checksum(arena, sd)
+    suite = _lib.MQ_SUITE_CHACHA20 if cfg == "b" else _lib.MQ_SUITE_AES128GCM
+    sw = workload.uniform_at(g, suite, keys=keys)
+    st = oracle.batch_seal(sw.keys, sw.arena, sw.seal_desc, sw.suite_hint, threads=min(16, os.cpu_count() or 1))
+    return int((st != 0).sum()), shard.tag_checksum(sw.arena, sw.seal_desc)
+
+
+# ---- CPU baselines (reported, not the target) -------------------------------------------------
+def cpu_threads():
+    """(1, the box's CPU share, every CPU the OS shows). The share is OMP_NUM_THREADS (16 per GPU
+    on the GPU box) or the affinity mask."""
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if share <= 0:
+        share = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return 1, share, os.cpu_count() or share
+
+
+def _sample(w, sample):
     n = min(sample, w.n)
     end = int(w.seal_desc["offset"][n - 1]) + int(w.seal_desc["len"][n - 1])
-    arena = w.arena[:end].copy()
     sd, od = w.seal_desc[:n].copy(), w.open_desc[:n].copy()
-    oracle.batch_seal(w.keys, arena.copy(), sd[: min(n, 256)].copy(), w.suite_hint, threads)  # warm
-    reps, t_seal, t_open = 0, 0.0, 0.0
-    while t_seal + t_open < min_seconds:
-        t0 = time.perf_counter()
-        st = oracle.batch_seal(w.keys, arena, sd, w.suite_hint, threads)
-        t1 = time.perf_counter()
-        st2, _ = oracle.batch_open(w.keys, arena, od, w.suite_hint, threads)
-        t2 = time.perf_counter()
-        assert (st == 0).all() and (st2 == 0).all(), "CPU oracle failed on its sample"
-        reps, t_seal, t_open = reps + 1, t_seal + (t1 - t0), t_open + (t2 - t1)
-    wire = int(sd["len"].astype(np.int64).sum())
-    gibs = wire * 2 * reps / (t_seal + t_open) / 2 ** 30
-    return {"value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": f"{n} packets ({wire / 1e6:.1f} MB) of the same workload, seal+open repeated {reps}x "
-                      f"(seal {t_seal:.1f}s + open {t_open:.1f}s), oracle/mq_oracle.c on {threads} host threads"}
+    return n, end, sd, od, int(sd["len"].astype(np.int64).sum())
 
 
-def cpu_openssl(w, sample, threads, min_seconds=3.0):
+def cpu_baseline(w, sample, min_seconds=8.0):
+    """The C oracle (oracle/mq_oracle.c, byte-wise scalar "port") timed on seal + open of the first
+    `sample` packets of the same workload, repeated until min_seconds of work were timed, at 1
+    thread, the CPU share and all CPUs. `value` is the CPU-share figure."""
+    from oracle import oracle
+    oracle.load()
+    n, end, sd, od, wire = _sample(w, sample)
+    one, share, allc = cpu_threads()
+    res = {}
+    for label, thr, secs in (("value_1core", one, min_seconds / 2), ("value", share, min_seconds),
+                             ("value_all_cpus", allc, min_seconds / 2)):
+        if label == "value_all_cpus" and allc == share:
+            continue
+        arena = w.arena[:end].copy()
+        oracle.batch_seal(w.keys, arena.copy(), sd[: min(n, 256)].copy(), w.suite_hint, thr)  # warm
+        reps, t = 0, 0.0
+        while t < secs:
+            t0 = time.perf_counter()
+            st = oracle.batch_seal(w.keys, arena, sd, w.suite_hint, thr)
+            st2, _ = oracle.batch_open(w.keys, arena, od, w.suite_hint, thr)
+            t += time.perf_counter() - t0
+            assert (st == 0).all() and (st2 == 0).all(), "CPU oracle failed on its sample"
+            reps += 1
+        res[label] = round(wire * 2 * reps / t / 2 ** 30, 3)
+    return {"value": res["value"], "unit": "GiB/s", "cores": share, "kind": "port",
+            "value_1core": res["value_1core"], "value_all_cpus": res.get("value_all_cpus"),
+            "cpus_visible": allc,
+            "sample": f"{n} packets ({wire / 1e6:.1f} MB) of the same workload, seal+open repeated; "
+                      f"oracle/mq_oracle.c on {share} threads (the box's CPU share), also 1 and {allc}"}
+
+
+def cpu_openssl(w, sample, min_seconds=3.0):
     """OpenSSL 3 EVP (libcrypto.so.3, dlopen'ed; its AVX2/AVX-512/AES-NI code paths) running the
-    same seal + open composites (oracle/ossl_baseline.c) on the same bounded sample, on `threads`
-    host threads and on one: the like-for-like stand-in for the reference's RustCrypto backends
-    (SURVEY §8d). None when libcrypto.so.3 is absent."""
+    same seal + open composites (oracle/ossl_baseline.c) on the same bounded sample, at 1 thread,
+    the CPU share and all CPUs: the like-for-like stand-in for the reference's RustCrypto backends
+    (SURVEY §8d). OpenSSL 3.0's per-packet EVP re-initialisation serialises across threads
+    (tools/ossl_scaling.c), so value_1core x cores is its uncontended projection.
+    None when libcrypto.so.3 is absent."""
     from oracle import oracle
     if not oracle.ossl_available():
         return None
-    n = min(sample, w.n)
-    end = int(w.seal_desc["offset"][n - 1]) + int(w.seal_desc["len"][n - 1])
-    sd, od = w.seal_desc[:n].copy(), w.open_desc[:n].copy()
-    wire = int(sd["len"].astype(np.int64).sum())
-    out = {"unit": "GiB/s", "kind": "openssl-evp"}
-    for key, thr in (("value", threads), ("value_1core", 1)):
+    n, end, sd, od, wire = _sample(w, sample)
+    one, share, allc = cpu_threads()
+    out = {"unit": "GiB/s", "kind": "openssl-evp", "cores": share, "cpus_visible": allc}
+    for label, thr in (("value_1core", one), ("value", share), ("value_all_cpus", allc)):
+        if label == "value_all_cpus" and allc == share:
+            continue
         arena = w.arena[:end].copy()
         reps, t = 0, 0.0
         while t < min_seconds:
@@ -101,61 +216,79 @@ def cpu_openssl(w, sample, threads, min_seconds=3.0):
             t += time.perf_counter() - t0
             assert (st == 0).all() and (st2 == 0).all(), "OpenSSL leg failed on its sample"
             reps += 1
-        out[key] = round(wire * 2 * reps / t / 2 ** 30, 3)
-    out["cores"] = threads
-    out["sample"] = f"{n} packets ({wire / 1e6:.1f} MB) of the same workload, seal+open, {threads} threads and 1"
+        out[label] = round(wire * 2 * reps / t / 2 ** 30, 3)
+    out["uncontended_projection"] = round(out["value_1core"] * share, 3)
+    out["sample"] = f"{n} packets ({wire / 1e6:.1f} MB) of the same workload, seal+open, 1/{share}/{allc} threads"
     return out
 
 
+# ---- end-to-end (host-resident) ---------------------------------------------------------------
 def end_to_end(torch, batch, kt, w, sd, od, dev, chunks=8, reps=3):
     """Host-resident rate (the path starts and ends in a socket buffer): pinned host arena ->
     H2D -> seal -> D2H, then H2D -> open -> D2H, pipelined over `chunks` descriptor ranges on
-    two streams so copies overlap kernels. Returns GiB/s of wire bytes per direction."""
+    two streams so copies overlap kernels. Returns GiB/s of wire bytes per direction, next to the
+    ceiling: the best plain pinned H2D + D2H of the same bytes (no kernel) over 2-4 streams and
+    8-32 chunks, and the pipeline's fraction of it."""
     n = w.n
     host = torch.from_numpy(w.arena).pin_memory()
     back = torch.empty_like(host).pin_memory()
     arena = torch.empty(host.numel(), dtype=torch.uint8, device=dev)
     st = torch.zeros(n, dtype=torch.uint8, device=dev)
     pn = torch.zeros(n, dtype=torch.int64, device=dev)
-    per = (n + chunks - 1) // chunks
-    wsl = [torch.empty(max(batch.workspace_bytes(per), 256), dtype=torch.uint8, device=dev) for _ in range(2)]
     offs = w.seal_desc["offset"].astype(np.int64)
     ends = offs + w.seal_desc["len"].astype(np.int64)
-    bounds = [(n * k) // chunks for k in range(chunks + 1)]
-    streams = [torch.cuda.Stream(device=dev) for _ in range(2)]
 
-    def one_pass(desc, open_):
-        for k in range(chunks):
-            lo, hi = bounds[k], bounds[k + 1]
-            if hi == lo:
-                continue
-            a, b = int(offs[lo:hi].min()), int(ends[lo:hi].max())
-            s = streams[k % 2]
-            with torch.cuda.stream(s):
-                arena[a:b].copy_(host[a:b], non_blocking=True)
-                if open_:
-                    batch.open_(kt, arena, desc[32 * lo:32 * hi], st[lo:hi], pn[lo:hi], w.suite_hint,
-                                wsl[k % 2], s.cuda_stream)
-                else:
-                    batch.seal(kt, arena, desc[32 * lo:32 * hi], st[lo:hi], w.suite_hint, wsl[k % 2],
-                               s.cuda_stream)
-                back[a:b].copy_(arena[a:b], non_blocking=True)
-        torch.cuda.synchronize()
+    def run(desc, mode, nch, nstreams):
+        per = (n + nch - 1) // nch
+        wsl = [torch.empty(max(batch.workspace_bytes(per), 256), dtype=torch.uint8, device=dev)
+               for _ in range(nstreams)] if mode != "copy" else None
+        bounds = [(n * k) // nch for k in range(nch + 1)]
+        streams = [torch.cuda.Stream(device=dev) for _ in range(nstreams)]
 
-    res = {}
-    for name, desc, open_ in (("seal", sd, False), ("open", od, True)):
-        one_pass(desc, open_)  # warm
+        def one_pass():
+            for k in range(nch):
+                lo, hi = bounds[k], bounds[k + 1]
+                if hi == lo:
+                    continue
+                a, b = int(offs[lo:hi].min()), int(ends[lo:hi].max())
+                s = streams[k % nstreams]
+                with torch.cuda.stream(s):
+                    arena[a:b].copy_(host[a:b], non_blocking=True)
+                    if mode == "open":
+                        batch.open_(kt, arena, desc[32 * lo:32 * hi], st[lo:hi], pn[lo:hi], w.suite_hint,
+                                    wsl[k % nstreams], s.cuda_stream)
+                    elif mode == "seal":
+                        batch.seal(kt, arena, desc[32 * lo:32 * hi], st[lo:hi], w.suite_hint, wsl[k % nstreams],
+                                   s.cuda_stream)
+                    back[a:b].copy_(arena[a:b], non_blocking=True)
+            torch.cuda.synchronize()
+
+        one_pass()  # warm
         t0 = time.perf_counter()
         for _ in range(reps):
-            one_pass(desc, open_)
-        dt = (time.perf_counter() - t0) / reps
+            one_pass()
+        return (time.perf_counter() - t0) / reps
+
+    res = {}
+    for name, desc in (("seal", sd), ("open", od)):
+        dt = run(desc, name, chunks, 2)
         res[name] = round(w.wire_bytes / dt / 2 ** 30, 2)
-        if not open_:
+        if name == "seal":
             host.copy_(back)  # the open pass starts from the sealed bytes
-    return {"unit": "GiB/s of wire bytes, host-resident (pinned) in and out", "chunks": chunks,
-            "seal": res["seal"], "open": res["open"]}
+    best = None
+    for nstreams in (2, 3, 4):
+        for nch in (8, 16, 32):
+            dt = run(None, "copy", nch, nstreams)
+            r = w.wire_bytes / dt / 2 ** 30
+            if best is None or r > best[0]:
+                best = (r, nstreams, nch)
+    return {"unit": "GiB/s of wire bytes, host-resident (pinned) in and out", "chunks": chunks, "streams": 2,
+            "seal": res["seal"], "open": res["open"],
+            "copy_ceiling": round(best[0], 2), "copy_ceiling_config": {"streams": best[1], "chunks": best[2]},
+            "frac_of_copy_ceiling": {"seal": round(res["seal"] / best[0], 3), "open": round(res["open"] / best[0], 3)}}
 
 
+# ---- roofline bookkeeping ---------------------------------------------------------------------
 KERNELS = {"b": "mq_chacha_seal_kernel", "c": "mq_aes_seal_kernel", "e": None}
 
 
@@ -181,36 +314,30 @@ def load_traffic(cfg, kern):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # the N ranks are child processes; this one never touches the GPU
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # MQ_BENCH_BACKEND=gloo with more ranks than GPUs rehearses the N-rank path on one GPU
-    # (ranks then share devices: local % device_count); the driver's runs use RCCL, one GPU per rank
     backend = os.environ.get("MQ_BENCH_BACKEND", "nccl")
-    if backend == "gloo":
-        local = local % max(1, torch.cuda.device_count())
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
-    else:
-        torch.cuda.set_device(local)
+    rank, world, local = init_dist(backend)
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; using {world} ranks", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dd = dist if world > 1 else None
 
-    from milli_quic_amd import _lib, batch
+    from milli_quic_amd import _lib, batch, shard
     from milli_quic_amd.batch import KeyTable
     lib = _lib.load()
     rc = lib.mq_device_init(local)
     if rc != 0:
         raise SystemExit(f"libmq_aead: no usable gfx950 device ({_lib.status_str(rc)})")
 
-    w = build_workload(args.config, args.packets, rank)
-    dev = torch.device("cuda", local)
+    keys = rank_keys(args.config, args.keys, dd, dev)
+    w = build_shard(args.config, args.packets, rank, world, keys)
     kt = KeyTable(w.keys)
     arena = torch.from_numpy(w.arena).to(dev)
     sd = torch.from_numpy(w.seal_desc.view(np.uint8)).to(dev)
@@ -250,51 +377,76 @@ def main():
     fails += int((st != 0).sum())
     seal_ms = float(np.mean([ev[3 * i].elapsed_time(ev[3 * i + 1]) for i in range(args.steps)]))
     open_ms = float(np.mean([ev[3 * i + 1].elapsed_time(ev[3 * i + 2]) for i in range(args.steps)]))
+    pn_ok = bool((pn.cpu().numpy().view(np.uint64) == w.pns).all())
+
+    # cross-rank parity: after the steps every packet holds its plaintext and the tag the last seal
+    # wrote; all-reduce failures and tag checksums (whole shard, and the fixed global sample)
+    offs_t = torch.from_numpy(w.seal_desc["offset"].astype(np.int64)).to(dev)
+    lens_t = torch.from_numpy(w.seal_desc["len"].astype(np.int64)).to(dev)
+    g_sample, local_sample = sample_for_rank(args.config, args.packets, rank, world)
+    ls = torch.from_numpy(local_sample.astype(np.int64)).to(dev)
+    csum = shard.tag_checksum_torch(arena, offs_t, lens_t)
+    s_csum = shard.tag_checksum_torch(arena, offs_t[ls], lens_t[ls])
+    fails_all, csum_all, s_csum_all, pn_bad = shard.reduce_sums([fails, csum, s_csum, 0 if pn_ok else 1], dd, dev)
 
     wire = w.wire_bytes
-    from milli_quic_amd.shard import reduce_totals
-    tot = reduce_totals(elapsed, wire, fails, dist if world > 1 else None, dev)
-    elapsed, fails, total_wire = tot.elapsed, tot.failures, float(tot.wire_bytes)
+    tot = shard.reduce_totals(elapsed, wire, 0, dd, dev)
+    elapsed, total_wire = tot.elapsed, float(tot.wire_bytes)
     ms_per_step = elapsed / args.steps * 1e3
     value = total_wire * 2 / (elapsed / args.steps) / 2 ** 30
 
     if rank == 0:
-        # roofline kernel: seal — for configs b/c a single launch (mq_chacha_seal_kernel /
-        # mq_aes_seal_kernel) timed by events on its stream; open = pre-pass + packet kernel
         algo_bytes = 2.0 * wire  # per launch: read + write of every wire byte
         achieved = algo_bytes / (seal_ms * 1e-3) / 1e9
         kern = seal_kernel(args.config, len(w.keys))
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config, kern) if w.n == 1 << 20 else None,
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": load_traffic(args.config, kern) if (w.n == 1 << 20 and args.keys == 1) else None,
                 # north_star's "HBM-read roofline" fraction: wire bytes read per seal ÷ 8 TB/s
                 "read_frac": round(wire / (seal_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "kernel": kern or "seal batch (partition + AES + ChaCha kernels)",
                 "seal_ms": round(seal_ms, 4), "open_ms": round(open_ms, 4),
+                "open_frac": round(algo_bytes / (open_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "algorithmic_bytes_per_launch": int(algo_bytes)}
+        # the checker (CPU oracle) on the fixed sample of global indices, outside the timed region
+        o_fail, o_csum = oracle_sample_checksum(args.config, w, g_sample, keys)
+        parity = {"failures": fails_all, "pn_mismatch_ranks": pn_bad, "tag_checksum": csum_all,
+                  "sample_packets": int(len(g_sample)), "sample_tag_checksum": s_csum_all,
+                  "oracle_sample_tag_checksum": o_csum,
+                  "sample_scope": "rank 0's batch" if args.config == "e" else f"global batch of {world * args.packets}",
+                  "match": bool(o_fail == 0 and o_csum == s_csum_all and fails_all == 0 and pn_bad == 0)}
         cpu = ossl = None
         if world == 1 and not args.no_cpu_baseline:
-            thr = min(16, os.cpu_count() or 1)
-            cpu = cpu_baseline(w, args.cpu_sample, thr, args.cpu_seconds)
-            ossl = cpu_openssl(w, args.cpu_sample, thr)
+            cpu = cpu_baseline(w, args.cpu_sample, args.cpu_seconds)
+            ossl = cpu_openssl(w, args.cpu_sample)
         names = {"b": "configs[1]: 1M x 1200B ChaCha20-Poly1305 seal+open, 1-RTT short header",
                  "c": "configs[2]: 1M x 1200B AES-128-GCM seal+open + header protection",
                  "e": "configs[4]: mixed 64-1350B batch, Initial + 1-RTT, ChaCha20/AES-GCM interleaved"}
+        workload_name = names[args.config]
+        if world > 1 and args.config == "b":
+            workload_name = (f"configs[3]: {world}x{args.packets // (1 << 20) or args.packets}M x 1200B "
+                             f"ChaCha20-Poly1305 batch sharded across {world} GPUs")
         out = {
             "metric": "GiB/s device-resident AEAD seal+open, 1M×1200B QUIC packets, 1/2/4/8 GPU",
             "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
-            "config": {"workload": names[args.config], "packets_per_gpu": w.n,
+            "config": {"workload": workload_name, "packets_per_gpu": w.n, "key_rows": len(w.keys),
                        "wire_bytes_per_gpu": wire, "parallelism": f"dp{world} (independent packet shards)",
-                       "seal_failures_or_open_failures": fails},
-            "roofline": roof, "cpu_baseline": cpu,
+                       "collectives": "key broadcast + failure/checksum all-reduce + barriers (no data path)",
+                       "backend": backend if world > 1 else None,
+                       "seal_failures_or_open_failures": fails_all},
+            "roofline": roof, "parity": parity, "cpu_baseline": cpu,
         }
         if ossl is not None:
             out["cpu_openssl"] = ossl
         if args.e2e and world == 1:
             out["end_to_end"] = end_to_end(torch, batch, kt, w, sd, od, dev)
         print(json.dumps(out), flush=True)
+        if not parity["match"]:
+            print("bench.py: PARITY CHECK FAILED " + json.dumps(parity), file=sys.stderr)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

@@ -78,6 +78,16 @@ typedef struct mq_key_material {
                                      seal `reserved` = the inner content type. Seal writes the
                                      header (23, 0x0303, len - 5) and the inner content type
                                      byte, then seals with AAD = header (connection.rs:561-600) */
+#define MQ_PKT_NO_RECV_LIMIT 0x08 /* open only: lift the receive composite's 2048-byte limit.
+                                     By default, as in the reference — recv_short and
+                                     decrypt_long_packet copy the packet into a 2048-B stack
+                                     buffer and return Err(BufferTooSmall { needed: len })
+                                     above that (recv.rs:356-360, 962-965) — a header-protected
+                                     packet with len > 2048 gets MQ_ERR_BUFFER_TOO_SMALL
+                                     (needed = its desc.len) and is left untouched. With this
+                                     flag such packets are opened (a deliberate divergence for
+                                     callers with larger receive buffers).                    */
+#define MQ_RECV_MAX_PACKET 2048
 
 typedef struct mq_pkt_desc {
   uint64_t offset;     /* byte offset of the packet's first header byte in the arena            */
@@ -299,13 +309,21 @@ int mq_batch_protect(const mq_keytable* kt, const mq_conn_send* conns, uint32_t 
  * their bytes. pkts receives up to max_pkts records in arrival order, *n_pkts (device) their
  * count; conns is updated (largest_recv_pn, key phase / rotation). Initial keys must already be
  * installed (mq_batch_derive_initial). All pointers are device memory; workspace has
- * mq_batch_recv_workspace_size(n_dgrams, max_pkts, n_conns) bytes. */
+ * mq_batch_recv_workspace_size(n_dgrams, max_pkts, n_conns) bytes.
+ * *n_pkts is the number of packets the datagrams split into, which can EXCEED max_pkts: only the
+ * first max_pkts (in arrival order) are processed and recorded; the rest are neither opened nor
+ * reflected in conns — resubmit their datagrams (or size max_pkts from *n_pkts).
+ * A packet that opened under keys other than the ones the sequential reference would have chosen
+ * (possible only when an earlier packet of its connection failed where the batch speculated it
+ * would open) reports MQ_ERR_CRYPTO, as the reference would; its bytes then hold the plaintext. */
 size_t mq_batch_recv_workspace_size(uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_conns);
 int mq_batch_recv(const mq_keytable* kt, mq_conn_recv* conns, uint32_t n_conns, uint8_t* arena,
                   uint64_t arena_len, const mq_dgram* dgrams, uint32_t n_dgrams, mq_recv_pkt* pkts,
                   uint32_t max_pkts, uint32_t* n_pkts, void* workspace, void* stream);
 
-/* Batched HeaderProtection::mask: masks[i*5..] = mask(key_table[key_ids[i]].hp, samples[i*16..]) */
+/* Batched HeaderProtection::mask: masks[i*5..] = mask(key_table[key_ids[i]].hp, samples[i*16..]).
+ * An entry whose key id is out of range or whose row holds no valid suite gets an all-zero mask
+ * (the call still returns MQ_OK: validate key ids on the caller's side). */
 int mq_batch_hp_mask(const mq_keytable* kt, const uint32_t* key_ids, const uint8_t* samples,
                      uint8_t* masks, uint32_t n, void* stream);
 

@@ -30,6 +30,8 @@ MQ_SUITE_MIXED = 0xFF
 MQ_PKT_LONG_HEADER = 0x01
 MQ_PKT_NO_HP = 0x02
 MQ_PKT_TLS_RECORD = 0x06  # implies MQ_PKT_NO_HP
+MQ_PKT_NO_RECV_LIMIT = 0x08  # open: lift the reference's 2048-B receive limit (recv.rs:356-360)
+MQ_RECV_MAX_PACKET = 2048
 
 MQ_LEVEL_INITIAL, MQ_LEVEL_HANDSHAKE, MQ_LEVEL_APPLICATION = 0, 1, 2
 MQ_SEND_PAD_TO_MIN = 0x01

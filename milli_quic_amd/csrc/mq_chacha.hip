@@ -375,7 +375,13 @@ extern "C" __global__ __launch_bounds__(256) void mq_chacha_hp_kernel(
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t kid = key_ids[i];
-  if (kid >= n_rows || kt[kid].suite != MQ_SUITE_CHACHA20) return;
+  if (kid >= n_rows || kt[kid].suite != MQ_SUITE_CHACHA20) {
+    // rows of neither suite (bad key id, empty row): all-zero mask (include/mq_aead.h); AES
+    // rows are the AES kernel's
+    if (kid >= n_rows || kt[kid].suite != MQ_SUITE_AES128GCM)
+      for (int b = 0; b < 5; ++b) masks[5 * (size_t)i + b] = 0;
+    return;
+  }
   GlobalSpace sp{const_cast<uint8_t*>(samples), (uint64_t)n * 16};
   uint32_t m0, m1;
   ChaChaPolicy::hp_mask(sp, (uint64_t)i * 16, kt + kid, m0, m1);

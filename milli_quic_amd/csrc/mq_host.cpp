@@ -325,18 +325,22 @@ struct Scratch {
   }
 };
 
-// Run one packet through the seal/open kernel of `row.suite`. pkt = aad || payload || tag area,
-// `len` bytes; descriptor in NO_HP mode with pn = 0 (the caller's nonce sits in row.iv).
-int run_one(Scratch& sc, const KeyRow& row, uint8_t* pkt, uint32_t len, uint32_t aad_len, bool open) {
+// Run one packet through the seal/open kernel of `row.suite`. The packet is aad || body, where
+// body = `body_len` bytes of buf (plaintext for seal, ciphertext || tag for open), staged straight
+// into the pinned scratch (no heap allocation per call); `pkt_len` = aad_len + body_len (+ 16 on
+// seal: the tag area). Descriptor in NO_HP mode with pn = 0 (the caller's nonce sits in row.iv).
+// On MQ_OK the transformed body (`out_len` bytes) is copied back into buf.
+int run_one(Scratch& sc, const KeyRow& row, const uint8_t* aad, uint32_t aad_len, uint8_t* buf,
+            uint32_t body_len, uint32_t pkt_len, uint32_t out_len, bool open) {
   int rc = ensure_device();
   if (rc) return rc;
-  rc = sc.ensure(len);
+  rc = sc.ensure(pkt_len);
   if (rc) return rc;
   std::memcpy(sc.host, &row, sizeof row);
   mq_pkt_desc d;
   std::memset(&d, 0, sizeof d);
   d.offset = Scratch::kHdr;
-  d.len = len;
+  d.len = pkt_len;
   d.key_id = 0;
   d.pn = 0;
   d.pn_offset = (uint16_t)aad_len;
@@ -344,8 +348,11 @@ int run_one(Scratch& sc, const KeyRow& row, uint8_t* pkt, uint32_t len, uint32_t
   d.flags = MQ_PKT_NO_HP;
   std::memcpy(sc.host + Scratch::kDesc, &d, sizeof d);
   std::memset(sc.host + Scratch::kStatus, 0xff, 16);
-  std::memcpy(sc.host + Scratch::kHdr, pkt, len);
-  const size_t bytes = Scratch::kHdr + len;
+  uint8_t* pkt = sc.host + Scratch::kHdr;
+  if (aad_len) std::memcpy(pkt, aad, aad_len);
+  std::memcpy(pkt + aad_len, buf, body_len);
+  if (pkt_len > aad_len + body_len) std::memset(pkt + aad_len + body_len, 0, pkt_len - aad_len - body_len);
+  const size_t bytes = Scratch::kHdr + pkt_len;
   if (hipMemcpyAsync(sc.dev, sc.host, bytes, hipMemcpyHostToDevice, sc.stream) != hipSuccess) return MQ_ERR_HIP;
   const KeyRow* kt = (const KeyRow*)sc.dev;
   const mq_pkt_desc* dd = (const mq_pkt_desc*)(sc.dev + Scratch::kDesc);
@@ -356,14 +363,15 @@ int run_one(Scratch& sc, const KeyRow& row, uint8_t* pkt, uint32_t len, uint32_t
                      ? mq_launch_chacha(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, st, pn, nullptr, sc.stream)
                      : mq_launch_aes(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, st, pn, nullptr, sc.stream);
   if (e != hipSuccess) return MQ_ERR_HIP;
+  // status and the transformed body in one read-back (status sits just before the packet)
   if (hipMemcpyAsync(sc.host + Scratch::kStatus, st, 16, hipMemcpyDeviceToHost, sc.stream) != hipSuccess)
     return MQ_ERR_HIP;
-  if (hipMemcpyAsync(sc.host + Scratch::kHdr, sc.dev + Scratch::kHdr, len, hipMemcpyDeviceToHost,
-                     sc.stream) != hipSuccess)
+  if (hipMemcpyAsync(pkt + aad_len, sc.dev + Scratch::kHdr + aad_len, out_len, hipMemcpyDeviceToHost, sc.stream) !=
+      hipSuccess)
     return MQ_ERR_HIP;
   if (hipStreamSynchronize(sc.stream) != hipSuccess) return MQ_ERR_HIP;
   const int status = sc.host[Scratch::kStatus];
-  if (status == MQ_OK) std::memcpy(pkt, sc.host + Scratch::kHdr, len);
+  if (status == MQ_OK) std::memcpy(buf, pkt + aad_len, out_len);
   return status;
 }
 
@@ -449,12 +457,9 @@ int mq_aead_seal_in_place(const mq_aead_ctx* ctx, const uint8_t* nonce, size_t n
   std::lock_guard<std::mutex> lk(ctx->sc.mu);
   KeyRow row = ctx->row;
   for (int i = 0; i < 3; ++i) row.iv[i] = le32(nonce + 4 * i);
-  std::vector<uint8_t> pkt(aad_len + total);
-  if (aad_len) std::memcpy(pkt.data(), aad, aad_len);
-  std::memcpy(pkt.data() + aad_len, buf, payload_len);
-  const int rc = run_one(ctx->sc, row, pkt.data(), (uint32_t)pkt.size(), (uint32_t)aad_len, false);
+  const int rc = run_one(ctx->sc, row, aad, (uint32_t)aad_len, buf, (uint32_t)payload_len,
+                         (uint32_t)(aad_len + total), (uint32_t)total, false);
   if (rc) return rc;
-  std::memcpy(buf, pkt.data() + aad_len, total);
   if (out_len) *out_len = total;
   return MQ_OK;
 }
@@ -470,12 +475,9 @@ int mq_aead_open_in_place(const mq_aead_ctx* ctx, const uint8_t* nonce, size_t n
   std::lock_guard<std::mutex> lk(ctx->sc.mu);
   KeyRow row = ctx->row;
   for (int i = 0; i < 3; ++i) row.iv[i] = le32(nonce + 4 * i);
-  std::vector<uint8_t> pkt(aad_len + ct_len);
-  if (aad_len) std::memcpy(pkt.data(), aad, aad_len);
-  std::memcpy(pkt.data() + aad_len, buf, ct_len);
-  const int rc = run_one(ctx->sc, row, pkt.data(), (uint32_t)pkt.size(), (uint32_t)aad_len, true);
+  const int rc = run_one(ctx->sc, row, aad, (uint32_t)aad_len, buf, (uint32_t)ct_len, (uint32_t)(aad_len + ct_len),
+                         (uint32_t)(ct_len - 16), true);
   if (rc) return rc;  // buffer untouched on failure
-  std::memcpy(buf, pkt.data() + aad_len, ct_len - 16);
   if (out_len) *out_len = ct_len - 16;
   return MQ_OK;
 }
@@ -892,17 +894,36 @@ int mq_batch_time_seal_open(const mq_keytable* kt, uint8_t* arena, uint64_t aren
   int rc = ensure_device();
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
-  std::vector<hipEvent_t> ev(2 * iters + 1);
+  std::vector<hipEvent_t> ev(2 * iters + 1, nullptr);
+  auto destroy = [&] {
+    for (auto& x : ev)
+      if (x) (void)hipEventDestroy(x);
+  };
   for (auto& x : ev)
-    if (hipEventCreate(&x) != hipSuccess) return MQ_ERR_HIP;
-  (void)hipEventRecord(ev[0], s);
-  for (int i = 0; i < iters && rc == MQ_OK; ++i) {
-    rc = mq_batch_seal(kt, arena, arena_len, desc, n, status, suite_hint, workspace, stream);
-    (void)hipEventRecord(ev[2 * i + 1], s);
-    if (rc == MQ_OK) rc = mq_batch_open(kt, arena, arena_len, desc, n, status, pn_out, suite_hint, workspace, stream);
-    (void)hipEventRecord(ev[2 * i + 2], s);
+    if (hipEventCreate(&x) != hipSuccess) {
+      x = nullptr;
+      destroy();
+      return MQ_ERR_HIP;
+    }
+  if (hipEventRecord(ev[0], s) != hipSuccess) {
+    destroy();
+    return MQ_ERR_HIP;
   }
-  (void)hipEventSynchronize(ev[2 * iters]);
+  for (int i = 0; i < iters; ++i) {
+    rc = mq_batch_seal(kt, arena, arena_len, desc, n, status, suite_hint, workspace, stream);
+    if (rc == MQ_OK && hipEventRecord(ev[2 * i + 1], s) != hipSuccess) rc = MQ_ERR_HIP;
+    if (rc == MQ_OK) rc = mq_batch_open(kt, arena, arena_len, desc, n, status, pn_out, suite_hint, workspace, stream);
+    if (rc == MQ_OK && hipEventRecord(ev[2 * i + 2], s) != hipSuccess) rc = MQ_ERR_HIP;
+    if (rc != MQ_OK) {  // nothing meaningful to time: drain what was enqueued and stop
+      (void)hipStreamSynchronize(s);
+      destroy();
+      return rc;
+    }
+  }
+  if (hipEventSynchronize(ev[2 * iters]) != hipSuccess) {
+    destroy();
+    return MQ_ERR_HIP;
+  }
   double ts = 0, to = 0;
   for (int i = 0; i < iters; ++i) {
     float a = 0, b = 0;
@@ -911,10 +932,10 @@ int mq_batch_time_seal_open(const mq_keytable* kt, uint8_t* arena, uint64_t aren
     ts += a;
     to += b;
   }
-  for (auto& x : ev) (void)hipEventDestroy(x);
+  destroy();
   *seal_ms = (float)(ts / iters);
   *open_ms = (float)(to / iters);
-  return rc;
+  return MQ_OK;
 }
 
 #ifdef MQ_STAMPS

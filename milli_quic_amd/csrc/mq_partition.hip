@@ -79,8 +79,12 @@ __device__ __forceinline__ uint32_t class_ppt(uint32_t c) {
 }  // namespace
 
 // Entries of one suite's list: every class segment is whole tiles of 8 entries, holes included.
+// A class of c packets at p <= 8 per tile takes 8 * ceil(c / p) < 8c / kMinPpt + 8 entries, so a
+// list of n packets spread over its classes needs at most 8n / kMinPpt + 8 per class. List 0 holds
+// two class groups (hot AES key, other AES keys: 2 * kLenClasses classes), list 1 one; the cap
+// covers the larger.
 uint32_t mq_partition_list_cap(uint32_t n) {
-  const uint64_t c = ((uint64_t)n * kPktsPerTile + kMinPpt - 1) / kMinPpt + kPktsPerTile * kLenClasses;
+  const uint64_t c = ((uint64_t)n * kPktsPerTile + kMinPpt - 1) / kMinPpt + kPktsPerTile * 2 * kLenClasses;
   return (uint32_t)((c + kPktsPerTile - 1) & ~(uint64_t)(kPktsPerTile - 1));
 }
 
@@ -160,7 +164,9 @@ extern "C" __global__ __launch_bounds__(1024) void mq_part_scan_kernel(uint32_t*
       const uint32_t ppt = class_ppt(c);
       e += kPktsPerTile * ((s_tot[c] + ppt - 1) / ppt);
     }
-    counts[s] = e;
+    // mq_partition_list_cap bounds e; the clamp only keeps a broken bound from running a suite
+    // kernel over the other list
+    counts[s] = min(e, cap);
   }
 }
 

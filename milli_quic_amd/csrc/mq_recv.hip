@@ -349,10 +349,24 @@ extern "C" __global__ __launch_bounds__(64) void mq_recv_walk_kernel(
       const uint8_t o = o_cur;
       const RecvPlan t = t_cur;
       const bool same = o != kNone && t.pn == p.pn && t.row == p.row && t.retry == p.retry && t.gen == p.gen;
-      if (same || o == kOk1 || o == kOk0) {  // known outcome (an opened packet keeps its inputs)
-        used = same ? p : t;
-        st = (o == kOk1 || o == kOk0) ? (uint8_t)MQ_OK : (uint8_t)MQ_ERR_CRYPTO;
-        gen = o == kOk0 ? 0 : used.gen;
+      if (o == kOk1 || o == kOk0) {
+        // Opened (its bytes are already plaintext, so it is never attempted again). A packet
+        // authenticates under exactly one (key row, pn), the one that opened it, so the
+        // reference's outcome for its own decision p follows: p.row first, then p.retry
+        // (recv.rs:412-474); for a next-generation open the rotation is p's (gen 2).
+        const uint32_t opened = o == kOk1 ? t.row : t.retry;
+        used = p;
+        if (t.pn == p.pn && opened == p.row) {
+          st = MQ_OK;
+          gen = p.gen;
+        } else if (t.pn == p.pn && opened == p.retry) {
+          st = MQ_OK;
+          gen = 0;
+        } else {  // the reference's keys fail on it: Error::Crypto (bytes hold the plaintext)
+          st = MQ_ERR_CRYPTO;
+        }
+      } else if (same) {  // failed with exactly the reference's inputs
+        st = MQ_ERR_CRYPTO;
       } else if (final_walk) {
         st = MQ_ERR_DEFERRED;
       } else {  // (re)attempt with the inputs the reference would use; speculate it opens

@@ -78,6 +78,8 @@ __device__ __forceinline__ int validate(const mq_pkt_desc& d, const KeyRow* kt, 
     if ((uint64_t)d.len < (uint64_t)d.pn_offset + d.pn_len + 16) return MQ_ERR_BUFFER_TOO_SMALL;
     if (!no_hp && (uint64_t)d.pn_offset + 20 > d.len) return MQ_ERR_CRYPTO;
   } else {
+    // recv.rs:356-360 / :962-965: the packet is copied into a 2048-B buffer first
+    if (!no_hp && !(d.flags & MQ_PKT_NO_RECV_LIMIT) && d.len > MQ_RECV_MAX_PACKET) return MQ_ERR_BUFFER_TOO_SMALL;
     if (!no_hp && (uint64_t)d.pn_offset + 20 > d.len) return MQ_ERR_CRYPTO;
     if (no_hp && (uint64_t)d.len < (uint64_t)d.pn_offset + d.pn_len + 16) return MQ_ERR_CRYPTO;
   }

@@ -81,6 +81,71 @@ def tag_checksum(arena, desc):
     return int((tags[:, 0::2] + (tags[:, 1::2] << 8)).sum())
 
 
+def tag_checksum_torch(arena, offsets, lens):
+    """tag_checksum() on torch tensors (device-resident arena, int64 offsets / lens of the packets
+    to cover): the same sum of the tags' little-endian 16-bit words, computed where the arena
+    lives (the bench's arena never leaves HBM)."""
+    import torch
+    if offsets.numel() == 0:
+        return 0
+    end = offsets.to(torch.int64) + lens.to(torch.int64)
+    idx = (end - 16)[:, None] + torch.arange(16, device=end.device, dtype=torch.int64)[None, :]
+    tags = arena[idx.reshape(-1)].to(torch.int64).reshape(-1, 16)
+    return int((tags[:, 0::2] + (tags[:, 1::2] << 8)).sum().item())
+
+
+def keys_to_bytes(rows):
+    """Serialise key rows (mq_key_material, 88 B each) for a broadcast."""
+    import ctypes
+    return b"".join(ctypes.string_at(ctypes.addressof(r), ctypes.sizeof(r)) for r in rows)
+
+
+def keys_from_bytes(blob):
+    from . import _lib
+    import ctypes
+    sz = ctypes.sizeof(_lib.KeyMaterial)
+    if len(blob) % sz:
+        raise ValueError("key blob is not a whole number of mq_key_material rows")
+    return [_lib.KeyMaterial.from_buffer_copy(blob[k:k + sz]) for k in range(0, len(blob), sz)]
+
+
+def broadcast_keys(rows, dist=None, device=None):
+    """Rank 0's key rows on every rank (torch.distributed broadcast: RCCL over xGMI on the GPU box,
+    a device tensor; gloo in the CPU tests, a host tensor). Non-zero ranks pass rows=None."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return list(rows)
+    import torch
+    if dist.get_backend() != "nccl":
+        device = "cpu"
+    n = torch.tensor([len(keys_to_bytes(rows)) if dist.get_rank() == 0 else 0], dtype=torch.int64, device=device)
+    dist.broadcast(n, src=0)
+    if dist.get_rank() == 0:
+        buf = torch.frombuffer(bytearray(keys_to_bytes(rows)), dtype=torch.uint8).to(device)
+    else:
+        buf = torch.empty(int(n.item()), dtype=torch.uint8, device=device)
+    dist.broadcast(buf, src=0)
+    return keys_from_bytes(buf.cpu().numpy().tobytes())
+
+
+def reduce_sums(values, dist=None, device=None):
+    """Whole-job sums of integer counters (failures, tag checksums) — exact int64 all-reduce."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return [int(v) for v in values]
+    import torch
+    if dist.get_backend() != "nccl":
+        device = "cpu"
+    t = torch.tensor([int(v) for v in values], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [int(x) for x in t.cpu().tolist()]
+
+
+def sample_indices(n_total, target=4096):
+    """The fixed sample of global packet indices a sharded run checks against the oracle: every
+    stride-th packet, stride = max(1, n_total // target)."""
+    stride = max(1, n_total // target)
+    return np.arange(0, n_total, stride, dtype=np.int64)
+
+
 def reduce_checksum(value, dist=None, device=None):
     """Whole-job sum of per-rank tag checksums."""
     if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:

@@ -31,7 +31,7 @@ _M2 = np.uint64(0x94D049BB133111EB)
 
 
 def splitmix_words(n, seed=SEED, start=0):
-    """n SplitMix64 outputs (state_k = seed + (k+1)*golden), vectorized."""
+    """n SplitMix64 outputs (state_k = seed + (k+1)*golden) for word indices start..start+n-1."""
     with np.errstate(over="ignore"):
         z = (np.arange(start + 1, start + n + 1, dtype=np.uint64) * _G) + np.uint64(seed)
         z = (z ^ (z >> np.uint64(30))) * _M1
@@ -39,14 +39,20 @@ def splitmix_words(n, seed=SEED, start=0):
         return z ^ (z >> np.uint64(31))
 
 
-def splitmix_bytes(nbytes, seed=SEED, chunk=1 << 24):
+def splitmix_bytes(nbytes, seed=SEED, chunk=1 << 24, start=0):
+    """Bytes [start, start + nbytes) of the SplitMix64 byte stream (words little-endian), so any
+    slice of a global batch can be generated on its own (config D shards, sampled packets)."""
     out = np.empty(nbytes, dtype=np.uint8)
-    nwords = (nbytes + 7) // 8
+    w_first, skip = divmod(start, 8)
+    nwords = (skip + nbytes + 7) // 8
+    pos = 0
     for w0 in range(0, nwords, chunk):
-        w = splitmix_words(min(chunk, nwords - w0), seed, w0)
-        b = w.view(np.uint8)
-        lo = w0 * 8
-        out[lo:lo + len(b)] = b[: max(0, min(len(b), nbytes - lo))]
+        b = splitmix_words(min(chunk, nwords - w0), seed, w_first + w0).view(np.uint8)
+        if w0 == 0:
+            b = b[skip:]
+        k = min(len(b), nbytes - pos)
+        out[pos:pos + k] = b[:k]
+        pos += k
     return out
 
 
@@ -69,31 +75,72 @@ class Workload:
         return int(self.seal_desc["len"].astype(np.int64).sum())
 
 
-def uniform(n, suite, L=1200, pn_len=4, dcid=DCID8, seed=SEED, n_keys=1):
-    """Configs B (ChaCha20) and C (AES-128-GCM): n x L-byte short-header packets."""
+def uniform_keys(suite, n_keys=1):
+    """Key rows of configs B / C: row 0 from the RFC 9001 A.5 secret (ChaCha20) or the A.1 server
+    secret (AES-128-GCM); the K-key variant adds rows from secrets A.5 + k (byte-wise)."""
     if suite == _lib.MQ_SUITE_CHACHA20:
         base = key_material(suite, A5_SECRET)
     else:
         base = key_material(suite, A1_SERVER_SECRET)
     keys = [base]
     for k in range(1, n_keys):  # variant: K distinct keys, key_id = i mod K
-        km = key_material(suite, bytes(((b + k) & 0xFF) for b in A5_SECRET))
-        keys.append(km)
-    arena = splitmix_bytes(n * L, seed)
-    view = arena.reshape(n, L)
-    pn0 = 0x10000000
-    pns = pn0 + np.arange(n, dtype=np.uint64)
+        keys.append(key_material(suite, bytes(((b + k) & 0xFF) for b in A5_SECRET)))
+    return keys
+
+
+def _uniform_headers(view, pns, pn_len, dcid, L):
     hdr_len = 1 + len(dcid)
     view[:, 0] = 0x40 | (pn_len - 1)
     view[:, 1:hdr_len] = np.frombuffer(dcid, dtype=np.uint8)
     for j in range(pn_len):
         view[:, hdr_len + j] = ((pns >> np.uint64(8 * (pn_len - 1 - j))) & np.uint64(0xFF)).astype(np.uint8)
     view[:, L - 16:] = 0
+
+
+PN0 = 0x10000000
+
+
+def uniform(n, suite, L=1200, pn_len=4, dcid=DCID8, seed=SEED, n_keys=1, start=0, keys=None):
+    """Configs B (ChaCha20) and C (AES-128-GCM): n x L-byte short-header packets.
+
+    Packets are those of global indices start .. start + n - 1 of one global batch: packet g has
+    pn = 0x10000000 + g, key row g mod n_keys and payload bytes [g L, (g + 1) L) of the SplitMix64
+    stream, so a shard of config D (start = rank x n) is exactly its slice of the 8M batch.
+    `keys` (rows) may be passed in, e.g. received from rank 0 (bench.py broadcasts them)."""
+    if keys is None:
+        keys = uniform_keys(suite, n_keys)
+    n_keys = len(keys)
+    arena = splitmix_bytes(n * L, seed, start=start * L)
+    view = arena.reshape(n, L)
+    g = np.arange(start, start + n, dtype=np.uint64)
+    pns = np.uint64(PN0) + g
+    _uniform_headers(view, pns, pn_len, dcid, L)
+    hdr_len = 1 + len(dcid)
     offs = np.arange(n, dtype=np.uint64) * np.uint64(L)
-    kid = (np.arange(n) % n_keys).astype(np.uint32)
+    kid = (g % np.uint64(n_keys)).astype(np.uint32)
     seal = make_descs(offs, L, kid, pns, hdr_len, pn_len, 0)
     opn = make_descs(offs, L, kid, pns - np.uint64(1), hdr_len, 0, 0)
     return Workload(f"{n}x{L}B-{'chacha' if suite == 2 else 'aes'}", arena, seal, opn, keys, suite, pns)
+
+
+def uniform_at(indices, suite, L=1200, pn_len=4, dcid=DCID8, seed=SEED, keys=None, n_keys=1):
+    """The packets of the given global indices of uniform()'s global batch, packed back to back
+    (sampled parity checks of sharded runs: the oracle seals exactly these)."""
+    if keys is None:
+        keys = uniform_keys(suite, n_keys)
+    g = np.asarray(indices, dtype=np.uint64)
+    n = len(g)
+    arena = np.empty(n * L, dtype=np.uint8)
+    view = arena.reshape(n, L)
+    for k, gi in enumerate(g):
+        view[k] = splitmix_bytes(L, seed, start=int(gi) * L)
+    pns = np.uint64(PN0) + g
+    _uniform_headers(view, pns, pn_len, dcid, L)
+    offs = np.arange(n, dtype=np.uint64) * np.uint64(L)
+    kid = (g % np.uint64(len(keys))).astype(np.uint32)
+    seal = make_descs(offs, L, kid, pns, 1 + len(dcid), pn_len, 0)
+    opn = make_descs(offs, L, kid, pns - np.uint64(1), 1 + len(dcid), 0, 0)
+    return Workload(f"sample-{n}x{L}B", arena, seal, opn, keys, suite, pns)
 
 
 def config_b(n=1 << 20, **kw):

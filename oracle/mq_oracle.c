@@ -608,6 +608,9 @@ int orc_unprotect_packet(const mq_key_material* km, uint8_t* pkt, const mq_pkt_d
   size_t klen = suite_key_len(km->suite);
   if (!klen) return MQ_ERR_SUITE;
   if (d->flags & 0x04) return orc_open_record(km, pkt, d, pn_out);
+  /* recv.rs:356-360 (recv_short) / :962-965 (decrypt_long_packet): copy into a 2048-B stack buffer,
+   * Err(BufferTooSmall { needed: len }) above that — before the sample check (:364-366) */
+  if (!no_hp && !(d->flags & MQ_PKT_NO_RECV_LIMIT) && d->len > MQ_RECV_MAX_PACKET) return MQ_ERR_BUFFER_TOO_SMALL;
   uint8_t* tmp = (uint8_t*)malloc(d->len ? d->len : 1);
   memcpy(tmp, pkt, d->len);
   size_t pn_len;

@@ -15,7 +15,10 @@ from milli_quic_amd import _lib, packet, recv, send
 from milli_quic_amd.key_schedule import derive_initial_secrets, key_material
 
 
-def build_traffic(orc, seed=1, n_conns=12, n_app=30):
+def build_traffic(orc, seed=1, n_conns=12, n_app=30, tamper_flip=False):
+    """tamper_flip: the first packet of the new key phase is corrupted on every connection, so
+    the key update is confirmed by the packet after it (the speculative walk had
+    rotated at the flip packet)."""
     rng = np.random.default_rng(seed)
     keys = [_lib.KeyMaterial()]  # row 0: unused
     conns = np.zeros(n_conns, dtype=recv.CONN_DTYPE)
@@ -46,7 +49,8 @@ def build_traffic(orc, seed=1, n_conns=12, n_app=30):
         for k in range(n_app):
             pn += int(rng.choice([1, 1, 1, 2, 3, 200, 40000]))
             gen = "g1" if k >= flip else "g0"
-            tamper = bool(rng.random() < 0.08) and k not in (flip, flip - 1)
+            tamper = bool(rng.random() < 0.08) and k not in (flip, flip - 1, flip + 1)
+            tamper = tamper or (tamper_flip and k == flip)
             dg.append([(gen, 2, 1 if gen == "g1" else 0, pn, rng.bytes(int(rng.integers(0, 1300))), tamper)])
         scripts.append((dcid, rows, dg))
     return keys, conns, scripts

@@ -1,0 +1,51 @@
+"""bench.py's N-GPU path on CPU (world 2, gloo): `bench.launch_ranks` starts the ranks as
+`python bench.py --gpus N` does (torch.distributed.run in a child process), and the ranks run
+bench.py's key broadcast, global-batch sharding (config D: rank s = packets [s n, (s+1) n) of one
+batch), checksum all-reduce and rank 0's sampled oracle check (tests/dist_bench_worker.py; the
+oracle stands in for the device seal there)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytest.importorskip("torch")
+
+import bench  # noqa: E402
+from milli_quic_amd import shard, workload  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.mark.parametrize("keys", [1, 5])
+def test_launch_two_ranks_sharded_global_batch(tmp_path, orc, keys):
+    out = tmp_path / "r0.json"
+    os.environ["MQ_TEST_OUT"] = str(out)
+    n = 1500
+    rc = bench.launch_ranks(2, ["--gpus", "2", "--packets", str(n), "--keys", str(keys)],
+                            script=os.path.join(HERE, "dist_bench_worker.py"))
+    assert rc == 0
+    r = json.loads(out.read_text())
+    assert r["world"] == 2 and r["fails"] == 0 and r["key_rows"] == keys
+    assert r["first_pn"] == workload.PN0  # rank 0 holds global packets 0..n-1
+    # the sampled global indices span both ranks; the ranks' reduced checksum equals the oracle's
+    assert r["n_sample"] == len(shard.sample_indices(2 * n)) and r["oracle_fail"] == 0
+    assert r["sample_csum"] == r["oracle_sample_csum"]
+    # the two shards are exactly the single-process global batch of 2n packets
+    w = workload.uniform(2 * n, 2, keys=workload.uniform_keys(2, keys))
+    st = orc.batch_seal(w.keys, w.arena, w.seal_desc, w.suite_hint, threads=4)
+    assert (st == 0).all()
+    assert r["csum"] == shard.tag_checksum(w.arena, w.seal_desc)
+    assert r["wire"] == 2 * n * 1200 and r["elapsed"] == 0.5  # summed bytes, max of elapsed
+
+
+def test_sample_indices_and_shard_positions():
+    for n, world in ((1 << 20, 8), (1000, 3), (5, 2)):
+        g = shard.sample_indices(n * world)
+        got = []
+        for rank in range(world):
+            gs, local = bench.sample_for_rank("b", n, rank, world)
+            assert (gs == g).all() and ((local >= 0) & (local < n)).all()
+            got.append(local + rank * n)
+        assert (np.concatenate(got) == g).all()
+    assert len(shard.sample_indices(8 << 20)) == 4096

@@ -255,11 +255,19 @@ def test_mixed_batch_vs_oracle(orc, n, lmin, lmax):
     assert (o_st == 0).all()
     assert (g_st == o_st).all()
     assert g_out.tobytes() == o_out.tobytes()
-    g_back, g_st, g_pn = gpu_run(w.keys, g_out, w.open_desc, w.suite_hint, open_=True)
-    o_back, o_st, o_pn = oracle_run(orc, w.keys, o_out, w.open_desc, w.suite_hint, open_=True)
-    assert (g_st == 0).all() and (g_st == o_st).all()
-    assert (g_pn == o_pn).all() and (g_pn == w.pns).all()
-    assert g_back.tobytes() == o_back.tobytes()
+    # receive side: packets over 2048 B get BufferTooSmall and stay sealed (recv.rs:356-360,
+    # 962-965); with MQ_PKT_NO_RECV_LIMIT every packet opens
+    big = w.open_desc["len"] > _lib.MQ_RECV_MAX_PACKET
+    assert big.any() == (lmax > _lib.MQ_RECV_MAX_PACKET)
+    lifted = w.open_desc.copy()
+    lifted["flags"] |= _lib.MQ_PKT_NO_RECV_LIMIT
+    for od, want_st in ((w.open_desc, np.where(big, _lib.MQ_ERR_BUFFER_TOO_SMALL, 0)), (lifted, 0)):
+        g_back, g_st, g_pn = gpu_run(w.keys, g_out, od, w.suite_hint, open_=True)
+        o_back, o_st, o_pn = oracle_run(orc, w.keys, o_out, od, w.suite_hint, open_=True)
+        assert (o_st == want_st).all() and (g_st == o_st).all()
+        ok = o_st == 0
+        assert (g_pn[ok] == o_pn[ok]).all() and (g_pn[ok] == w.pns[ok]).all()
+        assert g_back.tobytes() == o_back.tobytes()
 
 
 @pytest.mark.parametrize("suite,mixed", [(1, False), (2, False), (1, True), (2, True)])
@@ -345,9 +353,12 @@ def test_small_and_odd_sizes(orc, L):
             assert (g_pn[ok] == o_pn[ok]).all() and (g_pn[ok] == w.pns[ok]).all(), (suite, L, use_ws)
 
 
-def test_full_size_roundtrip_config_b(orc):
-    # BASELINE configs[1] at full size: 2^20 x 1200 B ChaCha20-Poly1305
-    w = workload.config_b(1 << 20)
+@pytest.mark.parametrize("cfg", ["b", "c"])
+def test_full_size_roundtrip(orc, cfg):
+    # BASELINE configs[1] / configs[2] at full size: 2^20 x 1200 B ChaCha20-Poly1305 / AES-128-GCM.
+    # Every sealed byte of a 4096-packet sample (uniform_at: the same global packets, sealed by
+    # the oracle) is compared; the full batch must round-trip to the plaintext with every PN.
+    w = workload.config_b(1 << 20) if cfg == "b" else workload.config_c(1 << 20)
     kt = KeyTable(w.keys)
     a = to_dev(w.arena)
     sd, od = to_dev(w.seal_desc), to_dev(w.open_desc)
@@ -356,17 +367,14 @@ def test_full_size_roundtrip_config_b(orc):
     batch.seal(kt, a, sd, st, w.suite_hint)
     torch.cuda.synchronize()
     assert int((st != 0).sum()) == 0
-    sealed = a.cpu().numpy()
-    # sampled oracle parity on the full-size arena
+    sealed = a.cpu().numpy().reshape(w.n, 1200)
     rng = np.random.default_rng(11)
-    idx = np.sort(rng.choice(w.n, size=512, replace=False))
-    sub_desc = w.seal_desc[idx].copy()
-    o_arena = w.arena.copy()
-    o_st = orc.batch_seal(w.keys, o_arena, sub_desc, w.suite_hint)
-    assert (o_st == 0).all()
-    for i in idx:
-        lo = int(w.seal_desc["offset"][i])
-        assert sealed[lo:lo + 1200].tobytes() == o_arena[lo:lo + 1200].tobytes()
+    idx = np.sort(np.concatenate([rng.choice(w.n, size=4090, replace=False), [0, 1, w.n - 2, w.n - 1]]))
+    idx = np.unique(idx)
+    sw = workload.uniform_at(idx, w.suite_hint, keys=w.keys)
+    o_st = orc.batch_seal(sw.keys, sw.arena, sw.seal_desc, sw.suite_hint, threads=8)
+    assert (o_st == 0).all() and len(idx) >= 4090
+    assert sealed[idx].tobytes() == sw.arena.tobytes()
     batch.open_(kt, a, od, st, pn, w.suite_hint)
     torch.cuda.synchronize()
     assert int((st != 0).sum()) == 0
@@ -402,3 +410,62 @@ def test_tile_count_edges_aes(orc):
         g_out, g_st, _ = gpu_run(w.keys, w.arena, w.seal_desc, w.suite_hint)
         o_out, o_st, _ = oracle_run(orc, w.keys, w.arena, w.seal_desc, w.suite_hint)
         assert (g_st == 0).all() and g_out.tobytes() == o_out.tobytes()
+
+
+def _short_packets(keys_and_lens, seed=5):
+    """Short-header packets (8-B DCID, pn_len 4) packed back to back: [(key row, L), ...]."""
+    lens = np.array([L for _, L in keys_and_lens], dtype=np.int64)
+    offs = np.zeros(len(lens), dtype=np.int64)
+    offs[1:] = np.cumsum(lens[:-1])
+    arena = workload.splitmix_bytes(int(lens.sum()) + 64, seed)
+    pns = np.uint64(0x10000000) + np.arange(len(lens), dtype=np.uint64)
+    for i, (o, L) in enumerate(zip(offs, lens)):
+        arena[o] = 0x43
+        arena[o + 1:o + 9] = np.frombuffer(workload.DCID8, dtype=np.uint8)
+        arena[o + 9:o + 13] = np.frombuffer(int(pns[i]).to_bytes(4, "big"), dtype=np.uint8)
+        arena[o + L - 16:o + L] = 0
+    kid = np.array([k for k, _ in keys_and_lens], dtype=np.uint32)
+    seal = make_descs(offs.astype(np.uint64), lens.astype(np.uint32), kid, pns, 9, 4, 0)
+    opn = make_descs(offs.astype(np.uint64), lens.astype(np.uint32), kid, pns - np.uint64(1), 9, 0, 0)
+    return arena, seal, opn, pns
+
+
+@pytest.mark.parametrize("extra_chacha", [2, 0, 40])
+def test_mixed_partition_sparse_classes(orc, extra_chacha):
+    # ADVICE r01 (high): two AES keys each covering 21 length classes put 42 one-packet classes
+    # (42 tiles = 336 list entries) into the AES list of a 44-packet batch; the list capacity must
+    # hold every class's round-up, or AES entries spill into the ChaCha list and packets are
+    # never processed (status unwritten)
+    keys = [key_schedule.key_material(_lib.MQ_SUITE_CHACHA20, workload.A5_SECRET),
+            key_schedule.key_material(_lib.MQ_SUITE_AES128GCM, workload.A1_SERVER_SECRET),
+            key_schedule.key_material(_lib.MQ_SUITE_AES128GCM, bytes(range(32)))]
+    spec = [(k, 64 * b + 40) for k in (1, 2) for b in range(21)]
+    spec += [(0, 100 + 37 * c) for c in range(extra_chacha)]
+    order = np.random.default_rng(extra_chacha).permutation(len(spec))
+    spec = [spec[i] for i in order]
+    arena, seal, opn, pns = _short_packets(spec)
+    g_out, g_st, _ = gpu_run(keys, arena, seal, _lib.MQ_SUITE_MIXED)
+    o_out, o_st, _ = oracle_run(orc, keys, arena, seal, _lib.MQ_SUITE_MIXED)
+    assert (o_st == 0).all() and (g_st == o_st).all(), g_st
+    assert g_out.tobytes() == o_out.tobytes()
+    g_back, g_st, g_pn = gpu_run(keys, g_out, opn, _lib.MQ_SUITE_MIXED, open_=True)
+    o_back, o_st, _ = oracle_run(orc, keys, o_out, opn, _lib.MQ_SUITE_MIXED, open_=True)
+    assert (g_st == 0).all() and (o_st == 0).all() and (g_pn == pns).all()
+    assert g_back.tobytes() == o_back.tobytes()
+
+
+def test_batch_hp_mask_bad_key_ids(hp_vectors):
+    # ADVICE r01: entries with an out-of-range key id or an empty row (suite 0) get an all-zero
+    # mask instead of stale bytes (include/mq_aead.h, mq_batch_hp_mask)
+    rows = [key_schedule.make_key_material(c["suite"], bytes(32), bytes(12), bytes.fromhex(c["hp"]))
+            for c in hp_vectors[:4]] + [_lib.KeyMaterial()]  # last row: suite 0
+    kt = KeyTable(rows)
+    ids = torch.tensor([0, 1, 99, 4, 2, 1 << 30, 3], dtype=torch.int32, device=DEV)
+    samples = to_dev(np.frombuffer(b"".join(bytes.fromhex(hp_vectors[k % 4]["sample"]) for k in
+                                           (0, 1, 2, 3, 2, 3, 3)), dtype=np.uint8))
+    masks = torch.full((5 * 7,), 0xCC, dtype=torch.uint8, device=DEV)
+    batch.hp_mask(kt, ids, samples, masks)
+    got = masks.cpu().numpy().reshape(7, 5)
+    for i, k in enumerate((0, 1, None, None, 2, None, 3)):
+        want = bytes(5).hex() if k is None else hp_vectors[k]["mask"]
+        assert got[i].tobytes().hex() == want, i

@@ -128,3 +128,43 @@ def test_random_records_vs_oracle(orc, suite):
     assert g_back.tobytes() == o_back.tobytes()
     ok = o_st == 0
     assert (g_info[ok] == o_info[ok]).all()
+
+
+# find_inner_content_type mirrors (reference tcp_tls/connection.rs:1019-1038): the inner
+# plaintexts basic [41 42 43 17], padded [41 16 00 00] and all-zero [00 00 00 00]
+INNER_CASES = [(bytes([0x41, 0x42, 0x43, 23]), (3, 23)), (bytes([0x41, 22, 0, 0]), (1, 22)), (bytes(4), None)]
+
+
+@pytest.mark.parametrize("suite,klen", [(1, 16), (2, 32)])
+def test_find_inner_content_type_mirrors(suite, klen):
+    key, iv = bytes(range(klen)), bytes(range(100, 112))
+    prov = crypto.Aes128GcmProvider() if suite == 1 else crypto.ChaCha20Provider()
+    aead = prov.aead(key)
+    recs = []
+    for k, (inner, want) in enumerate(INNER_CASES):
+        nonce = tls_record.build_nonce(iv, k)
+        hdr = tls_record.encode_record_header(23, len(inner) + 16)
+        buf = bytearray(inner) + bytearray(16)
+        assert aead.seal_in_place(nonce, hdr, buf, len(inner)) == len(inner) + 16
+        recs.append(hdr + bytes(buf))
+        # per record (mq_record_open)
+        b = bytearray(buf)
+        if want is None:
+            with pytest.raises(crypto.TlsError):          # find_inner_content_type_empty
+                tls_record.open_record(aead, nonce, b, len(b), hdr)
+            assert bytes(b[:4]) == inner                   # plaintext in place, as the reference
+        else:
+            assert tls_record.open_record(aead, nonce, b, len(b), hdr) == want
+    # batch (mq_batch_open_records), one record each, unaligned
+    offs = np.array([0, 27, 61], dtype=np.uint64)
+    arena = np.zeros(128, dtype=np.uint8)
+    for o, r in zip(offs, recs):
+        arena[int(o):int(o) + len(r)] = np.frombuffer(r, dtype=np.uint8)
+    km = make_key_material(suite, key, iv, bytes(32))
+    od = tls_record.record_descs(offs, [len(r) for r in recs], [0, 0, 0], [0, 1, 2])
+    back, st, info = gpu_records([km], arena, od, suite, open_=True)
+    dl, ct = tls_record.unpack_info(info)
+    assert list(st) == [0, 0, _lib.MQ_ERR_TLS]
+    assert (int(dl[0]), int(ct[0])) == (3, 23) and (int(dl[1]), int(ct[1])) == (1, 22)
+    for (inner, _), o in zip(INNER_CASES, offs):
+        assert back[int(o) + 5:int(o) + 9].tobytes() == inner

@@ -39,9 +39,13 @@ def gpu_recv(keys, conns, arena, dgrams, max_pkts):
             a.cpu().numpy())
 
 
-@pytest.mark.parametrize("seed,n_conns,n_app", [(3, 6, 20), (11, 64, 60)])
-def test_recv_vs_oracle(orc, seed, n_conns, n_app):
-    keys, conns, scripts = build_traffic(orc, seed=seed, n_conns=n_conns, n_app=n_app)
+@pytest.mark.parametrize("seed,n_conns,n_app,tamper_flip", [(3, 6, 20, False), (11, 64, 60, False),
+                                                            (5, 16, 30, True)])
+def test_recv_vs_oracle(orc, seed, n_conns, n_app, tamper_flip):
+    # tamper_flip: the first packet after a key-phase flip fails to open, so the
+    # walk's speculation (it rotated there) is wrong; the next packet must be reported as the
+    # reference's next-generation open (key_gen 2) and rotate the connection
+    keys, conns, scripts = build_traffic(orc, seed=seed, n_conns=n_conns, n_app=n_app, tamper_flip=tamper_flip)
     arena, dgrams = assemble(orc, keys, conns, scripts, seed=seed)
     oc, oa = conns.copy(), arena.copy()
     o_pk, o_n = orc.batch_recv(keys, oc, oa, dgrams, 1 << 16)

@@ -136,3 +136,33 @@ def test_decode_pn_rfc9000_a3(orc):
         pn_len = int(rng.integers(1, 5))
         trunc = int(rng.integers(0, 1 << (8 * pn_len)))
         assert orc.decode_pn(trunc, pn_len, largest) == decode_pn(trunc, pn_len, largest)
+
+
+@pytest.mark.parametrize("suite", [_lib.MQ_SUITE_AES128GCM, _lib.MQ_SUITE_CHACHA20])
+def test_receive_limit_2048(orc, suite):
+    # recv.rs:356-360 / :962-965: the receive composite copies the packet into a 2048-B stack
+    # buffer and returns Err(BufferTooSmall { needed: len }) above that, before any crypto; the
+    # packet stays as received. MQ_PKT_NO_RECV_LIMIT lifts it (documented divergence).
+    from milli_quic_amd import workload
+    for L, flags in ((2048, 0), (2049, 0), (3000, 0), (2049, _lib.MQ_PKT_NO_RECV_LIMIT)):
+        w = workload.uniform(4, suite, L=L)
+        st = orc.batch_seal(w.keys, w.arena, w.seal_desc, suite)
+        assert (st == 0).all()  # the send side has no such limit (transmit.rs:625-755)
+        sealed = w.arena.copy()
+        od = w.open_desc.copy()
+        od["flags"] |= flags
+        st, pn = orc.batch_open(w.keys, w.arena, od, suite)
+        if L > 2048 and not flags:
+            assert (st == _lib.MQ_ERR_BUFFER_TOO_SMALL).all() and w.arena.tobytes() == sealed.tobytes()
+        else:
+            assert (st == 0).all() and (pn == w.pns).all()
+    # records (MQ_PKT_TLS_RECORD) and plain AEAD rows (MQ_PKT_NO_HP) are not QUIC receive
+    # composites: no limit
+    w = workload.uniform(2, suite, L=3000)
+    sd, od = w.seal_desc.copy(), w.open_desc.copy()
+    for d in (sd, od):
+        d["flags"] = _lib.MQ_PKT_NO_HP
+        d["pn_len"] = 4
+    od["pn"] = sd["pn"]  # plain AEAD: the descriptor's pn is the nonce's pn
+    assert (orc.batch_seal(w.keys, w.arena, sd, suite) == 0).all()
+    assert (orc.batch_open(w.keys, w.arena, od, suite)[0] == 0).all()

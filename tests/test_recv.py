@@ -10,8 +10,14 @@ from milli_quic_amd import _lib, recv
 from recv_traffic import assemble, build_traffic
 
 
-def test_oracle_recv_traffic(orc):
-    keys, conns, scripts = build_traffic(orc, seed=3, n_conns=6, n_app=20)
+import pytest
+
+
+@pytest.mark.parametrize("tamper_flip", [False, True])
+def test_oracle_recv_traffic(orc, tamper_flip):
+    # tamper_flip: the first packet of the new key phase fails; the next one confirms the
+    # update (recv.rs:476-509), so the rotation still happens exactly once
+    keys, conns, scripts = build_traffic(orc, seed=3, n_conns=6, n_app=20, tamper_flip=tamper_flip)
     arena, dgrams = assemble(orc, keys, conns, scripts, seed=3)
     c2 = conns.copy()
     a2 = arena.copy()

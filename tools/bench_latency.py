@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""Per-packet latency of the drop-in trait path: microseconds per call of
+mq_aead_seal_in_place / mq_aead_open_in_place / mq_hp_mask on one 1200-B packet (13-B AAD,
+1171-B payload), called through ctypes exactly as the reference calls Aead / HeaderProtection
+once per packet (transmit.rs:713-719, recv.rs:416-421). Each call is a batch of one: H2D of
+row + descriptor + packet, the tile kernel, D2H, stream sync. Prints one JSON line (median and
+p99 over `--calls` calls, after warm-up), for both suites. The batch API is the throughput path;
+this measures the correctness shim."""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--calls", type=int, default=3000)
+    args = ap.parse_args()
+    from milli_quic_amd import _lib
+    lib = _lib.load()
+    assert lib.mq_device_init(0) == 0
+    out = {"unit": "us per call", "packet": "1200 B (13 B AAD, 1171 B payload, 16 B tag)", "calls": args.calls}
+    for suite, klen in ((_lib.MQ_SUITE_CHACHA20, 32), (_lib.MQ_SUITE_AES128GCM, 16)):
+        ctx, hp = ctypes.c_void_p(), ctypes.c_void_p()
+        assert lib.mq_aead_new(suite, bytes(range(klen)), klen, ctypes.byref(ctx)) == 0
+        assert lib.mq_hp_new(suite, bytes(range(klen)), klen, ctypes.byref(hp)) == 0
+        nonce = (ctypes.c_uint8 * 12)(*range(12))
+        aad = (ctypes.c_uint8 * 13)(*range(13))
+        buf = (ctypes.c_uint8 * 1200)()
+        sample = (ctypes.c_uint8 * 16)(*range(16))
+        mask = (ctypes.c_uint8 * 5)()
+        ol, nd = ctypes.c_size_t(), ctypes.c_size_t()
+        P = 1171
+
+        def seal():
+            return lib.mq_aead_seal_in_place(ctx, nonce, 12, aad, 13, buf, 1200, P, ctypes.byref(ol), ctypes.byref(nd))
+
+        def open_():
+            return lib.mq_aead_open_in_place(ctx, nonce, 12, aad, 13, buf, 1200, P + 16, ctypes.byref(ol))
+
+        def pair():
+            assert seal() == 0
+            assert open_() == 0
+
+        def hpm():
+            return lib.mq_hp_mask(hp, sample, 16, mask)
+
+        res = {}
+        for name, fn in (("seal_open_pair", pair), ("hp_mask", hpm)):
+            for _ in range(200):
+                fn()
+            t = np.empty(args.calls)
+            for k in range(args.calls):
+                t0 = time.perf_counter()
+                fn()
+                t[k] = time.perf_counter() - t0
+            res[name] = {"median": round(float(np.median(t)) * 1e6, 2), "p99": round(float(np.quantile(t, 0.99)) * 1e6, 2)}
+        # seal and open separately (open needs a sealed buffer: reseal before each timed open)
+        ts, to = np.empty(args.calls), np.empty(args.calls)
+        for k in range(args.calls):
+            t0 = time.perf_counter()
+            assert seal() == 0
+            t1 = time.perf_counter()
+            assert open_() == 0
+            t2 = time.perf_counter()
+            ts[k], to[k] = t1 - t0, t2 - t1
+        res["seal"] = {"median": round(float(np.median(ts)) * 1e6, 2), "p99": round(float(np.quantile(ts, 0.99)) * 1e6, 2)}
+        res["open"] = {"median": round(float(np.median(to)) * 1e6, 2), "p99": round(float(np.quantile(to, 0.99)) * 1e6, 2)}
+        # ctypes call overhead alone (a call that returns at the argument checks)
+        t = np.empty(args.calls)
+        for k in range(args.calls):
+            t0 = time.perf_counter()
+            lib.mq_aead_seal_in_place(ctx, nonce, 11, aad, 13, buf, 1200, P, ctypes.byref(ol), ctypes.byref(nd))
+            t[k] = time.perf_counter() - t0
+        res["ctypes_overhead_median"] = round(float(np.median(t)) * 1e6, 3)
+        out["chacha20" if suite == _lib.MQ_SUITE_CHACHA20 else "aes128gcm"] = res
+        lib.mq_aead_free(ctx)
+        lib.mq_hp_free(hp)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
