@@ -113,16 +113,37 @@ __device__ __forceinline__ GfOp gf_prepare(const uint32_t (&b)[4]) {
   return op;
 }
 
+// 3-input XOR and bit select in one v_bitop3_b32 (gfx950): on this chip every VALU op other than
+// add / xor / or / and issues at about half their rate (tools/ubench/ubench4.hip), so one bitop3
+// replaces two of them profitably, not three.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t sel3(uint32_t m, uint32_t a, uint32_t b) {  // m ? a : b, bitwise
+  return __builtin_amdgcn_bitop3_b32(m, a, b, 0xca);  // LUT index = 4 src0 + 2 src1 + src2
+}
+__device__ __forceinline__ uint64_t xor4_64(uint64_t a, uint64_t b, uint64_t c, uint64_t d) {
+  const uint32_t lo = xor3((uint32_t)a, (uint32_t)b, (uint32_t)c) ^ (uint32_t)d;
+  const uint32_t hi = xor3((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32)) ^ (uint32_t)(d >> 32);
+  return (uint64_t)hi << 32 | lo;
+}
+
 // 32x32 -> 64 carry-less product with holes
 __device__ __forceinline__ uint64_t bmul32(uint32_t x, const uint32_t (&y)[4]) {
   uint32_t xh[4];
   holes(x, xh);
-  const uint64_t z0 = (uint64_t)xh[0] * y[0] ^ (uint64_t)xh[1] * y[3] ^ (uint64_t)xh[2] * y[2] ^ (uint64_t)xh[3] * y[1];
-  const uint64_t z1 = (uint64_t)xh[0] * y[1] ^ (uint64_t)xh[1] * y[0] ^ (uint64_t)xh[2] * y[3] ^ (uint64_t)xh[3] * y[2];
-  const uint64_t z2 = (uint64_t)xh[0] * y[2] ^ (uint64_t)xh[1] * y[1] ^ (uint64_t)xh[2] * y[0] ^ (uint64_t)xh[3] * y[3];
-  const uint64_t z3 = (uint64_t)xh[0] * y[3] ^ (uint64_t)xh[1] * y[2] ^ (uint64_t)xh[2] * y[1] ^ (uint64_t)xh[3] * y[0];
-  return (z0 & 0x1111111111111111ull) | (z1 & 0x2222222222222222ull) | (z2 & 0x4444444444444444ull) |
-         (z3 & 0x8888888888888888ull);
+  const uint64_t z0 = xor4_64((uint64_t)xh[0] * y[0], (uint64_t)xh[1] * y[3], (uint64_t)xh[2] * y[2], (uint64_t)xh[3] * y[1]);
+  const uint64_t z1 = xor4_64((uint64_t)xh[0] * y[1], (uint64_t)xh[1] * y[0], (uint64_t)xh[2] * y[3], (uint64_t)xh[3] * y[2]);
+  const uint64_t z2 = xor4_64((uint64_t)xh[0] * y[2], (uint64_t)xh[1] * y[1], (uint64_t)xh[2] * y[0], (uint64_t)xh[3] * y[3]);
+  const uint64_t z3 = xor4_64((uint64_t)xh[0] * y[3], (uint64_t)xh[1] * y[2], (uint64_t)xh[2] * y[1], (uint64_t)xh[3] * y[0]);
+  // keep bit class k of z_k: (z0 at 0x1.., z1 at 0x2..) and (z2 at 0x4.., z3 at 0x8..), then
+  // the two halves by class 0|1 — three bit selects
+  auto pick = [](uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    return sel3(0x33333333u, sel3(0x11111111u, a, b), sel3(0x44444444u, c, d));
+  };
+  const uint32_t lo = pick((uint32_t)z0, (uint32_t)z1, (uint32_t)z2, (uint32_t)z3);
+  const uint32_t hi = pick((uint32_t)(z0 >> 32), (uint32_t)(z1 >> 32), (uint32_t)(z2 >> 32), (uint32_t)(z3 >> 32));
+  return (uint64_t)hi << 32 | lo;
 }
 
 // 256-bit product p7..p0 -> a = p mod (x^128 + x^7 + x^2 + x + 1): x^(128+j) -> x^j + x^(j+1) +
@@ -230,17 +251,22 @@ __device__ __forceinline__ void aes128_block(const AesRk& rk, const TwLane& L, u
   s0 = o0; s1 = o1; s2 = o2; s3 = o3;
 }
 
-// Two independent blocks a, b through the wide table with their rounds interleaved: twice the
-// independent LDS reads per round, so the lookup latency of one block hides behind the other's.
-__device__ __forceinline__ void aes128_block2(const AesRk& rk, const TwLane& L, uint32_t (&a)[4], uint32_t (&b)[4]) {
+// Rounds FIRST..9 and the final round of two independent blocks a, b through the wide table, their
+// rounds interleaved: twice the independent LDS reads per round, so the lookup latency of one
+// block hides behind the other's. FIRST = 1: a, b are AES inputs (round-0 key added here);
+// FIRST = 3: a, b are states after round 2 (from the CTR cache).
+template <int FIRST>
+__device__ __forceinline__ void aes128_rounds2(const AesRk& rk, const TwLane& L, uint32_t (&a)[4], uint32_t (&b)[4]) {
 #if MQ_PROF_SKIP & 16
   a[0] ^= rk.w[0]; a[1] ^= rk.w[41]; a[2] ^= L.r0; b[0] ^= rk.w[1]; b[1] ^= rk.w[42]; b[3] ^= L.r2;
   return;
 #endif
+  if (FIRST == 1) {
 #pragma unroll
-  for (int q = 0; q < 4; ++q) { a[q] ^= rk.w[q]; b[q] ^= rk.w[q]; }
+    for (int q = 0; q < 4; ++q) { a[q] ^= rk.w[q]; b[q] ^= rk.w[q]; }
+  }
 #pragma unroll
-  for (int r = 1; r < 10; ++r) {
+  for (int r = FIRST; r < 10; ++r) {
     // all 32 lookups of the round are issued before any is consumed (sched_barrier), so the LDS
     // queue streams them with up to 15 in flight instead of draining after every column
     uint32_t la[16], lb[16];
@@ -276,6 +302,93 @@ __device__ __forceinline__ void aes128_block2(const AesRk& rk, const TwLane& L, 
     b[q] = (__builtin_amdgcn_perm(lb[4 * q], lb[4 * q + 1], 0x07020c0cu) |
             __builtin_amdgcn_perm(lb[4 * q + 2], lb[4 * q + 3], 0x0c0c0500u)) ^ rk.w[40 + q];
   }
+}
+
+__device__ __forceinline__ void aes128_block2(const AesRk& rk, const TwLane& L, uint32_t (&a)[4], uint32_t (&b)[4]) {
+  aes128_rounds2<1>(rk, L, a, b);
+}
+
+// CTR caching (counter-mode AES with counters < 256): the input of block c of a packet is
+// (nonce words n0..n2, counter c), so after AddRoundKey only byte 0 of column 3 depends on c.
+// Round 1 therefore has three constant columns and one column with a single varying lookup
+// (T2 of that byte, rotated), and round 2 — whose input differs only in column 0 — has one
+// varying lookup per column. The per-packet constants below replace 27 of the block's 176
+// lookups and most of two rounds of VALU work.
+struct AesCtrCache {
+  uint32_t k0;      // round-1 column 0 without its varying term
+  uint32_t d[4];    // round-2 columns without their varying terms
+  uint32_t x;       // low byte of round key word 3 (xored with the counter's low byte)
+};
+
+__device__ __forceinline__ AesCtrCache ctr_cache(const AesRk& rk, const TwLane& L, const uint32_t (&nb)[3]) {
+  const uint32_t s0 = nb[0] ^ rk.w[0], s1 = nb[1] ^ rk.w[1], s2 = nb[2] ^ rk.w[2], s3 = rk.w[3];
+  AesCtrCache c;
+  c.x = rk.w[3] & 0xffu;
+  // round 1 (column q = T0[b3 s_q] ^ T2[b1 s_q+2] ^ ror8(T0[b2 s_q+1] ^ T2[b0 s_q+3]) ^ k);
+  // byte 0 of s3 (the counter's) only enters column 0
+  c.k0 = twl(s0, 3, L.r0) ^ twl(s2, 1, L.r2) ^ ror(twl(s1, 2, L.r0), 8) ^ rk.w[4];
+  const uint32_t k1 = twl(s1, 3, L.r0) ^ twl(s3, 1, L.r2) ^ ror(twl(s2, 2, L.r0) ^ twl(s0, 0, L.r2), 8) ^ rk.w[5];
+  const uint32_t k2 = twl(s2, 3, L.r0) ^ twl(s0, 1, L.r2) ^ ror(twl(s3, 2, L.r0) ^ twl(s1, 0, L.r2), 8) ^ rk.w[6];
+  const uint32_t k3 = twl(s3, 3, L.r0) ^ twl(s1, 1, L.r2) ^ ror(twl(s0, 2, L.r0) ^ twl(s2, 0, L.r2), 8) ^ rk.w[7];
+  // round 2 with t1..t3 = k1..k3 constant: every column has one term from t0
+  c.d[0] = twl(k2, 1, L.r2) ^ ror(twl(k1, 2, L.r0) ^ twl(k3, 0, L.r2), 8) ^ rk.w[8];
+  c.d[1] = twl(k1, 3, L.r0) ^ twl(k3, 1, L.r2) ^ ror(twl(k2, 2, L.r0), 8) ^ rk.w[9];
+  c.d[2] = twl(k2, 3, L.r0) ^ ror(twl(k3, 2, L.r0) ^ twl(k1, 0, L.r2), 8) ^ rk.w[10];
+  c.d[3] = twl(k3, 3, L.r0) ^ twl(k1, 1, L.r2) ^ ror(twl(k2, 0, L.r2), 8) ^ rk.w[11];
+  return c;
+}
+
+// state after round 2 of the CTR block with counter `ctr` (< 256)
+__device__ __forceinline__ void ctr_round2(const AesCtrCache& c, const TwLane& L, uint32_t ctr, uint32_t (&s)[4]) {
+  const uint32_t t0 = c.k0 ^ ror(twl(ctr ^ c.x, 0, L.r2), 8);
+  s[0] = c.d[0] ^ twl(t0, 3, L.r0);
+  s[1] = c.d[1] ^ ror(twl(t0, 0, L.r2), 8);
+  s[2] = c.d[2] ^ twl(t0, 1, L.r2);
+  s[3] = c.d[3] ^ ror(twl(t0, 2, L.r0), 8);
+}
+
+// one block from the state after round 2 (rounds 3..10)
+__device__ __forceinline__ void aes128_rounds_from3(const AesRk& rk, const TwLane& L, uint32_t (&s)[4]) {
+#pragma unroll
+  for (int r = 3; r < 10; ++r) {
+    uint32_t l[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int q1 = (q + 1) & 3, q2 = (q + 2) & 3, q3 = (q + 3) & 3;
+      l[4 * q] = twl(s[q], 3, L.r0); l[4 * q + 1] = twl(s[q2], 1, L.r2);
+      l[4 * q + 2] = twl(s[q1], 2, L.r0); l[4 * q + 3] = twl(s[q3], 0, L.r2);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s[q] = l[4 * q] ^ l[4 * q + 1] ^ ror(l[4 * q + 2] ^ l[4 * q + 3], 8) ^ rk.w[4 * r + q];
+  }
+  uint32_t l[16];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int q1 = (q + 1) & 3, q2 = (q + 2) & 3, q3 = (q + 3) & 3;
+    l[4 * q] = twl(s[q], 3, L.r2); l[4 * q + 1] = twl(s[q1], 2, L.r0);
+    l[4 * q + 2] = twl(s[q2], 1, L.r0); l[4 * q + 3] = twl(s[q3], 0, L.r2);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    s[q] = (__builtin_amdgcn_perm(l[4 * q], l[4 * q + 1], 0x07020c0cu) |
+            __builtin_amdgcn_perm(l[4 * q + 2], l[4 * q + 3], 0x0c0c0500u)) ^ rk.w[40 + q];
+}
+
+// CTR block with counter `ctr` (< 256) from the cache
+__device__ __forceinline__ void aes128_ctr1(const AesRk& rk, const TwLane& L, const AesCtrCache& c, uint32_t ctr,
+                                            uint32_t (&s)[4]) {
+  ctr_round2(c, L, ctr, s);
+  aes128_rounds_from3(rk, L, s);
+}
+
+// CTR blocks with counters ca and cb (both < 256) from the cache
+__device__ __forceinline__ void aes128_ctr2(const AesRk& rk, const TwLane& L, const AesCtrCache& c, uint32_t ca,
+                                            uint32_t cb, uint32_t (&a)[4], uint32_t (&b)[4]) {
+  ctr_round2(c, L, ca, a);
+  ctr_round2(c, L, cb, b);
+  aes128_rounds2<3>(rk, L, a, b);
 }
 
 // a = x^i * h (reflected basis), 0 <= i < 128: shift into 8 words, then fold
@@ -340,7 +453,7 @@ __device__ __forceinline__ void gh_mul_tab(uint32_t (&a)[4]) {
     for (int m = 0; m < 4; ++m) {
       const uint4 e0 = *(const uint4*)((const uint8_t*)g_aes_lds + 256u * (8 * w + 2 * m) + byte_of(lo, m));
       const uint4 e1 = *(const uint4*)((const uint8_t*)g_aes_lds + 256u * (8 * w + 2 * m + 1) + byte_of(hi, m));
-      r0 ^= e0.x ^ e1.x; r1 ^= e0.y ^ e1.y; r2 ^= e0.z ^ e1.z; r3 ^= e0.w ^ e1.w;
+      r0 = xor3(r0, e0.x, e1.x); r1 = xor3(r1, e0.y, e1.y); r2 = xor3(r2, e0.z, e1.z); r3 = xor3(r3, e0.w, e1.w);
     }
   }
   a[0] = r0; a[1] = r1; a[2] = r2; a[3] = r3;

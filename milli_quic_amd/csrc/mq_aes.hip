@@ -133,6 +133,22 @@ struct AesPolicyT {
     for (int q = 0; q < 4; ++q) { ks[q] = bswap32(x[q]); ks2[q] = bswap32(y[q]); }
   }
 
+  // the same from the packet's CTR cache (every counter of the wave's packets < 256)
+  static __device__ __forceinline__ void ctr_block2c(const AesRk& rk, const TwLane& rb, const AesCtrCache& cc,
+                                                     uint32_t b, uint32_t (&ks)[4], uint32_t (&ks2)[4]) {
+    uint32_t x[4], y[4];
+    aes128_ctr2(rk, rb, cc, b == 0 ? 1u : b + 1, b + kLanesPerPkt + 1, x, y);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { ks[q] = bswap32(x[q]); ks2[q] = bswap32(y[q]); }
+  }
+  static __device__ __forceinline__ void ctr_blockc(const AesRk& rk, const TwLane& rb, const AesCtrCache& cc,
+                                                    uint32_t b, uint32_t (&ks)[4]) {
+    uint32_t x[4];
+    aes128_ctr1(rk, rb, cc, b == 0 ? 1u : b + 1, x);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ks[q] = bswap32(x[q]);
+  }
+
   template <class S>
   static __device__ __forceinline__ void xor_block(const S& sp, typename S::off_t pay, uint32_t b,
                                                    uint32_t P, const uint32_t (&ks)[4]) {
@@ -210,6 +226,10 @@ struct AesPolicyT {
       for (int k = 0; k < 44; ++k) pin(rk.w[k]);
       pin(nb[0]); pin(nb[1]); pin(nb[2]);
       stg.issue();
+      // CTR cache while the packets land in LDS (counters of every active packet < 256)
+      const bool cached = !wave_any(c.act && nblk > 255u);
+      AesCtrCache cc{};
+      if (cached) cc = ctr_cache(rk, rb, nb);
       auto first_iter = [&]() {  // before any packet byte is touched
         stg.complete();
         MQ_STAMP(c.tile, 2);
@@ -238,7 +258,8 @@ struct AesPolicyT {
         // ciphertext of iteration 0, and its lane needs the HP key)
         if (it + 1 < Imax && !wave_any(is_hp || hp_next)) {
           uint32_t ks[4], ks2[4];
-          ctr_block2(rk, rb, nb, b, ks, ks2);
+          if (cached) ctr_block2c(rk, rb, cc, b, ks, ks2);
+          else ctr_block2(rk, rb, nb, b, ks, ks2);
           if (it == 0) first_iter();
           use_block(b, ks);
           use_block(b + kLanesPerPkt, ks2);
@@ -259,6 +280,8 @@ struct AesPolicyT {
           aes128_block(hk, rb, s0, s1, s2, s3);
           ks[0] = bswap32(s0); ks[1] = bswap32(s1); ks[2] = bswap32(s2); ks[3] = bswap32(s3);
           if (is_hp) { m0 = ks[0]; m1 = s1 >> 24; have_mask = true; }
+        } else if (cached) {
+          ctr_blockc(rk, rb, cc, b, ks);
         } else {
           ctr_block(rk, rb, nb, b, ks);
         }
@@ -320,9 +343,16 @@ struct AesPolicyT {
     const uint32_t Cmax = wave_max_u32(c.act ? C : 0u);
     AesRk rk;
     uint32_t ks0[4];  // block j: E(J0) on lane 0, keystream elsewhere
+    const bool cached = !wave_any(c.act && nblk > 255u);
+    AesCtrCache cc{};
     if (TAB) {  // round keys in SGPRs: cheap to keep across the GHASH
       load_rk(row->aes_rk, rk);
-      ctr_block(rk, rb, nb, (uint32_t)j, ks0);
+      if (cached) {
+        cc = ctr_cache(rk, rb, nb);
+        ctr_blockc(rk, rb, cc, (uint32_t)j, ks0);
+      } else {
+        ctr_block(rk, rb, nb, (uint32_t)j, ks0);
+      }
     }
     if (c.pre_hp) stg.complete();
     MQ_STAMP(c.tile, 2);
@@ -334,7 +364,12 @@ struct AesPolicyT {
     MQ_STAMP(c.tile, 4);
     if (!TAB) {
       load_rk(row->aes_rk, rk);
-      ctr_block(rk, rb, nb, (uint32_t)j, ks0);
+      if (cached) {
+        cc = ctr_cache(rk, rb, nb);
+        ctr_blockc(rk, rb, cc, (uint32_t)j, ks0);
+      } else {
+        ctr_block(rk, rb, nb, (uint32_t)j, ks0);
+      }
     }
     uint32_t ej0[4];
 #pragma unroll
@@ -354,14 +389,16 @@ struct AesPolicyT {
     for (; it + 1 < Cmax; it += 2) {  // two iterations per pass (interleaved AES rounds)
       const uint32_t b = (uint32_t)j + kLanesPerPkt * it;
       uint32_t ks[4], ks2[4];
-      ctr_block2(rk, rb, nb, b, ks, ks2);
+      if (cached) ctr_block2c(rk, rb, cc, b, ks, ks2);
+      else ctr_block2(rk, rb, nb, b, ks, ks2);
       if (c.act && b < nblk) xor_block(sp, pay, b, P, ks);
       if (c.act && b + kLanesPerPkt < nblk) xor_block(sp, pay, b + kLanesPerPkt, P, ks2);
     }
     if (it < Cmax) {
       const uint32_t b = (uint32_t)j + kLanesPerPkt * it;
       uint32_t ks[4];
-      ctr_block(rk, rb, nb, b, ks);
+      if (cached) ctr_blockc(rk, rb, cc, b, ks);
+      else ctr_block(rk, rb, nb, b, ks);
       if (c.act && b < nblk) xor_block(sp, pay, b, P, ks);
     }
     if (direct && hdr_written && !c.act) {

@@ -37,7 +37,14 @@ __global__ __launch_bounds__(256) void k_rate(uint32_t* out, uint32_t seed) {
     if (K == 19) asm volatile("v_mul_u32_u24 %0, %0, %1\n v_mul_u32_u24 %0, %0, %1" : "+v"(a##I) : "v"(b)); \
     if (K == 20) asm volatile("v_mov_b32_sdwa %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0\n v_mov_b32_sdwa %0, %1 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1" : "+v"(a##I) : "v"(b)); \
     if (K == 21) asm volatile("v_bfi_b32 %0, %0, %1, %0\n v_bfi_b32 %0, %0, %1, %0" : "+v"(a##I) : "v"(b)); \
-    if (K == 22) asm volatile("v_add_co_u32 %0, vcc, %0, %1\n v_addc_co_u32 %0, vcc, %0, %1, vcc" : "+v"(a##I) : "v"(b) : "vcc");
+    if (K == 22) asm volatile("v_add_co_u32 %0, vcc, %0, %1\n v_addc_co_u32 %0, vcc, %0, %1, vcc" : "+v"(a##I) : "v"(b) : "vcc"); \
+    if (K == 27) asm volatile("v_bitop3_b32 %0, %0, %1, %1 bitop3:0x96\n v_bitop3_b32 %0, %0, %1, %1 bitop3:0x96" : "+v"(a##I) : "v"(b)); \
+    if (K == 28) asm volatile("v_pk_add_u16 %0, %0, 0 op_sel:[1,0] op_sel_hi:[0,1]\n v_pk_add_u16 %0, %0, 0 op_sel:[1,0] op_sel_hi:[0,1]" : "+v"(a##I)); \
+    if (K == 29) asm volatile("v_alignbyte_b32 %0, %0, %0, 2\n v_alignbyte_b32 %0, %0, %0, 2" : "+v"(a##I)); \
+    if (K == 31) asm volatile("v_xor_b32_e64 %0, %0, %1\n v_xor_b32_e64 %0, %0, %1" : "+v"(a##I) : "v"(b)); \
+    if (K == 32) asm volatile("v_and_or_b32 %0, %0, %1, %1\n v_and_or_b32 %0, %0, %1, %1" : "+v"(a##I) : "v"(b)); \
+    if (K == 33) asm volatile("v_xor_b32_dpp %0, %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n v_xor_b32_dpp %0, %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(a##I) : "v"(b)); \
+    if (K == 34) asm volatile("v_pk_add_u16 %0, %0, %1\n v_pk_add_u16 %0, %0, %1" : "+v"(a##I) : "v"(b));
     R2(0) R2(1) R2(2) R2(3) R2(4) R2(5) R2(6) R2(7)
     if (K == 9) {  // 64-bit mad: 4 chains x 4
 #define M4(I) asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0\n v_mad_u64_u32 %0, vcc, %1, %2, %0\n v_mad_u64_u32 %0, vcc, %1, %2, %0\n v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(w##I) : "v"(a0), "v"(b) : "vcc");
@@ -112,7 +119,21 @@ int run(const char* name, int instr_per_iter, int waves_per_simd) {
   return 0;
 }
 
-int main() {
+int main(int argc, char** argv) {
+  if (argc > 1) {  // round-2 additions: 3-input / packed / DPP forms
+    for (int w : {2, 4, 8}) {
+      run<1>("v_xor_b32", 16, w);
+      run<31>("v_xor_b32_e64", 16, w);
+      run<27>("v_bitop3_b32", 16, w);
+      run<28>("v_pk_add_u16 swap", 16, w);
+      run<34>("v_pk_add_u16", 16, w);
+      run<29>("v_alignbyte_b32", 16, w);
+      run<32>("v_and_or_b32", 16, w);
+      run<33>("v_xor_b32_dpp", 16, w);
+      run<2>("v_alignbit_b32", 16, w);
+    }
+    return 0;
+  }
   for (int w : {2, 4, 8}) {
     run<23>("grp8 add/xor/align", 24, w);
     run<24>("grp8 add/xor", 16, w);
