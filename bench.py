@@ -269,12 +269,18 @@ def end_to_end(torch, batch, kt, w, sd, od, dev, chunks=8, reps=3):
             one_pass()
         return (time.perf_counter() - t0) / reps
 
-    res = {}
+    res, cfg_used = {}, {}
     for name, desc in (("seal", sd), ("open", od)):
-        dt = run(desc, name, chunks, 2)
-        res[name] = round(w.wire_bytes / dt / 2 ** 30, 2)
-        if name == "seal":
-            host.copy_(back)  # the open pass starts from the sealed bytes
+        best_rate = 0.0
+        for nstreams, nch in ((2, chunks), (3, 16), (4, 32)):
+            host.copy_(torch.from_numpy(w.arena) if name == "seal" else sealed)
+            dt = run(desc, name, nch, nstreams)
+            r = w.wire_bytes / dt / 2 ** 30
+            if r > best_rate:
+                best_rate, cfg_used[name] = r, {"streams": nstreams, "chunks": nch}
+            if name == "seal":
+                sealed = back.clone()  # the open pass starts from the sealed bytes
+        res[name] = round(best_rate, 2)
     best = None
     for nstreams in (2, 3, 4):
         for nch in (8, 16, 32):
@@ -282,7 +288,7 @@ def end_to_end(torch, batch, kt, w, sd, od, dev, chunks=8, reps=3):
             r = w.wire_bytes / dt / 2 ** 30
             if best is None or r > best[0]:
                 best = (r, nstreams, nch)
-    return {"unit": "GiB/s of wire bytes, host-resident (pinned) in and out", "chunks": chunks, "streams": 2,
+    return {"unit": "GiB/s of wire bytes, host-resident (pinned) in and out", "pipeline_config": cfg_used,
             "seal": res["seal"], "open": res["open"],
             "copy_ceiling": round(best[0], 2), "copy_ceiling_config": {"streams": best[1], "chunks": best[2]},
             "frac_of_copy_ceiling": {"seal": round(res["seal"] / best[0], 3), "open": round(res["open"] / best[0], 3)}}

@@ -31,6 +31,8 @@ static struct {
   EVP_CIPHER_CTX* (*ctx_new)(void);
   void (*ctx_free)(EVP_CIPHER_CTX*);
   EVP_CIPHER* (*fetch)(void*, const char*, const char*);
+  void* (*libctx_new)(void);
+  void (*libctx_free)(void*);
   int (*enc_init)(EVP_CIPHER_CTX*, const EVP_CIPHER*, void*, const uint8_t*, const uint8_t*);
   int (*enc_update)(EVP_CIPHER_CTX*, uint8_t*, int*, const uint8_t*, int);
   int (*enc_final)(EVP_CIPHER_CTX*, uint8_t*, int*);
@@ -50,7 +52,7 @@ static void load_libcrypto(void) {
   if (!h) return;
 #define SYM(f, n) *(void**)(&E.f) = dlsym(h, n); if (!E.f) return;
   SYM(ctx_new, "EVP_CIPHER_CTX_new") SYM(ctx_free, "EVP_CIPHER_CTX_free")
-  SYM(fetch, "EVP_CIPHER_fetch")
+  SYM(fetch, "EVP_CIPHER_fetch") SYM(libctx_new, "OSSL_LIB_CTX_new") SYM(libctx_free, "OSSL_LIB_CTX_free")
   SYM(enc_init, "EVP_EncryptInit_ex") SYM(enc_update, "EVP_EncryptUpdate") SYM(enc_final, "EVP_EncryptFinal_ex")
   SYM(dec_init, "EVP_DecryptInit_ex") SYM(dec_update, "EVP_DecryptUpdate") SYM(dec_final, "EVP_DecryptFinal_ex")
   SYM(ctrl, "EVP_CIPHER_CTX_ctrl")
@@ -62,9 +64,13 @@ static void load_libcrypto(void) {
   E.ok = 1;
 }
 
-/* Explicitly fetched ciphers, one set per thread: the legacy EVP_chacha20_poly1305() objects
- * re-fetch from the provider (under a global lock) on every init, and a cipher object shared by
- * all threads has its reference count bounced between cores on every init. */
+/* Explicitly fetched ciphers, one set per thread, each from the thread's own library context
+ * (OSSL_LIB_CTX_new): the legacy EVP_chacha20_poly1305() objects re-fetch from the provider
+ * (under a global lock) on every init, and in OpenSSL 3.0 every EVP_*Init_ex — including the
+ * per-packet re-IV — serialises on state of the library context its cipher came from. Measured on
+ * the GPU box's host (tools/ossl_scaling.c, profiles/r02_ossl_scaling.txt): re-IV calls 21.3 M/s
+ * on 1 thread, 21.7 M/s on 16 with the default context; 21.0 M/s PER THREAD on 16 and 19.4 M/s
+ * per thread on 64 with one context per thread. */
 static const char* const kCipherNames[4] = {"ChaCha20-Poly1305", "ChaCha20", "AES-128-GCM", "AES-128-ECB"};
 
 int ossl_available(void) {
@@ -164,7 +170,8 @@ static void* worker(void* p) {
   Ctx c[2];
   const uint32_t suites[2] = {MQ_SUITE_CHACHA20, MQ_SUITE_AES128GCM};
   EVP_CIPHER* ciph[4];
-  for (int i = 0; i < 4; ++i) ciph[i] = E.fetch(NULL, kCipherNames[i], NULL);
+  void* lc = E.libctx_new();  /* NULL on failure: the default context (still correct, slower) */
+  for (int i = 0; i < 4; ++i) ciph[i] = E.fetch(lc, kCipherNames[i], NULL);
   for (int s = 0; s < 2; ++s) {
     c[s].suite = suites[s];
     c[s].row = 0xffffffffu;
@@ -182,6 +189,7 @@ static void* worker(void* p) {
   }
   for (int s = 0; s < 2; ++s) { E.ctx_free(c[s].aead_e); E.ctx_free(c[s].aead_d); E.ctx_free(c[s].hp); }
   for (int i = 0; i < 4; ++i) E.cipher_free(ciph[i]);
+  if (lc) E.libctx_free(lc);
   return NULL;
 }
 
