@@ -161,6 +161,16 @@ struct AesPolicyT {
 
   // AesHeaderProtection::mask (rustcrypto.rs:175-186): AES-ECB(hp, sample)[0..5]
   // (rb: TwLane in the tile kernels, the small table's replica offset in the per-lane kernels)
+  template <class T>
+  static __device__ __forceinline__ void hp_mask_words(const uint32_t (&smp)[4], const KeyRow* row, const T& rb,
+                                                       uint32_t& m0, uint32_t& m1) {
+    AesRk hk;
+    load_rk(row->hp_rk, hk);
+    uint32_t s0 = bswap32(smp[0]), s1 = bswap32(smp[1]), s2 = bswap32(smp[2]), s3 = bswap32(smp[3]);
+    aes128_block(hk, rb, s0, s1, s2, s3);
+    m0 = bswap32(s0);
+    m1 = s1 >> 24;
+  }
   template <class S, class T>
   static __device__ __forceinline__ void hp_mask(const S& sp, typename S::off_t sample_at,
                                                  const KeyRow* row, const T& rb, uint32_t& m0, uint32_t& m1) {
@@ -497,8 +507,18 @@ __global__ __launch_bounds__(256) void mq_aes_open_hp_kernel(
     return;
   GlobalSpace sp{const_cast<uint8_t*>(arena), arena_len};
   uint32_t m0, m1;
-  AesPolicyT<false>::hp_mask(sp, at, row, (threadIdx.x & (kTReplicas - 1)) * 4, m0, m1);
-  hpm[i] = DECODE ? prepass_decode(arena, d, m0, m1) : make_uint2(m0, m1);
+  const uint32_t rb = (threadIdx.x & (kTReplicas - 1)) * 4;
+  if (DECODE) {  // PN bytes and sample (contiguous) and the first byte in one round of loads
+    uint32_t w[5];
+    load_words<5>(sp, at - 4, w);
+    const uint8_t b0 = arena[d.offset];
+    const uint32_t smp[4] = {w[1], w[2], w[3], w[4]};
+    AesPolicyT<false>::hp_mask_words(smp, row, rb, m0, m1);
+    hpm[i] = prepass_decode_words(b0, w[0], d, m0, m1);
+  } else {
+    AesPolicyT<false>::hp_mask(sp, at, row, rb, m0, m1);
+    hpm[i] = make_uint2(m0, m1);
+  }
 }
 
 // Persistent grid: one workgroup per CU (152 KiB of LDS each), capped by the tile count.

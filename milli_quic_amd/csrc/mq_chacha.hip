@@ -165,16 +165,20 @@ struct ChaChaPolicy {
 
   // ChaChaHeaderProtection::mask (rustcrypto.rs:197-220): block(hp, ctr = sample[0..4] LE,
   // nonce = sample[4..16]); the mask is keystream bytes 0..4.
-  template <class S>
-  static __device__ __forceinline__ void hp_mask(const S& sp, typename S::off_t sample_at,
-                                                 const KeyRow* row, uint32_t& m0, uint32_t& m1) {
-    uint32_t smp[4];
-    load_words<4>(sp, sample_at, smp);
+  static __device__ __forceinline__ void hp_mask_words(const uint32_t (&smp)[4], const KeyRow* row, uint32_t& m0,
+                                                       uint32_t& m1) {
     uint32_t hk[8], blk[16];
     load_key8(row->hp, hk);
     chacha20_block(hk, smp[0], smp[1], smp[2], smp[3], blk);
     m0 = blk[0];
     m1 = blk[1];
+  }
+  template <class S>
+  static __device__ __forceinline__ void hp_mask(const S& sp, typename S::off_t sample_at,
+                                                 const KeyRow* row, uint32_t& m0, uint32_t& m1) {
+    uint32_t smp[4];
+    load_words<4>(sp, sample_at, smp);
+    hp_mask_words(smp, row, m0, m1);
   }
 
   // send composite (transmit.rs:625-755): seal, then header protection from the sample.
@@ -407,8 +411,17 @@ __global__ __launch_bounds__(256) void mq_chacha_open_hp_kernel(
     return;
   GlobalSpace sp{const_cast<uint8_t*>(arena), arena_len};
   uint32_t m0, m1;
-  ChaChaPolicy::hp_mask(sp, at, row, m0, m1);
-  hpm[i] = DECODE ? prepass_decode(arena, d, m0, m1) : make_uint2(m0, m1);
+  if (DECODE) {  // PN bytes and sample (contiguous) and the first byte in one round of loads
+    uint32_t w[5];
+    load_words<5>(sp, at - 4, w);
+    const uint8_t b0 = arena[d.offset];
+    const uint32_t smp[4] = {w[1], w[2], w[3], w[4]};
+    ChaChaPolicy::hp_mask_words(smp, row, m0, m1);
+    hpm[i] = prepass_decode_words(b0, w[0], d, m0, m1);
+  } else {
+    ChaChaPolicy::hp_mask(sp, at, row, m0, m1);
+    hpm[i] = make_uint2(m0, m1);
+  }
 }
 
 // ---- host-side launchers (called from mq_host.cpp) -------------------------------------------

@@ -291,12 +291,17 @@ void hmac_sha256(const uint8_t* key, size_t key_len, const uint8_t* m1, size_t l
 }
 
 // ---------------------------------------------------------------------------------------------
-// pinned staging + device scratch for the per-packet (batch of one) calls
+// Scratch of the per-packet (batch of one) calls: [row][desc 32][status 16][pn 8][pad][packet ...]
+// in pinned host memory. Zero-copy (default): the buffer is mapped into the device's address
+// space and the kernel reads and writes it over PCIe directly — a call is one kernel launch and
+// one stream sync, no copies. MQ_PER_PACKET_COPY=1 selects the copy path instead (a device mirror,
+// H2D before and D2H after the kernel), kept for comparison (tools/bench_latency.py).
 struct Scratch {
   hipStream_t stream = nullptr;
-  uint8_t* dev = nullptr;   // [row][desc 32][status 16][pn 8][pad][packet ...]
-  uint8_t* host = nullptr;  // pinned mirror
+  uint8_t* dev = nullptr;   // what the kernel addresses: device mirror, or the mapped host buffer
+  uint8_t* host = nullptr;  // pinned host buffer
   size_t cap = 0;
+  bool zero_copy = true;
   std::mutex mu;
 
   static constexpr size_t kDesc = sizeof(KeyRow);  // descriptor (AEAD) / key id (HP)
@@ -306,21 +311,43 @@ struct Scratch {
   static constexpr size_t kHdr = 1024;              // the packet
   static_assert(kPn + 8 <= kHdr && kPn % 8 == 0, "scratch header layout");
 
-  int ensure(size_t pkt_bytes) {
-    const size_t need = kHdr + ((pkt_bytes + 255) & ~(size_t)255) + 256;
-    if (!stream && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return MQ_ERR_HIP;
-    if (need <= cap) return MQ_OK;
-    if (dev) (void)hipFree(dev);
+  void release() {
+    if (dev && !zero_copy) (void)hipFree(dev);
     if (host) (void)hipHostFree(host);
     dev = nullptr; host = nullptr; cap = 0;
-    if (hipMalloc(&dev, need) != hipSuccess) return MQ_ERR_HIP;
-    if (hipHostMalloc(&host, need, hipHostMallocDefault) != hipSuccess) return MQ_ERR_HIP;
+  }
+  int ensure(size_t pkt_bytes) {
+    const size_t need = kHdr + ((pkt_bytes + 255) & ~(size_t)255) + 256;
+    if (!stream) {
+      if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return MQ_ERR_HIP;
+      const char* e = std::getenv("MQ_PER_PACKET_COPY");
+      zero_copy = !(e && e[0] == '1');
+    }
+    if (need <= cap) return MQ_OK;
+    release();
+    if (zero_copy) {
+      if (hipHostMalloc(&host, need, hipHostMallocMapped) != hipSuccess) return MQ_ERR_HIP;
+      if (hipHostGetDevicePointer((void**)&dev, host, 0) != hipSuccess) { release(); return MQ_ERR_HIP; }
+    } else {
+      if (hipMalloc(&dev, need) != hipSuccess) return MQ_ERR_HIP;
+      if (hipHostMalloc(&host, need, hipHostMallocDefault) != hipSuccess) { release(); return MQ_ERR_HIP; }
+    }
     cap = need;
     return MQ_OK;
   }
+  // host -> what the kernel reads (no-op when zero-copy)
+  int upload(size_t bytes) {
+    if (zero_copy) return MQ_OK;
+    return hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, stream) == hipSuccess ? MQ_OK : MQ_ERR_HIP;
+  }
+  // [off, off + bytes) back to the host buffer (no-op when zero-copy), then wait for the stream
+  int finish(size_t off, size_t bytes) {
+    if (!zero_copy && hipMemcpyAsync(host + off, dev + off, bytes, hipMemcpyDeviceToHost, stream) != hipSuccess)
+      return MQ_ERR_HIP;
+    return hipStreamSynchronize(stream) == hipSuccess ? MQ_OK : MQ_ERR_HIP;
+  }
   ~Scratch() {
-    if (dev) (void)hipFree(dev);
-    if (host) (void)hipHostFree(host);
+    release();
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -353,7 +380,7 @@ int run_one(Scratch& sc, const KeyRow& row, const uint8_t* aad, uint32_t aad_len
   std::memcpy(pkt + aad_len, buf, body_len);
   if (pkt_len > aad_len + body_len) std::memset(pkt + aad_len + body_len, 0, pkt_len - aad_len - body_len);
   const size_t bytes = Scratch::kHdr + pkt_len;
-  if (hipMemcpyAsync(sc.dev, sc.host, bytes, hipMemcpyHostToDevice, sc.stream) != hipSuccess) return MQ_ERR_HIP;
+  if ((rc = sc.upload(bytes)) != MQ_OK) return rc;
   const KeyRow* kt = (const KeyRow*)sc.dev;
   const mq_pkt_desc* dd = (const mq_pkt_desc*)(sc.dev + Scratch::kDesc);
   uint8_t* st = sc.dev + Scratch::kStatus;
@@ -363,13 +390,8 @@ int run_one(Scratch& sc, const KeyRow& row, const uint8_t* aad, uint32_t aad_len
                      ? mq_launch_chacha(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, st, pn, nullptr, sc.stream)
                      : mq_launch_aes(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, st, pn, nullptr, sc.stream);
   if (e != hipSuccess) return MQ_ERR_HIP;
-  // status and the transformed body in one read-back (status sits just before the packet)
-  if (hipMemcpyAsync(sc.host + Scratch::kStatus, st, 16, hipMemcpyDeviceToHost, sc.stream) != hipSuccess)
-    return MQ_ERR_HIP;
-  if (hipMemcpyAsync(pkt + aad_len, sc.dev + Scratch::kHdr + aad_len, out_len, hipMemcpyDeviceToHost, sc.stream) !=
-      hipSuccess)
-    return MQ_ERR_HIP;
-  if (hipStreamSynchronize(sc.stream) != hipSuccess) return MQ_ERR_HIP;
+  // status and the transformed packet in one read-back (the status sits before the packet)
+  if ((rc = sc.finish(Scratch::kStatus, Scratch::kHdr - Scratch::kStatus + pkt_len)) != MQ_OK) return rc;
   const int status = sc.host[Scratch::kStatus];
   if (status == MQ_OK) std::memcpy(buf, pkt + aad_len, out_len);
   return status;
@@ -517,18 +539,14 @@ int mq_hp_mask(const mq_hp_ctx* ctx, const uint8_t* sample, size_t sample_len, u
   std::memcpy(sc.host + Scratch::kDesc, &kid, 4);
   std::memcpy(sc.host + Scratch::kSample, sample, 16);
   std::memset(sc.host + Scratch::kStatus, 0, 8);
-  if (hipMemcpyAsync(sc.dev, sc.host, Scratch::kStatus + 8, hipMemcpyHostToDevice, sc.stream) != hipSuccess)
-    return MQ_ERR_HIP;
+  if ((rc = sc.upload(Scratch::kStatus + 8)) != MQ_OK) return rc;
   const KeyRow* kt = (const KeyRow*)sc.dev;
   const uint32_t* kids = (const uint32_t*)(sc.dev + Scratch::kDesc);
   hipError_t e = ctx->suite == MQ_SUITE_CHACHA20
                      ? mq_launch_chacha_hp(kt, 1, kids, sc.dev + Scratch::kSample, sc.dev + Scratch::kStatus, 1, sc.stream)
                      : mq_launch_aes_hp(kt, 1, kids, sc.dev + Scratch::kSample, sc.dev + Scratch::kStatus, 1, sc.stream);
   if (e != hipSuccess) return MQ_ERR_HIP;
-  if (hipMemcpyAsync(sc.host + Scratch::kStatus, sc.dev + Scratch::kStatus, 8, hipMemcpyDeviceToHost, sc.stream) !=
-      hipSuccess)
-    return MQ_ERR_HIP;
-  if (hipStreamSynchronize(sc.stream) != hipSuccess) return MQ_ERR_HIP;
+  if ((rc = sc.finish(Scratch::kStatus, 8)) != MQ_OK) return rc;
   std::memcpy(mask, sc.host + Scratch::kStatus, 5);
   return MQ_OK;
 }

@@ -248,6 +248,19 @@ __device__ __forceinline__ uint2 prepass_decode(const uint8_t* __restrict__ aren
   return make_uint2(trunc, 0x100u | b0);
 }
 
+// prepass_decode from registers: b0 = the received first byte, pnw = the 4 received bytes at
+// pn_offset (little-endian word), loaded together with the sample so that the pre-pass waits on
+// memory once per packet
+__device__ __forceinline__ uint2 prepass_decode_words(uint8_t b0raw, uint32_t pnw, const mq_pkt_desc& d,
+                                                      uint32_t m0, uint32_t m1) {
+  const uint8_t fb = (d.flags & MQ_PKT_LONG_HEADER) ? 0x0f : 0x1f;
+  const uint8_t b0 = b0raw ^ ((uint8_t)m0 & fb);
+  const uint32_t pn_len = (b0 & 3u) + 1, x = pnw ^ ((m0 >> 8) | (m1 << 24));
+  uint32_t trunc = 0;
+  for (uint32_t b = 0; b < pn_len; ++b) trunc = (trunc << 8) | ((x >> (8 * b)) & 0xffu);
+  return make_uint2(trunc, 0x100u | b0);
+}
+
 // Open, header part (recv.rs:363-395 / :968-997) with the pre-pass values: pn_len, truncated PN,
 // decode_pn and the PN range check. Returns the unmasked first byte.
 __device__ __forceinline__ uint8_t header_from_prepass(PktCtx& c, uint32_t& pn_len, uint32_t& trunc) {

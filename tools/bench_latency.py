@@ -2,10 +2,12 @@
 """Per-packet latency of the drop-in trait path: microseconds per call of
 mq_aead_seal_in_place / mq_aead_open_in_place / mq_hp_mask on one 1200-B packet (13-B AAD,
 1171-B payload), called through ctypes exactly as the reference calls Aead / HeaderProtection
-once per packet (transmit.rs:713-719, recv.rs:416-421). Each call is a batch of one: H2D of
-row + descriptor + packet, the tile kernel, D2H, stream sync. Prints one JSON line (median and
-p99 over `--calls` calls, after warm-up), for both suites. The batch API is the throughput path;
-this measures the correctness shim."""
+once per packet (transmit.rs:713-719, recv.rs:416-421). Each call is a batch of one: the packet
+is staged in a pinned scratch that the kernel reads and writes over PCIe (zero-copy, default),
+or — MQ_PER_PACKET_COPY=1, timed as "copy" — copied H2D before and D2H after the kernel; then
+the stream is synchronised. Prints one JSON line (median and p99 over `--calls` calls, after
+warm-up), for both suites and both modes. The batch API is the throughput path; this measures
+the correctness shim."""
 import argparse
 import ctypes
 import json
@@ -26,6 +28,14 @@ def main():
     lib = _lib.load()
     assert lib.mq_device_init(0) == 0
     out = {"unit": "us per call", "packet": "1200 B (13 B AAD, 1171 B payload, 16 B tag)", "calls": args.calls}
+    for mode in ("zero_copy", "copy"):
+        os.environ["MQ_PER_PACKET_COPY"] = "1" if mode == "copy" else "0"
+        out[mode] = measure(lib, _lib, args.calls)
+    print(json.dumps(out), flush=True)
+
+
+def measure(lib, _lib, calls):
+    out = {}
     for suite, klen in ((_lib.MQ_SUITE_CHACHA20, 32), (_lib.MQ_SUITE_AES128GCM, 16)):
         ctx, hp = ctypes.c_void_p(), ctypes.c_void_p()
         assert lib.mq_aead_new(suite, bytes(range(klen)), klen, ctypes.byref(ctx)) == 0
@@ -55,15 +65,15 @@ def main():
         for name, fn in (("seal_open_pair", pair), ("hp_mask", hpm)):
             for _ in range(200):
                 fn()
-            t = np.empty(args.calls)
-            for k in range(args.calls):
+            t = np.empty(calls)
+            for k in range(calls):
                 t0 = time.perf_counter()
                 fn()
                 t[k] = time.perf_counter() - t0
             res[name] = {"median": round(float(np.median(t)) * 1e6, 2), "p99": round(float(np.quantile(t, 0.99)) * 1e6, 2)}
         # seal and open separately (open needs a sealed buffer: reseal before each timed open)
-        ts, to = np.empty(args.calls), np.empty(args.calls)
-        for k in range(args.calls):
+        ts, to = np.empty(calls), np.empty(calls)
+        for k in range(calls):
             t0 = time.perf_counter()
             assert seal() == 0
             t1 = time.perf_counter()
@@ -73,8 +83,8 @@ def main():
         res["seal"] = {"median": round(float(np.median(ts)) * 1e6, 2), "p99": round(float(np.quantile(ts, 0.99)) * 1e6, 2)}
         res["open"] = {"median": round(float(np.median(to)) * 1e6, 2), "p99": round(float(np.quantile(to, 0.99)) * 1e6, 2)}
         # ctypes call overhead alone (a call that returns at the argument checks)
-        t = np.empty(args.calls)
-        for k in range(args.calls):
+        t = np.empty(calls)
+        for k in range(calls):
             t0 = time.perf_counter()
             lib.mq_aead_seal_in_place(ctx, nonce, 11, aad, 13, buf, 1200, P, ctypes.byref(ol), ctypes.byref(nd))
             t[k] = time.perf_counter() - t0
@@ -82,7 +92,7 @@ def main():
         out["chacha20" if suite == _lib.MQ_SUITE_CHACHA20 else "aes128gcm"] = res
         lib.mq_aead_free(ctx)
         lib.mq_hp_free(hp)
-    print(json.dumps(out), flush=True)
+    return out
 
 
 if __name__ == "__main__":
