@@ -188,8 +188,10 @@ __device__ __forceinline__ void gf_mul(uint32_t (&a)[4], const GfOp& b) {
 //                   T2[x] = ror(T0[x], 16). Lane l reads replica l & 31, so the 32 lanes of each
 //                   ds_read_b32 lane group hit 32 distinct banks. The byte address of
 //                   "row = byte k of s" is perm(s, 4 (l & 31) [+ 128 for T2]) — one v_perm_b32.
+//  [72 KiB, ...)    round keys: per wave, the AEAD and HP key schedules of its 8 packets
+//                   (kRkSlotBytes each; multi-key kernels), or one row's (single-key kernels)
 constexpr uint32_t kGhBytes = 8192, kTwBytes = 65536;
-constexpr int kAesWaves = 8;  // tile waves per workgroup: 72 KiB tables + 8 x 10 KiB images = 152 KiB
+constexpr uint32_t kRkSlotBytes = 2 * 176;  // aes_rk || hp_rk
 __shared__ __attribute__((aligned(16))) uint32_t g_aes_lds[(kGhBytes + kTwBytes) / 4];
 // multi-key tile kernels: the key row whose H^8 the GHASH table holds (the batch's most frequent
 // AES key, found by the mixed-batch partition), or nullptr when the table is not built
@@ -219,93 +221,79 @@ __device__ __forceinline__ uint32_t twl(uint32_t s, int k, uint32_t rsel) {
   return *(const uint32_t*)((const uint8_t*)g_aes_lds + kGhBytes + addr);
 }
 
-// AES-128 encryption of a block of big-endian column words with the wide table:
-// T1[x] = ror(T0[x], 8) and T3[x] = ror(T2[x], 8), so each output column is
-// T0[a] ^ T2[c] ^ ror(T0[b] ^ T2[d], 8) ^ k; the final round takes S[x] from T2 byte 3,
-// T0 byte 2, T0 byte 1 and T2 byte 0.
-__device__ __forceinline__ void aes128_block(const AesRk& rk, const TwLane& L, uint32_t& s0, uint32_t& s1,
-                                             uint32_t& s2, uint32_t& s3) {
-#if MQ_PROF_SKIP & 16
-  s0 ^= rk.w[0]; s1 ^= rk.w[41]; s2 ^= rk.w[42] ^ L.r0; s3 ^= rk.w[43];
-  return;
-#endif
-  s0 ^= rk.w[0]; s1 ^= rk.w[1]; s2 ^= rk.w[2]; s3 ^= rk.w[3];
-#pragma unroll
-  for (int r = 1; r < 10; ++r) {
-    const uint32_t l0 = twl(s0, 3, L.r0), l1 = twl(s2, 1, L.r2), l2 = twl(s1, 2, L.r0), l3 = twl(s3, 0, L.r2);
-    const uint32_t l4 = twl(s1, 3, L.r0), l5 = twl(s3, 1, L.r2), l6 = twl(s2, 2, L.r0), l7 = twl(s0, 0, L.r2);
-    const uint32_t l8 = twl(s2, 3, L.r0), l9 = twl(s0, 1, L.r2), l10 = twl(s3, 2, L.r0), l11 = twl(s1, 0, L.r2);
-    const uint32_t l12 = twl(s3, 3, L.r0), l13 = twl(s1, 1, L.r2), l14 = twl(s0, 2, L.r0), l15 = twl(s2, 0, L.r2);
-    __builtin_amdgcn_sched_barrier(0);  // all 16 lookups in flight before the first is consumed
-    s0 = l0 ^ l1 ^ ror(l2 ^ l3, 8) ^ rk.w[4 * r];
-    s1 = l4 ^ l5 ^ ror(l6 ^ l7, 8) ^ rk.w[4 * r + 1];
-    s2 = l8 ^ l9 ^ ror(l10 ^ l11, 8) ^ rk.w[4 * r + 2];
-    s3 = l12 ^ l13 ^ ror(l14 ^ l15, 8) ^ rk.w[4 * r + 3];
+// Round-key sources: registers (SGPRs when wave-uniform) or an LDS key schedule (a per-lane
+// pointer, so lanes of one wave may use different keys at no register cost). k(r) = the four
+// words of round key r.
+struct RkRegs {
+  const AesRk& rk;
+  __device__ __forceinline__ uint4 operator()(int r) const {
+    return make_uint4(rk.w[4 * r], rk.w[4 * r + 1], rk.w[4 * r + 2], rk.w[4 * r + 3]);
   }
-  auto fin = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
-    return (__builtin_amdgcn_perm(twl(a, 3, L.r2), twl(b, 2, L.r0), 0x07020c0cu) |
-            __builtin_amdgcn_perm(twl(c, 1, L.r0), twl(d, 0, L.r2), 0x0c0c0500u)) ^ k;
-  };
-  const uint32_t o0 = fin(s0, s1, s2, s3, rk.w[40]), o1 = fin(s1, s2, s3, s0, rk.w[41]),
-                 o2 = fin(s2, s3, s0, s1, rk.w[42]), o3 = fin(s3, s0, s1, s2, rk.w[43]);
-  s0 = o0; s1 = o1; s2 = o2; s3 = o3;
-}
+};
+struct RkLds {
+  const uint32_t* p;  // LDS
+  __device__ __forceinline__ uint4 operator()(int r) const { return *(const uint4*)(p + 4 * r); }
+};
+__device__ __forceinline__ uint32_t u4at(const uint4& v, int q) { return q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w; }
 
-// Rounds FIRST..9 and the final round of two independent blocks a, b through the wide table, their
-// rounds interleaved: twice the independent LDS reads per round, so the lookup latency of one
-// block hides behind the other's. FIRST = 1: a, b are AES inputs (round-0 key added here);
-// FIRST = 3: a, b are states after round 2 (from the CTR cache).
-template <int FIRST>
-__device__ __forceinline__ void aes128_rounds2(const AesRk& rk, const TwLane& L, uint32_t (&a)[4], uint32_t (&b)[4]) {
-#if MQ_PROF_SKIP & 16
-  a[0] ^= rk.w[0]; a[1] ^= rk.w[41]; a[2] ^= L.r0; b[0] ^= rk.w[1]; b[1] ^= rk.w[42]; b[3] ^= L.r2;
-  return;
-#endif
-  if (FIRST == 1) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) { a[q] ^= rk.w[q]; b[q] ^= rk.w[q]; }
-  }
-#pragma unroll
-  for (int r = FIRST; r < 10; ++r) {
-    // all 32 lookups of the round are issued before any is consumed (sched_barrier), so the LDS
-    // queue streams them with up to 15 in flight instead of draining after every column
-    uint32_t la[16], lb[16];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int q1 = (q + 1) & 3, q2 = (q + 2) & 3, q3 = (q + 3) & 3;
-      la[4 * q] = twl(a[q], 3, L.r0); la[4 * q + 1] = twl(a[q2], 1, L.r2);
-      la[4 * q + 2] = twl(a[q1], 2, L.r0); la[4 * q + 3] = twl(a[q3], 0, L.r2);
-      lb[4 * q] = twl(b[q], 3, L.r0); lb[4 * q + 1] = twl(b[q2], 1, L.r2);
-      lb[4 * q + 2] = twl(b[q1], 2, L.r0); lb[4 * q + 3] = twl(b[q3], 0, L.r2);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      a[q] = la[4 * q] ^ la[4 * q + 1] ^ ror(la[4 * q + 2] ^ la[4 * q + 3], 8) ^ rk.w[4 * r + q];
-      b[q] = lb[4 * q] ^ lb[4 * q + 1] ^ ror(lb[4 * q + 2] ^ lb[4 * q + 3], 8) ^ rk.w[4 * r + q];
-    }
-  }
-  uint32_t la[16], lb[16];
+// One round from state s (rounds 1..9) through the wide table: all 16 lookups (and the key)
+// are issued before any is consumed, so the LDS queue streams them.
+template <class K>
+__device__ __forceinline__ void aes_round(const K& key, int r, const TwLane& L, uint32_t (&s)[4]) {
+  uint32_t l[16];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int q1 = (q + 1) & 3, q2 = (q + 2) & 3, q3 = (q + 3) & 3;
-    la[4 * q] = twl(a[q], 3, L.r2); la[4 * q + 1] = twl(a[q1], 2, L.r0);
-    la[4 * q + 2] = twl(a[q2], 1, L.r0); la[4 * q + 3] = twl(a[q3], 0, L.r2);
-    lb[4 * q] = twl(b[q], 3, L.r2); lb[4 * q + 1] = twl(b[q1], 2, L.r0);
-    lb[4 * q + 2] = twl(b[q2], 1, L.r0); lb[4 * q + 3] = twl(b[q3], 0, L.r2);
+    l[4 * q] = twl(s[q], 3, L.r0); l[4 * q + 1] = twl(s[q2], 1, L.r2);
+    l[4 * q + 2] = twl(s[q1], 2, L.r0); l[4 * q + 3] = twl(s[q3], 0, L.r2);
   }
+  const uint4 kr = key(r);
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    a[q] = (__builtin_amdgcn_perm(la[4 * q], la[4 * q + 1], 0x07020c0cu) |
-            __builtin_amdgcn_perm(la[4 * q + 2], la[4 * q + 3], 0x0c0c0500u)) ^ rk.w[40 + q];
-    b[q] = (__builtin_amdgcn_perm(lb[4 * q], lb[4 * q + 1], 0x07020c0cu) |
-            __builtin_amdgcn_perm(lb[4 * q + 2], lb[4 * q + 3], 0x0c0c0500u)) ^ rk.w[40 + q];
-  }
+  for (int q = 0; q < 4; ++q) s[q] = l[4 * q] ^ l[4 * q + 1] ^ ror(l[4 * q + 2] ^ l[4 * q + 3], 8) ^ u4at(kr, q);
 }
 
-__device__ __forceinline__ void aes128_block2(const AesRk& rk, const TwLane& L, uint32_t (&a)[4], uint32_t (&b)[4]) {
-  aes128_rounds2<1>(rk, L, a, b);
+// final round: SubBytes + ShiftRows (S[x] from T2 byte 3, T0 byte 2, T0 byte 1, T2 byte 0) +
+// AddRoundKey
+template <class K>
+__device__ __forceinline__ void aes_final(const K& key, const TwLane& L, uint32_t (&s)[4]) {
+  uint32_t l[16];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int q1 = (q + 1) & 3, q2 = (q + 2) & 3, q3 = (q + 3) & 3;
+    l[4 * q] = twl(s[q], 3, L.r2); l[4 * q + 1] = twl(s[q1], 2, L.r0);
+    l[4 * q + 2] = twl(s[q2], 1, L.r0); l[4 * q + 3] = twl(s[q3], 0, L.r2);
+  }
+  const uint4 kr = key(10);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    s[q] = (__builtin_amdgcn_perm(l[4 * q], l[4 * q + 1], 0x07020c0cu) |
+            __builtin_amdgcn_perm(l[4 * q + 2], l[4 * q + 3], 0x0c0c0500u)) ^ u4at(kr, q);
+}
+
+// AES-128 encryption of a block of big-endian column words with the wide table:
+// T1[x] = ror(T0[x], 8) and T3[x] = ror(T2[x], 8), so each output column is
+// T0[a] ^ T2[c] ^ ror(T0[b] ^ T2[d], 8) ^ k.
+template <class K>
+__device__ __forceinline__ void aes128_enc(const K& key, const TwLane& L, uint32_t (&s)[4]) {
+#if MQ_PROF_SKIP & 16
+  const uint4 k0 = key(0);
+  s[0] ^= k0.x; s[1] ^= k0.y; s[2] ^= k0.z ^ L.r0; s[3] ^= k0.w;
+  return;
+#endif
+  const uint4 k0 = key(0);
+  s[0] ^= k0.x; s[1] ^= k0.y; s[2] ^= k0.z; s[3] ^= k0.w;
+#pragma unroll
+  for (int r = 1; r < 10; ++r) aes_round(key, r, L, s);
+  aes_final(key, L, s);
+}
+
+__device__ __forceinline__ void aes128_block(const AesRk& rk, const TwLane& L, uint32_t& s0, uint32_t& s1,
+                                             uint32_t& s2, uint32_t& s3) {
+  uint32_t s[4] = {s0, s1, s2, s3};
+  aes128_enc(RkRegs{rk}, L, s);
+  s0 = s[0]; s1 = s[1]; s2 = s[2]; s3 = s[3];
 }
 
 // CTR caching (counter-mode AES with counters < 256): the input of block c of a packet is
@@ -320,21 +308,23 @@ struct AesCtrCache {
   uint32_t x;       // low byte of round key word 3 (xored with the counter's low byte)
 };
 
-__device__ __forceinline__ AesCtrCache ctr_cache(const AesRk& rk, const TwLane& L, const uint32_t (&nb)[3]) {
-  const uint32_t s0 = nb[0] ^ rk.w[0], s1 = nb[1] ^ rk.w[1], s2 = nb[2] ^ rk.w[2], s3 = rk.w[3];
+template <class K>
+__device__ __forceinline__ AesCtrCache ctr_cache(const K& key, const TwLane& L, const uint32_t (&nb)[3]) {
+  const uint4 r0 = key(0), r1 = key(1), r2 = key(2);
+  const uint32_t s0 = nb[0] ^ r0.x, s1 = nb[1] ^ r0.y, s2 = nb[2] ^ r0.z, s3 = r0.w;
   AesCtrCache c;
-  c.x = rk.w[3] & 0xffu;
+  c.x = r0.w & 0xffu;
   // round 1 (column q = T0[b3 s_q] ^ T2[b1 s_q+2] ^ ror8(T0[b2 s_q+1] ^ T2[b0 s_q+3]) ^ k);
   // byte 0 of s3 (the counter's) only enters column 0
-  c.k0 = twl(s0, 3, L.r0) ^ twl(s2, 1, L.r2) ^ ror(twl(s1, 2, L.r0), 8) ^ rk.w[4];
-  const uint32_t k1 = twl(s1, 3, L.r0) ^ twl(s3, 1, L.r2) ^ ror(twl(s2, 2, L.r0) ^ twl(s0, 0, L.r2), 8) ^ rk.w[5];
-  const uint32_t k2 = twl(s2, 3, L.r0) ^ twl(s0, 1, L.r2) ^ ror(twl(s3, 2, L.r0) ^ twl(s1, 0, L.r2), 8) ^ rk.w[6];
-  const uint32_t k3 = twl(s3, 3, L.r0) ^ twl(s1, 1, L.r2) ^ ror(twl(s0, 2, L.r0) ^ twl(s2, 0, L.r2), 8) ^ rk.w[7];
+  c.k0 = twl(s0, 3, L.r0) ^ twl(s2, 1, L.r2) ^ ror(twl(s1, 2, L.r0), 8) ^ r1.x;
+  const uint32_t k1 = twl(s1, 3, L.r0) ^ twl(s3, 1, L.r2) ^ ror(twl(s2, 2, L.r0) ^ twl(s0, 0, L.r2), 8) ^ r1.y;
+  const uint32_t k2 = twl(s2, 3, L.r0) ^ twl(s0, 1, L.r2) ^ ror(twl(s3, 2, L.r0) ^ twl(s1, 0, L.r2), 8) ^ r1.z;
+  const uint32_t k3 = twl(s3, 3, L.r0) ^ twl(s1, 1, L.r2) ^ ror(twl(s0, 2, L.r0) ^ twl(s2, 0, L.r2), 8) ^ r1.w;
   // round 2 with t1..t3 = k1..k3 constant: every column has one term from t0
-  c.d[0] = twl(k2, 1, L.r2) ^ ror(twl(k1, 2, L.r0) ^ twl(k3, 0, L.r2), 8) ^ rk.w[8];
-  c.d[1] = twl(k1, 3, L.r0) ^ twl(k3, 1, L.r2) ^ ror(twl(k2, 2, L.r0), 8) ^ rk.w[9];
-  c.d[2] = twl(k2, 3, L.r0) ^ ror(twl(k3, 2, L.r0) ^ twl(k1, 0, L.r2), 8) ^ rk.w[10];
-  c.d[3] = twl(k3, 3, L.r0) ^ twl(k1, 1, L.r2) ^ ror(twl(k2, 0, L.r2), 8) ^ rk.w[11];
+  c.d[0] = twl(k2, 1, L.r2) ^ ror(twl(k1, 2, L.r0) ^ twl(k3, 0, L.r2), 8) ^ r2.x;
+  c.d[1] = twl(k1, 3, L.r0) ^ twl(k3, 1, L.r2) ^ ror(twl(k2, 2, L.r0), 8) ^ r2.y;
+  c.d[2] = twl(k2, 3, L.r0) ^ ror(twl(k3, 2, L.r0) ^ twl(k1, 0, L.r2), 8) ^ r2.z;
+  c.d[3] = twl(k3, 3, L.r0) ^ twl(k1, 1, L.r2) ^ ror(twl(k2, 0, L.r2), 8) ^ r2.w;
   return c;
 }
 
@@ -347,48 +337,18 @@ __device__ __forceinline__ void ctr_round2(const AesCtrCache& c, const TwLane& L
   s[3] = c.d[3] ^ ror(twl(t0, 2, L.r0), 8);
 }
 
-// one block from the state after round 2 (rounds 3..10)
-__device__ __forceinline__ void aes128_rounds_from3(const AesRk& rk, const TwLane& L, uint32_t (&s)[4]) {
-#pragma unroll
-  for (int r = 3; r < 10; ++r) {
-    uint32_t l[16];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int q1 = (q + 1) & 3, q2 = (q + 2) & 3, q3 = (q + 3) & 3;
-      l[4 * q] = twl(s[q], 3, L.r0); l[4 * q + 1] = twl(s[q2], 1, L.r2);
-      l[4 * q + 2] = twl(s[q1], 2, L.r0); l[4 * q + 3] = twl(s[q3], 0, L.r2);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) s[q] = l[4 * q] ^ l[4 * q + 1] ^ ror(l[4 * q + 2] ^ l[4 * q + 3], 8) ^ rk.w[4 * r + q];
-  }
-  uint32_t l[16];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int q1 = (q + 1) & 3, q2 = (q + 2) & 3, q3 = (q + 3) & 3;
-    l[4 * q] = twl(s[q], 3, L.r2); l[4 * q + 1] = twl(s[q1], 2, L.r0);
-    l[4 * q + 2] = twl(s[q2], 1, L.r0); l[4 * q + 3] = twl(s[q3], 0, L.r2);
-  }
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-    s[q] = (__builtin_amdgcn_perm(l[4 * q], l[4 * q + 1], 0x07020c0cu) |
-            __builtin_amdgcn_perm(l[4 * q + 2], l[4 * q + 3], 0x0c0c0500u)) ^ rk.w[40 + q];
-}
-
-// CTR block with counter `ctr` (< 256) from the cache
-__device__ __forceinline__ void aes128_ctr1(const AesRk& rk, const TwLane& L, const AesCtrCache& c, uint32_t ctr,
+// CTR block with counter `ctr` (< 256) from the cache: rounds 3..10
+template <class K>
+__device__ __forceinline__ void aes128_ctr1(const K& key, const TwLane& L, const AesCtrCache& c, uint32_t ctr,
                                             uint32_t (&s)[4]) {
+#if MQ_PROF_SKIP & 16
+  s[0] = c.d[0] ^ ctr; s[1] = c.d[1]; s[2] = c.d[2] ^ L.r0; s[3] = c.d[3];
+  return;
+#endif
   ctr_round2(c, L, ctr, s);
-  aes128_rounds_from3(rk, L, s);
-}
-
-// CTR blocks with counters ca and cb (both < 256) from the cache
-__device__ __forceinline__ void aes128_ctr2(const AesRk& rk, const TwLane& L, const AesCtrCache& c, uint32_t ca,
-                                            uint32_t cb, uint32_t (&a)[4], uint32_t (&b)[4]) {
-  ctr_round2(c, L, ca, a);
-  ctr_round2(c, L, cb, b);
-  aes128_rounds2<3>(rk, L, a, b);
+#pragma unroll
+  for (int r = 3; r < 10; ++r) aes_round(key, r, L, s);
+  aes_final(key, L, s);
 }
 
 // a = x^i * h (reflected basis), 0 <= i < 128: shift into 8 words, then fold
@@ -443,20 +403,43 @@ __device__ __forceinline__ uint32_t byte_of(uint32_t x, int m) {
 
 // a = a * H^8 through the GHASH table: nibble 2m of word w sits (times 16) in byte m of
 // (a[w] << 4) & 0xf0f0f0f0, nibble 2m+1 in byte m of a[w] & 0xf0f0f0f0 — each a ready byte offset
-// of its entry within its position's 256-B row.
+// of its entry within its position's 256-B row. The 32 reads go in 8 groups of 4 with at most two
+// groups in flight: group g's addresses take a fake dependency (empty asm) on the accumulator
+// after group g - 2, because the scheduler would otherwise issue all 32 at once (128 VGPRs) and
+// the 4-waves/SIMD streaming kernels would spill.
+__device__ __forceinline__ void gh_group(const uint32_t (&a)[4], int g, uint4 (&e)[4], const uint32_t* dep) {
+  const int w = g >> 1, mb = 2 * (g & 1);
+  const uint32_t lo = (a[w] << 4) & 0xf0f0f0f0u, hi = a[w] & 0xf0f0f0f0u;
+  uint32_t ad[4] = {byte_of(lo, mb), byte_of(hi, mb), byte_of(lo, mb + 1), byte_of(hi, mb + 1)};
+  if (dep)
+    asm volatile("" : "+v"(ad[0]), "+v"(ad[1]), "+v"(ad[2]), "+v"(ad[3]) : "v"(dep[0]), "v"(dep[1]), "v"(dep[2]), "v"(dep[3]));
+  const uint8_t* t = (const uint8_t*)g_aes_lds + 256u * (8 * w + 2 * mb);
+  e[0] = *(const uint4*)(t + ad[0]);
+  e[1] = *(const uint4*)(t + 256 + ad[1]);
+  e[2] = *(const uint4*)(t + 512 + ad[2]);
+  e[3] = *(const uint4*)(t + 768 + ad[3]);
+}
+__device__ __forceinline__ void gh_fold(uint32_t (&r)[4], const uint4 (&e)[4]) {
+  r[0] = xor3(r[0], e[0].x, e[1].x); r[1] = xor3(r[1], e[0].y, e[1].y);
+  r[2] = xor3(r[2], e[0].z, e[1].z); r[3] = xor3(r[3], e[0].w, e[1].w);
+  r[0] = xor3(r[0], e[2].x, e[3].x); r[1] = xor3(r[1], e[2].y, e[3].y);
+  r[2] = xor3(r[2], e[2].z, e[3].z); r[3] = xor3(r[3], e[2].w, e[3].w);
+}
 __device__ __forceinline__ void gh_mul_tab(uint32_t (&a)[4]) {
-  uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+  uint32_t r[4] = {0, 0, 0, 0};
+  uint4 e0[4], e1[4];
+  gh_group(a, 0, e0, nullptr);
+  gh_group(a, 1, e1, nullptr);
 #pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    const uint32_t lo = (a[w] << 4) & 0xf0f0f0f0u, hi = a[w] & 0xf0f0f0f0u;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const uint4 e0 = *(const uint4*)((const uint8_t*)g_aes_lds + 256u * (8 * w + 2 * m) + byte_of(lo, m));
-      const uint4 e1 = *(const uint4*)((const uint8_t*)g_aes_lds + 256u * (8 * w + 2 * m + 1) + byte_of(hi, m));
-      r0 = xor3(r0, e0.x, e1.x); r1 = xor3(r1, e0.y, e1.y); r2 = xor3(r2, e0.z, e1.z); r3 = xor3(r3, e0.w, e1.w);
-    }
+  for (int g = 2; g < 8; g += 2) {
+    gh_fold(r, e0);
+    gh_group(a, g, e0, r);
+    gh_fold(r, e1);
+    gh_group(a, g + 1, e1, r);
   }
-  a[0] = r0; a[1] = r1; a[2] = r2; a[3] = r3;
+  gh_fold(r, e0);
+  gh_fold(r, e1);
+  a[0] = r[0]; a[1] = r[1]; a[2] = r[2]; a[3] = r[3];
 }
 
 }  // namespace mq

@@ -8,14 +8,24 @@
 //   * AES-128 rounds use the wide T-table (T0 and T2, 32 replicas each, 64 KiB per workgroup,
 //     mq_aes.h): one v_perm_b32 per lookup address, conflict-free ds_read_b32, one rotation per
 //     round column; round keys in SGPRs (single-key kernels) or VGPRs;
-//   * GHASH: in the single-key kernels every Horner step's multiply by H^8 is 32 table reads
-//     (mq_aes.h gh_mul_tab, built per workgroup from H^8); the final multiply by H^(8-j) and all
-//     multiplies of the multi-key kernels use the bit-holed integer product (gf_mul).
-// Workgroups of kAesWaves waves are persistent (one per CU, LDS-bound), so the 72 KiB of tables
-// are built once per CU and each wave walks tiles w, w + stride, ...
-// Work split per tile (mq_tile.h): keystream block b of a packet (b = 0: E_K(J0), b >= 1:
-// counter b+1) on lane b % 8; GHASH interleaved over the octet with H^8 (precomputed on the
-// host per key) and a final multiply by H^(8-j).
+//   * GHASH: every Horner step's multiply by H^8 is 32 reads of an LDS table of H^8 (mq_aes.h
+//     gh_mul_tab, built per workgroup) in the single-key kernels and, in the multi-key kernels,
+//     in waves whose packets all use the table's (hot) key; otherwise, and for the final multiply
+//     by H^e, the bit-holed integer product (gf_mul).
+//
+// STREAMING tiles (r02): a wave = 8 packets x 8 lanes (mq_tile.h), slot b of a packet on lane
+// b % 8 in iteration b / 8. Slot b >= 1 is CTR block b (counter b + 1) over payload bytes
+// [16(b-1), 16b); slot 0 is E_K(J0); slots 1-A .. 0 carry the A AAD blocks and slot nblk the
+// GHASH length block; slot nblk (or 8) the header-protection block of seal. GHASH block i sits in
+// slot i - A + 1, so lane j's GHASH blocks are exactly its own CTR blocks: each lane loads its
+// 16 B of packet straight from HBM into VGPRs (one iteration ahead), XORs the keystream, stores,
+// and absorbs the ciphertext into its Horner accumulator (multiplier H^8) in the same iteration;
+// a final multiply by H^e (e = blocks after the lane's last one, 1..8) and an octet XOR give the
+// tag. No LDS packet image: the workgroup's LDS is the 72 KiB of tables, so 16 waves per CU
+// (4 per SIMD) fit where the staged design (10-KiB images, r01) ran 8 — measured 1.41 vs 2.23 ms
+// for a config-C seal (tools/ubench/ubench6.hip). Open decrypts in the same single pass,
+// storing plaintext speculatively; a packet whose tag fails is restored by XORing the same
+// keystream again, so every failed packet ends byte-identical to its input (recv.rs:416-421).
 #include "mq_aes.h"
 #include "mq_tile.h"
 
@@ -23,397 +33,339 @@
 
 namespace mq {
 
-// Interleaved GHASH over AAD||pad||CT||pad||[len(A)]64||[len(C)]64 (bit lengths): lane j takes
-// blocks 8k + j with multiplier H^8, then one final multiply by H^(8-j) (row->H[7-j], computed on
-// the host per key), then the octet XOR. Every lane of the octet returns the same value
-// (reflected basis). The H^8 multiplies go through the LDS table in the single-key kernels (TAB)
-// and, in the multi-key kernels, in waves whose active packets all use the table's row
-// (g_aes_hot_row); otherwise through the bit-holed integer product.
-template <bool TAB, class S>
-__device__ __forceinline__ void ghash_impl(const S& sp, typename S::off_t pkt, typename S::off_t pay,
-                                           uint32_t aad_len, uint32_t ct_len, const KeyRow* row, int j,
-                                           bool act, uint32_t (&y)[4]) {
-#if MQ_PROF_SKIP & 2
-  for (int w = 0; w < 4; ++w) y[w] = row->H[0][w] ^ aad_len ^ ct_len;
-  return;
-#endif
-  uint32_t hp[4];
-  GfOp m8, mlast;
-  {
-    if (!TAB) {
-#pragma unroll
-      for (int w = 0; w < 4; ++w) hp[w] = brev(row->H[7][w]);
-      m8 = gf_prepare(hp);
-    }
-    const int e = 7 - j;  // H^(8-j)
-#pragma unroll
-    for (int w = 0; w < 4; ++w) hp[w] = brev(row->H[e][w]);
-    mlast = gf_prepare(hp);
-  }
-  const uint32_t A = (aad_len + 15) >> 4, T = (ct_len + 15) >> 4, nb = A + T + 1;
-  const uint32_t K = (nb + kLanesPerPkt - 1) / kLanesPerPkt;
-  const uint32_t Kmax = wave_max_u32(act ? K : 0u);
-  const int z = (int)(kLanesPerPkt * Kmax) - (int)nb;
-  uint32_t acc[4] = {0, 0, 0, 0};
-  struct Blk { typename S::off_t src; int rem; bool lens; };
-  auto where = [&](uint32_t k) {
-    const int i = (int)(kLanesPerPkt * k) + j - z;
-    Blk b{pkt, 0, false};
-    if (act && i >= 0) {
-      if ((uint32_t)i < A) {
-        b.src = pkt + 16 * (uint32_t)i; b.rem = (int)aad_len - 16 * i;
-      } else if ((uint32_t)i < A + T) {
-        b.src = pay + 16 * ((uint32_t)i - A); b.rem = (int)ct_len - 16 * (i - (int)A);
-      } else {
-        b.lens = true;
-      }
-    }
-    return b;
-  };
-  auto absorb = [&](const Blk& b, uint32_t (&m)[4]) {
-#pragma unroll
-    for (int w = 0; w < 4; ++w) m[w] = refl(m[w] & byte_mask(b.rem, w));
-    if (b.lens) {
-      const uint64_t ab = (uint64_t)aad_len * 8, cb = (uint64_t)ct_len * 8;
-      m[0] = brev((uint32_t)(ab >> 32)); m[1] = brev((uint32_t)ab);
-      m[2] = brev((uint32_t)(cb >> 32)); m[3] = brev((uint32_t)cb);
-    }
-#pragma unroll
-    for (int w = 0; w < 4; ++w) acc[w] ^= m[w];
-  };
-  if (Kmax > 0) {
-    Blk b = where(0);
-    uint32_t m[4];
-    load_words<4>(sp, b.src, m);
-    for (uint32_t k = 0; k + 1 < Kmax; ++k) {
-      absorb(b, m);
-      b = where(k + 1);
-      load_words<4>(sp, b.src, m);
-      if (TAB) gh_mul_tab(acc);
-      else gf_mul(acc, m8);
-    }
-    absorb(b, m);
-    gf_mul(acc, mlast);
-  }
-#pragma unroll
-  for (int w = 0; w < 4; ++w) y[w] = oct_xor(acc[w]);
+// 16-B packet accesses at any byte alignment (global_load/store_dwordx4; gfx950 runs with
+// unaligned access enabled)
+typedef uint4 __attribute__((aligned(1))) uint4_u;
+__device__ __forceinline__ uint4 ld16(const uint8_t* p) { return *(const uint4_u*)p; }
+__device__ __forceinline__ void st16(uint8_t* p, const uint32_t (&w)[4]) {
+  *(uint4_u*)p = make_uint4(w[0], w[1], w[2], w[3]);
+}
+__device__ __forceinline__ void st_bytes(uint8_t* p, const uint32_t (&w)[4], uint32_t n) {
+  for (uint32_t k = 0; k < n; ++k) p[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+}
+__device__ __forceinline__ void st_block(uint8_t* p, const uint32_t (&w)[4], uint32_t rem) {
+  if (rem >= 16) st16(p, w);
+  else st_bytes(p, w, rem);
+}
+__device__ __forceinline__ void u4w(uint4 v, uint32_t (&w)[4]) { w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w; }
+
+// DirectionalKeys::nonce (src/crypto/mod.rs:66-74), as big-endian AES input words
+__device__ __forceinline__ void nonce_be(const KeyRow* row, uint64_t pn, uint32_t (&nb)[3]) {
+  nb[0] = bswap32(row->iv[0]);
+  nb[1] = bswap32(row->iv[1]) ^ (uint32_t)(pn >> 32);
+  nb[2] = bswap32(row->iv[2]) ^ (uint32_t)pn;
 }
 
-// Two instantiations, so that a wave holds the registers of one multiply method only.
-template <bool TAB, class S>
-__device__ __forceinline__ void ghash(const S& sp, typename S::off_t pkt, typename S::off_t pay,
-                                      uint32_t aad_len, uint32_t ct_len, const KeyRow* row, int j,
-                                      bool act, uint32_t (&y)[4]) {
-  if (TAB || (g_aes_hot_row != nullptr && !wave_any(act && row != g_aes_hot_row)))
-    ghash_impl<true>(sp, pkt, pay, aad_len, ct_len, row, j, act, y);
-  else
-    ghash_impl<false>(sp, pkt, pay, aad_len, ct_len, row, j, act, y);
+// AesHeaderProtection::mask (rustcrypto.rs:175-186): AES-ECB(hp, sample)[0..5], sample as
+// little-endian words. rb: TwLane in the tile kernels, the small table's replica offset in the
+// one-packet-per-lane kernels.
+template <class T>
+__device__ __forceinline__ void aes_hp_mask_words(const uint32_t (&smp)[4], const KeyRow* row, const T& rb,
+                                                  uint32_t& m0, uint32_t& m1) {
+  AesRk hk;
+  load_rk(row->hp_rk, hk);
+  uint32_t s0 = bswap32(smp[0]), s1 = bswap32(smp[1]), s2 = bswap32(smp[2]), s3 = bswap32(smp[3]);
+  aes128_block(hk, rb, s0, s1, s2, s3);
+  m0 = bswap32(s0);
+  m1 = s1 >> 24;
 }
 
-// TAB: single-key kernel with the GHASH table of H^8 in LDS
-template <bool TAB>
-struct AesPolicyT {
-  static constexpr uint32_t kSuite = MQ_SUITE_AES128GCM;
+// GHASH length block: [len(A)]64 || [len(C)]64 in bits, reflected words
+__device__ __forceinline__ void len_block(uint32_t aad_len, uint32_t ct_len, uint32_t (&x)[4]) {
+  const uint64_t ab = (uint64_t)aad_len * 8, cb = (uint64_t)ct_len * 8;
+  x[0] = brev((uint32_t)(ab >> 32)); x[1] = brev((uint32_t)ab);
+  x[2] = brev((uint32_t)(cb >> 32)); x[3] = brev((uint32_t)cb);
+}
 
-  // keystream of block index b (0: E(J0), b >= 1: counter b + 1) as little-endian data words
-  static __device__ __forceinline__ void ctr_block(const AesRk& rk, const TwLane& rb, const uint32_t (&nb)[3],
-                                                   uint32_t b, uint32_t (&ks)[4]) {
-    uint32_t s0 = nb[0], s1 = nb[1], s2 = nb[2], s3 = b == 0 ? 1u : b + 1;
-    aes128_block(rk, rb, s0, s1, s2, s3);
-    ks[0] = bswap32(s0); ks[1] = bswap32(s1); ks[2] = bswap32(s2); ks[3] = bswap32(s3);
-  }
-
-  // blocks b and b + 8 (the lane's next iteration) at once
-  static __device__ __forceinline__ void ctr_block2(const AesRk& rk, const TwLane& rb, const uint32_t (&nb)[3],
-                                                    uint32_t b, uint32_t (&ks)[4], uint32_t (&ks2)[4]) {
-    uint32_t x[4] = {nb[0], nb[1], nb[2], b == 0 ? 1u : b + 1};
-    uint32_t y[4] = {nb[0], nb[1], nb[2], b + kLanesPerPkt + 1};
-    aes128_block2(rk, rb, x, y);
+// GHASH data block from little-endian memory words, the first `rem` bytes kept
+__device__ __forceinline__ void gh_block(const uint32_t (&m)[4], uint32_t rem, uint32_t (&x)[4]) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) { ks[q] = bswap32(x[q]); ks2[q] = bswap32(y[q]); }
-  }
+  for (int w = 0; w < 4; ++w) x[w] = refl(m[w] & byte_mask((int)rem, w));
+}
 
-  // the same from the packet's CTR cache (every counter of the wave's packets < 256)
-  static __device__ __forceinline__ void ctr_block2c(const AesRk& rk, const TwLane& rb, const AesCtrCache& cc,
-                                                     uint32_t b, uint32_t (&ks)[4], uint32_t (&ks2)[4]) {
-    uint32_t x[4], y[4];
-    aes128_ctr2(rk, rb, cc, b == 0 ? 1u : b + 1, b + kLanesPerPkt + 1, x, y);
+// Per-packet, per-lane state of a streaming tile (octet-uniform fields are equal on the 8 lanes)
+struct AesPkt {
+  bool act, rec, hp;
+  uint32_t aad_len, P, A, nblk;
+  uint64_t pkt, pay;
+  uint32_t nb[3];
+};
+
+// Byte x of the unmasked header (open): byte 0 -> b0, PN bytes -> the truncated PN (big-endian)
+__device__ __forceinline__ void patch_header(uint32_t (&m)[4], uint32_t at, uint8_t b0, uint32_t pn_off,
+                                             uint32_t pn_len, uint32_t trunc) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) { ks[q] = bswap32(x[q]); ks2[q] = bswap32(y[q]); }
+  for (int k = 0; k < 16; ++k) {
+    const uint32_t x = at + (uint32_t)k;
+    const uint32_t sh = 8u * (k & 3);
+    uint32_t v = 0x100;  // none
+    if (x == 0) v = b0;
+    else if (x >= pn_off && x < pn_off + pn_len) v = (trunc >> (8u * (pn_len - 1u - (x - pn_off)))) & 0xffu;
+    if (v != 0x100) m[k >> 2] = (m[k >> 2] & ~(0xffu << sh)) | (v << sh);
   }
-  static __device__ __forceinline__ void ctr_blockc(const AesRk& rk, const TwLane& rb, const AesCtrCache& cc,
-                                                    uint32_t b, uint32_t (&ks)[4]) {
-    uint32_t x[4];
-    aes128_ctr1(rk, rb, cc, b == 0 ? 1u : b + 1, x);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) ks[q] = bswap32(x[q]);
-  }
+}
 
-  template <class S>
-  static __device__ __forceinline__ void xor_block(const S& sp, typename S::off_t pay, uint32_t b,
-                                                   uint32_t P, const uint32_t (&ks)[4]) {
-    const uint32_t o = 16 * (b - 1);
-    const int ln = (int)min(16u, P - o);
-    uint32_t raw[5];
-    load_raw<4>(sp, pay + o, raw);
-    xor_words<4>(sp, pay + o, ks, ln, raw);
-  }
-
-  // AesHeaderProtection::mask (rustcrypto.rs:175-186): AES-ECB(hp, sample)[0..5]
-  // (rb: TwLane in the tile kernels, the small table's replica offset in the per-lane kernels)
-  template <class T>
-  static __device__ __forceinline__ void hp_mask_words(const uint32_t (&smp)[4], const KeyRow* row, const T& rb,
-                                                       uint32_t& m0, uint32_t& m1) {
-    AesRk hk;
-    load_rk(row->hp_rk, hk);
-    uint32_t s0 = bswap32(smp[0]), s1 = bswap32(smp[1]), s2 = bswap32(smp[2]), s3 = bswap32(smp[3]);
-    aes128_block(hk, rb, s0, s1, s2, s3);
-    m0 = bswap32(s0);
-    m1 = s1 >> 24;
-  }
-  template <class S, class T>
-  static __device__ __forceinline__ void hp_mask(const S& sp, typename S::off_t sample_at,
-                                                 const KeyRow* row, const T& rb, uint32_t& m0, uint32_t& m1) {
-    uint32_t smp[4];
-    load_words<4>(sp, sample_at, smp);
-    AesRk hk;
-    load_rk(row->hp_rk, hk);
-    uint32_t s0 = bswap32(smp[0]), s1 = bswap32(smp[1]), s2 = bswap32(smp[2]), s3 = bswap32(smp[3]);
-    aes128_block(hk, rb, s0, s1, s2, s3);
-    m0 = bswap32(s0);
-    m1 = s1 >> 24;
-  }
-
-  static __device__ __forceinline__ void nonce_be(const KeyRow* row, uint64_t pn, uint32_t (&nb)[3]) {
-    // DirectionalKeys::nonce (src/crypto/mod.rs:66-74), as big-endian AES input words
-    nb[0] = bswap32(row->iv[0]);
-    nb[1] = bswap32(row->iv[1]) ^ (uint32_t)(pn >> 32);
-    nb[2] = bswap32(row->iv[2]) ^ (uint32_t)pn;
-  }
-
-  static __device__ __forceinline__ void tag_words(const uint32_t (&y)[4], const uint32_t (&ej0)[4],
-                                                   uint32_t (&tag)[4]) {
-#pragma unroll
-    for (int w = 0; w < 4; ++w) tag[w] = bswap32(brev(y[w])) ^ ej0[w];
-  }
-
-  template <class S>
-  static __device__ __forceinline__ void apply_hp(const S& sp, typename S::off_t pkt, const mq_pkt_desc& d,
-                                                  uint32_t m0, uint32_t m1) {
-    const uint8_t fb = (d.flags & MQ_PKT_LONG_HEADER) ? 0x0f : 0x1f;
-    sp.st8(pkt, sp.ld8(pkt) ^ ((uint8_t)m0 & fb));
-    const uint32_t mk = (m0 >> 8) | (m1 << 24);
-    for (uint32_t b = 0; b < d.pn_len; ++b)
-      sp.st8(pkt + d.pn_offset + b, sp.ld8(pkt + d.pn_offset + b) ^ (uint8_t)(mk >> (8 * b)));
-  }
-
-  // send composite: CTR block b (0 = E_K(J0)) on lane b % 8 in iteration b / 8; the HP block runs
-  // in the first free slot after the blocks holding the sample (b = 1, 2), or in a separate phase
-  // when the sample reaches into the tag.
-  template <class S, class G>
-  static __device__ __forceinline__ void seal(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j, G& stg) {
-    const mq_pkt_desc& d = c.d;
-    const TwLane rb = tw_lane();
-    const uint32_t aad_len = c.act ? (uint32_t)d.pn_offset + d.pn_len : 0u;
-    const uint32_t P = c.act ? d.len - aad_len - 16 : 0u;
-    const typename S::off_t pay = pkt + aad_len;
-    uint32_t nb[3];
-    nonce_be(row, c.pn, nb);
-    const uint32_t nblk = 1 + (P + 15) / 16;
-    const bool hp_on = c.act && !(d.flags & MQ_PKT_NO_HP);
-    const bool hp_post = hp_on && 20 > P + d.pn_len;
-    uint32_t hp_it = nblk / kLanesPerPkt, hp_lane = nblk % kLanesPerPkt;
-    if (hp_it == 0) { hp_it = 1; hp_lane = 0; }
-    const uint32_t iters = max((nblk + kLanesPerPkt - 1) / kLanesPerPkt, (hp_on && !hp_post) ? hp_it + 1 : 0u);
-    const uint32_t Imax = wave_max_u32(c.act ? iters : 0u);
-    uint32_t ej0[4] = {0, 0, 0, 0};
-    uint32_t m0 = 0, m1 = 0;
-    bool have_mask = false;
-    {
-      AesRk rk;
-      load_rk(row->aes_rk, rk);
-#pragma unroll
-      for (int k = 0; k < 44; ++k) pin(rk.w[k]);
-      pin(nb[0]); pin(nb[1]); pin(nb[2]);
-      stg.issue();
-      // CTR cache while the packets land in LDS (counters of every active packet < 256)
-      const bool cached = !wave_any(c.act && nblk > 255u);
-      AesCtrCache cc{};
-      if (cached) cc = ctr_cache(rk, rb, nb);
-      auto first_iter = [&]() {  // before any packet byte is touched
-        stg.complete();
-        MQ_STAMP(c.tile, 2);
-        const bool rec = c.act && is_record(d);
-        if (wave_any(rec)) {  // TLS record: header (AAD) and inner content type before any use
-          if (rec && j == 0) write_record_header(sp, pkt, d);
-          wave_sync();
-        }
-      };
-      auto use_block = [&](uint32_t b, const uint32_t (&ks)[4]) {
-        if (c.act && b < nblk) {
-          if (b == 0) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) ej0[k] = ks[k];
-          } else {
-            xor_block(sp, pay, b, P, ks);
-          }
-        }
-      };
-      uint32_t it = 0;
-      while (it < Imax) {
-        const uint32_t b = (uint32_t)j + kLanesPerPkt * it;
-        const bool is_hp = hp_on && !hp_post && it == hp_it && (uint32_t)j == hp_lane;
-        const bool hp_next = hp_on && !hp_post && it + 1 == hp_it && (uint32_t)j == hp_lane;
-        // iterations it and it + 1 together unless either carries an HP block (its sample is
-        // ciphertext of iteration 0, and its lane needs the HP key)
-        if (it + 1 < Imax && !wave_any(is_hp || hp_next)) {
-          uint32_t ks[4], ks2[4];
-          if (cached) ctr_block2c(rk, rb, cc, b, ks, ks2);
-          else ctr_block2(rk, rb, nb, b, ks, ks2);
-          if (it == 0) first_iter();
-          use_block(b, ks);
-          use_block(b + kLanesPerPkt, ks2);
-          wave_sync();
-          it += 2;
-          continue;
-        }
-        uint32_t ks[4];
-        if (wave_any(is_hp)) {  // iteration carrying HP blocks: per-lane key/input
-          AesRk hk;
-          load_rk(row->hp_rk, hk);
-          uint32_t smp[4];
-          load_words<4>(sp, pkt + (c.act ? d.pn_offset + 4u : 0u), smp);
-#pragma unroll
-          for (int k = 0; k < 44; ++k) hk.w[k] = is_hp ? hk.w[k] : rk.w[k];
-          uint32_t s0 = nb[0], s1 = nb[1], s2 = nb[2], s3 = b == 0 ? 1u : b + 1;
-          if (is_hp) { s0 = bswap32(smp[0]); s1 = bswap32(smp[1]); s2 = bswap32(smp[2]); s3 = bswap32(smp[3]); }
-          aes128_block(hk, rb, s0, s1, s2, s3);
-          ks[0] = bswap32(s0); ks[1] = bswap32(s1); ks[2] = bswap32(s2); ks[3] = bswap32(s3);
-          if (is_hp) { m0 = ks[0]; m1 = s1 >> 24; have_mask = true; }
-        } else if (cached) {
-          ctr_blockc(rk, rb, cc, b, ks);
-        } else {
-          ctr_block(rk, rb, nb, b, ks);
-        }
-        if (it == 0) first_iter();
-        if (!is_hp) use_block(b, ks);
-        wave_sync();  // this iteration's ciphertext (the HP sample) is visible to the next
-        it += 1;
-      }
-      if (Imax == 0) stg.complete();
-    }
-    MQ_STAMP(c.tile, 3);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) ej0[k] = oct_bcast0(ej0[k]);
-    uint32_t y[4], tag[4];
-    ghash<TAB>(sp, pkt, pay, aad_len, P, row, j, c.act, y);
-    tag_words(y, ej0, tag);
-    if (c.act && j == 0) store_words<4>(sp, pay + P, tag);
-    wave_sync();
-    MQ_STAMP(c.tile, 4);
-    if (wave_any(hp_post)) {
-      uint32_t t0, t1;
-      hp_mask(sp, pkt + (c.act ? d.pn_offset + 4u : 0u), row, rb, t0, t1);
-      if (hp_post && j == 0) { m0 = t0; m1 = t1; have_mask = true; }
-    }
-    if (have_mask) apply_hp(sp, pkt, d, m0, m1);
-    MQ_STAMP(c.tile, 5);
-  }
-
-  template <class S, class G>
-  static __device__ __forceinline__ void open(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j,
-                              bool direct, G& stg) {
-    const mq_pkt_desc& d = c.d;
-    stg.issue();
-    const TwLane rb = tw_lane();
-    uint32_t pn_len = d.pn_len, trunc = 0;
-    uint8_t orig_b0 = 0, b0 = 0;
-    uint32_t orig_pn = 0;
-    const bool hp = c.act && !(d.flags & MQ_PKT_NO_HP);
-    // header (recv.rs:363-395): from the pre-pass values when present (wave-uniform), so that
-    // in the single-key kernels the nonce and the first CTR block are computed while the packet
-    // is still landing in LDS
-    if (c.pre_hp) {
-      if (hp) b0 = header_from_prepass(c, pn_len, trunc);
+// The streaming tile of one wave. TAB: H^8 multiplies through the LDS table (single-key kernels,
+// or a multi-key wave whose packets all use the hot row).
+template <bool SINGLE, bool TAB>
+struct AesStream {
+  // AES of slot b (b >= 0) from the CTR cache or full rounds; keystream as little-endian words
+  template <bool CACHED, class K>
+  static __device__ __forceinline__ void ctr(const K& key, const TwLane& L, const AesPkt& k,
+                                             const AesCtrCache& cc, uint32_t b, uint32_t (&ks)[4]) {
+    const uint32_t cnt = b == 0 ? 1u : b + 1;
+    uint32_t s[4];
+    if (CACHED) {
+      aes128_ctr1(key, L, cc, cnt, s);
     } else {
-      stg.complete();
-      if (hp) {
-        uint32_t m0, m1;
-        hp_mask(sp, pkt + d.pn_offset + 4, row, rb, m0, m1);
-        b0 = header_from_mask(sp, pkt, c, m0, m1, pn_len, trunc);
-      }
+      s[0] = k.nb[0]; s[1] = k.nb[1]; s[2] = k.nb[2]; s[3] = cnt;
+      aes128_enc(key, L, s);
     }
-    const uint32_t aad_len = c.act ? (uint32_t)d.pn_offset + pn_len : 0u;
-    const uint32_t P = c.act ? d.len - aad_len - 16 : 0u;
-    const typename S::off_t pay = pkt + aad_len;
-    uint32_t nb[3];
-    nonce_be(row, c.pn, nb);
-    const uint32_t nblk = 1 + (P + 15) / 16;
-    const uint32_t C = (nblk + kLanesPerPkt - 1) / kLanesPerPkt;
-    const uint32_t Cmax = wave_max_u32(c.act ? C : 0u);
-    AesRk rk;
-    uint32_t ks0[4];  // block j: E(J0) on lane 0, keystream elsewhere
-    const bool cached = !wave_any(c.act && nblk > 255u);
-    AesCtrCache cc{};
-    if (TAB) {  // round keys in SGPRs: cheap to keep across the GHASH
-      load_rk(row->aes_rk, rk);
-      if (cached) {
-        cc = ctr_cache(rk, rb, nb);
-        ctr_blockc(rk, rb, cc, (uint32_t)j, ks0);
-      } else {
-        ctr_block(rk, rb, nb, (uint32_t)j, ks0);
-      }
-    }
-    if (c.pre_hp) stg.complete();
-    MQ_STAMP(c.tile, 2);
-    const bool hdr_written = hp && write_unmasked_header(sp, pkt, c, j, b0, pn_len, trunc, orig_b0, orig_pn);
-    wave_sync();
-    uint32_t y[4];
-    MQ_STAMP(c.tile, 3);
-    ghash<TAB>(sp, pkt, pay, aad_len, P, row, j, c.act, y);
-    MQ_STAMP(c.tile, 4);
-    if (!TAB) {
-      load_rk(row->aes_rk, rk);
-      if (cached) {
-        cc = ctr_cache(rk, rb, nb);
-        ctr_blockc(rk, rb, cc, (uint32_t)j, ks0);
-      } else {
-        ctr_block(rk, rb, nb, (uint32_t)j, ks0);
-      }
-    }
-    uint32_t ej0[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) ej0[k] = oct_bcast0(ks0[k]);
-    uint32_t tag[4], got[4];
-    tag_words(y, ej0, tag);
-    load_words<4>(sp, pay + P, got);
-    const uint32_t diff = (tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) | (tag[3] ^ got[3]);
-    if (c.act && diff != 0) {
+    for (int q = 0; q < 4; ++q) ks[q] = bswap32(s[q]);
+  }
+
+  // Horner step acc = (acc ^ x) * H^8 for a lane holding GHASH block x; the lane's last block is
+  // only added (its multiplier H^e comes in finish)
+  static __device__ __forceinline__ void gh_step(uint32_t (&acc)[4], const GfOp& m8, bool has, bool last,
+                                                 const uint32_t (&x)[4]) {
+#pragma unroll
+    for (int w = 0; w < 4; ++w) acc[w] ^= has ? x[w] : 0u;
+#if MQ_PROF_SKIP & 2
+    for (int w = 0; w < 4; ++w) acc[w] += m8.y[0][w & 3];
+    return;
+#endif
+    uint32_t t[4] = {acc[0], acc[1], acc[2], acc[3]};
+    if (TAB) gh_mul_tab(t);
+    else gf_mul(t, m8);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) acc[w] = (has && !last) ? t[w] : acc[w];
+  }
+
+  // tag = GHASH (final multiply by H^e, octet XOR) ^ E_K(J0) (lane 0's, broadcast)
+  static __device__ __forceinline__ void finish(uint32_t (&acc)[4], const KeyRow* row, int j, const AesPkt& k,
+                                                const uint32_t (&ej0)[4], uint32_t (&tag)[4]) {
+    uint32_t hp[4];
+    uint32_t e1 = (k.nblk + 8u - (uint32_t)j) & 7u;  // H^(e1 + 1): blocks after the lane's last
+    pin(e1);  // keeps the H^e load and its preparation (36 VGPRs) after the tile loop
+#pragma unroll
+    for (int w = 0; w < 4; ++w) hp[w] = brev(row->H[e1][w]);
+    const GfOp ml = gf_prepare(hp);
+    gf_mul(acc, ml);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) tag[w] = bswap32(brev(oct_xor(acc[w]))) ^ oct_bcast0(ej0[w]);
+  }
+
+  static __device__ __forceinline__ GfOp prep_m8(const KeyRow* row) {
+    GfOp m8;
+    if (!TAB) {
+      uint32_t h[4];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) h[w] = brev(row->H[7][w]);
+      m8 = gf_prepare(h);
+    }
+    return m8;
+  }
+
+  // send composite (transmit.rs:625-755): seal, then header protection from the sample
+  // send composite, AEAD part (transmit.rs:625-755): the header protection from the sample runs
+  // afterwards in mq_aes_seal_hp_kernel, so GHASH reads the unprotected header as the reference's
+  // seal does. key: the AEAD key source (SGPRs in single-key kernels, LDS otherwise).
+  // CACHED: every counter of the wave's packets < 256 (aes128_ctr1).
+  template <bool CACHED, class K>
+  static __device__ void seal(uint8_t* __restrict__ arena, PktCtx& c, const KeyRow* row, int j, const K& key) {
+    const mq_pkt_desc& d = c.d;
+    const TwLane L = tw_lane();
+    AesPkt k;
+    k.act = c.act;
+    k.rec = k.act && is_record(d);
+    k.aad_len = k.act ? (uint32_t)d.pn_offset + d.pn_len : 0u;
+    k.P = k.act ? d.len - k.aad_len - 16 : 0u;
+    k.pkt = k.act ? d.offset : 0;
+    k.pay = k.pkt + k.aad_len;
+    k.A = (k.aad_len + 15) >> 4;
+    k.nblk = 1 + ((k.P + 15) >> 4);
+    const int it_lo = -(int)wave_max_u32(k.act ? (k.A + 6) / 8 : 0u);
+    const int it_hi = (int)wave_max_u32(k.act ? k.nblk / 8 + 1 : 0u);
+    nonce_be(row, c.pn, k.nb);
+    AesCtrCache cc{};
+    if (CACHED) cc = ctr_cache(key, L, k.nb);
+    const GfOp m8 = prep_m8(row);
+    // TLS record (seal_record, record.rs:88-113): header = ApplicationData, 0x0303, len - 5 (the
+    // AAD, built in registers), the inner content type at payload byte P - 1 (patched into the
+    // plaintext before encryption)
+    const uint32_t rlen = d.len - 5u;
+    if (k.rec && j == 0) {
+      uint8_t* h = arena + k.pkt;
+      h[0] = 23; h[1] = 3; h[2] = 3; h[3] = (uint8_t)(rlen >> 8); h[4] = (uint8_t)rlen;
+    }
+    auto data = [&](int b) -> uint4 {
+      if (k.act && b >= 1 && (uint32_t)b < k.nblk) return ld16(arena + k.pay + 16ull * (uint32_t)(b - 1));
+      if (k.act && !k.rec && b <= 0 && b >= 1 - (int)k.A)
+        return ld16(arena + k.pkt + 16ull * (uint32_t)((int)k.A + b - 1));
+      return make_uint4(0, 0, 0, 0);
+    };
+    uint32_t acc[4] = {0, 0, 0, 0}, ej0[4] = {0, 0, 0, 0};
+    uint4 cur = data(j + kLanesPerPkt * it_lo);
+#pragma nounroll
+    for (int it = it_lo; it < it_hi; ++it) {
+      const int b = j + kLanesPerPkt * it;
+      const uint32_t ub = (uint32_t)b;
+      const uint4 nxt = data(b + kLanesPerPkt);  // next iteration's block, in flight during this one
+      uint32_t ks[4] = {0, 0, 0, 0};
+      if (it >= 0) ctr<CACHED>(key, L, k, cc, ub, ks);  // wave-uniform: slots >= 0 run AES
+      uint32_t x[4] = {0, 0, 0, 0};
+      bool has = false;
+      if (k.act && b >= 1 && ub < k.nblk) {  // payload block b - 1
+        uint32_t pt[4], ct[4];
+        u4w(cur, pt);
+        const uint32_t off = 16u * (ub - 1), rem = min(16u, k.P - off);
+        if (k.rec && k.P - 1 - off < 16u) {  // inner content type
+          const uint32_t at = k.P - 1 - off, sh = 8u * (at & 3);
+          pt[at >> 2] = (pt[at >> 2] & ~(0xffu << sh)) | ((d.reserved & 0xffu) << sh);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ct[q] = pt[q] ^ ks[q];
+        st_block(arena + k.pay + off, ct, rem);
+        gh_block(ct, rem, x);
+        has = true;
+      } else if (k.act && b <= 0 && b >= 1 - (int)k.A) {  // AAD block A + b - 1
+        uint32_t m[4];
+        u4w(cur, m);
+        if (k.rec) { m[0] = 23u | 3u << 8 | 3u << 16 | (rlen >> 8 & 0xffu) << 24; m[1] = rlen & 0xffu; }
+        gh_block(m, k.aad_len - 16u * (uint32_t)((int)k.A + b - 1), x);
+        has = true;
+      } else if (k.act && ub == k.nblk) {  // length block
+        len_block(k.aad_len, k.P, x);
+        has = true;
+      }
+      if (b == 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ej0[q] = ks[q];
+      }
+      gh_step(acc, m8, has, ub + kLanesPerPkt > k.nblk, x);
+      cur = nxt;
+    }
+    uint32_t tag[4];
+    finish(acc, row, j, k, ej0, tag);
+    if (k.act && j == 0) st16(arena + k.pay + k.P, tag);
+  }
+
+  // receive composite (recv.rs:340-421 / 953-1025): HP removal, decode_pn, open. Plaintext is
+  // stored as it is produced; a packet whose tag then fails gets its ciphertext back (the same
+  // keystream XORed again) and its header untouched, as the reference leaves a failed packet.
+  template <bool CACHED, class K>
+  static __device__ void open(uint8_t* __restrict__ arena, PktCtx& c, const KeyRow* row, int j, const K& key,
+                              const uint32_t* kl) {
+    const mq_pkt_desc& d = c.d;
+    const TwLane L = tw_lane();
+    AesPkt k;
+    k.hp = c.act && !(d.flags & MQ_PKT_NO_HP);
+    uint32_t pn_len = d.pn_len, trunc = 0;
+    uint8_t b0 = 0;
+    // recv.rs:363-395 / :968-997: mask, unmask byte 0, pn_len, unmask PN, decode_pn — from the
+    // pre-pass values (batch path) or computed here (one AES block per lane)
+    if (c.pre_hp) {
+      if (k.hp) b0 = header_from_prepass(c, pn_len, trunc);
+    } else if (wave_any(k.hp)) {
+      uint32_t smp[4] = {0, 0, 0, 0};
+      if (k.hp) u4w(ld16(arena + d.offset + d.pn_offset + 4), smp);
+      uint32_t t[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) t[q] = bswap32(smp[q]);
+      aes128_enc(RkLds{kl + 44}, L, t);
+      const uint32_t m0 = bswap32(t[0]), m1 = t[1] >> 24;
+      if (k.hp) {
+        GlobalSpace sp{arena, d.offset + d.len};
+        b0 = header_from_mask(sp, d.offset, c, m0, m1, pn_len, trunc);
+      }
+    }
+    k.act = c.act;  // PN > 2^62 - 1 fails the packet here
+    k.rec = k.act && is_record(d);
+    k.aad_len = k.act ? (uint32_t)d.pn_offset + pn_len : 0u;
+    k.P = k.act ? d.len - k.aad_len - 16 : 0u;
+    k.pkt = k.act ? d.offset : 0;
+    k.pay = k.pkt + k.aad_len;
+    k.A = (k.aad_len + 15) >> 4;
+    k.nblk = 1 + ((k.P + 15) >> 4);
+    const int it_lo = -(int)wave_max_u32(k.act ? (k.A + 6) / 8 : 0u);
+    const int it_hi = (int)wave_max_u32(k.act ? k.nblk / 8 + 1 : 0u);
+    uint32_t got[4] = {0, 0, 0, 0};
+    if (k.act) u4w(ld16(arena + k.pay + k.P), got);
+    nonce_be(row, c.pn, k.nb);
+    AesCtrCache cc{};
+    if (CACHED) cc = ctr_cache(key, L, k.nb);
+    const GfOp m8 = prep_m8(row);
+    auto data = [&](int b) -> uint4 {
+      if (k.act && b >= 1 && (uint32_t)b < k.nblk) return ld16(arena + k.pay + 16ull * (uint32_t)(b - 1));
+      if (k.act && b <= 0 && b >= 1 - (int)k.A) return ld16(arena + k.pkt + 16ull * (uint32_t)((int)k.A + b - 1));
+      return make_uint4(0, 0, 0, 0);
+    };
+    uint32_t acc[4] = {0, 0, 0, 0}, ej0[4] = {0, 0, 0, 0};
+    uint4 cur = data(j + kLanesPerPkt * it_lo);
+#pragma nounroll
+    for (int it = it_lo; it < it_hi; ++it) {
+      const int b = j + kLanesPerPkt * it;
+      const uint32_t ub = (uint32_t)b;
+      const uint4 nxt = data(b + kLanesPerPkt);
+      uint32_t ks[4] = {0, 0, 0, 0};
+      if (it >= 0) ctr<CACHED>(key, L, k, cc, ub, ks);
+      uint32_t x[4] = {0, 0, 0, 0};
+      bool has = false;
+      if (k.act && b >= 1 && ub < k.nblk) {  // ciphertext block b - 1
+        uint32_t m[4], pt[4];
+        u4w(cur, m);
+        const uint32_t off = 16u * (ub - 1), rem = min(16u, k.P - off);
+        gh_block(m, rem, x);
+        has = true;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pt[q] = m[q] ^ ks[q];
+        st_block(arena + k.pay + off, pt, rem);
+      } else if (k.act && b <= 0 && b >= 1 - (int)k.A) {  // AAD block: the unprotected header
+        uint32_t m[4];
+        u4w(cur, m);
+        const uint32_t at = 16u * (uint32_t)((int)k.A + b - 1);
+        if (k.hp) patch_header(m, at, b0, d.pn_offset, pn_len, trunc);
+        gh_block(m, k.aad_len - at, x);
+        has = true;
+      } else if (k.act && ub == k.nblk) {
+        len_block(k.aad_len, k.P, x);
+        has = true;
+      }
+      if (b == 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ej0[q] = ks[q];
+      }
+      gh_step(acc, m8, has, ub + kLanesPerPkt > k.nblk, x);
+      cur = nxt;
+    }
+    uint32_t tag[4];
+    finish(acc, row, j, k, ej0, tag);
+    const bool bad = k.act && ((tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) | (tag[3] ^ got[3])) != 0;
+    if (bad) {  // Error::Crypto (rustcrypto.rs:60-94)
       c.st = MQ_ERR_CRYPTO;
       c.act = false;
     }
-    wave_sync();
-    MQ_STAMP(c.tile, 5);
-    if (c.act && j >= 1 && (uint32_t)j < nblk) xor_block(sp, pay, (uint32_t)j, P, ks0);
-    uint32_t it = 1;
-    for (; it + 1 < Cmax; it += 2) {  // two iterations per pass (interleaved AES rounds)
-      const uint32_t b = (uint32_t)j + kLanesPerPkt * it;
-      uint32_t ks[4], ks2[4];
-      if (cached) ctr_block2c(rk, rb, cc, b, ks, ks2);
-      else ctr_block2(rk, rb, nb, b, ks, ks2);
-      if (c.act && b < nblk) xor_block(sp, pay, b, P, ks);
-      if (c.act && b + kLanesPerPkt < nblk) xor_block(sp, pay, b + kLanesPerPkt, P, ks2);
+    if (wave_any(bad)) {  // restore the ciphertext of failed packets
+#pragma nounroll
+      for (int it = 0; it < it_hi; ++it) {
+        const uint32_t b = (uint32_t)j + kLanesPerPkt * (uint32_t)it;
+        uint32_t ks[4];
+        ctr<CACHED>(key, L, k, cc, b, ks);
+        if (bad && b >= 1 && b < k.nblk) {
+          const uint32_t off = 16u * (b - 1), rem = min(16u, k.P - off);
+          uint32_t m[4];
+          u4w(ld16(arena + k.pay + off), m);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) m[q] ^= ks[q];
+          st_block(arena + k.pay + off, m, rem);
+        }
+      }
     }
-    if (it < Cmax) {
-      const uint32_t b = (uint32_t)j + kLanesPerPkt * it;
-      uint32_t ks[4];
-      if (cached) ctr_blockc(rk, rb, cc, b, ks);
-      else ctr_block(rk, rb, nb, b, ks);
-      if (c.act && b < nblk) xor_block(sp, pay, b, P, ks);
-    }
-    if (direct && hdr_written && !c.act) {
-      sp.st8(pkt, orig_b0);
-      for (uint32_t b = 0; b < pn_len; ++b) sp.st8(pkt + d.pn_offset + b, (uint8_t)(orig_pn >> (8 * b)));
+    if (c.act && k.hp && j == 0) {  // the unprotected header of an opened packet
+      uint8_t* h = arena + k.pkt;
+      h[0] = b0;
+      for (uint32_t q = 0; q < pn_len; ++q) h[d.pn_offset + q] = (uint8_t)(trunc >> (8 * (pn_len - 1 - q)));
     }
   }
 };
@@ -422,14 +374,20 @@ struct AesPolicyT {
 
 using namespace mq;
 
-// Tile kernels: persistent workgroups of kAesWaves waves share the LDS tables (built once per
-// workgroup); wave w walks tiles blockIdx.x * kAesWaves + w + k * gridDim.x * kAesWaves. The "1"
-// variants run when the key table has a single row: round keys and H powers in SGPRs, and the
-// GHASH table of that row's H^8.
+// Tile kernels: persistent workgroups of kAesStreamWaves waves share the LDS tables (built once
+// per workgroup); wave w walks tiles blockIdx.x * kAesStreamWaves + w + k * gridDim.x *
+// kAesStreamWaves. The "1" variants run when the key table has a single row: round keys in SGPRs
+// and the GHASH table of that row's H^8.
+constexpr int kAesStreamWaves = 16;
+// key schedules in LDS: multi-key kernels, per wave and packet (copied per tile); single-key
+// kernels, row 0's in slot 0 (copied once per workgroup)
+__shared__ __attribute__((aligned(16))) uint32_t g_aes_keys[kAesStreamWaves * kPktsPerTile * kRkSlotBytes / 4];
+
 template <bool SINGLE>
 __device__ __forceinline__ void aes_tables(const KeyRow* __restrict__ kt, uint32_t n_rows,
                                            const uint32_t* __restrict__ hot) {
   build_tw(threadIdx.x, blockDim.x);
+  if (SINGLE && threadIdx.x < kRkSlotBytes / 4) g_aes_keys[threadIdx.x] = kt[0].aes_rk[threadIdx.x];  // aes_rk || hp_rk
   // multi-key kernels: a GHASH table for the hot row when the partition found one (`hot` points
   // at its index in the workspace; an out-of-range index means none)
   const uint32_t r = SINGLE ? 0u : (hot ? *hot : 0xFFFFFFFFu);
@@ -445,29 +403,81 @@ __device__ __forceinline__ void aes_tables(const KeyRow* __restrict__ kt, uint32
   }
 }
 
+template <bool SINGLE, bool OPEN, bool TAB, bool CACHED, class K>
+__device__ __forceinline__ void aes_run(uint8_t* __restrict__ arena, PktCtx& c, const KeyRow* row, int j, const K& key,
+                                        const uint32_t* kl) {
+  if (OPEN) AesStream<SINGLE, TAB>::template open<CACHED>(arena, c, row, j, key, kl);
+  else AesStream<SINGLE, TAB>::template seal<CACHED>(arena, c, row, j, key);
+}
+
+template <bool SINGLE, bool OPEN>
+__device__ __forceinline__ void aes_stream_tiles(const KeyRow* __restrict__ kt, uint32_t n_rows,
+                                                 uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                 const mq_pkt_desc* __restrict__ desc, uint32_t n,
+                                                 const uint32_t* __restrict__ index,
+                                                 const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status,
+                                                 uint64_t* __restrict__ pn_out, const uint2* __restrict__ hpm) {
+  const uint32_t w = threadIdx.x >> 6;
+  const int j = (int)(threadIdx.x & (kLanesPerPkt - 1));
+  for_tiles<OPEN>(blockIdx.x * kAesStreamWaves + w, gridDim.x * kAesStreamWaves, desc, n, index, n_dev, hpm,
+                  [&](uint32_t t, const TilePrefetch& pf) {
+    PktCtx c;
+    const KeyRow* row;
+    if (!tile_ctx<MQ_SUITE_AES128GCM, OPEN, SINGLE>(t, kt, n_rows, arena_len, desc, n, index, n_dev, hpm, pf, c,
+                                                    row))
+      return;
+    MQ_STAMP(t, 0);
+    // this packet's key schedules into the wave's LDS slots (multi-key: lane j copies words
+    // 11j .. 11j + 10 of aes_rk || hp_rk, contiguous in the row)
+    const uint32_t p = (threadIdx.x & (kWave - 1)) / kLanesPerPkt;
+    uint32_t* kl = SINGLE ? g_aes_keys : g_aes_keys + (w * kPktsPerTile + p) * (kRkSlotBytes / 4);
+    if (!SINGLE) {
+      const uint32_t* src = row->aes_rk + 11 * j;
+      uint32_t v[11];
+#pragma unroll
+      for (int q = 0; q < 11; ++q) v[q] = src[q];
+#pragma unroll
+      for (int q = 0; q < 11; ++q) kl[11 * j + q] = v[q];
+      wave_sync();
+    }
+    // the H^8 table serves a wave whose active packets all use its row; others multiply by
+    // the bit-holed product (two instantiations: a wave holds one method's registers). CTR
+    // caching needs every counter < 256: packets of at most 4080 bytes.
+    const bool tab = SINGLE || (g_aes_hot_row != nullptr && !wave_any(c.act && row != g_aes_hot_row));
+    const bool cached = !wave_any(c.act && c.d.len > 4080u);
+    if (SINGLE) {
+      AesRk rk;
+      load_rk(kt[0].aes_rk, rk);  // wave-uniform: SGPRs
+      if (cached) aes_run<SINGLE, OPEN, true, true>(arena, c, row, j, RkRegs{rk}, kl);
+      else aes_run<SINGLE, OPEN, true, false>(arena, c, row, j, RkRegs{rk}, kl);
+    } else if (tab) {
+      if (cached) aes_run<SINGLE, OPEN, true, true>(arena, c, row, j, RkLds{kl}, kl);
+      else aes_run<SINGLE, OPEN, true, false>(arena, c, row, j, RkLds{kl}, kl);
+    } else {
+      if (cached) aes_run<SINGLE, OPEN, false, true>(arena, c, row, j, RkLds{kl}, kl);
+      else aes_run<SINGLE, OPEN, false, false>(arena, c, row, j, RkLds{kl}, kl);
+    }
+    MQ_STAMP(t, 7);
+    tile_status<OPEN>(c, j, status, pn_out);
+  });
+}
+
 #define MQ_AES_KERNELS(NAME_SEAL, NAME_OPEN, SINGLE)                                                      \
-  extern "C" __global__ __launch_bounds__(64 * kAesWaves) void NAME_SEAL(                                 \
+  extern "C" __global__ __launch_bounds__(64 * kAesStreamWaves) void NAME_SEAL(                           \
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
       const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, const uint32_t* __restrict__ hot) { \
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];                                        \
     aes_tables<SINGLE>(kt, n_rows, hot);                                                                  \
-    const uint32_t w = threadIdx.x >> 6;                                                                  \
-    run_tiles<AesPolicyT<SINGLE>, false, SINGLE>(smem + w * kLdsBytes, blockIdx.x * kAesWaves + w,        \
-                                                 gridDim.x * kAesWaves, kt, n_rows, arena, arena_len, desc,\
-                                                 n, index, n_dev, status, nullptr, nullptr);              \
+    aes_stream_tiles<SINGLE, false>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr,  \
+                                    nullptr);                                                             \
   }                                                                                                       \
-  extern "C" __global__ __launch_bounds__(64 * kAesWaves) void NAME_OPEN(                                 \
+  extern "C" __global__ __launch_bounds__(64 * kAesStreamWaves) void NAME_OPEN(                           \
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
       const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,    \
       const uint2* __restrict__ hpm, const uint32_t* __restrict__ hot) {                                  \
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];                                        \
     aes_tables<SINGLE>(kt, n_rows, hot);                                                                  \
-    const uint32_t w = threadIdx.x >> 6;                                                                  \
-    run_tiles<AesPolicyT<SINGLE>, true, SINGLE>(smem + w * kLdsBytes, blockIdx.x * kAesWaves + w,         \
-                                                gridDim.x * kAesWaves, kt, n_rows, arena, arena_len, desc, \
-                                                n, index, n_dev, status, pn_out, hpm);                    \
+    aes_stream_tiles<SINGLE, true>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm); \
   }
 MQ_AES_KERNELS(mq_aes_seal_kernel, mq_aes_open_kernel, false)
 MQ_AES_KERNELS(mq_aes_seal1_kernel, mq_aes_open1_kernel, true)
@@ -482,8 +492,9 @@ extern "C" __global__ __launch_bounds__(256) void mq_aes_hp_kernel(
   const uint32_t kid = key_ids[i];
   if (kid >= n_rows || kt[kid].suite != MQ_SUITE_AES128GCM) return;
   GlobalSpace sp{const_cast<uint8_t*>(samples), (uint64_t)n * 16};
-  uint32_t m0, m1;
-  AesPolicyT<false>::hp_mask(sp, (uint64_t)i * 16, kt + kid, (threadIdx.x & (kTReplicas - 1)) * 4, m0, m1);
+  uint32_t smp[4], m0, m1;
+  load_words<4>(sp, (uint64_t)i * 16, smp);
+  aes_hp_mask_words(smp, kt + kid, (uint32_t)(threadIdx.x & (kTReplicas - 1)) * 4, m0, m1);
   for (int b = 0; b < 4; ++b) masks[5 * (size_t)i + b] = (uint8_t)(m0 >> (8 * b));
   masks[5 * (size_t)i + 4] = (uint8_t)m1;
 }
@@ -513,12 +524,41 @@ __global__ __launch_bounds__(256) void mq_aes_open_hp_kernel(
     load_words<5>(sp, at - 4, w);
     const uint8_t b0 = arena[d.offset];
     const uint32_t smp[4] = {w[1], w[2], w[3], w[4]};
-    AesPolicyT<false>::hp_mask_words(smp, row, rb, m0, m1);
+    aes_hp_mask_words(smp, row, rb, m0, m1);
     hpm[i] = prepass_decode_words(b0, w[0], d, m0, m1);
   } else {
-    AesPolicyT<false>::hp_mask(sp, at, row, rb, m0, m1);
+    uint32_t smp[4];
+    load_words<4>(sp, at, smp);
+    aes_hp_mask_words(smp, row, rb, m0, m1);
     hpm[i] = make_uint2(m0, m1);
   }
+}
+
+// Seal post-pass: header protection of every packet the tile kernel sealed (transmit.rs:713-719
+// with AesHeaderProtection::mask, rustcrypto.rs:175-186), one packet per lane: sample = the 16
+// bytes at pn_offset + 4 (ciphertext, reaching into the tag for tiny payloads), mask applied to
+// byte 0 (low 4 / 5 bits) and the PN bytes (RFC 9001 §5.4.1).
+__global__ __launch_bounds__(256) void mq_aes_seal_hp_kernel(
+    const KeyRow* __restrict__ kt, uint8_t* __restrict__ arena, uint64_t arena_len,
+    const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,
+    const uint32_t* __restrict__ n_dev, const uint8_t* __restrict__ status) {
+  build_t0(threadIdx.x, blockDim.x);
+  __syncthreads();
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t count = n_dev ? *n_dev : n;
+  if (t >= count) return;
+  const uint32_t i = index ? index[t] : t;
+  if (i == kListHole || status[i] != MQ_OK) return;
+  const mq_pkt_desc d = desc[i];
+  if (d.flags & (MQ_PKT_NO_HP | MQ_PKT_TLS_RECORD)) return;
+  GlobalSpace sp{arena, arena_len};
+  uint32_t smp[4], m0, m1;
+  load_words<4>(sp, d.offset + d.pn_offset + 4, smp);
+  aes_hp_mask_words(smp, kt + d.key_id, (uint32_t)(threadIdx.x & (kTReplicas - 1)) * 4, m0, m1);
+  uint8_t* h = arena + d.offset;
+  h[0] ^= (uint8_t)m0 & ((d.flags & MQ_PKT_LONG_HEADER) ? 0x0f : 0x1f);
+  const uint32_t mk = (m0 >> 8) | (m1 << 24);
+  for (uint32_t b = 0; b < d.pn_len; ++b) h[d.pn_offset + b] ^= (uint8_t)(mk >> (8 * b));
 }
 
 // Persistent grid: one workgroup per CU (152 KiB of LDS each), capped by the tile count.
@@ -534,7 +574,7 @@ static uint32_t aes_grid(uint32_t tiles) {
     const char* e = getenv("MQ_AES_WGS_PER_CU");
     per_cu = e ? max(atoi(e), 0) : 1;
   }
-  const uint32_t wgs = (tiles + kAesWaves - 1) / kAesWaves;
+  const uint32_t wgs = (tiles + kAesStreamWaves - 1) / kAesStreamWaves;
   if (per_cu == 0) return wgs;
   return wgs < (uint32_t)(cus * per_cu) ? wgs : (uint32_t)(cus * per_cu);
 }
@@ -545,19 +585,23 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
   const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
   if (tiles == 0) return hipSuccess;
   const uint32_t blocks = aes_grid(tiles);
-  const size_t dyn = (size_t)kLdsBytes * kAesWaves;
   if (open && hpm) {
     hipLaunchKernelGGL(mq_aes_open_hp_kernel<true>, dim3((n + 255) / 256), dim3(256), 0, s, kt, n_rows, arena,
                        arena_len, desc, n, index, n_dev, hpm);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  if (open)
-    hipLaunchKernelGGL(n_rows == 1 ? mq_aes_open1_kernel : mq_aes_open_kernel, dim3(blocks), dim3(64 * kAesWaves),
-                       dyn, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm, hot);
-  else
-    hipLaunchKernelGGL(n_rows == 1 ? mq_aes_seal1_kernel : mq_aes_seal_kernel, dim3(blocks), dim3(64 * kAesWaves),
-                       dyn, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, hot);
+  if (open) {
+    hipLaunchKernelGGL(n_rows == 1 ? mq_aes_open1_kernel : mq_aes_open_kernel, dim3(blocks), dim3(64 * kAesStreamWaves),
+                       0, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm, hot);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(n_rows == 1 ? mq_aes_seal1_kernel : mq_aes_seal_kernel, dim3(blocks), dim3(64 * kAesStreamWaves),
+                     0, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, hot);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(mq_aes_seal_hp_kernel, dim3((n + 255) / 256), dim3(256), 0, s, kt, arena, arena_len, desc, n,
+                     index, n_dev, status);
   return hipGetLastError();
 }
 

@@ -326,26 +326,22 @@ __device__ __forceinline__ uint32_t oct_lane(uint32_t x) {  // lane K of the oct
   return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x18 | (K << 5));
 }
 
-template <class Policy, bool OPEN, bool SINGLE_KEY = false>
-__device__ __forceinline__ void run_tile(uint8_t* smem, uint32_t tile_id, const KeyRow* __restrict__ kt,
-                                         uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
-                                         const mq_pkt_desc* __restrict__ desc, uint32_t n,
-                                         const uint32_t* __restrict__ index,
-                                         const uint32_t* __restrict__ n_dev,
-                                         uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,
-                                         const uint2* __restrict__ hpm,
-                                         TilePrefetch pf = TilePrefetch{false, 0u, 0u}) {
-  const int lane = threadIdx.x & (kWave - 1), p = lane / kLanesPerPkt, j = lane % kLanesPerPkt;
+// Per-lane packet context of tile `tile_id` (descriptor from the prefetch or from memory, HP
+// pre-pass values, validation). Returns false when the tile lies past the batch (wave-uniform).
+template <uint32_t SUITE, bool OPEN, bool SINGLE_KEY>
+__device__ __forceinline__ bool tile_ctx(uint32_t tile_id, const KeyRow* __restrict__ kt, uint32_t n_rows,
+                                         uint64_t arena_len, const mq_pkt_desc* __restrict__ desc, uint32_t n,
+                                         const uint32_t* __restrict__ index, const uint32_t* __restrict__ n_dev,
+                                         const uint2* __restrict__ hpm, const TilePrefetch& pf, PktCtx& c,
+                                         const KeyRow*& row) {
+  const int lane = threadIdx.x & (kWave - 1), p = lane / kLanesPerPkt;
   const uint32_t count = n_dev ? *n_dev : n;
   const uint32_t tile0 = tile_id * kPktsPerTile;
-  if (tile0 >= count) return;  // wave-uniform
-  MQ_STAMP(tile_id, 0);
-  PktCtx c;
+  if (tile0 >= count) return false;  // wave-uniform
   c.tile = tile_id;
   const uint32_t t = tile0 + p;
   c.valid = t < count;
   c.pre_hp = OPEN && hpm != nullptr;
-  c.otk = (uint32_t*)(smem + kLdsBytes - kScratchBytes + 32u * (uint32_t)p);
   c.hm0 = c.hm1 = 0;
   if (pf.on) {  // flat batch, words already in registers
     c.i = t;
@@ -373,10 +369,40 @@ __device__ __forceinline__ void run_tile(uint8_t* smem, uint32_t tile_id, const 
       c.hm1 = m.y;
     }
   }
-  c.st = c.valid ? validate<Policy::kSuite, OPEN, SINGLE_KEY>(c.d, kt, n_rows, arena_len) : (int)MQ_ERR_INVALID_ARG;
+  c.st = c.valid ? validate<SUITE, OPEN, SINGLE_KEY>(c.d, kt, n_rows, arena_len) : (int)MQ_ERR_INVALID_ARG;
   c.act = c.valid && c.st == MQ_OK;
   c.pn = c.d.pn;
-  const KeyRow* row = SINGLE_KEY ? kt : kt + (c.act ? c.d.key_id : 0u);
+  row = SINGLE_KEY ? kt : kt + (c.act ? c.d.key_id : 0u);
+  return true;
+}
+
+// Status (and, for open, the decoded PN) of the tile's packets: octet lane 0.
+template <bool OPEN>
+__device__ __forceinline__ void tile_status(const PktCtx& c, int j, uint8_t* __restrict__ status,
+                                            uint64_t* __restrict__ pn_out) {
+  if (c.valid && j == 0) {
+    status[c.i] = (uint8_t)c.st;
+    if (OPEN && pn_out && c.st == MQ_OK) pn_out[c.i] = c.pn;
+  }
+}
+
+template <class Policy, bool OPEN, bool SINGLE_KEY = false>
+__device__ __forceinline__ void run_tile(uint8_t* smem, uint32_t tile_id, const KeyRow* __restrict__ kt,
+                                         uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
+                                         const mq_pkt_desc* __restrict__ desc, uint32_t n,
+                                         const uint32_t* __restrict__ index,
+                                         const uint32_t* __restrict__ n_dev,
+                                         uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,
+                                         const uint2* __restrict__ hpm,
+                                         TilePrefetch pf = TilePrefetch{false, 0u, 0u}) {
+  const int lane = threadIdx.x & (kWave - 1), p = lane / kLanesPerPkt, j = lane % kLanesPerPkt;
+  PktCtx c;
+  const KeyRow* row;
+  if (!tile_ctx<Policy::kSuite, OPEN, SINGLE_KEY>(tile_id, kt, n_rows, arena_len, desc, n, index, n_dev, hpm, pf,
+                                                  c, row))
+    return;
+  MQ_STAMP(tile_id, 0);
+  c.otk = (uint32_t*)(smem + kLdsBytes - kScratchBytes + 32u * (uint32_t)p);
   const uint64_t off = c.act ? c.d.offset : 0;
   // chunks of the packet image, clamped so sums cannot overflow; a clamped (huge) packet always
   // exceeds the budget and sends the tile down the direct path
@@ -387,7 +413,11 @@ __device__ __forceinline__ void run_tile(uint8_t* smem, uint32_t tile_id, const 
   const uint32_t nch = (uint32_t)(nch64 < 0xFFFFu ? nch64 : 0xFFFFu);
   const uint32_t incl = oct_incl_scan(nch);
   const uint32_t total = lane_u32(incl, kWave - 1);
+#if MQ_PROF_SKIP & 32
+  if ((void)total, false) {  // diagnostic: every tile on the direct path
+#else
   if (total * 16u <= kDataBudget) {
+#endif
     pl.slot = incl - nch;
     DmaStager stg{smem, arena, arena_len, lane, j, pl};
     LdsSpace sp{smem};
@@ -405,27 +435,21 @@ __device__ __forceinline__ void run_tile(uint8_t* smem, uint32_t tile_id, const 
     if (OPEN) Policy::template open<GlobalSpace>(sp, off, c, row, j, true, stg);
     else Policy::template seal<GlobalSpace>(sp, off, c, row, j, stg);
   }
-  if (c.valid && j == 0) {
-    status[c.i] = (uint8_t)c.st;
-    if (OPEN && pn_out && c.st == MQ_OK) pn_out[c.i] = c.pn;
-  }
+  tile_status<OPEN>(c, j, status, pn_out);
 }
 
-// Persistent tile loop: this wave runs tiles first, first + stride, ... For flat batches (no
-// index list) the next tile's descriptor words (and HP masks) are loaded while the current tile
-// is processed, so a tile starts without waiting on a descriptor fetch.
-template <class Policy, bool OPEN, bool SINGLE_KEY = false>
-__device__ __forceinline__ void run_tiles(uint8_t* smem, uint32_t first, uint32_t stride, const KeyRow* __restrict__ kt,
-                                          uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
-                                          const mq_pkt_desc* __restrict__ desc, uint32_t n,
-                                          const uint32_t* __restrict__ index, const uint32_t* __restrict__ n_dev,
-                                          uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,
-                                          const uint2* __restrict__ hpm) {
+// Persistent tile loop: this wave runs tiles first, first + stride, ... calling
+// body(tile, prefetch). For flat batches (no index list) the next tile's descriptor words (and HP
+// masks) are loaded while the current tile is processed, so a tile starts without waiting on a
+// descriptor fetch.
+template <bool OPEN, class F>
+__device__ __forceinline__ void for_tiles(uint32_t first, uint32_t stride, const mq_pkt_desc* __restrict__ desc,
+                                          uint32_t n, const uint32_t* __restrict__ index,
+                                          const uint32_t* __restrict__ n_dev, const uint2* __restrict__ hpm,
+                                          F&& body) {
   const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
   if (index || n_dev) {
-    for (uint32_t t = first; t < tiles; t += stride)
-      run_tile<Policy, OPEN, SINGLE_KEY>(smem, t, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status,
-                                         pn_out, hpm);
+    for (uint32_t t = first; t < tiles; t += stride) body(t, TilePrefetch{false, 0u, 0u});
     return;
   }
   const uint32_t lane = threadIdx.x & (kWave - 1), p = lane / kLanesPerPkt, j = lane % kLanesPerPkt;
@@ -440,8 +464,7 @@ __device__ __forceinline__ void run_tiles(uint8_t* smem, uint32_t first, uint32_
   for (uint32_t t = first; t < tiles; t += stride) {
     const TilePrefetch pf{true, dw, hm};
     fetch(t + stride, dw, hm);
-    run_tile<Policy, OPEN, SINGLE_KEY>(smem, t, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status,
-                                       pn_out, hpm, pf);
+    body(t, pf);
   }
 }
 

@@ -1,9 +1,9 @@
 """Randomised differential tests of the batch API against the oracle (GPU vs CPU restatement).
 
 Each seeded batch mixes everything a descriptor can say at once: short and long QUIC headers
-(pn_offset 1..60, pn_len 1..4), plain AEAD rows (MQ_PKT_NO_HP), TLS records, packets of 21 B to
-2.6 kB (so some exceed the receive composite's 2048-B limit, recv.rs:356-360, with and without
-MQ_PKT_NO_RECV_LIMIT), arbitrary byte alignments and gaps, both suites on several key rows plus
+(pn_offset 1..320: AAD up to 21 GHASH blocks), plain AEAD rows (MQ_PKT_NO_HP), TLS records,
+packets of 21 B to 5.2 kB (past 4080 B the AES counters exceed 255: no CTR cache; past 2048 B the
+receive composite's limit, recv.rs:356-360, with and without MQ_PKT_NO_RECV_LIMIT), arbitrary byte alignments and gaps, both suites on several key rows plus
 out-of-range and empty (suite 0) key ids, PNs near 2^62 (ProtocolViolation on open), lengths too
 short for the sample or the tag, and tampered ciphertexts. The bar is the oracle's: identical
 status for every packet, identical bytes in the whole arena (failed packets untouched, gap bytes
@@ -54,7 +54,8 @@ def random_batch(seed, n):
         if kind[i] == 0:
             pn_off[i] = 1 + int(rng.integers(0, 21))
         elif kind[i] == 1:
-            pn_off[i] = int(rng.integers(7, 61))
+            # long headers; some as long as an Initial with a token (AAD over 144 B)
+            pn_off[i] = int(rng.integers(7, 61)) if rng.random() < 0.9 else int(rng.integers(61, 320))
             flags[i] = _lib.MQ_PKT_LONG_HEADER
         elif kind[i] == 2:
             pn_off[i] = int(rng.integers(0, 40))
@@ -70,11 +71,14 @@ def random_batch(seed, n):
             lens[i] = int(rng.integers(max(1, lo - 8), lo + 4))        # around the minimum
         elif r < 0.12:
             lens[i] = int(rng.integers(2040, 2600))                   # around the receive limit
+        elif r < 0.14:
+            lens[i] = int(rng.integers(4060, 5200))                   # counters past 255 (no CTR cache)
         else:
             lens[i] = int(rng.integers(lo, 1400))
         if kind[i] != 3 and rng.random() < 0.2:
             flags[i] |= _lib.MQ_PKT_NO_RECV_LIMIT
     lens = np.maximum(lens, 1)
+    lens = np.maximum(lens, np.where((kind == 1) & (pn_off > 60), pn_off + pn_len + 40, 0))
     gaps = rng.integers(0, 40, size=n)
     offs = np.zeros(n, dtype=np.int64)
     offs[1:] = np.cumsum(lens[:-1] + gaps[:-1])

@@ -2,7 +2,9 @@
 
 Times seal and open of one workload with the product library and with each variant that skips
 one phase (1 ChaCha rounds, 2 MAC, 4 LDS->HBM store, 8 HBM->LDS staging, 16 AES rounds, 12 both
-copies); the difference is what that phase costs. Diagnostic only: variants compute garbage.
+copies, 32 every tile on the direct path); the difference is what that phase costs.
+MQ_PROF_DIR names the variants' directory (default milli_quic_amd/prof, which gpurun does not ship:
+copy them under tools/ab_libs/ for a GPU run). Diagnostic only: variants compute garbage.
 Usage: python tools/phase_cost.py [b|c|e] [packets]
 """
 import os
@@ -10,7 +12,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-BUILD = os.path.join(ROOT, "milli_quic_amd", "prof")
+BUILD = os.environ.get("MQ_PROF_DIR", os.path.join(ROOT, "milli_quic_amd", "prof"))
 
 
 def child(lib, cfg, n):
@@ -55,7 +57,7 @@ def main():
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
     libs = [("product", os.path.join(ROOT, "milli_quic_amd", "libmq_aead.so"))]
     names = {1: "no chacha rounds", 2: "no MAC", 4: "no store", 8: "no staging", 16: "no AES rounds",
-             12: "no store+staging"}
+             12: "no store+staging", 32: "all direct"}
     for m, nm in names.items():
         p = os.path.join(BUILD, f"prof_{m}.so")
         if os.path.exists(p):
