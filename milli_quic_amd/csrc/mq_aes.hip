@@ -168,12 +168,16 @@ struct AesStream {
   }
 
   // send composite (transmit.rs:625-755): seal, then header protection from the sample
-  // send composite, AEAD part (transmit.rs:625-755): the header protection from the sample runs
-  // afterwards in mq_aes_seal_hp_kernel, so GHASH reads the unprotected header as the reference's
-  // seal does. key: the AEAD key source (SGPRs in single-key kernels, LDS otherwise).
-  // CACHED: every counter of the wave's packets < 256 (aes128_ctr1).
+  // send composite (transmit.rs:625-755): seal, then header protection from the sample. For
+  // packets of at least 7 CTR blocks (nblk >= 8) the HP block runs in slot nblk — a free slot of
+  // the last iteration, after iteration 0 produced the sample — with the HP key through its LDS
+  // pointer; shorter packets get theirs from mq_aes_seal_hp_kernel afterwards (an extra iteration
+  // for them cost more than that pass). key: the AEAD key source (SGPRs in single-key kernels,
+  // LDS otherwise); kl: this packet's LDS key schedules. CACHED: every counter of the wave's
+  // packets < 256 (aes128_ctr1).
   template <bool CACHED, class K>
-  static __device__ void seal(uint8_t* __restrict__ arena, PktCtx& c, const KeyRow* row, int j, const K& key) {
+  static __device__ __forceinline__ void seal(uint8_t* __restrict__ arena, PktCtx& c, const KeyRow* row, int j, const K& key,
+                              const uint32_t* kl) {
     const mq_pkt_desc& d = c.d;
     const TwLane L = tw_lane();
     AesPkt k;
@@ -185,6 +189,8 @@ struct AesStream {
     k.pay = k.pkt + k.aad_len;
     k.A = (k.aad_len + 15) >> 4;
     k.nblk = 1 + ((k.P + 15) >> 4);
+    k.hp = k.act && !(d.flags & MQ_PKT_NO_HP);
+    const bool hp_slot = k.hp && k.nblk >= (uint32_t)kLanesPerPkt;  // else mq_aes_seal_hp_kernel
     const int it_lo = -(int)wave_max_u32(k.act ? (k.A + 6) / 8 : 0u);
     const int it_hi = (int)wave_max_u32(k.act ? k.nblk / 8 + 1 : 0u);
     nonce_be(row, c.pn, k.nb);
@@ -205,7 +211,9 @@ struct AesStream {
         return ld16(arena + k.pkt + 16ull * (uint32_t)((int)k.A + b - 1));
       return make_uint4(0, 0, 0, 0);
     };
-    uint32_t acc[4] = {0, 0, 0, 0}, ej0[4] = {0, 0, 0, 0};
+    uint32_t acc[4] = {0, 0, 0, 0}, ej0[4] = {0, 0, 0, 0}, smp[4] = {0, 0, 0, 0};
+    uint32_t m0 = 0, m1 = 0;
+    bool have_mask = false;
     uint4 cur = data(j + kLanesPerPkt * it_lo);
 #pragma nounroll
     for (int it = it_lo; it < it_hi; ++it) {
@@ -213,11 +221,23 @@ struct AesStream {
       const uint32_t ub = (uint32_t)b;
       const uint4 nxt = data(b + kLanesPerPkt);  // next iteration's block, in flight during this one
       uint32_t ks[4] = {0, 0, 0, 0};
-      if (it >= 0) ctr<CACHED>(key, L, k, cc, ub, ks);  // wave-uniform: slots >= 0 run AES
-      uint32_t x[4] = {0, 0, 0, 0};
+      if (it >= 0) {  // wave-uniform: slots >= 0 run AES
+        const bool is_hp = hp_slot && ub == k.nblk;
+        if (wave_any(is_hp)) {  // full rounds, the HP lanes with the HP key and the sample
+          uint32_t s[4] = {k.nb[0], k.nb[1], k.nb[2], ub + 1};
+          if (is_hp) { s[0] = bswap32(smp[0]); s[1] = bswap32(smp[1]); s[2] = bswap32(smp[2]); s[3] = bswap32(smp[3]); }
+          aes128_enc(RkLds{is_hp ? kl + 44 : kl}, L, s);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) ks[q] = bswap32(s[q]);
+          if (is_hp) { m0 = ks[0]; m1 = s[1] >> 24; have_mask = true; }
+        } else {
+          ctr<CACHED>(key, L, k, cc, ub, ks);
+        }
+      }
+      uint32_t x[4] = {0, 0, 0, 0}, ct[4] = {0, 0, 0, 0};
       bool has = false;
       if (k.act && b >= 1 && ub < k.nblk) {  // payload block b - 1
-        uint32_t pt[4], ct[4];
+        uint32_t pt[4];
         u4w(cur, pt);
         const uint32_t off = 16u * (ub - 1), rem = min(16u, k.P - off);
         if (k.rec && k.P - 1 - off < 16u) {  // inner content type
@@ -243,19 +263,33 @@ struct AesStream {
 #pragma unroll
         for (int q = 0; q < 4; ++q) ej0[q] = ks[q];
       }
-      gh_step(acc, m8, has, ub + kLanesPerPkt > k.nblk, x);
+      if (it == 0) {  // the HP sample: payload bytes [4 - pn_len, 20 - pn_len) from slots 1 and 2
+        uint32_t src[8];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { src[q] = oct_lane<1>(ct[q]); src[4 + q] = oct_lane<2>(ct[q]); }
+        const uint32_t o = 4u - (k.hp ? d.pn_len : 4u);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) smp[q] = __builtin_amdgcn_alignbyte(src[q + 1], src[q], o);
+      }
+      gh_step(acc, m8, has, b + kLanesPerPkt > (int)k.nblk, x);
       cur = nxt;
     }
     uint32_t tag[4];
     finish(acc, row, j, k, ej0, tag);
     if (k.act && j == 0) st16(arena + k.pay + k.P, tag);
+    if (have_mask) {  // after the MAC read the unprotected header (RFC 9001 §5.4.1)
+      uint8_t* h = arena + k.pkt;
+      h[0] ^= (uint8_t)m0 & ((d.flags & MQ_PKT_LONG_HEADER) ? 0x0f : 0x1f);
+      const uint32_t mk = (m0 >> 8) | (m1 << 24);
+      for (uint32_t q = 0; q < d.pn_len; ++q) h[d.pn_offset + q] ^= (uint8_t)(mk >> (8 * q));
+    }
   }
 
   // receive composite (recv.rs:340-421 / 953-1025): HP removal, decode_pn, open. Plaintext is
   // stored as it is produced; a packet whose tag then fails gets its ciphertext back (the same
   // keystream XORed again) and its header untouched, as the reference leaves a failed packet.
   template <bool CACHED, class K>
-  static __device__ void open(uint8_t* __restrict__ arena, PktCtx& c, const KeyRow* row, int j, const K& key,
+  static __device__ __forceinline__ void open(uint8_t* __restrict__ arena, PktCtx& c, const KeyRow* row, int j, const K& key,
                               const uint32_t* kl) {
     const mq_pkt_desc& d = c.d;
     const TwLane L = tw_lane();
@@ -336,7 +370,7 @@ struct AesStream {
 #pragma unroll
         for (int q = 0; q < 4; ++q) ej0[q] = ks[q];
       }
-      gh_step(acc, m8, has, ub + kLanesPerPkt > k.nblk, x);
+      gh_step(acc, m8, has, b + kLanesPerPkt > (int)k.nblk, x);
       cur = nxt;
     }
     uint32_t tag[4];
@@ -407,7 +441,7 @@ template <bool SINGLE, bool OPEN, bool TAB, bool CACHED, class K>
 __device__ __forceinline__ void aes_run(uint8_t* __restrict__ arena, PktCtx& c, const KeyRow* row, int j, const K& key,
                                         const uint32_t* kl) {
   if (OPEN) AesStream<SINGLE, TAB>::template open<CACHED>(arena, c, row, j, key, kl);
-  else AesStream<SINGLE, TAB>::template seal<CACHED>(arena, c, row, j, key);
+  else AesStream<SINGLE, TAB>::template seal<CACHED>(arena, c, row, j, key, kl);
 }
 
 template <bool SINGLE, bool OPEN>
@@ -420,7 +454,7 @@ __device__ __forceinline__ void aes_stream_tiles(const KeyRow* __restrict__ kt, 
   const uint32_t w = threadIdx.x >> 6;
   const int j = (int)(threadIdx.x & (kLanesPerPkt - 1));
   for_tiles<OPEN>(blockIdx.x * kAesStreamWaves + w, gridDim.x * kAesStreamWaves, desc, n, index, n_dev, hpm,
-                  [&](uint32_t t, const TilePrefetch& pf) {
+                  [&](uint32_t t, const TilePrefetch& pf) __attribute__((always_inline)) {
     PktCtx c;
     const KeyRow* row;
     if (!tile_ctx<MQ_SUITE_AES128GCM, OPEN, SINGLE>(t, kt, n_rows, arena_len, desc, n, index, n_dev, hpm, pf, c,
@@ -534,10 +568,11 @@ __global__ __launch_bounds__(256) void mq_aes_open_hp_kernel(
   }
 }
 
-// Seal post-pass: header protection of every packet the tile kernel sealed (transmit.rs:713-719
-// with AesHeaderProtection::mask, rustcrypto.rs:175-186), one packet per lane: sample = the 16
-// bytes at pn_offset + 4 (ciphertext, reaching into the tag for tiny payloads), mask applied to
-// byte 0 (low 4 / 5 bits) and the PN bytes (RFC 9001 §5.4.1).
+// Seal post-pass: header protection of the sealed packets shorter than 7 CTR blocks (their HP
+// block has no free slot in the tile; transmit.rs:713-719 with AesHeaderProtection::mask,
+// rustcrypto.rs:175-186), one packet per lane: sample = the 16 bytes at pn_offset + 4
+// (ciphertext, reaching into the tag for tiny payloads), mask applied to byte 0 (low 4 / 5 bits)
+// and the PN bytes (RFC 9001 §5.4.1).
 __global__ __launch_bounds__(256) void mq_aes_seal_hp_kernel(
     const KeyRow* __restrict__ kt, uint8_t* __restrict__ arena, uint64_t arena_len,
     const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,
@@ -550,7 +585,8 @@ __global__ __launch_bounds__(256) void mq_aes_seal_hp_kernel(
   const uint32_t i = index ? index[t] : t;
   if (i == kListHole || status[i] != MQ_OK) return;
   const mq_pkt_desc d = desc[i];
-  if (d.flags & (MQ_PKT_NO_HP | MQ_PKT_TLS_RECORD)) return;
+  const uint32_t P = d.len - ((uint32_t)d.pn_offset + d.pn_len) - 16, nblk = 1 + ((P + 15) >> 4);
+  if ((d.flags & MQ_PKT_NO_HP) || nblk >= (uint32_t)kLanesPerPkt) return;  // records are NO_HP
   GlobalSpace sp{arena, arena_len};
   uint32_t smp[4], m0, m1;
   load_words<4>(sp, d.offset + d.pn_offset + 4, smp);
