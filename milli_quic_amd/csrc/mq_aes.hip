@@ -33,22 +33,6 @@
 
 namespace mq {
 
-// 16-B packet accesses at any byte alignment (global_load/store_dwordx4; gfx950 runs with
-// unaligned access enabled)
-typedef uint4 __attribute__((aligned(1))) uint4_u;
-__device__ __forceinline__ uint4 ld16(const uint8_t* p) { return *(const uint4_u*)p; }
-__device__ __forceinline__ void st16(uint8_t* p, const uint32_t (&w)[4]) {
-  *(uint4_u*)p = make_uint4(w[0], w[1], w[2], w[3]);
-}
-__device__ __forceinline__ void st_bytes(uint8_t* p, const uint32_t (&w)[4], uint32_t n) {
-  for (uint32_t k = 0; k < n; ++k) p[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
-}
-__device__ __forceinline__ void st_block(uint8_t* p, const uint32_t (&w)[4], uint32_t rem) {
-  if (rem >= 16) st16(p, w);
-  else st_bytes(p, w, rem);
-}
-__device__ __forceinline__ void u4w(uint4 v, uint32_t (&w)[4]) { w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w; }
-
 // DirectionalKeys::nonce (src/crypto/mod.rs:66-74), as big-endian AES input words
 __device__ __forceinline__ void nonce_be(const KeyRow* row, uint64_t pn, uint32_t (&nb)[3]) {
   nb[0] = bswap32(row->iv[0]);
