@@ -67,6 +67,18 @@ __device__ __forceinline__ void gh_block(const uint32_t (&m)[4], uint32_t rem, u
   for (int w = 0; w < 4; ++w) x[w] = refl(m[w] & byte_mask((int)rem, w));
 }
 
+// minimum over the wave of an octet-uniform value
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) { return ~wave_max_u32(~x); }
+
+// End of the iterations in which every active packet's lanes all hold a whole payload block that
+// is not their last GHASH block (slots 8it .. 8it + 7 with 8it + 14 <= full blocks), the range
+// [1, lean_end) that the tile loops run without the edge cases (AAD, length block, partial block,
+// HP slot, last-block multiplier).
+__device__ __forceinline__ int lean_end(bool act, uint32_t P) {
+  const uint32_t F = P >> 4;
+  return (int)wave_min_u32(!act ? 0xFFFFFFFFu : (F >= 14 ? (F - 14) / 8 + 1 : 0u));
+}
+
 // Per-packet, per-lane state of a streaming tile (octet-uniform fields are equal on the 8 lanes)
 struct AesPkt {
   bool act, rec, hp;
@@ -199,11 +211,23 @@ struct AesStream {
     uint32_t m0 = 0, m1 = 0;
     bool have_mask = false;
     uint4 cur = data(j + kLanesPerPkt * it_lo);
+    const int it_lean = lean_end(k.act, k.P);
 #pragma nounroll
     for (int it = it_lo; it < it_hi; ++it) {
       const int b = j + kLanesPerPkt * it;
       const uint32_t ub = (uint32_t)b;
       const uint4 nxt = data(b + kLanesPerPkt);  // next iteration's block, in flight during this one
+      if (it >= 1 && it < it_lean) {  // interior iteration (wave-uniform)
+        uint32_t ks[4], ct[4], x[4];
+        ctr<CACHED>(key, L, k, cc, ub, ks);
+        ct[0] = cur.x ^ ks[0]; ct[1] = cur.y ^ ks[1]; ct[2] = cur.z ^ ks[2]; ct[3] = cur.w ^ ks[3];
+        if (k.act) st16(arena + k.pay + 16ull * (ub - 1), ct);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[q] = refl(ct[q]);
+        gh_step(acc, m8, true, false, x);
+        cur = nxt;
+        continue;
+      }
       uint32_t ks[4] = {0, 0, 0, 0};
       if (it >= 0) {  // wave-uniform: slots >= 0 run AES
         const bool is_hp = hp_slot && ub == k.nblk;
@@ -321,11 +345,22 @@ struct AesStream {
     };
     uint32_t acc[4] = {0, 0, 0, 0}, ej0[4] = {0, 0, 0, 0};
     uint4 cur = data(j + kLanesPerPkt * it_lo);
+    const int it_lean = lean_end(k.act, k.P);
 #pragma nounroll
     for (int it = it_lo; it < it_hi; ++it) {
       const int b = j + kLanesPerPkt * it;
       const uint32_t ub = (uint32_t)b;
       const uint4 nxt = data(b + kLanesPerPkt);
+      if (it >= 1 && it < it_lean) {  // interior iteration (wave-uniform)
+        uint32_t ks[4], pt[4], x[4];
+        ctr<CACHED>(key, L, k, cc, ub, ks);
+        x[0] = refl(cur.x); x[1] = refl(cur.y); x[2] = refl(cur.z); x[3] = refl(cur.w);
+        pt[0] = cur.x ^ ks[0]; pt[1] = cur.y ^ ks[1]; pt[2] = cur.z ^ ks[2]; pt[3] = cur.w ^ ks[3];
+        if (k.act) st16(arena + k.pay + 16ull * (ub - 1), pt);
+        gh_step(acc, m8, true, false, x);
+        cur = nxt;
+        continue;
+      }
       uint32_t ks[4] = {0, 0, 0, 0};
       if (it >= 0) ctr<CACHED>(key, L, k, cc, ub, ks);
       uint32_t x[4] = {0, 0, 0, 0};
@@ -392,11 +427,14 @@ struct AesStream {
 
 using namespace mq;
 
-// Tile kernels: persistent workgroups of kAesStreamWaves waves share the LDS tables (built once
-// per workgroup); wave w walks tiles blockIdx.x * kAesStreamWaves + w + k * gridDim.x *
-// kAesStreamWaves. The "1" variants run when the key table has a single row: round keys in SGPRs
+// Tile kernels: persistent workgroups of aes_waves(SINGLE) waves share the LDS tables (built once
+// per workgroup); wave w walks tiles blockIdx.x * W + w + k * gridDim.x * W. Single-key kernels
+// fit 128 VGPRs (16 waves per CU); the multi-key ones hold more state per packet (LDS key
+// pointers, the bit-holed GHASH operand) and run 12 waves in 168. The "1" variants run when the
+// key table has a single row: round keys in SGPRs
 // and the GHASH table of that row's H^8.
-constexpr int kAesStreamWaves = 16;
+constexpr int kAesStreamWaves = 16;  // the most waves of any variant (LDS key slots)
+constexpr int aes_waves(bool single) { return single ? 16 : 12; }
 // key schedules in LDS: multi-key kernels, per wave and packet (copied per tile); single-key
 // kernels, row 0's in slot 0 (copied once per workgroup)
 __shared__ __attribute__((aligned(16))) uint32_t g_aes_keys[kAesStreamWaves * kPktsPerTile * kRkSlotBytes / 4];
@@ -437,7 +475,8 @@ __device__ __forceinline__ void aes_stream_tiles(const KeyRow* __restrict__ kt, 
                                                  uint64_t* __restrict__ pn_out, const uint2* __restrict__ hpm) {
   const uint32_t w = threadIdx.x >> 6;
   const int j = (int)(threadIdx.x & (kLanesPerPkt - 1));
-  for_tiles<OPEN>(blockIdx.x * kAesStreamWaves + w, gridDim.x * kAesStreamWaves, desc, n, index, n_dev, hpm,
+  constexpr uint32_t W = aes_waves(SINGLE);
+  for_tiles<OPEN>(blockIdx.x * W + w, gridDim.x * W, desc, n, index, n_dev, hpm,
                   [&](uint32_t t, const TilePrefetch& pf) __attribute__((always_inline)) {
     PktCtx c;
     const KeyRow* row;
@@ -481,7 +520,7 @@ __device__ __forceinline__ void aes_stream_tiles(const KeyRow* __restrict__ kt, 
 }
 
 #define MQ_AES_KERNELS(NAME_SEAL, NAME_OPEN, SINGLE)                                                      \
-  extern "C" __global__ __launch_bounds__(64 * kAesStreamWaves) void NAME_SEAL(                           \
+  extern "C" __global__ __launch_bounds__(64 * aes_waves(SINGLE)) void NAME_SEAL(                           \
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
       const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, const uint32_t* __restrict__ hot) { \
@@ -489,7 +528,7 @@ __device__ __forceinline__ void aes_stream_tiles(const KeyRow* __restrict__ kt, 
     aes_stream_tiles<SINGLE, false>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr,  \
                                     nullptr);                                                             \
   }                                                                                                       \
-  extern "C" __global__ __launch_bounds__(64 * kAesStreamWaves) void NAME_OPEN(                           \
+  extern "C" __global__ __launch_bounds__(64 * aes_waves(SINGLE)) void NAME_OPEN(                           \
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
       const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,    \
@@ -582,7 +621,7 @@ __global__ __launch_bounds__(256) void mq_aes_seal_hp_kernel(
 }
 
 // Persistent grid: one workgroup per CU (152 KiB of LDS each), capped by the tile count.
-static uint32_t aes_grid(uint32_t tiles) {
+static uint32_t aes_grid(uint32_t tiles, uint32_t waves) {
   static int cus = 0;
   if (cus == 0) {
     int dev = 0, v = 0;
@@ -594,7 +633,7 @@ static uint32_t aes_grid(uint32_t tiles) {
     const char* e = getenv("MQ_AES_WGS_PER_CU");
     per_cu = e ? max(atoi(e), 0) : 1;
   }
-  const uint32_t wgs = (tiles + kAesStreamWaves - 1) / kAesStreamWaves;
+  const uint32_t wgs = (tiles + waves - 1) / waves;
   if (per_cu == 0) return wgs;
   return wgs < (uint32_t)(cus * per_cu) ? wgs : (uint32_t)(cus * per_cu);
 }
@@ -604,7 +643,7 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
                          uint8_t* status, uint64_t* pn_out, uint2* hpm, hipStream_t s, const uint32_t* hot) {
   const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
   if (tiles == 0) return hipSuccess;
-  const uint32_t blocks = aes_grid(tiles);
+  const uint32_t waves = aes_waves(n_rows == 1), blocks = aes_grid(tiles, waves);
   if (open && hpm) {
     hipLaunchKernelGGL(mq_aes_open_hp_kernel<true>, dim3((n + 255) / 256), dim3(256), 0, s, kt, n_rows, arena,
                        arena_len, desc, n, index, n_dev, hpm);
@@ -612,11 +651,11 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
     if (e != hipSuccess) return e;
   }
   if (open) {
-    hipLaunchKernelGGL(n_rows == 1 ? mq_aes_open1_kernel : mq_aes_open_kernel, dim3(blocks), dim3(64 * kAesStreamWaves),
+    hipLaunchKernelGGL(n_rows == 1 ? mq_aes_open1_kernel : mq_aes_open_kernel, dim3(blocks), dim3(64 * waves),
                        0, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm, hot);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(n_rows == 1 ? mq_aes_seal1_kernel : mq_aes_seal_kernel, dim3(blocks), dim3(64 * kAesStreamWaves),
+  hipLaunchKernelGGL(n_rows == 1 ? mq_aes_seal1_kernel : mq_aes_seal_kernel, dim3(blocks), dim3(64 * waves),
                      0, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, hot);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
