@@ -102,7 +102,26 @@ __device__ __forceinline__ void poly_tag(const S& sp, typename S::off_t pkt, typ
     // need no per-step recomputation
     const uint32_t sel_pay = sel_load((uint32_t)(pay & 3));
     const int ct_full_end = (int)A + (int)(ct_len >> 4);  // first index past the whole CT blocks
+    // lean steps k in [k_lo, k_hi): every active lane absorbs a whole ciphertext block and loads
+    // the next whole one (8j + ... - z in [A, ct_full_end - 8)), so no masks, 2^128 bit selects
+    // or address recomputation
+    const int zA = (int)A + z;
+    const uint32_t k_lo = act ? (uint32_t)((zA + kLanesPerPkt - 1) / kLanesPerPkt) : 0u;
+    const int hi = ct_full_end + z - 2 * kLanesPerPkt + 1;  // lean iff 8k + 15 - z < ct_full_end
+    const uint32_t k_hi = !act ? 0xFFFFFFFFu : (hi <= 0 ? 0u : (uint32_t)((hi + kLanesPerPkt - 1) / kLanesPerPkt));
+    const uint32_t klo = wave_max_u32(k_lo), khi = ~wave_max_u32(~k_hi);
     for (uint32_t k = 0; k + 1 < Kmax; ++k) {
+      if (k >= klo && k < khi) {  // wave-uniform
+        const P26 x = p26_from_words(m[0], m[1], m[2], m[3], 1u);
+#pragma unroll
+        for (int l = 0; l < 5; ++l) acc.l[l] += x.l[l];
+        i += kLanesPerPkt;
+        b.src += 128;
+        b.rem -= 128;
+        load_words_sel<4>(sp, b.src & ~(typename S::off_t)3, sel_pay, m);
+        p26_mul(acc, m8);
+        continue;
+      }
       absorb(b, m);
       const bool steady = !act || (i >= (int)A && i + kLanesPerPkt < ct_full_end);
       i += kLanesPerPkt;
