@@ -67,9 +67,6 @@ __device__ __forceinline__ void gh_block(const uint32_t (&m)[4], uint32_t rem, u
   for (int w = 0; w < 4; ++w) x[w] = refl(m[w] & byte_mask((int)rem, w));
 }
 
-// minimum over the wave of an octet-uniform value
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) { return ~wave_max_u32(~x); }
-
 // End of the iterations in which every active packet's lanes all hold a whole payload block that
 // is not their last GHASH block (slots 8it .. 8it + 7 with 8it + 14 <= full blocks), the range
 // [1, lean_end) that the tile loops run without the edge cases (AAD, length block, partial block,

@@ -161,6 +161,69 @@ __device__ __forceinline__ void apply_hp(const S& sp, typename S::off_t pkt, con
     sp.st8(pkt + d.pn_offset + b, sp.ld8(pkt + d.pn_offset + b) ^ (uint8_t)(mk >> (8 * b)));
 }
 
+// ---- open: keystream pool of a workgroup (kCcOpenWaves waves, one staged tile each) ----------
+// Opening a 1200-B packet takes 20 ChaCha20 blocks (one-time key and 19 keystream; the HP mask
+// comes from the pre-pass), but an octet runs 24 slots in three iterations, so 1/6 of the rounds
+// went idle. Each wave now runs iterations 0 and 1 of its own packets; every later keystream
+// block (slot >= 16) goes to the workgroup's pool, which all its lanes work off together between
+// two barriers once the MACs have read the ciphertext: 4 waves x 8 packets x 4 blocks = 128
+// blocks, two wave-iterations for the four instead of a 4/8-full third one each. (Measured at 2,
+// 4 and 8 waves: 8 in lockstep lose most of the gain to staging waits that no longer overlap. For
+// seal the HP block fills the idle slot for free; a pool would have to move HP to a post-pass,
+// which costs more than the pool saves.)
+#ifndef MQ_CC_OPEN_WAVES
+#define MQ_CC_OPEN_WAVES 4
+#endif
+constexpr int kCcOpenWaves = MQ_CC_OPEN_WAVES;
+constexpr uint32_t kCcPoolSlot = 2 * kLanesPerPkt;  // first pooled slot (iterations 0 and 1 are the wave's)
+
+// this packet's 32-B pool record in its wave's scratch: [0] pooled blocks, [1] payload LDS
+// offset (workgroup) | P << 17, [3] key row, [4..6] nonce words
+struct CcPool {
+  bool on;              // wave-uniform: staged tile whose slots >= 16 go to the pool
+  uint8_t* wg;          // the workgroup's LDS
+  uint32_t base;        // this wave's region in it
+  uint32_t* rec;        // this packet's record
+  const KeyRow* kt;
+};
+
+template <bool SINGLE>
+__device__ __forceinline__ void cc_pool_run(const CcPool& pool) {
+  constexpr uint32_t kQ = kPktsPerTile * kCcOpenWaves;  // packets of the workgroup
+  static_assert(kQ <= kWave, "one packet per lane in the pool scan");
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint32_t w = threadIdx.x >> 6;
+  auto rec = [&](uint32_t q) -> const uint32_t* {
+    return (const uint32_t*)(pool.wg + (q >> 3) * kLdsBytes + kDataBudget + 32u * (q & 7));
+  };
+  const uint32_t nq = (uint32_t)lane < kQ ? rec((uint32_t)lane)[0] : 0u;  // lane q: packet q
+  const uint32_t incl = wave_incl_scan(nq), excl = incl - nq;
+  const uint32_t T = lane_u32(incl, kWave - 1);
+  const LdsSpace sp{pool.wg};
+  for (uint32_t e0 = kWave * w; e0 < T; e0 += kWave * kCcOpenWaves) {  // wave-uniform
+    const uint32_t e = e0 + (uint32_t)lane;
+    uint32_t q = 0;  // the packet of entry e: the last q with excl[q] <= e
+#pragma unroll
+    for (uint32_t step = kQ / 2; step >= 1; step >>= 1) {
+      const uint32_t v = (uint32_t)__shfl((int)excl, (int)(q + step), kWave);
+      if (v <= e) q += step;
+    }
+    const uint32_t eq = (uint32_t)__shfl((int)excl, (int)q, kWave);
+    const bool act = e < T;
+    const uint32_t* r = rec(q);
+    const uint32_t r1 = r[1], pay = r1 & 0x1ffffu, P = r1 >> 17;
+    const uint32_t cb = kCcPoolSlot + (e - eq), o = 64u * (cb - 1);
+    const KeyRow* row = SINGLE || !act ? pool.kt : pool.kt + r[3];  // an idle lane's record may be stale
+    uint32_t key[8];
+    load_key8(row->key, key);
+    uint32_t raw[17];
+    load_raw<16>(sp, act ? pay + o : 0u, raw);  // in flight during the rounds
+    uint32_t ks[16];
+    chacha20_block(key, cb, r[4], r[5], r[6], ks);
+    if (act) xor_words<16>(sp, pay + o, ks, (int)min(64u, P - o), raw);
+  }
+}
+
 struct ChaChaPolicy {
   static constexpr uint32_t kSuite = MQ_SUITE_CHACHA20;
 
@@ -288,9 +351,9 @@ struct ChaChaPolicy {
   }
 
   // receive composite (recv.rs:340-421 / 953-1025): HP removal, decode_pn, open.
-  template <class S, class G>
+  template <bool SINGLE, class S, class G>
   static __device__ __forceinline__ void open(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j,
-                              bool direct, G& stg) {
+                              bool direct, G& stg, const CcPool& pool) {
     const mq_pkt_desc& d = c.d;
     stg.issue();
     uint32_t pn_len = d.pn_len, trunc = 0;
@@ -345,7 +408,8 @@ struct ChaChaPolicy {
       load_block(sp, pay, ctr0, w);
       store_block(sp, pay, ctr0, P, ks0, w);
     }
-    for (uint32_t it = 1; it < Cmax; ++it) {
+    const uint32_t Cown = pool.on ? min(Cmax, 2u) : Cmax;  // later slots: the workgroup's pool
+    for (uint32_t it = 1; it < Cown; ++it) {
       const uint32_t ctr = (uint32_t)j + kLanesPerPkt * it;
       const bool a = c.act && ctr < nblk;
       uint32_t w[17];
@@ -354,6 +418,18 @@ struct ChaChaPolicy {
       chacha20_block(key, ctr, n0, n1, n2, ks);
       if (a) store_block(sp, pay, ctr, P, ks, w);
     }
+    if (j == 0) {  // pool record: only verified packets are decrypted
+      const uint32_t np = pool.on && c.act && nblk > kCcPoolSlot ? nblk - kCcPoolSlot : 0u;
+      pool.rec[0] = np;
+      if (np) {
+        pool.rec[1] = (pool.base + (uint32_t)pay) | P << 17;
+        pool.rec[3] = d.key_id;
+        pool.rec[4] = n0; pool.rec[5] = n1; pool.rec[6] = n2;
+      }
+    }
+    __syncthreads();  // every wave's MAC has read its ciphertext
+    cc_pool_run<SINGLE>(pool);
+    __syncthreads();
     MQ_STAMP(c.tile, 5);
     if (direct && hdr_written && !c.act) {  // direct path writes HBM in place: undo the unmask
       sp.st8(pkt, orig_b0);
@@ -366,28 +442,85 @@ struct ChaChaPolicy {
 
 using namespace mq;
 
-// Tile kernels: one wave per workgroup, one tile per wave. (A persistent grid of 16 waves per CU
-// walking tiles with prefetched descriptors, as the AES kernels use, measured 10 % slower here:
-// identical waves stay in phase, so their staging waits line up; 2x oversubscribed, 4 % slower.)
-// The "1" variants are launched when the key table has a single row (every
-// valid packet on row 0): key material then lives in SGPRs.
+// Tile kernels: one tile per wave, each with its private 10 KiB LDS image. Seal runs one wave per
+// workgroup (its HP block fills an otherwise idle slot, so a pool would gain nothing); open runs
+// kCcOpenWaves-wave workgroups sharing the keystream pool above between two barriers. Every wave
+// of an open workgroup runs both barriers: waves past the batch with an empty record,
+// direct-path tiles (images over the budget) with nothing pooled. (A persistent grid walking
+// tiles, as the AES kernels use, measured 10 % slower here: identical waves stay in phase, so
+// their staging waits line up.) The "1" variants are launched when the key table has a single
+// row (every valid packet on row 0): key material then lives in SGPRs.
+template <bool OPEN, bool SINGLE>
+__device__ __forceinline__ void chacha_tile(const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena,
+                                            uint64_t arena_len, const mq_pkt_desc* __restrict__ desc, uint32_t n,
+                                            const uint32_t* __restrict__ index, const uint32_t* __restrict__ n_dev,
+                                            uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,
+                                            const uint2* __restrict__ hpm) {
+  constexpr uint32_t W = OPEN ? kCcOpenWaves : 1;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t w = W > 1 ? threadIdx.x >> 6 : 0u;
+  uint8_t* wsm = smem + w * kLdsBytes;
+  const int lane = threadIdx.x & (kWave - 1), p = lane / kLanesPerPkt, j = lane % kLanesPerPkt;
+  const uint32_t tile_id = blockIdx.x * W + w;
+  PktCtx c;
+  const KeyRow* row;
+  CcPool pool{false, smem, w * kLdsBytes, (uint32_t*)(wsm + kDataBudget + 32u * (uint32_t)p), kt};
+  if (!tile_ctx<MQ_SUITE_CHACHA20, OPEN, SINGLE>(tile_id, kt, n_rows, arena_len, desc, n, index, n_dev, hpm,
+                                                 TilePrefetch{false, 0u, 0u}, c, row)) {
+    // past the batch (list capacities exceed the count): a whole workgroup leaves at once, a
+    // wave of a live open workgroup only joins its barriers and pool
+    if (W == 1 || blockIdx.x * W * kPktsPerTile >= (n_dev ? *n_dev : n)) return;  // workgroup-uniform
+    if (j == 0) pool.rec[0] = 0;
+    __syncthreads();
+    cc_pool_run<SINGLE>(pool);
+    __syncthreads();
+    return;
+  }
+  MQ_STAMP(tile_id, 0);
+  c.otk = (uint32_t*)(wsm + kLdsBytes - 32u * kPktsPerTile + 32u * (uint32_t)p);
+  const uint64_t off = c.act ? c.d.offset : 0;
+  Placement pl;
+  pl.off = off;
+  pl.len = c.act ? c.d.len : 0u;
+  const uint64_t nch64 = c.act ? ((off & 15) + (uint64_t)c.d.len + 15) >> 4 : 0u;
+  const uint32_t nch = (uint32_t)(nch64 < 0xFFFFu ? nch64 : 0xFFFFu);
+  const uint32_t incl = oct_incl_scan(nch);
+  const uint32_t total = lane_u32(incl, kWave - 1);
+  if (total * 16u <= kDataBudget) {
+    pl.slot = incl - nch;
+    pool.on = W > 1;
+    DmaStager stg{wsm, arena, arena_len, lane, j, pl};
+    LdsSpace sp{wsm};
+    MQ_STAMP(tile_id, 1);
+    const uint32_t pkt = pl.slot * 16u + pl.head();
+    if (OPEN) ChaChaPolicy::template open<SINGLE, LdsSpace>(sp, pkt, c, row, j, false, stg, pool);
+    else ChaChaPolicy::template seal<LdsSpace>(sp, pkt, c, row, j, stg);
+    MQ_STAMP(tile_id, 6);
+    wave_sync();
+    stage_out(wsm, arena, lane, c.act, pl);
+    MQ_STAMP(tile_id, 7);
+  } else {
+    GlobalSpace sp{arena, arena_len};
+    NoStager stg;
+    if (OPEN) ChaChaPolicy::template open<SINGLE, GlobalSpace>(sp, off, c, row, j, true, stg, pool);
+    else ChaChaPolicy::template seal<GlobalSpace>(sp, off, c, row, j, stg);
+  }
+  tile_status<OPEN>(c, j, status, pn_out);
+}
+
 #define MQ_CHACHA_KERNELS(NAME_SEAL, NAME_OPEN, SINGLE)                                                   \
-  extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void NAME_SEAL(     \
+  extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void NAME_SEAL(    \
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
       const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status) {                                 \
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];                                        \
-    run_tile<ChaChaPolicy, false, SINGLE>(smem, blockIdx.x, kt, n_rows, arena, arena_len, desc, n, index, \
-                                          n_dev, status, nullptr, nullptr);                               \
+    chacha_tile<false, SINGLE>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr, nullptr); \
   }                                                                                                       \
-  extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void NAME_OPEN(     \
+  extern "C" __global__ __launch_bounds__(64 * kCcOpenWaves) __attribute__((amdgpu_waves_per_eu(4))) void NAME_OPEN( \
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
       const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,    \
       const uint2* __restrict__ hpm) {                                                                    \
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];                                        \
-    run_tile<ChaChaPolicy, true, SINGLE>(smem, blockIdx.x, kt, n_rows, arena, arena_len, desc, n, index,  \
-                                         n_dev, status, pn_out, hpm);                                     \
+    chacha_tile<true, SINGLE>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm); \
   }
 MQ_CHACHA_KERNELS(mq_chacha_seal_kernel, mq_chacha_open_kernel, false)
 MQ_CHACHA_KERNELS(mq_chacha_seal1_kernel, mq_chacha_open1_kernel, true)
@@ -457,11 +590,12 @@ hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_
     if (e != hipSuccess) return e;
   }
   if (open)
-    hipLaunchKernelGGL(n_rows == 1 ? mq_chacha_open1_kernel : mq_chacha_open_kernel, dim3(tiles), dim3(kWave),
-                       kLdsBytes, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm);
+    hipLaunchKernelGGL(n_rows == 1 ? mq_chacha_open1_kernel : mq_chacha_open_kernel,
+                       dim3((tiles + kCcOpenWaves - 1) / kCcOpenWaves), dim3(kWave * kCcOpenWaves), kLdsBytes * kCcOpenWaves, s, kt,
+                       n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm);
   else
-    hipLaunchKernelGGL(n_rows == 1 ? mq_chacha_seal1_kernel : mq_chacha_seal_kernel, dim3(tiles), dim3(kWave),
-                       kLdsBytes, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status);
+    hipLaunchKernelGGL(n_rows == 1 ? mq_chacha_seal1_kernel : mq_chacha_seal_kernel, dim3(tiles), dim3(kWave), kLdsBytes,
+                       s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status);
   return hipGetLastError();
 }
 

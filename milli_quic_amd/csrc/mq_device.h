@@ -25,7 +25,6 @@ constexpr int kPktsPerTile = 8;
 constexpr int kLanesPerPkt = kWave / kPktsPerTile;  // 8: one octet of lanes per packet
 constexpr uint32_t kLdsBytes = 10240;                // LDS per tile (wave) -> 16 waves/CU
 constexpr uint32_t kCuLdsBytes = 160 * 1024;         // LDS per CU (gfx950)
-constexpr uint32_t kSlack = 64;                      // over-read room after the last slot
 
 // Device key-table row (576 B). Filled on the host by mq_keytable_create (mq_host.cpp).
 struct alignas(16) KeyRow {
@@ -302,6 +301,18 @@ __device__ __forceinline__ uint32_t oct_incl_scan(uint32_t x) {
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);   // row_shr:8
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast15
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast31
+  return x;
+}
+// minimum over the wave of an octet-uniform value
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) { return ~wave_max_u32(~x); }
+// inclusive prefix sum over the 64 lanes of a wave (DPP row shifts + row broadcasts)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
   return x;
 }
 __device__ __forceinline__ bool wave_any(bool b) { return __builtin_amdgcn_ballot_w64(b) != 0; }

@@ -127,17 +127,6 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_count_kernel(
   if (threadIdx.x < kClasses) hist[(size_t)threadIdx.x * nblocks + blockIdx.x] = s_cnt[threadIdx.x];
 }
 
-// inclusive prefix sum over the 64 lanes of a wave (DPP row shifts + row broadcasts)
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
-  return x;
-}
-
 // Single workgroup: per class, the exclusive scan of its per-block counts (in place: the rank of
 // the block's first packet inside the class); then the class segments (whole tiles) are laid out
 // list by list (groups 0 and 1: list 0, group 2: list 1 at `cap`): seg[c] = first list entry of

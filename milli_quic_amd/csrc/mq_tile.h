@@ -13,8 +13,10 @@
 
 namespace mq {
 
-constexpr uint32_t kScratchBytes = 32 * kPktsPerTile;              // per-packet 32-B scratch (MAC key)
-constexpr uint32_t kDataBudget = kLdsBytes - kScratchBytes - kSlack;  // bytes of packet images
+// per-wave scratch after the image: per packet a 32-B ChaCha pool record (mq_chacha.hip) and the
+// 32-B one-time MAC key. No slack: reads past the last packet's image land in the scratch.
+constexpr uint32_t kScratchBytes = 64 * kPktsPerTile;
+constexpr uint32_t kDataBudget = kLdsBytes - kScratchBytes;  // bytes of packet images (9728: 8 x 1216)
 constexpr uint64_t kMaxPn = (1ull << 62) - 1;         // varint::MAX_VARINT
 constexpr uint32_t kListHole = 0xFFFFFFFFu;            // index-list entry without a packet (mq_partition.hip)
 
