@@ -7,8 +7,8 @@
 // c0, counts[1] = c1, cap = mq_partition_list_cap(n). Inside each suite list the packets are
 // grouped by 64-B length class, longest class first (the tail of the grid then runs the short
 // tiles); inside a class the order is the descriptor order per wave of 64 descriptors. Every class
-// starts on a tile boundary, and a long class puts only as many packets in a tile as fit the
-// LDS image at its longest length; the rest of the tile's entries are holes (kListHole), which
+// starts on a tile boundary, and a long ChaCha class puts only as many packets in a tile as fit
+// the LDS image at its longest length; the rest of the tile's entries are holes (kListHole), which
 // the tile kernels skip. Packets are independent and processed in place, so
 // the order changes nothing but the tile composition: a tile runs as long as its longest packet,
 // and a uniformly mixed 64-1350-B batch otherwise pays for 8 x its maximum in nearly every tile.
@@ -65,12 +65,13 @@ __device__ __forceinline__ uint2 block_vote(uint2 v) {  // 256 threads
   return s_v[0];
 }
 
-// Packets per tile of a class: as many as fit the LDS image budget at the class's longest
-// length and worst alignment (4b + 5 chunks), so the class's tiles stay on the staged path;
-// classes that would need fewer than kMinPpt per tile (and the open-ended last one) keep 8 and
-// take the direct path.
+// Packets per tile of a class: AES tiles stream from HBM (no LDS image), so always 8. ChaCha
+// tiles take as many as fit the LDS image budget at the class's longest length and worst
+// alignment (4b + 5 chunks), so the class's tiles stay on the staged path; classes that would
+// need fewer than kMinPpt per tile (and the open-ended last one) keep 8 and take the direct path.
 constexpr uint32_t kMinPpt = 5;
 __device__ __forceinline__ uint32_t class_ppt(uint32_t c) {
+  if (c < 2 * kLenClasses) return kPktsPerTile;  // groups 0 and 1: AES
   const uint32_t b = kLenClasses - 1 - (c % kLenClasses);
   if (b == kLenClasses - 1) return kPktsPerTile;
   const uint32_t x = kBudgetChunks / (4 * b + 5);
