@@ -271,7 +271,10 @@ int mq_batch_derive_initial(mq_keytable* kt, uint32_t first_row, const uint8_t* 
  * at most 2^30 packets per mixed batch, else MQ_ERR_INVALID_ARG).
  * `workspace` is optional for single-suite batches; given to mq_batch_open it also enables the
  * header-protection pre-pass (one lane per packet computes the mask, so the packet kernel spends
- * no keystream slot on it) — same results, faster. Workspace contents need not be initialised.
+ * no keystream slot on it), and given with an AES batch over a key table of several rows it
+ * routes the batch through the same partition, which also groups AES packets by key (tiles of
+ * one key run their GHASH through a table) — same results, faster. Workspace contents need not
+ * be initialised.
  * `stream` is a hipStream_t (NULL = default stream). Returns MQ_OK once the work is enqueued. */
 size_t mq_batch_workspace_size(uint32_t n);
 int mq_batch_seal(const mq_keytable* kt, uint8_t* arena, uint64_t arena_len,

@@ -193,9 +193,9 @@ __device__ __forceinline__ void gf_mul(uint32_t (&a)[4], const GfOp& b) {
 constexpr uint32_t kGhBytes = 8192, kTwBytes = 65536;
 constexpr uint32_t kRkSlotBytes = 2 * 176;  // aes_rk || hp_rk
 __shared__ __attribute__((aligned(16))) uint32_t g_aes_lds[(kGhBytes + kTwBytes) / 4];
-// multi-key tile kernels: the key row whose H^8 the GHASH table holds (the batch's most frequent
-// AES key, found by the mixed-batch partition), or nullptr when the table is not built
-__shared__ const KeyRow* g_aes_hot_row;
+// multi-key tile kernels: per wave, the GHASH half table (gh_mul_half) of its tile's key
+constexpr uint32_t kGhHalfBytes = 4096, kAesMultiWaves = 12;
+__shared__ __attribute__((aligned(16))) uint32_t g_aes_wtab[kAesMultiWaves * kGhHalfBytes / 4];
 
 __device__ __forceinline__ uint32_t xtime8(uint32_t s) { return ((s << 1) ^ ((s & 0x80) ? 0x11bu : 0u)) & 0xffu; }
 
@@ -407,13 +407,13 @@ __device__ __forceinline__ uint32_t byte_of(uint32_t x, int m) {
 // groups in flight: group g's addresses take a fake dependency (empty asm) on the accumulator
 // after group g - 2, because the scheduler would otherwise issue all 32 at once (128 VGPRs) and
 // the 4-waves/SIMD streaming kernels would spill.
-__device__ __forceinline__ void gh_group(const uint32_t (&a)[4], int g, uint4 (&e)[4], const uint32_t* dep) {
+__device__ __forceinline__ void gh_group(const uint32_t (&a)[4], int g, uint4 (&e)[4], const uint32_t* dep,
+                                         const uint8_t* t) {
   const int w = g >> 1, mb = 2 * (g & 1);
   const uint32_t lo = (a[w] << 4) & 0xf0f0f0f0u, hi = a[w] & 0xf0f0f0f0u;
   uint32_t ad[4] = {byte_of(lo, mb), byte_of(hi, mb), byte_of(lo, mb + 1), byte_of(hi, mb + 1)};
   if (dep)
     asm volatile("" : "+v"(ad[0]), "+v"(ad[1]), "+v"(ad[2]), "+v"(ad[3]) : "v"(dep[0]), "v"(dep[1]), "v"(dep[2]), "v"(dep[3]));
-  const uint8_t* t = (const uint8_t*)g_aes_lds + 256u * (8 * w + 2 * mb);
   e[0] = *(const uint4*)(t + ad[0]);
   e[1] = *(const uint4*)(t + 256 + ad[1]);
   e[2] = *(const uint4*)(t + 512 + ad[2]);
@@ -425,21 +425,87 @@ __device__ __forceinline__ void gh_fold(uint32_t (&r)[4], const uint4 (&e)[4]) {
   r[0] = xor3(r[0], e[2].x, e[3].x); r[1] = xor3(r[1], e[2].y, e[3].y);
   r[2] = xor3(r[2], e[2].z, e[3].z); r[3] = xor3(r[3], e[2].w, e[3].w);
 }
+__device__ __forceinline__ const uint8_t* gh_row_full(int g) {  // table row of group g's first nibble
+  return (const uint8_t*)g_aes_lds + 256u * (8 * (g >> 1) + 4 * (g & 1));
+}
 __device__ __forceinline__ void gh_mul_tab(uint32_t (&a)[4]) {
   uint32_t r[4] = {0, 0, 0, 0};
   uint4 e0[4], e1[4];
-  gh_group(a, 0, e0, nullptr);
-  gh_group(a, 1, e1, nullptr);
+  gh_group(a, 0, e0, nullptr, gh_row_full(0));
+  gh_group(a, 1, e1, nullptr, gh_row_full(1));
 #pragma unroll
   for (int g = 2; g < 8; g += 2) {
     gh_fold(r, e0);
-    gh_group(a, g, e0, r);
+    gh_group(a, g, e0, r, gh_row_full(g));
     gh_fold(r, e1);
-    gh_group(a, g + 1, e1, r);
+    gh_group(a, g + 1, e1, r, gh_row_full(g + 1));
   }
   gh_fold(r, e0);
   gh_fold(r, e1);
   a[0] = r[0]; a[1] = r[1]; a[2] = r[2]; a[3] = r[3];
+}
+
+// ---- per-wave GHASH half table (multi-key kernels, waves whose packets share one key) -----------
+// Entry (p, v) of the wave's 4 KiB, p = 0..15, v = 0..15, at byte 256 p + 16 v: (v x^(4p)) * H^8 —
+// the low 16 nibble positions of the full table. a * H^8 = T(a_hi) x^64 + T(a_lo): the high
+// half's nibbles read the same entries and one fold (x^64 mod the GCM polynomial) shifts their
+// sum up before the low half's entries are added. 12 such tables fit beside the T-table where 12
+// full ones would not. Built by the wave without branches or LDS reads: lane l takes position
+// l / 4 and the four values whose top two bits are l % 4 — basis x^(4p+b) H for b = 0..3 (one
+// multiply by x^(4p), then three by x), the top-bit part by selects, the four entries by XOR.
+__device__ __forceinline__ void gf_mul_x(uint32_t (&a)[4]) {  // a * x
+  const uint32_t c = a[3] >> 31;
+  a[3] = __builtin_amdgcn_alignbit(a[3], a[2], 31);
+  a[2] = __builtin_amdgcn_alignbit(a[2], a[1], 31);
+  a[1] = __builtin_amdgcn_alignbit(a[1], a[0], 31);
+  a[0] = (a[0] << 1) ^ (c ? 0x87u : 0u);
+}
+__device__ __forceinline__ void build_gh_half(uint8_t* tab, const uint32_t (&h)[4], int lane) {
+  const uint32_t p = (uint32_t)lane >> 2, vh = (uint32_t)lane & 3u;
+  uint32_t b0[4], b1[4], b2[4], b3[4];
+  gf_mul_xi(h, 4u * p, b0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) b1[q] = b0[q];
+  gf_mul_x(b1);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) b2[q] = b1[q];
+  gf_mul_x(b2);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) b3[q] = b2[q];
+  gf_mul_x(b3);
+  uint32_t hi[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) hi[q] = ((vh & 1u) ? b2[q] : 0u) ^ ((vh & 2u) ? b3[q] : 0u);
+  uint4* e = (uint4*)(tab + 256u * p + 64u * vh);  // entries (p, 4 vh .. 4 vh + 3)
+  e[0] = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+  e[1] = make_uint4(hi[0] ^ b0[0], hi[1] ^ b0[1], hi[2] ^ b0[2], hi[3] ^ b0[3]);
+  e[2] = make_uint4(hi[0] ^ b1[0], hi[1] ^ b1[1], hi[2] ^ b1[2], hi[3] ^ b1[3]);
+  e[3] = make_uint4(hi[0] ^ b0[0] ^ b1[0], hi[1] ^ b0[1] ^ b1[1], hi[2] ^ b0[2] ^ b1[2], hi[3] ^ b0[3] ^ b1[3]);
+  wave_sync();
+}
+__device__ __forceinline__ void gh_mul_half(uint32_t (&a)[4], const uint8_t* tab) {
+  auto row = [tab](int g) { return tab + 256u * (8 * ((g >> 1) & 1) + 4 * (g & 1)); };
+  uint32_t r[4] = {0, 0, 0, 0};
+  uint4 e0[4], e1[4];
+  gh_group(a, 4, e0, nullptr, row(4));  // words 2, 3 first: T(a_hi)
+  gh_group(a, 5, e1, nullptr, row(5));
+  gh_fold(r, e0);
+  gh_group(a, 6, e0, r, row(6));
+  gh_fold(r, e1);
+  gh_group(a, 7, e1, r, row(7));
+  gh_fold(r, e0);
+  gh_group(a, 0, e0, r, row(0));  // words 0, 1 in flight during the x^64 fold
+  gh_fold(r, e1);
+  gh_group(a, 1, e1, r, row(1));
+  uint32_t s[4];
+  gf_fold(0u, 0u, r[0], r[1], r[2], r[3], 0u, 0u, s);  // T(a_hi) * x^64
+  gh_fold(s, e0);
+  gh_group(a, 2, e0, s, row(2));
+  gh_fold(s, e1);
+  gh_group(a, 3, e1, s, row(3));
+  gh_fold(s, e0);
+  gh_fold(s, e1);
+  a[0] = s[0]; a[1] = s[1]; a[2] = s[2]; a[3] = s[3];
 }
 
 }  // namespace mq

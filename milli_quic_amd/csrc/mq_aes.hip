@@ -8,10 +8,11 @@
 //   * AES-128 rounds use the wide T-table (T0 and T2, 32 replicas each, 64 KiB per workgroup,
 //     mq_aes.h): one v_perm_b32 per lookup address, conflict-free ds_read_b32, one rotation per
 //     round column; round keys in SGPRs (single-key kernels) or VGPRs;
-//   * GHASH: every Horner step's multiply by H^8 is 32 reads of an LDS table of H^8 (mq_aes.h
-//     gh_mul_tab, built per workgroup) in the single-key kernels and, in the multi-key kernels,
-//     in waves whose packets all use the table's (hot) key; otherwise, and for the final multiply
-//     by H^e, the bit-holed integer product (gf_mul).
+//   * GHASH: every Horner step's multiply by H^8 is 32 reads of an LDS table of H^8: one full
+//     table per workgroup in the single-key kernels (mq_aes.h gh_mul_tab), and in the multi-key
+//     kernels a half table per wave, built for the tile's key whenever all its packets share one
+//     (gh_mul_half; the mixed-batch partition lays AES packets out key by key so they do);
+//     otherwise, and for the final multiply by H^e, the bit-holed integer product (gf_mul).
 //
 // STREAMING tiles (r02): a wave = 8 packets x 8 lanes (mq_tile.h), slot b of a packet on lane
 // b % 8 in iteration b / 8. Slot b >= 1 is CTR block b (counter b + 1) over payload bytes
@@ -98,9 +99,12 @@ __device__ __forceinline__ void patch_header(uint32_t (&m)[4], uint32_t at, uint
   }
 }
 
-// The streaming tile of one wave. TAB: H^8 multiplies through the LDS table (single-key kernels,
-// or a multi-key wave whose packets all use the hot row).
-template <bool SINGLE, bool TAB>
+// How a streaming tile multiplies by H^8: the workgroup's full table (single-key kernels), the
+// wave's half table (multi-key kernels, key-uniform tile) or the bit-holed product (mixed keys)
+enum GhMode { kGhWorkgroup, kGhWave, kGhProduct };
+
+// The streaming tile of one wave.
+template <bool SINGLE, int GH>
 struct AesStream {
   // AES of slot b (b >= 0) from the CTR cache or full rounds; keystream as little-endian words
   template <bool CACHED, class K>
@@ -129,7 +133,8 @@ struct AesStream {
     return;
 #endif
     uint32_t t[4] = {acc[0], acc[1], acc[2], acc[3]};
-    if (TAB) gh_mul_tab(t);
+    if (GH == kGhWorkgroup) gh_mul_tab(t);
+    else if (GH == kGhWave) gh_mul_half(t, (const uint8_t*)g_aes_wtab + kGhHalfBytes * wave_id());
     else gf_mul(t, m8);
 #pragma unroll
     for (int w = 0; w < 4; ++w) acc[w] = (has && !last) ? t[w] : acc[w];
@@ -151,7 +156,7 @@ struct AesStream {
 
   static __device__ __forceinline__ GfOp prep_m8(const KeyRow* row) {
     GfOp m8;
-    if (!TAB) {
+    if (GH == kGhProduct) {
       uint32_t h[4];
 #pragma unroll
       for (int w = 0; w < 4; ++w) h[w] = brev(row->H[7][w]);
@@ -428,39 +433,39 @@ using namespace mq;
 // per workgroup); wave w walks tiles blockIdx.x * W + w + k * gridDim.x * W. Single-key kernels
 // fit 128 VGPRs (16 waves per CU); the multi-key ones hold more state per packet (LDS key
 // pointers, the bit-holed GHASH operand) and run 12 waves in 168. The "1" variants run when the
-// key table has a single row: round keys in SGPRs
-// and the GHASH table of that row's H^8.
-constexpr int kAesStreamWaves = 16;  // the most waves of any variant (LDS key slots)
-constexpr int aes_waves(bool single) { return single ? 16 : 12; }
-// key schedules in LDS: multi-key kernels, per wave and packet (copied per tile); single-key
-// kernels, row 0's in slot 0 (copied once per workgroup)
-__shared__ __attribute__((aligned(16))) uint32_t g_aes_keys[kAesStreamWaves * kPktsPerTile * kRkSlotBytes / 4];
+// key table has a single row: round keys in SGPRs and the GHASH table of that row's H^8.
+constexpr int aes_waves(bool single) { return single ? 16 : (int)kAesMultiWaves; }
+// multi-key kernels: consecutive tiles per wave (for_tiles chunks). Measured on configs E and C
+// with 1024 keys: chunks of 4 or 8 tiles (a key's tiles sharing one half-table build) lose more
+// to load imbalance than they save, so 1.
+#ifndef MQ_AES_CHUNK
+#define MQ_AES_CHUNK 1
+#endif
+constexpr uint32_t kAesChunk = MQ_AES_CHUNK;
+// key schedules in LDS: multi-key kernels, per wave and packet (copied per tile; a key-uniform
+// tile uses its wave's first slot); single-key kernels, row 0's in slot 0 (copied once per
+// workgroup)
+__shared__ __attribute__((aligned(16))) uint32_t g_aes_keys[kAesMultiWaves * kPktsPerTile * kRkSlotBytes / 4];
 
 template <bool SINGLE>
-__device__ __forceinline__ void aes_tables(const KeyRow* __restrict__ kt, uint32_t n_rows,
-                                           const uint32_t* __restrict__ hot) {
+__device__ __forceinline__ void aes_tables(const KeyRow* __restrict__ kt) {
   build_tw(threadIdx.x, blockDim.x);
-  if (SINGLE && threadIdx.x < kRkSlotBytes / 4) g_aes_keys[threadIdx.x] = kt[0].aes_rk[threadIdx.x];  // aes_rk || hp_rk
-  // multi-key kernels: a GHASH table for the hot row when the partition found one (`hot` points
-  // at its index in the workspace; an out-of-range index means none)
-  const uint32_t r = SINGLE ? 0u : (hot ? *hot : 0xFFFFFFFFu);
-  if (SINGLE || r < n_rows) {
-    if (!SINGLE && threadIdx.x == 0) g_aes_hot_row = kt + r;
+  if (SINGLE) {
+    if (threadIdx.x < kRkSlotBytes / 4) g_aes_keys[threadIdx.x] = kt[0].aes_rk[threadIdx.x];  // aes_rk || hp_rk
     uint32_t h8[4];
 #pragma unroll
-    for (int w = 0; w < 4; ++w) h8[w] = brev(kt[r].H[7][w]);
+    for (int w = 0; w < 4; ++w) h8[w] = brev(kt[0].H[7][w]);
     build_gh(h8, threadIdx.x, blockDim.x);  // ends with a barrier
   } else {
-    if (threadIdx.x == 0) g_aes_hot_row = nullptr;
     __syncthreads();
   }
 }
 
-template <bool SINGLE, bool OPEN, bool TAB, bool CACHED, class K>
+template <bool SINGLE, bool OPEN, int GH, bool CACHED, class K>
 __device__ __forceinline__ void aes_run(uint8_t* __restrict__ arena, PktCtx& c, const KeyRow* row, int j, const K& key,
                                         const uint32_t* kl) {
-  if (OPEN) AesStream<SINGLE, TAB>::template open<CACHED>(arena, c, row, j, key, kl);
-  else AesStream<SINGLE, TAB>::template seal<CACHED>(arena, c, row, j, key, kl);
+  if (OPEN) AesStream<SINGLE, GH>::template open<CACHED>(arena, c, row, j, key, kl);
+  else AesStream<SINGLE, GH>::template seal<CACHED>(arena, c, row, j, key, kl);
 }
 
 template <bool SINGLE, bool OPEN>
@@ -470,10 +475,11 @@ __device__ __forceinline__ void aes_stream_tiles(const KeyRow* __restrict__ kt, 
                                                  const uint32_t* __restrict__ index,
                                                  const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status,
                                                  uint64_t* __restrict__ pn_out, const uint2* __restrict__ hpm) {
-  const uint32_t w = threadIdx.x >> 6;
-  const int j = (int)(threadIdx.x & (kLanesPerPkt - 1));
+  const uint32_t w = wave_id();
+  const int lane = (int)(threadIdx.x & (kWave - 1)), j = lane & (kLanesPerPkt - 1);
   constexpr uint32_t W = aes_waves(SINGLE);
-  for_tiles<OPEN>(blockIdx.x * W + w, gridDim.x * W, desc, n, index, n_dev, hpm,
+  uint32_t wt_kid = 0xFFFFFFFFu;  // multi-key: the row whose half table and key schedules the wave holds
+  for_tiles<OPEN, SINGLE ? 1u : kAesChunk>(blockIdx.x * W + w, gridDim.x * W, desc, n, index, n_dev, hpm,
                   [&](uint32_t t, const TilePrefetch& pf) __attribute__((always_inline)) {
     PktCtx c;
     const KeyRow* row;
@@ -481,35 +487,49 @@ __device__ __forceinline__ void aes_stream_tiles(const KeyRow* __restrict__ kt, 
                                                     row))
       return;
     MQ_STAMP(t, 0);
-    // this packet's key schedules into the wave's LDS slots (multi-key: lane j copies words
-    // 11j .. 11j + 10 of aes_rk || hp_rk, contiguous in the row)
-    const uint32_t p = (threadIdx.x & (kWave - 1)) / kLanesPerPkt;
-    uint32_t* kl = SINGLE ? g_aes_keys : g_aes_keys + (w * kPktsPerTile + p) * (kRkSlotBytes / 4);
-    if (!SINGLE) {
-      const uint32_t* src = row->aes_rk + 11 * j;
-      uint32_t v[11];
-#pragma unroll
-      for (int q = 0; q < 11; ++q) v[q] = src[q];
-#pragma unroll
-      for (int q = 0; q < 11; ++q) kl[11 * j + q] = v[q];
-      wave_sync();
-    }
-    // the H^8 table serves a wave whose active packets all use its row; others multiply by
-    // the bit-holed product (two instantiations: a wave holds one method's registers). CTR
-    // caching needs every counter < 256: packets of at most 4080 bytes.
-    const bool tab = SINGLE || (g_aes_hot_row != nullptr && !wave_any(c.act && row != g_aes_hot_row));
+    // CTR caching needs every counter < 256: packets of at most 4080 bytes
     const bool cached = !wave_any(c.act && c.d.len > 4080u);
     if (SINGLE) {
       AesRk rk;
       load_rk(kt[0].aes_rk, rk);  // wave-uniform: SGPRs
-      if (cached) aes_run<SINGLE, OPEN, true, true>(arena, c, row, j, RkRegs{rk}, kl);
-      else aes_run<SINGLE, OPEN, true, false>(arena, c, row, j, RkRegs{rk}, kl);
-    } else if (tab) {
-      if (cached) aes_run<SINGLE, OPEN, true, true>(arena, c, row, j, RkLds{kl}, kl);
-      else aes_run<SINGLE, OPEN, true, false>(arena, c, row, j, RkLds{kl}, kl);
+      if (cached) aes_run<SINGLE, OPEN, kGhWorkgroup, true>(arena, c, row, j, RkRegs{rk}, g_aes_keys);
+      else aes_run<SINGLE, OPEN, kGhWorkgroup, false>(arena, c, row, j, RkRegs{rk}, g_aes_keys);
     } else {
-      if (cached) aes_run<SINGLE, OPEN, false, true>(arena, c, row, j, RkLds{kl}, kl);
-      else aes_run<SINGLE, OPEN, false, false>(arena, c, row, j, RkLds{kl}, kl);
+      // a tile whose active packets share one row: round keys in SGPRs, that row's H^8 half table
+      // (and key schedules for the HP block) in the wave's LDS, rebuilt only when the row changes
+      const uint32_t kid = __builtin_amdgcn_readfirstlane(wave_min_u32(c.act ? c.d.key_id : 0xFFFFFFFFu));
+      if (kid != 0xFFFFFFFFu && !wave_any(c.act && c.d.key_id != kid)) {
+        const KeyRow* urow = kt + kid;
+        uint32_t* kl = g_aes_keys + w * kPktsPerTile * (kRkSlotBytes / 4);
+        if (kid != wt_kid) {
+          uint32_t h8[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) h8[q] = brev(urow->H[7][q]);
+          build_gh_half((uint8_t*)g_aes_wtab + kGhHalfBytes * w, h8, lane);  // ends with wave_sync
+          for (int q = lane; q < (int)(kRkSlotBytes / 4); q += kWave) kl[q] = urow->aes_rk[q];  // aes_rk || hp_rk
+          wave_sync();
+          wt_kid = kid;
+        }
+        AesRk rk;
+        load_rk(urow->aes_rk, rk);
+        if (cached) aes_run<SINGLE, OPEN, kGhWave, true>(arena, c, urow, j, RkRegs{rk}, kl);
+        else aes_run<SINGLE, OPEN, kGhWave, false>(arena, c, urow, j, RkRegs{rk}, kl);
+      } else {
+        // mixed keys: each packet's key schedules into its own LDS slot (lane j copies words
+        // 11j .. 11j + 10 of aes_rk || hp_rk, contiguous in the row)
+        const uint32_t p = (uint32_t)lane / kLanesPerPkt;
+        uint32_t* kl = g_aes_keys + (w * kPktsPerTile + p) * (kRkSlotBytes / 4);
+        const uint32_t* src = row->aes_rk + 11 * j;
+        uint32_t v[11];
+#pragma unroll
+        for (int q = 0; q < 11; ++q) v[q] = src[q];
+#pragma unroll
+        for (int q = 0; q < 11; ++q) kl[11 * j + q] = v[q];
+        wave_sync();
+        wt_kid = 0xFFFFFFFFu;  // slot 0 no longer holds a key-uniform tile's schedules
+        if (cached) aes_run<SINGLE, OPEN, kGhProduct, true>(arena, c, row, j, RkLds{kl}, kl);
+        else aes_run<SINGLE, OPEN, kGhProduct, false>(arena, c, row, j, RkLds{kl}, kl);
+      }
     }
     MQ_STAMP(t, 7);
     tile_status<OPEN>(c, j, status, pn_out);
@@ -520,8 +540,8 @@ __device__ __forceinline__ void aes_stream_tiles(const KeyRow* __restrict__ kt, 
   extern "C" __global__ __launch_bounds__(64 * aes_waves(SINGLE)) void NAME_SEAL(                           \
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
-      const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, const uint32_t* __restrict__ hot) { \
-    aes_tables<SINGLE>(kt, n_rows, hot);                                                                  \
+      const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status) {                                 \
+    aes_tables<SINGLE>(kt);                                                                               \
     aes_stream_tiles<SINGLE, false>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr,  \
                                     nullptr);                                                             \
   }                                                                                                       \
@@ -529,8 +549,8 @@ __device__ __forceinline__ void aes_stream_tiles(const KeyRow* __restrict__ kt, 
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
       const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,    \
-      const uint2* __restrict__ hpm, const uint32_t* __restrict__ hot) {                                  \
-    aes_tables<SINGLE>(kt, n_rows, hot);                                                                  \
+      const uint2* __restrict__ hpm) {                                                                    \
+    aes_tables<SINGLE>(kt);                                                                               \
     aes_stream_tiles<SINGLE, true>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm); \
   }
 MQ_AES_KERNELS(mq_aes_seal_kernel, mq_aes_open_kernel, false)
@@ -637,7 +657,7 @@ static uint32_t aes_grid(uint32_t tiles, uint32_t waves) {
 
 hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena, uint64_t arena_len,
                          const mq_pkt_desc* desc, uint32_t n, const uint32_t* index, const uint32_t* n_dev,
-                         uint8_t* status, uint64_t* pn_out, uint2* hpm, hipStream_t s, const uint32_t* hot) {
+                         uint8_t* status, uint64_t* pn_out, uint2* hpm, hipStream_t s) {
   const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
   if (tiles == 0) return hipSuccess;
   const uint32_t waves = aes_waves(n_rows == 1), blocks = aes_grid(tiles, waves);
@@ -649,11 +669,11 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
   }
   if (open) {
     hipLaunchKernelGGL(n_rows == 1 ? mq_aes_open1_kernel : mq_aes_open_kernel, dim3(blocks), dim3(64 * waves),
-                       0, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm, hot);
+                       0, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(n_rows == 1 ? mq_aes_seal1_kernel : mq_aes_seal_kernel, dim3(blocks), dim3(64 * waves),
-                     0, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, hot);
+                     0, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(mq_aes_seal_hp_kernel, dim3((n + 255) / 256), dim3(256), 0, s, kt, arena, arena_len, desc, n,

@@ -281,6 +281,9 @@ __device__ __forceinline__ uint32_t oct_xor(uint32_t x) {
 // Wave-local barrier: tiles are private to one wave, so ordering the wave's own LDS / HBM
 // accesses (and keeping the compiler from moving them) is all a phase boundary needs. Unlike
 // __syncthreads() it is safe in multi-wave workgroups whose waves take different paths.
+// this wave's index in its workgroup (scalar)
+__device__ __forceinline__ uint32_t wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_wave_barrier();

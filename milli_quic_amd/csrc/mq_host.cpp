@@ -28,7 +28,7 @@ hipError_t mq_launch_chacha_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t
 hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena,
                          uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
                          const uint32_t* index, const uint32_t* n_dev, uint8_t* status,
-                         uint64_t* pn_out, uint2* hpm, hipStream_t s, const uint32_t* hot = nullptr);
+                         uint64_t* pn_out, uint2* hpm, hipStream_t s);
 hipError_t mq_launch_aes_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t* key_ids,
                             const uint8_t* samples, uint8_t* masks, uint32_t n, hipStream_t s);
 hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_desc* desc, uint32_t n,
@@ -680,12 +680,16 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
   uint2* hpm = (open && ws) ? (uint2*)ws : nullptr;
   if (suite_hint == MQ_SUITE_CHACHA20) {
     e = mq_launch_chacha(open, kt->dev, kt->rows, arena, arena_len, desc, n, nullptr, nullptr, status, pn_out, hpm, s);
-  } else if (suite_hint == MQ_SUITE_AES128GCM) {
+  } else if (suite_hint == MQ_SUITE_AES128GCM && (kt->rows == 1 || !ws || n > (1u << 30))) {
     e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, n, nullptr, nullptr, status, pn_out, hpm, s);
-  } else if (suite_hint == MQ_SUITE_MIXED) {
+  } else if (suite_hint == MQ_SUITE_MIXED || suite_hint == MQ_SUITE_AES128GCM) {
     // the two index lists (2 x mq_partition_list_cap(n) entries, holes included) are addressed
-    // with 32-bit positions: up to 2^30 packets per mixed batch
+    // with 32-bit positions: up to 2^30 packets per mixed batch. An AES batch over several key
+    // rows takes the partition too, for its key-uniform tiles; whatever it puts in the second
+    // list (packets of other suites, bad key ids) goes to the AES kernel as well, which rejects
+    // it exactly as the flat launch would.
     if (!ws || n > (1u << 30)) return MQ_ERR_INVALID_ARG;
+    const bool aes_only = suite_hint == MQ_SUITE_AES128GCM;
     uint8_t* pw = ws + ws_align(8 * (size_t)n);
     uint32_t* list = (uint32_t*)pw;
     size_t hist_off, counts_off;
@@ -696,9 +700,11 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
     const uint32_t cap = mq_partition_list_cap(n);
     e = mq_launch_partition(kt->dev, kt->rows, desc, n, list, hist, counts, s);
     if (e == hipSuccess)
-      e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list, counts, status, pn_out, hpm, s,
-                        counts + 2 /* the partition's hot AES key row */);
-    if (e == hipSuccess)
+      e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list, counts, status, pn_out, hpm, s);
+    if (e == hipSuccess && aes_only)
+      e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list + cap, counts + 1, status, pn_out,
+                        hpm, s);
+    else if (e == hipSuccess)
       e = mq_launch_chacha(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list + cap, counts + 1, status,
                            pn_out, hpm, s);
   } else {

@@ -13,14 +13,19 @@
 // the order changes nothing but the tile composition: a tile runs as long as its longest packet,
 // and a uniformly mixed 64-1350-B batch otherwise pays for 8 x its maximum in nearly every tile.
 //
-// AES packets are further split by key: the batch's majority AES key (Boyer-Moore vote; in a
-// server's mix the 1-RTT key of the busiest path) goes first in the AES list, so its tiles are
-// key-uniform and the multi-key AES kernels run their GHASH through the LDS table of that key's
-// H^8 (counts[2] = its row, or 0xFFFFFFFF). With no majority the vote's candidate is just some
-// key: results are the same, only fewer tiles use the table.
+// AES packets are further split by key, so that the multi-key AES kernels find key-uniform
+// tiles (they then multiply through a GHASH table of that key's H^8 instead of the bit-holed
+// product): the batch's majority AES key (Boyer-Moore vote; in a server's mix the 1-RTT key of
+// the busiest path; counts[2] = its row, or 0xFFFFFFFF) goes first, by length class; then, when
+// the key table is small enough for one counter per (row, 128-B length class) in the workspace
+// ("keyed" layout), every other AES key's packets follow key by key, each key's segment longest
+// class first and padded to whole tiles. Otherwise the other keys share length classes as the
+// majority key does. With no majority the vote's candidate is just some key: results are the
+// same either way, only the tile composition changes.
 //
-// Launches: per-block votes, one vote reduction, per-block class histograms (class-major), one
-// exclusive scan of the histograms, scatter.
+// Launches: per-block votes, one vote reduction, per-block class histograms (class-major) and,
+// keyed, per-(row, class) counts (global atomics, one per distinct bin per wave), one exclusive
+// scan of the histograms, keyed: one scan of the per-row counts into bin bases, scatter.
 #include "mq_tile.h"
 
 using namespace mq;
@@ -34,6 +39,7 @@ constexpr uint32_t kGroups = 3;       // AES with the hot key, other AES (both: 
 constexpr uint32_t kClasses = kGroups * kLenClasses;
 constexpr uint32_t kBudgetChunks = kDataBudget / 16;
 constexpr uint32_t kNoKey = 0xFFFFFFFFu;
+constexpr uint32_t kKeyClasses = 16;  // keyed layout: per row, min(len / 128, 15), longest first
 
 __device__ __forceinline__ bool is_aes(const KeyRow* kt, uint32_t n_rows, const mq_pkt_desc& d) {
   return d.key_id < n_rows && kt[d.key_id].suite == MQ_SUITE_AES128GCM;
@@ -45,6 +51,53 @@ __device__ __forceinline__ uint32_t part_class(const KeyRow* kt, uint32_t n_rows
   const uint32_t g = is_aes(kt, n_rows, d) ? (d.key_id == hot ? 0u : 1u) : 2u;
   const uint32_t b = min(d.len >> 6, kLenClasses - 1);
   return g * kLenClasses + (kLenClasses - 1 - b);
+}
+
+// keyed layout: the bin of a non-majority AES packet (row-major, longest class first)
+__device__ __forceinline__ uint32_t key_bin(const mq_pkt_desc& d) {
+  return d.key_id * kKeyClasses + (kKeyClasses - 1 - min(d.len >> 7, kKeyClasses - 1));
+}
+// Per distinct bin among the wave's lanes with `pend`, one atomicAdd of its lane count on
+// ctr[bin] — all issued by one instruction: the wave sorts its (bin, lane) pairs (bitonic, 21
+// steps), so equal bins form runs whose first lane adds the run length. With `claim`, every
+// pending lane gets the old value plus its rank in its run, as the list position of descriptor
+// `i` (the lane that receives it need not be the lane that holds it: position and index travel
+// together), returned through pos / idx (pos = 0xFFFFFFFF: nothing for this lane).
+template <bool CLAIM>
+__device__ __forceinline__ void wave_bin_add(uint32_t* ctr, uint32_t bin, bool pend, uint32_t i, uint32_t& pos,
+                                             uint32_t& idx) {
+  const int lane = threadIdx.x & 63;
+  constexpr uint32_t kNone = 0xFFFFFFFFu;
+  // key: bin (< 2^26) above the lane; idle lanes sort last
+  uint32_t k = pend ? (bin << 6 | (uint32_t)lane) : kNone;
+#pragma unroll
+  for (int sz = 2; sz <= 64; sz <<= 1) {
+#pragma unroll
+    for (int st = sz >> 1; st >= 1; st >>= 1) {
+      const uint32_t o = (uint32_t)__shfl_xor((int)k, st, kWave);
+      const bool up = (lane & sz) == 0, low = (lane & st) == 0;
+      k = (low == up) ? min(k, o) : max(k, o);
+    }
+  }
+  const bool valid = k != kNone;
+  const uint32_t b = k >> 6;
+  const uint32_t prev = (uint32_t)__shfl_up((int)k, 1, kWave) >> 6;
+  const bool head = lane == 0 || b != prev || !valid;  // idle lanes end the last run
+  const uint64_t heads = __ballot(head);
+  const uint64_t upto = ~0ull >> (63 - lane);  // lanes 0..lane
+  const int start = 63 - __clzll((long long)(heads & upto));
+  const uint64_t after = heads & ~upto;
+  const int end = after ? __ffsll((unsigned long long)after) - 1 : 64;
+  uint32_t base = 0;
+  if (valid && head) {
+    if (CLAIM) base = atomicAdd(&ctr[b], (uint32_t)(end - lane));
+    else atomicAdd(&ctr[b], (uint32_t)(end - lane));
+  }
+  if (CLAIM) {
+    base = (uint32_t)__shfl((int)base, start, kWave);
+    pos = valid ? base + (uint32_t)(lane - start) : kNone;
+    idx = (uint32_t)__shfl((int)i, (int)(k & 63u), kWave);  // descriptor of the sorted pair's lane
+  }
 }
 
 // Boyer-Moore majority pairs (candidate, count); combining any partition of the input in any
@@ -113,16 +166,24 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_vote_reduce_k
   if (threadIdx.x == 0) meta[0] = v.y ? v.x : kNoKey;
 }
 
+// keyed (bins != nullptr): non-majority AES packets are counted per (row, class) bin instead
 extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_count_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_pkt_desc* __restrict__ desc, uint32_t n,
-    uint32_t nblocks, const uint32_t* __restrict__ hot_p, uint32_t* __restrict__ hist) {
+    uint32_t nblocks, const uint32_t* __restrict__ hot_p, uint32_t* __restrict__ hist, uint32_t* __restrict__ bins) {
   __shared__ uint32_t s_cnt[kClasses];
   if (threadIdx.x < kClasses) s_cnt[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t hot = *hot_p;
   for (int k = 0; k < kPartItems; ++k) {
     const uint32_t i = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
-    if (i < n) atomicAdd(&s_cnt[part_class(kt, n_rows, hot, desc[i])], 1u);
+    const bool in = i < n;
+    mq_pkt_desc d{};
+    if (in) d = desc[i];
+    const uint32_t c = in ? part_class(kt, n_rows, hot, d) : 0u;
+    const bool keyed = bins && in && c / kLenClasses == 1;  // wave-uniform branch below
+    uint32_t pos, idx;
+    if (bins && __ballot(keyed)) wave_bin_add<false>(bins, keyed ? key_bin(d) : 0u, keyed, i, pos, idx);
+    if (in && !keyed) atomicAdd(&s_cnt[c], 1u);
   }
   __syncthreads();
   if (threadIdx.x < kClasses) hist[(size_t)threadIdx.x * nblocks + blockIdx.x] = s_cnt[threadIdx.x];
@@ -192,10 +253,62 @@ extern "C" __global__ __launch_bounds__(64 * kScanWaves) void mq_part_scan_kerne
   }
 }
 
+// Keyed layout, single workgroup: each row's segment (its bins' packets, whole tiles) follows
+// the majority key's classes in list 0; bins[b] becomes the list position of bin b's first
+// packet (the scatter's cursor) and counts[0] the list's entries.
+constexpr int kKeyScanThreads = 1024;
+extern "C" __global__ __launch_bounds__(kKeyScanThreads) void mq_part_key_scan_kernel(uint32_t* __restrict__ bins,
+                                                                                     uint32_t n_rows,
+                                                                                     uint32_t* __restrict__ counts) {
+  __shared__ uint32_t s_wave[kKeyScanThreads / kWave];
+  __shared__ uint32_t s_base;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_base = counts[0];  // the majority key's classes end on a tile boundary
+  __syncthreads();
+  for (uint32_t r0 = 0; r0 < n_rows; r0 += kKeyScanThreads) {  // one row per thread
+    const uint32_t r = r0 + threadIdx.x;
+    uint32_t c[kKeyClasses], tot = 0;
+    const uint4* src = (const uint4*)(bins + (size_t)r * kKeyClasses);
+#pragma unroll
+    for (int q = 0; q < (int)kKeyClasses / 4; ++q) {
+      const uint4 v = r < n_rows ? src[q] : make_uint4(0, 0, 0, 0);
+      c[4 * q] = v.x; c[4 * q + 1] = v.y; c[4 * q + 2] = v.z; c[4 * q + 3] = v.w;
+      tot += v.x + v.y + v.z + v.w;
+    }
+    const uint32_t ent = (tot + kPktsPerTile - 1) & ~(kPktsPerTile - 1);
+    const uint32_t incl = wave_incl_scan(ent);
+    if (lane == 63) s_wave[wave] = incl;
+    __syncthreads();
+    uint32_t before = s_base;
+    for (int q = 0; q < wave; ++q) before += s_wave[q];
+    uint32_t at = before + incl - ent;
+    if (r < n_rows) {
+      uint4* dst = (uint4*)(bins + (size_t)r * kKeyClasses);
+#pragma unroll
+      for (int q = 0; q < (int)kKeyClasses / 4; ++q) {
+        uint4 v;
+        v.x = at; at += c[4 * q];
+        v.y = at; at += c[4 * q + 1];
+        v.z = at; at += c[4 * q + 2];
+        v.w = at; at += c[4 * q + 3];
+        dst[q] = v;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t t = 0;
+      for (int q = 0; q < kKeyScanThreads / kWave; ++q) t += s_wave[q];
+      s_base += t;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) counts[0] = s_base;
+}
+
 extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_scatter_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_pkt_desc* __restrict__ desc, uint32_t n,
     uint32_t nblocks, const uint32_t* __restrict__ hot_p, const uint32_t* __restrict__ hist,
-    const uint32_t* __restrict__ seg, uint32_t* __restrict__ list) {
+    const uint32_t* __restrict__ seg, uint32_t* __restrict__ list, uint32_t* __restrict__ bins) {
   __shared__ uint32_t s_rank[kClasses];
   const uint32_t hot = *hot_p;
   const int lane = threadIdx.x & 63;
@@ -204,8 +317,16 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_scatter_kerne
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   for (int k = 0; k < kPartItems; ++k) {
     const uint32_t i = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
-    const bool in = i < n;
-    const uint32_t c = in ? part_class(kt, n_rows, hot, desc[i]) : 0u;
+    mq_pkt_desc d{};
+    if (i < n) d = desc[i];
+    const uint32_t c = i < n ? part_class(kt, n_rows, hot, d) : 0u;
+    const bool keyed = bins && i < n && c / kLenClasses == 1;
+    if (bins && __ballot(keyed)) {
+      uint32_t pos, idx;
+      wave_bin_add<true>(bins, keyed ? key_bin(d) : 0u, keyed, i, pos, idx);
+      if (pos != 0xFFFFFFFFu) list[pos] = idx;
+    }
+    const bool in = i < n && !keyed;
     // lanes of this wave with the same class (7 ballots), rank among them = peers below
     uint64_t peers = __ballot(in);
 #pragma unroll
@@ -226,6 +347,19 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_scatter_kerne
   }
 }
 
+// keyed layout bins: one counter per (row, class), within a budget of 2 per packet (at least
+// 64 Ki) and below 2^26 (wave_bin_add's sort keys), and only when the keyed list (at most 7
+// holes per row) fits the list capacity
+static size_t key_bins(uint32_t n) { return 2 * (size_t)n > 65536 ? 2 * (size_t)n : 65536; }
+static bool keyed_layout(uint32_t n, uint32_t n_rows) {
+  return (size_t)n_rows * kKeyClasses <= key_bins(n) && (size_t)n_rows * kKeyClasses < (1u << 26) &&
+         (uint64_t)n + kPktsPerTile * kLenClasses + (uint64_t)(kPktsPerTile - 1) * n_rows <= mq_partition_list_cap(n);
+}
+
+// list (2 x cap entries) | class histograms (kClasses per block) + votes (2 words per block) |
+// meta (2 totals, hot row, pad, kClasses segment starts) | keyed bins, 256-B aligned pieces
+static size_t part_align(size_t b) { return (b + 255) & ~(size_t)255; }
+
 hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_desc* desc, uint32_t n,
                                uint32_t* list, uint32_t* hist, uint32_t* counts, hipStream_t s) {
   const uint32_t nblocks = (n + kPartBlock - 1) / kPartBlock;
@@ -234,26 +368,28 @@ hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_d
   uint32_t* hot = counts + 2;  // meta: counts[0..1] | hot row | pad | seg[kClasses]
   uint32_t* seg = counts + 4;
   uint2* votes = (uint2*)(hist + (size_t)kClasses * nblocks);
+  uint32_t* bins = keyed_layout(n, n_rows) ? (uint32_t*)((uint8_t*)counts + part_align(sizeof(uint32_t) * (4 + kClasses)))
+                                           : nullptr;
   hipError_t e = hipMemsetAsync(list, 0xff, sizeof(uint32_t) * 2 * (size_t)cap, s);  // holes
+  if (e == hipSuccess && bins) e = hipMemsetAsync(bins, 0, sizeof(uint32_t) * kKeyClasses * (size_t)n_rows, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(mq_part_vote_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, kt, n_rows, desc, n, votes);
   hipLaunchKernelGGL(mq_part_vote_reduce_kernel, dim3(1), dim3(kPartThreads), 0, s, votes, nblocks, hot);
   hipLaunchKernelGGL(mq_part_count_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, kt, n_rows, desc, n,
-                     nblocks, hot, hist);
+                     nblocks, hot, hist, bins);
   hipLaunchKernelGGL(mq_part_scan_kernel, dim3(1), dim3(64 * kScanWaves), 0, s, hist, nblocks, cap, counts, seg);
+  if (bins)
+    hipLaunchKernelGGL(mq_part_key_scan_kernel, dim3(1), dim3(kKeyScanThreads), 0, s, bins, n_rows, counts);
   hipLaunchKernelGGL(mq_part_scatter_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, kt, n_rows, desc, n,
-                     nblocks, hot, hist, seg, list);
+                     nblocks, hot, hist, seg, list, bins);
   return hipGetLastError();
 }
-
-// list (2 x cap entries) | class histograms (kClasses per block) + votes (2 words per block) |
-// meta (2 totals, hot row, pad, kClasses segment starts), 256-B aligned pieces
-static size_t part_align(size_t b) { return (b + 255) & ~(size_t)255; }
 
 size_t mq_partition_workspace(uint32_t n) {
   const size_t nblocks = (n + kPartBlock - 1) / kPartBlock;
   return part_align(sizeof(uint32_t) * 2 * (size_t)mq_partition_list_cap(n)) +
-         part_align(sizeof(uint32_t) * (kClasses + 2) * nblocks) + part_align(sizeof(uint32_t) * (4 + kClasses));
+         part_align(sizeof(uint32_t) * (kClasses + 2) * nblocks) + part_align(sizeof(uint32_t) * (4 + kClasses)) +
+         part_align(sizeof(uint32_t) * key_bins(n));
 }
 
 // offsets of the pieces inside the partition workspace

@@ -315,12 +315,13 @@ __device__ __forceinline__ bool write_unmasked_header(const S& sp, typename S::o
 
 // SINGLE_KEY: the key table has one row, so every valid packet uses row 0; the policies then get
 // a wave-uniform row pointer and read key material with scalar loads into SGPRs.
-// Descriptor words of a tile fetched ahead of time (flat batches, run_tiles): lane 8p + j holds
-// dword j of packet p's descriptor (dw) and, for open, dword j < 2 of its HP mask (hm); octet
-// swizzles rebuild the descriptor, so a prefetch costs two VGPRs.
+// Descriptor words of a tile fetched ahead of time (for_tiles): lane 8p + j holds dword j of
+// packet p's descriptor (dw) and, for open, dword j < 2 of its HP mask (hm), and idx = packet p's
+// descriptor index (kListHole for a hole of an index list); octet swizzles rebuild the
+// descriptor, so a prefetch costs three VGPRs.
 struct TilePrefetch {
   bool on;  // wave-uniform
-  uint32_t dw, hm;
+  uint32_t dw, hm, idx;
 };
 
 template <int K>
@@ -345,8 +346,9 @@ __device__ __forceinline__ bool tile_ctx(uint32_t tile_id, const KeyRow* __restr
   c.valid = t < count;
   c.pre_hp = OPEN && hpm != nullptr;
   c.hm0 = c.hm1 = 0;
-  if (pf.on) {  // flat batch, words already in registers
-    c.i = t;
+  if (pf.on) {  // words already in registers
+    c.i = c.valid ? pf.idx : 0u;
+    if (c.i == kListHole) { c.valid = false; c.i = 0; }
     const uint32_t w0 = oct_lane<0>(pf.dw), w1 = oct_lane<1>(pf.dw), w2 = oct_lane<2>(pf.dw),
                    w3 = oct_lane<3>(pf.dw), w4 = oct_lane<4>(pf.dw), w5 = oct_lane<5>(pf.dw),
                    w6 = oct_lane<6>(pf.dw), w7 = oct_lane<7>(pf.dw);
@@ -356,6 +358,11 @@ __device__ __forceinline__ bool tile_ctx(uint32_t tile_id, const KeyRow* __restr
     c.d.pn_offset = (uint16_t)w6; c.d.pn_len = (uint8_t)(w6 >> 16); c.d.flags = (uint8_t)(w6 >> 24);
     c.d.reserved = w7;
     if (OPEN && hpm) { c.hm0 = oct_lane<0>(pf.hm); c.hm1 = oct_lane<1>(pf.hm); }
+    if (!c.valid) {
+      c.d.offset = 0; c.d.len = 0; c.d.key_id = 0; c.d.pn = 0; c.d.pn_offset = 0; c.d.pn_len = 0;
+      c.d.flags = 0; c.d.reserved = 0;
+      c.hm0 = c.hm1 = 0;
+    }
   } else {
     c.i = c.valid ? (index ? index[t] : t) : 0u;
     if (c.i == kListHole) { c.valid = false; c.i = 0; }
@@ -440,33 +447,45 @@ __device__ __forceinline__ void run_tile(uint8_t* smem, uint32_t tile_id, const 
   tile_status<OPEN>(c, j, status, pn_out);
 }
 
-// Persistent tile loop: this wave runs tiles first, first + stride, ... calling
-// body(tile, prefetch). For flat batches (no index list) the next tile's descriptor words (and HP
-// masks) are loaded while the current tile is processed, so a tile starts without waiting on a
-// descriptor fetch.
-template <bool OPEN, class F>
+// Persistent tile loop: this wave runs its tiles calling body(tile, prefetch), each tile's
+// descriptor words (and HP masks) loaded while the previous tile is processed, so a tile starts
+// without waiting on a descriptor fetch; with an index list the list entries are read one tile
+// further ahead still (list entry, then descriptor: two dependent loads off the critical path).
+// Tiles are taken in chunks of C consecutive ones — chunks first, first + stride, ... — so that
+// a multi-key wave meets a key's consecutive tiles (the partition lays them out together) in a
+// row. A device-side count without an index list runs unprefetched.
+template <bool OPEN, uint32_t C = 1, class F>
 __device__ __forceinline__ void for_tiles(uint32_t first, uint32_t stride, const mq_pkt_desc* __restrict__ desc,
                                           uint32_t n, const uint32_t* __restrict__ index,
                                           const uint32_t* __restrict__ n_dev, const uint2* __restrict__ hpm,
                                           F&& body) {
   const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
-  if (index || n_dev) {
-    for (uint32_t t = first; t < tiles; t += stride) body(t, TilePrefetch{false, 0u, 0u});
+  if (n_dev && !index) {
+    for (uint32_t t = first; t < tiles; t += stride) body(t, TilePrefetch{false, 0u, 0u, 0u});
     return;
   }
   const uint32_t lane = threadIdx.x & (kWave - 1), p = lane / kLanesPerPkt, j = lane % kLanesPerPkt;
-  auto fetch = [&](uint32_t t, uint32_t& dw, uint32_t& hm) {
-    const uint32_t i = t * kPktsPerTile + p;
-    const bool ok = t < tiles && i < n;
-    dw = ok ? reinterpret_cast<const uint32_t*>(desc)[(size_t)i * 8 + j] : 0u;
-    hm = (OPEN && hpm && ok && j < 2) ? reinterpret_cast<const uint32_t*>(hpm)[(size_t)i * 2 + j] : 0u;
+  auto next = [&](uint32_t t) { return (t + 1) % C != 0 ? t + 1 : t + 1 - C + stride * C; };
+  auto idx_of = [&](uint32_t t) -> uint32_t {  // packet p's descriptor index (list: a load)
+    const uint32_t e = t * kPktsPerTile + p;
+    if (t >= tiles || e >= n) return kListHole;
+    return index ? index[e] : e;
   };
-  uint32_t dw, hm;
-  fetch(first, dw, hm);
-  for (uint32_t t = first; t < tiles; t += stride) {
-    const TilePrefetch pf{true, dw, hm};
-    fetch(t + stride, dw, hm);
+  auto fetch = [&](uint32_t ix, uint32_t& dw, uint32_t& hm) {
+    const bool ok = ix != kListHole;
+    dw = ok ? reinterpret_cast<const uint32_t*>(desc)[(size_t)ix * 8 + j] : 0u;
+    hm = (OPEN && hpm && ok && j < 2) ? reinterpret_cast<const uint32_t*>(hpm)[(size_t)ix * 2 + j] : 0u;
+  };
+  uint32_t t = first * C, t1 = next(t);
+  uint32_t ix0 = idx_of(t), ix1 = idx_of(t1), dw, hm;
+  fetch(ix0, dw, hm);
+  while (t < tiles) {
+    const TilePrefetch pf{true, dw, hm, ix0};
+    const uint32_t t2 = next(t1);
+    const uint32_t ix2 = idx_of(t2);
+    fetch(ix1, dw, hm);
     body(t, pf);
+    t = t1; t1 = t2; ix0 = ix1; ix1 = ix2;
   }
 }
 

@@ -215,24 +215,33 @@ def oracle_run(orc, keys, arena, desc, hint, open_=False):
     return a, orc.batch_seal(keys, a, desc, hint, threads=8), None
 
 
-@pytest.mark.parametrize("n_keys,majority", [(97, False), (5, False), (2, True)])
-def test_mixed_hint_aes_keys_vs_oracle(orc, n_keys, majority):
-    # MQ_SUITE_MIXED over an all-AES batch: the partition's majority vote picks a hot key whose
-    # tiles run GHASH through the workgroup table; without a majority (97 or 5 keys round-robin)
-    # its candidate is one key among many, with a majority (2 keys, 3/4 of packets on key 0) it
-    # is key 0. Results equal the oracle either way.
-    w = workload.uniform(4000, _lib.MQ_SUITE_AES128GCM, L=700, n_keys=n_keys)
+@pytest.mark.parametrize("n,n_keys,majority,hint", [
+    (4000, 97, False, _lib.MQ_SUITE_MIXED), (4000, 5, False, _lib.MQ_SUITE_MIXED), (4000, 2, True, _lib.MQ_SUITE_MIXED),
+    (4000, 97, False, _lib.MQ_SUITE_AES128GCM), (20000, 1024, False, _lib.MQ_SUITE_AES128GCM),
+    (4000, 1024, False, _lib.MQ_SUITE_AES128GCM)])
+def test_mixed_hint_aes_keys_vs_oracle(orc, n, n_keys, majority, hint):
+    # An all-AES batch over several key rows, through the partition (MQ_SUITE_MIXED, or the AES
+    # hint with a workspace): the majority vote's key goes first by length class; without a
+    # majority (97, 5 or 1024 keys round-robin) its candidate is one key among many, with one (2
+    # keys, 3/4 of packets on key 0) it is key 0. The other keys' packets are laid out key by key
+    # (tiles of one key: GHASH through the wave's half table) when the rows fit the keyed bins and
+    # the list capacity — 4000 packets over 1024 rows do not, so they share length classes
+    # (mixed-key tiles: the bit-holed product). Results equal the oracle either way.
+    w = workload.uniform(n, _lib.MQ_SUITE_AES128GCM, L=700, n_keys=n_keys)
     seal, opn = w.seal_desc.copy(), w.open_desc.copy()
     if majority:
         k = (np.arange(w.n) % 4 == 3).astype(np.uint32)
         seal["key_id"] = k
         opn["key_id"] = k
-    g_out, g_st, _ = gpu_run(w.keys, w.arena, seal, _lib.MQ_SUITE_MIXED)
-    o_out, o_st, _ = oracle_run(orc, w.keys, w.arena, seal, _lib.MQ_SUITE_MIXED)
+    g_out, g_st, _ = gpu_run(w.keys, w.arena, seal, hint)
+    o_out, o_st, _ = oracle_run(orc, w.keys, w.arena, seal, hint)
     assert (o_st == 0).all() and (g_st == o_st).all()
     assert g_out.tobytes() == o_out.tobytes()
-    g_back, g_st, g_pn = gpu_run(w.keys, g_out, opn, _lib.MQ_SUITE_MIXED, open_=True)
-    o_back, o_st, o_pn = oracle_run(orc, w.keys, o_out, opn, _lib.MQ_SUITE_MIXED, open_=True)
+    if hint == _lib.MQ_SUITE_AES128GCM:  # no workspace: one flat launch, mixed-key tiles
+        f_out, f_st, _ = gpu_run(w.keys, w.arena, seal, hint, use_ws=False)
+        assert (f_st == 0).all() and f_out.tobytes() == o_out.tobytes()
+    g_back, g_st, g_pn = gpu_run(w.keys, g_out, opn, hint, open_=True)
+    o_back, o_st, o_pn = oracle_run(orc, w.keys, o_out, opn, hint, open_=True)
     assert (g_st == 0).all() and (g_st == o_st).all() and (g_pn == o_pn).all()
     assert g_back.tobytes() == o_back.tobytes()
     # open restores every plaintext byte; the 16 tag bytes of each packet stay as sealed (the

@@ -5,7 +5,7 @@ one phase (1 ChaCha rounds, 2 MAC, 4 LDS->HBM store, 8 HBM->LDS staging, 16 AES 
 copies, 32 every tile on the direct path); the difference is what that phase costs.
 MQ_PROF_DIR names the variants' directory (default milli_quic_amd/prof, which gpurun does not ship:
 copy them under tools/ab_libs/ for a GPU run). Diagnostic only: variants compute garbage.
-Usage: python tools/phase_cost.py [b|c|e] [packets]
+Usage: python tools/phase_cost.py [b|c|e|bk|ck] [packets]   (bk, ck: 1024 key rows)
 """
 import os
 import subprocess
@@ -23,7 +23,8 @@ def child(lib, cfg, n):
     _lib.LIB_PATH = lib
     from milli_quic_amd import batch, workload
     assert _lib.load().mq_device_init(0) == 0
-    w = {"b": workload.config_b, "c": workload.config_c, "e": workload.config_e}[cfg](n)
+    w = {"b": workload.config_b, "c": workload.config_c, "e": workload.config_e,
+         "bk": lambda m: workload.config_b(m, n_keys=1024), "ck": lambda m: workload.config_c(m, n_keys=1024)}[cfg](n)
     dev = torch.device("cuda", 0)
     kt = batch.KeyTable(w.keys)
     arena0 = torch.from_numpy(w.arena).to(dev)
