@@ -581,6 +581,7 @@ __global__ __launch_bounds__(256) void mq_aes_open_hp_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, const uint8_t* __restrict__ arena, uint64_t arena_len,
     const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,
     const uint32_t* __restrict__ n_dev, uint2* __restrict__ hpm) {
+  if (blockIdx.x * blockDim.x >= (n_dev ? *n_dev : n)) return;  // list mode: grids cover the list capacity
   build_t0(threadIdx.x, blockDim.x);
   __syncthreads();
   uint32_t i;
@@ -595,8 +596,8 @@ __global__ __launch_bounds__(256) void mq_aes_open_hp_kernel(
   const uint32_t rb = (threadIdx.x & (kTReplicas - 1)) * 4;
   if (DECODE) {  // PN bytes and sample (contiguous) and the first byte in one round of loads
     uint32_t w[5];
-    load_words<5>(sp, at - 4, w);
-    const uint8_t b0 = arena[d.offset];
+    uint8_t b0;
+    prepass_header(arena, d, b0, w);
     const uint32_t smp[4] = {w[1], w[2], w[3], w[4]};
     aes_hp_mask_words(smp, row, rb, m0, m1);
     hpm[i] = prepass_decode_words(b0, w[0], d, m0, m1);
@@ -617,24 +618,23 @@ __global__ __launch_bounds__(256) void mq_aes_seal_hp_kernel(
     const KeyRow* __restrict__ kt, uint8_t* __restrict__ arena, uint64_t arena_len,
     const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,
     const uint32_t* __restrict__ n_dev, const uint8_t* __restrict__ status) {
+  const uint32_t count = n_dev ? *n_dev : n;
+  if (blockIdx.x * blockDim.x >= count) return;  // list mode: grids cover the list capacity
   build_t0(threadIdx.x, blockDim.x);
   __syncthreads();
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t count = n_dev ? *n_dev : n;
   if (t >= count) return;
   const uint32_t i = index ? index[t] : t;
   if (i == kListHole || status[i] != MQ_OK) return;
   const mq_pkt_desc d = desc[i];
   const uint32_t P = d.len - ((uint32_t)d.pn_offset + d.pn_len) - 16, nblk = 1 + ((P + 15) >> 4);
   if ((d.flags & MQ_PKT_NO_HP) || nblk >= (uint32_t)kLanesPerPkt) return;  // records are NO_HP
-  GlobalSpace sp{arena, arena_len};
-  uint32_t smp[4], m0, m1;
-  load_words<4>(sp, d.offset + d.pn_offset + 4, smp);
+  uint32_t w[5], m0, m1;
+  uint8_t b0;
+  prepass_header(arena, d, b0, w);  // inside the packet (validated: pn_offset + 20 <= len)
+  const uint32_t smp[4] = {w[1], w[2], w[3], w[4]};
   aes_hp_mask_words(smp, kt + d.key_id, (uint32_t)(threadIdx.x & (kTReplicas - 1)) * 4, m0, m1);
-  uint8_t* h = arena + d.offset;
-  h[0] ^= (uint8_t)m0 & ((d.flags & MQ_PKT_LONG_HEADER) ? 0x0f : 0x1f);
-  const uint32_t mk = (m0 >> 8) | (m1 << 24);
-  for (uint32_t b = 0; b < d.pn_len; ++b) h[d.pn_offset + b] ^= (uint8_t)(mk >> (8 * b));
+  seal_apply_hp(arena, d, b0, w[0], m0, m1);
 }
 
 // Persistent grid: one workgroup per CU (152 KiB of LDS each), capped by the tile count.

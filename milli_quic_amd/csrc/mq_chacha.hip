@@ -150,6 +150,10 @@ __device__ __forceinline__ void load_key8(const uint32_t* src, uint32_t (&k)[8])
   k[0] = a.x; k[1] = a.y; k[2] = a.z; k[3] = a.w; k[4] = b.x; k[5] = b.y; k[6] = b.z; k[7] = b.w;
 }
 
+// Seal: the HP block (slot nblk) lies in an iteration the packet's keystream runs anyway — not in
+// iteration 0 (no ciphertext sample yet) and not alone in an extra iteration (nblk % 8 == 0)
+__device__ __forceinline__ bool cc_hp_in_slot(uint32_t nblk) { return nblk > (uint32_t)kLanesPerPkt && (nblk % kLanesPerPkt) != 0; }
+
 // RFC 9001 §5.4.1: apply the 5-byte mask to byte 0 (low 4 / 5 bits) and the PN bytes.
 template <class S>
 __device__ __forceinline__ void apply_hp(const S& sp, typename S::off_t pkt, const mq_pkt_desc& d,
@@ -268,7 +272,8 @@ struct ChaChaPolicy {
   // Poly1305 key); the HP block runs in the first free slot after ctr 1 (whose ciphertext holds
   // the sample) unless the sample reaches into the tag (tiny payloads: a separate phase).
   template <class S, class G>
-  static __device__ __forceinline__ void seal(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j, G& stg) {
+  static __device__ __forceinline__ void seal(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j, G& stg,
+                                              bool short_post) {
     const mq_pkt_desc& d = c.d;
     uint32_t key[8];
     load_key8(row->key, key);
@@ -284,17 +289,21 @@ struct ChaChaPolicy {
     stg.issue();  // packet bytes stream into LDS while the first keystream block is computed
     const uint32_t nblk = 1 + (P + 63) / 64;  // block 0 = Poly1305 key, 1.. = keystream
     const bool hp_on = c.act && !(d.flags & MQ_PKT_NO_HP);
-    const bool hp_post = hp_on && 20 > P + d.pn_len;  // sample reaches into the tag
+    // short_post (wave-uniform): packets whose HP block has no free slot in the iterations their
+    // keystream needs get it from mq_chacha_seal_hp_kernel afterwards
+    const bool hp_defer = short_post && hp_on && !cc_hp_in_slot(nblk);
+    const bool hp_post = hp_on && !hp_defer && 20 > P + d.pn_len;  // sample reaches into the tag
+    const bool hp_slot = hp_on && !hp_defer && !hp_post;
     uint32_t hp_it = nblk / kLanesPerPkt, hp_lane = nblk % kLanesPerPkt;
     if (hp_it == 0) { hp_it = 1; hp_lane = 0; }
-    const uint32_t iters = max((nblk + kLanesPerPkt - 1) / kLanesPerPkt, (hp_on && !hp_post) ? hp_it + 1 : 0u);
+    const uint32_t iters = max((nblk + kLanesPerPkt - 1) / kLanesPerPkt, hp_slot ? hp_it + 1 : 0u);
     const uint32_t Imax = wave_max_u32(c.act ? iters : 0u);
     uint32_t m0 = 0, m1 = 0;
     bool have_mask = false;
     for (uint32_t it = 0; it < Imax; ++it) {
       const uint32_t ctr = (uint32_t)j + kLanesPerPkt * it;
       const bool a = c.act && ctr < nblk;
-      const bool is_hp = hp_on && !hp_post && it == hp_it && (uint32_t)j == hp_lane;
+      const bool is_hp = hp_slot && it == hp_it && (uint32_t)j == hp_lane;
       uint32_t w[17];
       if (it > 0) load_block(sp, pay, a ? ctr : 0u, w);  // LDS reads in flight during the block function
       uint32_t cc = ctr;
@@ -455,7 +464,7 @@ __device__ __forceinline__ void chacha_tile(const KeyRow* __restrict__ kt, uint3
                                             uint64_t arena_len, const mq_pkt_desc* __restrict__ desc, uint32_t n,
                                             const uint32_t* __restrict__ index, const uint32_t* __restrict__ n_dev,
                                             uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,
-                                            const uint2* __restrict__ hpm) {
+                                            const uint2* __restrict__ hpm, bool short_post) {
   constexpr uint32_t W = OPEN ? kCcOpenWaves : 1;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t w = W > 1 ? threadIdx.x >> 6 : 0u;
@@ -494,7 +503,7 @@ __device__ __forceinline__ void chacha_tile(const KeyRow* __restrict__ kt, uint3
     MQ_STAMP(tile_id, 1);
     const uint32_t pkt = pl.slot * 16u + pl.head();
     if (OPEN) ChaChaPolicy::template open<SINGLE, LdsSpace>(sp, pkt, c, row, j, false, stg, pool);
-    else ChaChaPolicy::template seal<LdsSpace>(sp, pkt, c, row, j, stg);
+    else ChaChaPolicy::template seal<LdsSpace>(sp, pkt, c, row, j, stg, short_post);
     MQ_STAMP(tile_id, 6);
     wave_sync();
     stage_out(wsm, arena, lane, c.act, pl);
@@ -503,7 +512,7 @@ __device__ __forceinline__ void chacha_tile(const KeyRow* __restrict__ kt, uint3
     GlobalSpace sp{arena, arena_len};
     NoStager stg;
     if (OPEN) ChaChaPolicy::template open<SINGLE, GlobalSpace>(sp, off, c, row, j, true, stg, pool);
-    else ChaChaPolicy::template seal<GlobalSpace>(sp, off, c, row, j, stg);
+    else ChaChaPolicy::template seal<GlobalSpace>(sp, off, c, row, j, stg, short_post);
   }
   tile_status<OPEN>(c, j, status, pn_out);
 }
@@ -512,15 +521,16 @@ __device__ __forceinline__ void chacha_tile(const KeyRow* __restrict__ kt, uint3
   extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void NAME_SEAL(    \
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
-      const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status) {                                 \
-    chacha_tile<false, SINGLE>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr, nullptr); \
+      const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint32_t short_post) {            \
+    chacha_tile<false, SINGLE>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr, nullptr, \
+                               short_post != 0);                                                          \
   }                                                                                                       \
   extern "C" __global__ __launch_bounds__(64 * kCcOpenWaves) __attribute__((amdgpu_waves_per_eu(4))) void NAME_OPEN( \
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
       const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,    \
       const uint2* __restrict__ hpm) {                                                                    \
-    chacha_tile<true, SINGLE>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm); \
+    chacha_tile<true, SINGLE>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm, false); \
   }
 MQ_CHACHA_KERNELS(mq_chacha_seal_kernel, mq_chacha_open_kernel, false)
 MQ_CHACHA_KERNELS(mq_chacha_seal1_kernel, mq_chacha_open1_kernel, true)
@@ -565,8 +575,8 @@ __global__ __launch_bounds__(256) void mq_chacha_open_hp_kernel(
   uint32_t m0, m1;
   if (DECODE) {  // PN bytes and sample (contiguous) and the first byte in one round of loads
     uint32_t w[5];
-    load_words<5>(sp, at - 4, w);
-    const uint8_t b0 = arena[d.offset];
+    uint8_t b0;
+    prepass_header(arena, d, b0, w);
     const uint32_t smp[4] = {w[1], w[2], w[3], w[4]};
     ChaChaPolicy::hp_mask_words(smp, row, m0, m1);
     hpm[i] = prepass_decode_words(b0, w[0], d, m0, m1);
@@ -574,6 +584,30 @@ __global__ __launch_bounds__(256) void mq_chacha_open_hp_kernel(
     ChaChaPolicy::hp_mask(sp, at, row, m0, m1);
     hpm[i] = make_uint2(m0, m1);
   }
+}
+
+// Seal post-pass (list mode): header protection of the sealed packets whose HP block had no free
+// slot in their tile (short packets: nblk <= 8 or a multiple of 8, incl. samples reaching into the
+// tag) — transmit.rs:713-719 with ChaChaHeaderProtection::mask (rustcrypto.rs:197-220), one
+// packet per lane: sample = the 16 bytes at pn_offset + 4 of the sealed packet, mask applied to
+// byte 0 (low 4 / 5 bits) and the PN bytes (RFC 9001 §5.4.1).
+__global__ __launch_bounds__(256) void mq_chacha_seal_hp_kernel(
+    const KeyRow* __restrict__ kt, uint8_t* __restrict__ arena, const mq_pkt_desc* __restrict__ desc, uint32_t n,
+    const uint32_t* __restrict__ index, const uint32_t* __restrict__ n_dev, const uint8_t* __restrict__ status) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t count = n_dev ? *n_dev : n;
+  if (t >= count) return;
+  const uint32_t i = index ? index[t] : t;
+  if (i == kListHole || status[i] != MQ_OK) return;
+  const mq_pkt_desc d = desc[i];
+  const uint32_t P = d.len - ((uint32_t)d.pn_offset + d.pn_len) - 16, nblk = 1 + (P + 63) / 64;
+  if ((d.flags & MQ_PKT_NO_HP) || cc_hp_in_slot(nblk)) return;  // records are NO_HP
+  uint32_t w[5], m0, m1;
+  uint8_t b0;
+  prepass_header(arena, d, b0, w);  // inside the packet (validated: pn_offset + 20 <= len)
+  const uint32_t smp[4] = {w[1], w[2], w[3], w[4]};
+  ChaChaPolicy::hp_mask_words(smp, kt + d.key_id, m0, m1);
+  seal_apply_hp(arena, d, b0, w[0], m0, m1);
 }
 
 // ---- host-side launchers (called from mq_host.cpp) -------------------------------------------
@@ -593,9 +627,18 @@ hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_
     hipLaunchKernelGGL(n_rows == 1 ? mq_chacha_open1_kernel : mq_chacha_open_kernel,
                        dim3((tiles + kCcOpenWaves - 1) / kCcOpenWaves), dim3(kWave * kCcOpenWaves), kLdsBytes * kCcOpenWaves, s, kt,
                        n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm);
-  else
-    hipLaunchKernelGGL(n_rows == 1 ? mq_chacha_seal1_kernel : mq_chacha_seal_kernel, dim3(tiles), dim3(kWave), kLdsBytes,
-                       s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status);
+  if (open) return hipGetLastError();
+  // list mode (mixed batches: length-sorted tiles, the short classes at the end) defers the HP
+  // blocks that would cost their tile an extra iteration to the one-packet-per-lane post-pass
+  const uint32_t short_post = index ? 1u : 0u;
+  hipLaunchKernelGGL(n_rows == 1 ? mq_chacha_seal1_kernel : mq_chacha_seal_kernel, dim3(tiles), dim3(kWave), kLdsBytes,
+                     s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, short_post);
+  if (short_post) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(mq_chacha_seal_hp_kernel, dim3((n + 255) / 256), dim3(256), 0, s, kt, arena, desc, n, index,
+                       n_dev, status);
+  }
   return hipGetLastError();
 }
 

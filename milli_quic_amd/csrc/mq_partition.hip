@@ -15,24 +15,29 @@
 //
 // AES packets are further split by key, so that the multi-key AES kernels find key-uniform
 // tiles (they then multiply through a GHASH table of that key's H^8 instead of the bit-holed
-// product): the batch's majority AES key (Boyer-Moore vote; in a server's mix the 1-RTT key of
-// the busiest path; counts[2] = its row, or 0xFFFFFFFF) goes first, by length class; then, when
+// product): the batch's majority AES key (Boyer-Moore vote over a 4096-descriptor sample; in a
+// server's mix the 1-RTT key of the busiest path; counts[2] = its row, or 0xFFFFFFFF) goes
+// first, by length class; then, when
 // the key table is small enough for one counter per (row, 128-B length class) in the workspace
 // ("keyed" layout), every other AES key's packets follow key by key, each key's segment longest
 // class first and padded to whole tiles. Otherwise the other keys share length classes as the
 // majority key does. With no majority the vote's candidate is just some key: results are the
 // same either way, only the tile composition changes.
 //
-// Launches: per-block votes, one vote reduction, per-block class histograms (class-major) and,
-// keyed, per-(row, class) counts (global atomics, one per distinct bin per wave), one exclusive
-// scan of the histograms, keyed: one scan of the per-row counts into bin bases, scatter.
+// Launches: fill + sampled vote (mq_part_init_kernel); per-block class histograms
+// (class-major) and, keyed, per-(row, class) counts (global atomics, one per distinct bin per
+// wave); one workgroup for the exclusive scan of the histograms and, keyed, the scan of the
+// per-row counts into bin bases; scatter. (r02: five launches with a full vote pass took ~126 us per
+// mixed 2^20-packet partition.)
 #include "mq_tile.h"
 
 using namespace mq;
 
 namespace {
-constexpr int kPartThreads = 256;
-constexpr int kPartItems = 16;  // descriptors per thread
+// 1024-thread blocks of 4 descriptors per thread: 16 waves per CU hide the latency of the
+// dependent loads and atomics (r02: 256 x 16 ran one wave per SIMD)
+constexpr int kPartThreads = 1024;
+constexpr int kPartItems = 4;  // descriptors per thread
 constexpr int kPartBlock = kPartThreads * kPartItems;
 constexpr uint32_t kLenClasses = 32;  // per group: min(len / 64, 31), longest first
 constexpr uint32_t kGroups = 3;       // AES with the hot key, other AES (both: list 0), the rest (list 1)
@@ -41,21 +46,34 @@ constexpr uint32_t kBudgetChunks = kDataBudget / 16;
 constexpr uint32_t kNoKey = 0xFFFFFFFFu;
 constexpr uint32_t kKeyClasses = 16;  // keyed layout: per row, min(len / 128, 15), longest first
 
-__device__ __forceinline__ bool is_aes(const KeyRow* kt, uint32_t n_rows, const mq_pkt_desc& d) {
-  return d.key_id < n_rows && kt[d.key_id].suite == MQ_SUITE_AES128GCM;
+// What the partition reads of a descriptor: key row, length, and whether the row is AES-128-GCM.
+// A thread's kPartItems descriptors are fetched together (fields first, then the rows' suites),
+// so it waits on memory twice rather than twice per descriptor.
+struct PartItem { uint32_t key, len; bool aes; };
+__device__ __forceinline__ void part_fetch(const KeyRow* __restrict__ kt, uint32_t n_rows,
+                                           const mq_pkt_desc* __restrict__ desc, uint32_t n,
+                                           PartItem (&it)[kPartItems]) {
+  const uint32_t base = blockIdx.x * kPartBlock + threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < kPartItems; ++k) {
+    const uint32_t i = base + k * kPartThreads;
+    it[k].key = i < n ? desc[i].key_id : 0xFFFFFFFFu;
+    it[k].len = i < n ? desc[i].len : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < kPartItems; ++k) it[k].aes = it[k].key < n_rows && kt[it[k].key].suite == MQ_SUITE_AES128GCM;
 }
 
 // class = group * kLenClasses + (31 - length bucket)
-__device__ __forceinline__ uint32_t part_class(const KeyRow* kt, uint32_t n_rows, uint32_t hot,
-                                               const mq_pkt_desc& d) {
-  const uint32_t g = is_aes(kt, n_rows, d) ? (d.key_id == hot ? 0u : 1u) : 2u;
-  const uint32_t b = min(d.len >> 6, kLenClasses - 1);
+__device__ __forceinline__ uint32_t part_class(uint32_t hot, const PartItem& x) {
+  const uint32_t g = x.aes ? (x.key == hot ? 0u : 1u) : 2u;
+  const uint32_t b = min(x.len >> 6, kLenClasses - 1);
   return g * kLenClasses + (kLenClasses - 1 - b);
 }
 
 // keyed layout: the bin of a non-majority AES packet (row-major, longest class first)
-__device__ __forceinline__ uint32_t key_bin(const mq_pkt_desc& d) {
-  return d.key_id * kKeyClasses + (kKeyClasses - 1 - min(d.len >> 7, kKeyClasses - 1));
+__device__ __forceinline__ uint32_t key_bin(const PartItem& x) {
+  return x.key * kKeyClasses + (kKeyClasses - 1 - min(x.len >> 7, kKeyClasses - 1));
 }
 // Per distinct bin among the wave's lanes with `pend`, one atomicAdd of its lane count on
 // ctr[bin] — all issued by one instruction: the wave sorts its (bin, lane) pairs (bitonic, 21
@@ -107,15 +125,18 @@ __device__ __forceinline__ uint2 vote_join(uint2 a, uint2 b) {
   return a.y >= b.y ? make_uint2(a.x, a.y - b.y) : make_uint2(b.x, b.y - a.y);
 }
 
-__device__ __forceinline__ uint2 block_vote(uint2 v) {  // 256 threads
-  __shared__ uint2 s_v[kPartThreads];
-  s_v[threadIdx.x] = v;
+__device__ __forceinline__ uint2 block_vote(uint2 v) {  // kPartThreads threads: waves, then wave 0
+  __shared__ uint2 s_v[kPartThreads / kWave];
+#pragma unroll
+  for (int d = kWave / 2; d > 0; d >>= 1)
+    v = vote_join(v, make_uint2((uint32_t)__shfl_xor((int)v.x, d, kWave), (uint32_t)__shfl_xor((int)v.y, d, kWave)));
+  if ((threadIdx.x & (kWave - 1)) == 0) s_v[threadIdx.x / kWave] = v;
   __syncthreads();
-  for (int d = kPartThreads / 2; d > 0; d >>= 1) {
-    if ((int)threadIdx.x < d) s_v[threadIdx.x] = vote_join(s_v[threadIdx.x], s_v[threadIdx.x + d]);
-    __syncthreads();
-  }
-  return s_v[0];
+  v = (threadIdx.x & (kWave - 1)) < kPartThreads / kWave ? s_v[threadIdx.x & (kWave - 1)] : make_uint2(kNoKey, 0u);
+#pragma unroll
+  for (int d = kPartThreads / kWave / 2; d > 0; d >>= 1)
+    v = vote_join(v, make_uint2((uint32_t)__shfl_xor((int)v.x, d, kWave), (uint32_t)__shfl_xor((int)v.y, d, kWave)));
+  return v;  // every wave holds the result in every lane
 }
 
 // Packets per tile of a class: AES tiles stream from HBM (no LDS image), so always 8. ChaCha
@@ -142,47 +163,62 @@ uint32_t mq_partition_list_cap(uint32_t n) {
   return (uint32_t)((c + kPktsPerTile - 1) & ~(uint64_t)(kPktsPerTile - 1));
 }
 
-extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_vote_kernel(
-    const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_pkt_desc* __restrict__ desc, uint32_t n,
-    uint2* __restrict__ votes) {
-  uint2 v = make_uint2(kNoKey, 0u);
-  for (int k = 0; k < kPartItems; ++k) {
-    const uint32_t i = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
-    if (i < n) {
-      const mq_pkt_desc d = desc[i];
-      if (is_aes(kt, n_rows, d)) v = vote_join(v, make_uint2(d.key_id, 1u));
-    }
+// The batch's hot AES key: Boyer-Moore vote over a fixed sample of kVoteSample descriptors
+// (evenly spaced), one workgroup. The hot key only shapes tiles; any candidate gives the same
+// results.
+constexpr uint32_t kVoteSample = 4096;
+__device__ __forceinline__ uint32_t sampled_hot(const KeyRow* __restrict__ kt, uint32_t n_rows,
+                                                const mq_pkt_desc* __restrict__ desc, uint32_t n) {
+  constexpr int kPer = kVoteSample / kPartThreads;
+  const uint32_t S = min(n, kVoteSample), stride = n / S;
+  uint32_t key[kPer];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const uint32_t k = threadIdx.x + kPartThreads * q;
+    key[q] = k < S ? desc[k * stride].key_id : 0xFFFFFFFFu;
   }
-  v = block_vote(v);
-  if (threadIdx.x == 0) votes[blockIdx.x] = v;
-}
-
-// Single workgroup: the batch's vote; meta[0] = the hot key row (kNoKey if no AES packet)
-extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_vote_reduce_kernel(
-    const uint2* __restrict__ votes, uint32_t nblocks, uint32_t* __restrict__ meta) {
   uint2 v = make_uint2(kNoKey, 0u);
-  for (uint32_t k = threadIdx.x; k < nblocks; k += kPartThreads) v = vote_join(v, votes[k]);
+#pragma unroll
+  for (int q = 0; q < kPer; ++q)
+    if (key[q] < n_rows && kt[key[q]].suite == MQ_SUITE_AES128GCM) v = vote_join(v, make_uint2(key[q], 1u));
   v = block_vote(v);
-  if (threadIdx.x == 0) meta[0] = v.y ? v.x : kNoKey;
+  return v.y ? v.x : kNoKey;
+}
+// First launch: fills the lists with holes and zeroes the keyed bins (grid-stride, 16-B stores);
+// block 0 also runs the sampled vote, so it costs no launch of its own.
+extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_init_kernel(
+    const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_pkt_desc* __restrict__ desc, uint32_t n,
+    uint32_t* __restrict__ hot_p, uint4* __restrict__ list, uint32_t list_q, uint4* __restrict__ bins,
+    uint32_t bins_q) {
+  if (blockIdx.x == 0) {  // block-uniform
+    const uint32_t hot = sampled_hot(kt, n_rows, desc, n);
+    if (threadIdx.x == 0) *hot_p = hot;
+  }
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < list_q; q += stride)
+    list[q] = make_uint4(kListHole, kListHole, kListHole, kListHole);
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < bins_q; q += stride) bins[q] = make_uint4(0, 0, 0, 0);
 }
 
-// keyed (bins != nullptr): non-majority AES packets are counted per (row, class) bin instead
+// Per block: the class histogram of its kPartBlock descriptors; keyed (bins != nullptr):
+// non-majority AES packets are counted per (row, class) bin instead.
 extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_count_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_pkt_desc* __restrict__ desc, uint32_t n,
     uint32_t nblocks, const uint32_t* __restrict__ hot_p, uint32_t* __restrict__ hist, uint32_t* __restrict__ bins) {
   __shared__ uint32_t s_cnt[kClasses];
+  PartItem it[kPartItems];
+  part_fetch(kt, n_rows, desc, n, it);
   if (threadIdx.x < kClasses) s_cnt[threadIdx.x] = 0;
-  __syncthreads();
   const uint32_t hot = *hot_p;
+  __syncthreads();
+#pragma unroll
   for (int k = 0; k < kPartItems; ++k) {
     const uint32_t i = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
     const bool in = i < n;
-    mq_pkt_desc d{};
-    if (in) d = desc[i];
-    const uint32_t c = in ? part_class(kt, n_rows, hot, d) : 0u;
+    const uint32_t c = in ? part_class(hot, it[k]) : 0u;
     const bool keyed = bins && in && c / kLenClasses == 1;  // wave-uniform branch below
     uint32_t pos, idx;
-    if (bins && __ballot(keyed)) wave_bin_add<false>(bins, keyed ? key_bin(d) : 0u, keyed, i, pos, idx);
+    if (bins && __ballot(keyed)) wave_bin_add<false>(bins, keyed ? key_bin(it[k]) : 0u, keyed, i, pos, idx);
     if (in && !keyed) atomicAdd(&s_cnt[c], 1u);
   }
   __syncthreads();
@@ -198,10 +234,15 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_count_kernel(
 // kernel waits on memory once instead of once per class (r01: 26 us per partition, rocprof).
 constexpr int kScanWaves = 16, kClassesPerWave = kClasses / kScanWaves;
 static_assert(kClasses % kScanWaves == 0, "classes per scan wave");
+__device__ void key_scan(uint32_t* __restrict__ bins, uint32_t n_rows, uint32_t* __restrict__ counts, uint32_t base);
+
 extern "C" __global__ __launch_bounds__(64 * kScanWaves) void mq_part_scan_kernel(uint32_t* __restrict__ hist,
                                                                                  uint32_t nblocks, uint32_t cap,
                                                                                  uint32_t* __restrict__ counts,
-                                                                                 uint32_t* __restrict__ seg) {
+                                                                                 uint32_t* __restrict__ seg,
+                                                                                 uint32_t* __restrict__ bins,
+                                                                                 uint32_t n_rows) {
+  __shared__ uint32_t s_list0;
   __shared__ uint32_t s_tot[kClasses];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t carry[kClassesPerWave];
@@ -238,43 +279,56 @@ extern "C" __global__ __launch_bounds__(64 * kScanWaves) void mq_part_scan_kerne
     for (int q = 0; q < kClassesPerWave; ++q) s_tot[wave + kScanWaves * q] = carry[q];
   }
   __syncthreads();
-  if (threadIdx.x < 2) {
-    const uint32_t s = threadIdx.x;
-    const uint32_t c0 = s == 0 ? 0u : 2 * kLenClasses, c1 = s == 0 ? 2 * kLenClasses : kClasses;
-    uint32_t e = 0;
-    for (uint32_t c = c0; c < c1; ++c) {
-      seg[c] = s * cap + e;
-      const uint32_t ppt = class_ppt(c);
-      e += kPktsPerTile * ((s_tot[c] + ppt - 1) / ppt);
+  static_assert(2 * kLenClasses == kWave && kClasses - 2 * kLenClasses <= kWave, "one wave per list");
+  if (wave < 2) {  // wave s lays out list s: lane = class (list 0: classes 0..63, list 1: 64..95)
+    const uint32_t s = (uint32_t)wave, c = (s == 0 ? 0u : 2 * kLenClasses) + (uint32_t)lane;
+    const bool in = c < (s == 0 ? 2 * kLenClasses : kClasses);
+    const uint32_t ppt = in ? class_ppt(c) : 1u;
+    const uint32_t ent = in ? kPktsPerTile * ((s_tot[c] + ppt - 1) / ppt) : 0u;
+    const uint32_t incl = wave_incl_scan(ent), e = lane_u32(incl, kWave - 1);
+    if (in) seg[c] = s * cap + incl - ent;
+    if (lane == 0) {
+      // mq_partition_list_cap bounds e; the clamp only keeps a broken bound from running a suite
+      // kernel over the other list
+      counts[s] = min(e, cap);
+      if (s == 0) s_list0 = e;
     }
-    // mq_partition_list_cap bounds e; the clamp only keeps a broken bound from running a suite
-    // kernel over the other list
-    counts[s] = min(e, cap);
+  }
+  if (bins) {  // keyed layout: the other AES keys' segments follow (workgroup-uniform)
+    __syncthreads();
+    key_scan(bins, n_rows, counts, s_list0);
   }
 }
 
-// Keyed layout, single workgroup: each row's segment (its bins' packets, whole tiles) follows
-// the majority key's classes in list 0; bins[b] becomes the list position of bin b's first
-// packet (the scatter's cursor) and counts[0] the list's entries.
-constexpr int kKeyScanThreads = 1024;
-extern "C" __global__ __launch_bounds__(kKeyScanThreads) void mq_part_key_scan_kernel(uint32_t* __restrict__ bins,
-                                                                                     uint32_t n_rows,
-                                                                                     uint32_t* __restrict__ counts) {
+// Keyed layout (the scan kernel's workgroup, after the class segments): each row's segment (its
+// bins' packets, whole tiles) follows the majority key's classes in list 0, which end on a tile
+// boundary at `base`; bins[b] becomes the list position of bin b's first packet (the scatter's
+// cursor) and counts[0] the list's entries.
+static_assert(64 * kScanWaves == 1024, "key scan: one row per thread of a 1024-thread workgroup");
+__device__ void key_scan(uint32_t* __restrict__ bins, uint32_t n_rows, uint32_t* __restrict__ counts, uint32_t base) {
+  constexpr int kKeyScanThreads = 64 * kScanWaves;
   __shared__ uint32_t s_wave[kKeyScanThreads / kWave];
   __shared__ uint32_t s_base;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (threadIdx.x == 0) s_base = counts[0];  // the majority key's classes end on a tile boundary
+  if (threadIdx.x == 0) s_base = base;
   __syncthreads();
+  auto fetch = [&](uint32_t r, uint4 (&v)[kKeyClasses / 4]) {
+    const uint4* src = (const uint4*)(bins + (size_t)r * kKeyClasses);
+#pragma unroll
+    for (int q = 0; q < (int)kKeyClasses / 4; ++q) v[q] = r < n_rows ? src[q] : make_uint4(0, 0, 0, 0);
+  };
+  uint4 nxt[kKeyClasses / 4];
+  fetch(threadIdx.x, nxt);
   for (uint32_t r0 = 0; r0 < n_rows; r0 += kKeyScanThreads) {  // one row per thread
     const uint32_t r = r0 + threadIdx.x;
     uint32_t c[kKeyClasses], tot = 0;
-    const uint4* src = (const uint4*)(bins + (size_t)r * kKeyClasses);
 #pragma unroll
     for (int q = 0; q < (int)kKeyClasses / 4; ++q) {
-      const uint4 v = r < n_rows ? src[q] : make_uint4(0, 0, 0, 0);
+      const uint4 v = nxt[q];
       c[4 * q] = v.x; c[4 * q + 1] = v.y; c[4 * q + 2] = v.z; c[4 * q + 3] = v.w;
       tot += v.x + v.y + v.z + v.w;
     }
+    fetch(r + kKeyScanThreads, nxt);  // the next round's row, in flight during this one
     const uint32_t ent = (tot + kPktsPerTile - 1) & ~(kPktsPerTile - 1);
     const uint32_t incl = wave_incl_scan(ent);
     if (lane == 63) s_wave[wave] = incl;
@@ -310,20 +364,21 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_scatter_kerne
     uint32_t nblocks, const uint32_t* __restrict__ hot_p, const uint32_t* __restrict__ hist,
     const uint32_t* __restrict__ seg, uint32_t* __restrict__ list, uint32_t* __restrict__ bins) {
   __shared__ uint32_t s_rank[kClasses];
+  PartItem it[kPartItems];
+  part_fetch(kt, n_rows, desc, n, it);
   const uint32_t hot = *hot_p;
   const int lane = threadIdx.x & 63;
   if (threadIdx.x < kClasses) s_rank[threadIdx.x] = hist[(size_t)threadIdx.x * nblocks + blockIdx.x];
   __syncthreads();
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
   for (int k = 0; k < kPartItems; ++k) {
     const uint32_t i = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
-    mq_pkt_desc d{};
-    if (i < n) d = desc[i];
-    const uint32_t c = i < n ? part_class(kt, n_rows, hot, d) : 0u;
+    const uint32_t c = i < n ? part_class(hot, it[k]) : 0u;
     const bool keyed = bins && i < n && c / kLenClasses == 1;
     if (bins && __ballot(keyed)) {
       uint32_t pos, idx;
-      wave_bin_add<true>(bins, keyed ? key_bin(d) : 0u, keyed, i, pos, idx);
+      wave_bin_add<true>(bins, keyed ? key_bin(it[k]) : 0u, keyed, i, pos, idx);
       if (pos != 0xFFFFFFFFu) list[pos] = idx;
     }
     const bool in = i < n && !keyed;
@@ -356,7 +411,7 @@ static bool keyed_layout(uint32_t n, uint32_t n_rows) {
          (uint64_t)n + kPktsPerTile * kLenClasses + (uint64_t)(kPktsPerTile - 1) * n_rows <= mq_partition_list_cap(n);
 }
 
-// list (2 x cap entries) | class histograms (kClasses per block) + votes (2 words per block) |
+// list (2 x cap entries) | class histograms (kClasses per block) |
 // meta (2 totals, hot row, pad, kClasses segment starts) | keyed bins, 256-B aligned pieces
 static size_t part_align(size_t b) { return (b + 255) & ~(size_t)255; }
 
@@ -367,19 +422,15 @@ hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_d
   const uint32_t cap = mq_partition_list_cap(n);
   uint32_t* hot = counts + 2;  // meta: counts[0..1] | hot row | pad | seg[kClasses]
   uint32_t* seg = counts + 4;
-  uint2* votes = (uint2*)(hist + (size_t)kClasses * nblocks);
   uint32_t* bins = keyed_layout(n, n_rows) ? (uint32_t*)((uint8_t*)counts + part_align(sizeof(uint32_t) * (4 + kClasses)))
                                            : nullptr;
-  hipError_t e = hipMemsetAsync(list, 0xff, sizeof(uint32_t) * 2 * (size_t)cap, s);  // holes
-  if (e == hipSuccess && bins) e = hipMemsetAsync(bins, 0, sizeof(uint32_t) * kKeyClasses * (size_t)n_rows, s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(mq_part_vote_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, kt, n_rows, desc, n, votes);
-  hipLaunchKernelGGL(mq_part_vote_reduce_kernel, dim3(1), dim3(kPartThreads), 0, s, votes, nblocks, hot);
+  const uint32_t list_q = cap / 2, bins_q = bins ? kKeyClasses / 4 * n_rows : 0u;  // 16-B words
+  hipLaunchKernelGGL(mq_part_init_kernel, dim3(min(256u, (list_q + bins_q + kPartThreads - 1) / kPartThreads)),
+                     dim3(kPartThreads), 0, s, kt, n_rows, desc, n, hot, (uint4*)list, list_q, (uint4*)bins, bins_q);
   hipLaunchKernelGGL(mq_part_count_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, kt, n_rows, desc, n,
                      nblocks, hot, hist, bins);
-  hipLaunchKernelGGL(mq_part_scan_kernel, dim3(1), dim3(64 * kScanWaves), 0, s, hist, nblocks, cap, counts, seg);
-  if (bins)
-    hipLaunchKernelGGL(mq_part_key_scan_kernel, dim3(1), dim3(kKeyScanThreads), 0, s, bins, n_rows, counts);
+  hipLaunchKernelGGL(mq_part_scan_kernel, dim3(1), dim3(64 * kScanWaves), 0, s, hist, nblocks, cap, counts, seg,
+                     bins, n_rows);
   hipLaunchKernelGGL(mq_part_scatter_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, kt, n_rows, desc, n,
                      nblocks, hot, hist, seg, list, bins);
   return hipGetLastError();
@@ -388,7 +439,7 @@ hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_d
 size_t mq_partition_workspace(uint32_t n) {
   const size_t nblocks = (n + kPartBlock - 1) / kPartBlock;
   return part_align(sizeof(uint32_t) * 2 * (size_t)mq_partition_list_cap(n)) +
-         part_align(sizeof(uint32_t) * (kClasses + 2) * nblocks) + part_align(sizeof(uint32_t) * (4 + kClasses)) +
+         part_align(sizeof(uint32_t) * kClasses * nblocks) + part_align(sizeof(uint32_t) * (4 + kClasses)) +
          part_align(sizeof(uint32_t) * key_bins(n));
 }
 
@@ -396,5 +447,5 @@ size_t mq_partition_workspace(uint32_t n) {
 void mq_partition_layout(uint32_t n, size_t* hist_off, size_t* counts_off) {
   const size_t nblocks = (n + kPartBlock - 1) / kPartBlock;
   *hist_off = part_align(sizeof(uint32_t) * 2 * (size_t)mq_partition_list_cap(n));
-  *counts_off = *hist_off + part_align(sizeof(uint32_t) * (kClasses + 2) * nblocks);
+  *counts_off = *hist_off + part_align(sizeof(uint32_t) * kClasses * nblocks);
 }

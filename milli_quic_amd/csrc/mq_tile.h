@@ -236,6 +236,32 @@ __device__ __forceinline__ bool prepass_pick(uint32_t t, uint32_t suite, const K
   return true;
 }
 
+// Pre-pass header read: the received first byte and the 20 bytes at pn_offset (PN bytes, then the
+// sample) as 5 little-endian words, with one 16-B and one 4-B unaligned load — prepass_pick has
+// checked that the packet, and so these bytes, lie inside the arena
+typedef uint32_t __attribute__((aligned(1))) u32_u;
+__device__ __forceinline__ void prepass_header(const uint8_t* __restrict__ arena, const mq_pkt_desc& d, uint8_t& b0,
+                                               uint32_t (&w)[5]) {
+  const uint8_t* p = arena + d.offset + d.pn_offset;
+  const uint4 a = ld16(p);
+  w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+  w[4] = *(const u32_u*)(p + 16);
+  b0 = arena[d.offset];
+}
+
+// Seal post-pass: XOR the 5-byte HP mask (m0 = bytes 0..3, m1 = byte 4) into the sealed packet's
+// first byte (low 4 / 5 bits) and PN bytes. w0 = the 4 bytes at pn_offset as loaded by
+// prepass_header: the PN bytes change with one unaligned dword store (bytes past pn_len keep
+// their values; the tile kernel is done and no other lane owns them).
+__device__ __forceinline__ void seal_apply_hp(uint8_t* __restrict__ arena, const mq_pkt_desc& d, uint8_t b0,
+                                              uint32_t w0, uint32_t m0, uint32_t m1) {
+  uint8_t* h = arena + d.offset;
+  h[0] = b0 ^ ((uint8_t)m0 & ((d.flags & MQ_PKT_LONG_HEADER) ? 0x0f : 0x1f));
+  const uint32_t mk = (m0 >> 8) | (m1 << 24);
+  const uint32_t keep = d.pn_len >= 4 ? 0xffffffffu : (1u << (8 * d.pn_len)) - 1u;
+  *(u32_u*)(h + d.pn_offset) = w0 ^ (mk & keep);
+}
+
 // Batch-open pre-pass output: instead of the raw mask, what the tile kernel derives from it —
 // the unmasked first byte (| 0x100) and the unmasked truncated packet number (recv.rs:371-391) —
 // so the tile kernel knows pn_len and the nonce before its packet has landed in LDS.
