@@ -196,6 +196,9 @@ __shared__ __attribute__((aligned(16))) uint32_t g_aes_lds[(kGhBytes + kTwBytes)
 // multi-key tile kernels: per wave, the GHASH half table (gh_mul_half) of its tile's key
 constexpr uint32_t kGhHalfBytes = 4096, kAesMultiWaves = 12;
 __shared__ __attribute__((aligned(16))) uint32_t g_aes_wtab[kAesMultiWaves * kGhHalfBytes / 4];
+// single-key tile kernels: half tables of H^1 .. H^8 for the tag's final multiply (lane j of a
+// packet multiplies by H^e, e = 1..8 blocks after its last one: table e - 1)
+__shared__ __attribute__((aligned(16))) uint32_t g_aes_fin[8 * kGhHalfBytes / 4];
 
 __device__ __forceinline__ uint32_t xtime8(uint32_t s) { return ((s << 1) ^ ((s & 0x80) ? 0x11bu : 0u)) & 0xffu; }
 
@@ -278,9 +281,11 @@ __device__ __forceinline__ void aes_final(const K& key, const TwLane& L, uint32_
 template <class K>
 __device__ __forceinline__ void aes128_enc(const K& key, const TwLane& L, uint32_t (&s)[4]) {
 #if MQ_PROF_SKIP & 16
-  const uint4 k0 = key(0);
-  s[0] ^= k0.x; s[1] ^= k0.y; s[2] ^= k0.z ^ L.r0; s[3] ^= k0.w;
-  return;
+  {
+    const uint4 z = key(0);
+    s[0] ^= z.x; s[1] ^= z.y; s[2] ^= z.z ^ L.r0; s[3] ^= z.w;
+    return;
+  }
 #endif
   const uint4 k0 = key(0);
   s[0] ^= k0.x; s[1] ^= k0.y; s[2] ^= k0.z; s[3] ^= k0.w;

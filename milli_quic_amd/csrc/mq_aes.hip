@@ -143,13 +143,21 @@ struct AesStream {
   // tag = GHASH (final multiply by H^e, octet XOR) ^ E_K(J0) (lane 0's, broadcast)
   static __device__ __forceinline__ void finish(uint32_t (&acc)[4], const KeyRow* row, int j, const AesPkt& k,
                                                 const uint32_t (&ej0)[4], uint32_t (&tag)[4]) {
-    uint32_t hp[4];
     uint32_t e1 = (k.nblk + 8u - (uint32_t)j) & 7u;  // H^(e1 + 1): blocks after the lane's last
     pin(e1);  // keeps the H^e load and its preparation (36 VGPRs) after the tile loop
+#if MQ_PROF_SKIP & 64  // phase-cost diagnostic build only: no final multiply by H^e
+    acc[0] ^= e1; acc[1] ^= row->H[0][1];
+#else
+    if (GH == kGhWorkgroup) {  // single key: the workgroup's table of H^(e1 + 1), per lane
+      gh_mul_half(acc, (const uint8_t*)g_aes_fin + kGhHalfBytes * e1);
+    } else {
+      uint32_t hp[4];
 #pragma unroll
-    for (int w = 0; w < 4; ++w) hp[w] = brev(row->H[e1][w]);
-    const GfOp ml = gf_prepare(hp);
-    gf_mul(acc, ml);
+      for (int w = 0; w < 4; ++w) hp[w] = brev(row->H[e1][w]);
+      const GfOp ml = gf_prepare(hp);
+      gf_mul(acc, ml);
+    }
+#endif
 #pragma unroll
     for (int w = 0; w < 4; ++w) tag[w] = bswap32(brev(oct_xor(acc[w]))) ^ oct_bcast0(ej0[w]);
   }
@@ -452,9 +460,16 @@ __device__ __forceinline__ void aes_tables(const KeyRow* __restrict__ kt) {
   build_tw(threadIdx.x, blockDim.x);
   if (SINGLE) {
     if (threadIdx.x < kRkSlotBytes / 4) g_aes_keys[threadIdx.x] = kt[0].aes_rk[threadIdx.x];  // aes_rk || hp_rk
+    const uint32_t w = wave_id();
+    if (w < 8) {  // waves 0..7: the half table of H^(w + 1) for the tags' final multiplies
+      uint32_t hw[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) hw[q] = brev(kt[0].H[w][q]);
+      build_gh_half((uint8_t*)g_aes_fin + kGhHalfBytes * w, hw, (int)(threadIdx.x & (kWave - 1)));
+    }
     uint32_t h8[4];
 #pragma unroll
-    for (int w = 0; w < 4; ++w) h8[w] = brev(kt[0].H[7][w]);
+    for (int q = 0; q < 4; ++q) h8[q] = brev(kt[0].H[7][q]);
     build_gh(h8, threadIdx.x, blockDim.x);  // ends with a barrier
   } else {
     __syncthreads();

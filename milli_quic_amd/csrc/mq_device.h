@@ -220,7 +220,8 @@ __device__ __forceinline__ void u4w(uint4 v, uint32_t (&w)[4]) { w[0] = v.x; w[1
 // ------------------------------------------------------------------------------------------
 // MQ_PROF_SKIP (diagnostic builds from `make prof-variants`, never the product library): bit 1
 // skips the ChaCha rounds, 2 the MAC, 4 the LDS->HBM store, 8 the HBM->LDS staging, 16 the AES
-// rounds; the timing differences give each phase's cost under full load (tools/phase_cost.py).
+// rounds, 64 the AES tag's final multiply by H^e; the timing differences give each phase's cost
+// under full load (tools/phase_cost.py).
 #ifndef MQ_PROF_SKIP
 #define MQ_PROF_SKIP 0
 #endif
