@@ -109,18 +109,26 @@ __device__ __forceinline__ void poly_tag(const S& sp, typename S::off_t pkt, typ
     const uint32_t k_lo = act ? (uint32_t)((zA + kLanesPerPkt - 1) / kLanesPerPkt) : 0u;
     const int hi = ct_full_end + z - 2 * kLanesPerPkt + 1;  // lean iff 8k + 15 - z < ct_full_end
     const uint32_t k_hi = !act ? 0xFFFFFFFFu : (hi <= 0 ? 0u : (uint32_t)((hi + kLanesPerPkt - 1) / kLanesPerPkt));
-    const uint32_t klo = wave_max_u32(k_lo), khi = ~wave_max_u32(~k_hi);
+    const uint32_t klo = wave_max_u32(k_lo), khi = min(~wave_max_u32(~k_hi), Kmax - 1);
     for (uint32_t k = 0; k + 1 < Kmax; ++k) {
-      if (k >= klo && k < khi) {  // wave-uniform
-        const P26 x = p26_from_words(m[0], m[1], m[2], m[3], 1u);
+      if (k == klo && k < khi) {  // wave-uniform: the lean stretch, steps klo .. khi - 1
+        // only the block address advances; i, src and rem catch up once at the end
+        typename S::off_t a = b.src & ~(typename S::off_t)3;
+        uint32_t sel = sel_pay;
+        pin(sel);  // keep the selector in a register (hipcc rematerialised it every step)
+        for (; k < khi; ++k) {
+          const P26 x = p26_from_words(m[0], m[1], m[2], m[3], 1u);
 #pragma unroll
-        for (int l = 0; l < 5; ++l) acc.l[l] += x.l[l];
-        i += kLanesPerPkt;
-        b.src += 128;
-        b.rem -= 128;
-        load_words_sel<4>(sp, b.src & ~(typename S::off_t)3, sel_pay, m);
-        p26_mul(acc, m8);
-        continue;
+          for (int l = 0; l < 5; ++l) acc.l[l] += x.l[l];
+          a += 128;
+          load_words_sel<4>(sp, a, sel, m);
+          p26_mul(acc, m8);
+        }
+        const uint32_t nl = khi - klo;
+        i += (int)(kLanesPerPkt * nl);
+        b.src += 128 * nl;
+        b.rem -= (int)(128 * nl);
+        if (k + 1 >= Kmax) break;
       }
       absorb(b, m);
       const bool steady = !act || (i >= (int)A && i + kLanesPerPkt < ct_full_end);

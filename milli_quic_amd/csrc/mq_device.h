@@ -396,19 +396,19 @@ __device__ __forceinline__ P26 p26_from_words(uint32_t t0, uint32_t t1, uint32_t
   return h;
 }
 
-// h = h * m (mod 2^130 - 5), partially reduced (limbs < 2^26, l[1] < 2^26 + 2^8).
+// h = h * m (mod 2^130 - 5), partially reduced (limbs < 2^26, l[1] < 2^26 + 2^9). Inputs: limbs
+// < 2^27 (a product plus one absorbed block), multiplier limbs < 2^26 (s < 2^28.4), so every
+// column sum stays below 2^58 and each carry (d >> 26) below 2^32, so the top carry is a 32-bit
+// operand of the x5 fold.
 __device__ __forceinline__ void p26_mul(P26& h, const P26m& m) {
   const uint32_t h0 = h.l[0], h1 = h.l[1], h2 = h.l[2], h3 = h.l[3], h4 = h.l[4];
-  uint64_t d0 = (uint64_t)h0 * m.r[0] + (uint64_t)h1 * m.s[3] + (uint64_t)h2 * m.s[2] + (uint64_t)h3 * m.s[1] + (uint64_t)h4 * m.s[0];
-  uint64_t d1 = (uint64_t)h0 * m.r[1] + (uint64_t)h1 * m.r[0] + (uint64_t)h2 * m.s[3] + (uint64_t)h3 * m.s[2] + (uint64_t)h4 * m.s[1];
-  uint64_t d2 = (uint64_t)h0 * m.r[2] + (uint64_t)h1 * m.r[1] + (uint64_t)h2 * m.r[0] + (uint64_t)h3 * m.s[3] + (uint64_t)h4 * m.s[2];
-  uint64_t d3 = (uint64_t)h0 * m.r[3] + (uint64_t)h1 * m.r[2] + (uint64_t)h2 * m.r[1] + (uint64_t)h3 * m.r[0] + (uint64_t)h4 * m.s[3];
-  uint64_t d4 = (uint64_t)h0 * m.r[4] + (uint64_t)h1 * m.r[3] + (uint64_t)h2 * m.r[2] + (uint64_t)h3 * m.r[1] + (uint64_t)h4 * m.r[0];
-  d1 += d0 >> 26;
-  d2 += d1 >> 26;
-  d3 += d2 >> 26;
-  d4 += d3 >> 26;
-  uint64_t t = (uint64_t)((uint32_t)d0 & 0x3ffffff) + (d4 >> 26) * 5u;
+  const uint64_t d0 = (uint64_t)h0 * m.r[0] + (uint64_t)h1 * m.s[3] + (uint64_t)h2 * m.s[2] + (uint64_t)h3 * m.s[1] + (uint64_t)h4 * m.s[0];
+  const uint64_t d1 = (d0 >> 26) + (uint64_t)h0 * m.r[1] + (uint64_t)h1 * m.r[0] + (uint64_t)h2 * m.s[3] + (uint64_t)h3 * m.s[2] + (uint64_t)h4 * m.s[1];
+  const uint64_t d2 = (d1 >> 26) + (uint64_t)h0 * m.r[2] + (uint64_t)h1 * m.r[1] + (uint64_t)h2 * m.r[0] + (uint64_t)h3 * m.s[3] + (uint64_t)h4 * m.s[2];
+  const uint64_t d3 = (d2 >> 26) + (uint64_t)h0 * m.r[3] + (uint64_t)h1 * m.r[2] + (uint64_t)h2 * m.r[1] + (uint64_t)h3 * m.r[0] + (uint64_t)h4 * m.s[3];
+  const uint64_t d4 = (d3 >> 26) + (uint64_t)h0 * m.r[4] + (uint64_t)h1 * m.r[3] + (uint64_t)h2 * m.r[2] + (uint64_t)h3 * m.r[1] + (uint64_t)h4 * m.r[0];
+  const uint32_t c4 = (uint32_t)(d4 >> 26);
+  const uint64_t t = (uint64_t)((uint32_t)d0 & 0x3ffffff) + (uint64_t)c4 * 5u;
   h.l[0] = (uint32_t)t & 0x3ffffff;
   h.l[1] = ((uint32_t)d1 & 0x3ffffff) + (uint32_t)(t >> 26);
   h.l[2] = (uint32_t)d2 & 0x3ffffff;
