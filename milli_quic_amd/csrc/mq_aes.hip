@@ -635,15 +635,20 @@ __global__ __launch_bounds__(256) void mq_aes_seal_hp_kernel(
     const uint32_t* __restrict__ n_dev, const uint8_t* __restrict__ status) {
   const uint32_t count = n_dev ? *n_dev : n;
   if (blockIdx.x * blockDim.x >= count) return;  // list mode: grids cover the list capacity
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t i = t < count ? (index ? index[t] : t) : kListHole;
+  bool need = i != kListHole && status[i] == MQ_OK;
+  mq_pkt_desc d{};
+  if (need) {
+    d = desc[i];
+    const uint32_t P = d.len - ((uint32_t)d.pn_offset + d.pn_len) - 16, nblk = 1 + ((P + 15) >> 4);
+    need = !(d.flags & MQ_PKT_NO_HP) && nblk < (uint32_t)kLanesPerPkt;  // records are NO_HP
+  }
+  // the S-box table only for blocks with work (1200-B batches have none)
+  if (!__syncthreads_or(need)) return;
   build_t0(threadIdx.x, blockDim.x);
   __syncthreads();
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= count) return;
-  const uint32_t i = index ? index[t] : t;
-  if (i == kListHole || status[i] != MQ_OK) return;
-  const mq_pkt_desc d = desc[i];
-  const uint32_t P = d.len - ((uint32_t)d.pn_offset + d.pn_len) - 16, nblk = 1 + ((P + 15) >> 4);
-  if ((d.flags & MQ_PKT_NO_HP) || nblk >= (uint32_t)kLanesPerPkt) return;  // records are NO_HP
+  if (!need) return;
   uint32_t w[5], m0, m1;
   uint8_t b0;
   prepass_header(arena, d, b0, w);  // inside the packet (validated: pn_offset + 20 <= len)
@@ -672,11 +677,11 @@ static uint32_t aes_grid(uint32_t tiles, uint32_t waves) {
 
 hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena, uint64_t arena_len,
                          const mq_pkt_desc* desc, uint32_t n, const uint32_t* index, const uint32_t* n_dev,
-                         uint8_t* status, uint64_t* pn_out, uint2* hpm, hipStream_t s) {
+                         uint8_t* status, uint64_t* pn_out, uint2* hpm, bool own_hp, hipStream_t s) {
   const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
   if (tiles == 0) return hipSuccess;
   const uint32_t waves = aes_waves(n_rows == 1), blocks = aes_grid(tiles, waves);
-  if (open && hpm) {
+  if (open && hpm && own_hp) {  // !own_hp: mq_launch_mixed_hp covers both suites' lists
     hipLaunchKernelGGL(mq_aes_open_hp_kernel<true>, dim3((n + 255) / 256), dim3(256), 0, s, kt, n_rows, arena,
                        arena_len, desc, n, index, n_dev, hpm);
     const hipError_t e = hipGetLastError();
@@ -690,9 +695,86 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
   hipLaunchKernelGGL(n_rows == 1 ? mq_aes_seal1_kernel : mq_aes_seal_kernel, dim3(blocks), dim3(64 * waves),
                      0, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status);
   const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  if (e != hipSuccess || !own_hp) return e;
   hipLaunchKernelGGL(mq_aes_seal_hp_kernel, dim3((n + 255) / 256), dim3(256), 0, s, kt, arena, arena_len, desc, n,
                      index, n_dev, status);
+  return hipGetLastError();
+}
+
+// Mixed batches: the open pre-pass (OPEN) or the seal HP post-pass of BOTH partition lists in one
+// launch (list 0 = list[0, counts[0]), list 1 = list[cap, cap + counts[1])), one packet per lane,
+// either suite per lane — the two passes' memory latencies overlap instead of adding up. Seal:
+// the packets whose HP had no slot in their tile (AES: fewer than 7 CTR blocks; ChaCha20: all),
+// as mq_aes_seal_hp_kernel / mq_chacha_seal_hp_kernel do per list.
+template <bool OPEN>
+__global__ __launch_bounds__(256) void mq_mixed_hp_kernel(
+    const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
+    const mq_pkt_desc* __restrict__ desc, const uint32_t* __restrict__ list, uint32_t cap,
+    const uint32_t* __restrict__ counts, const uint8_t* __restrict__ status, uint2* __restrict__ hpm) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t sl = t >= cap ? 1u : 0u, e = t - sl * cap;
+  uint32_t i = t < 2 * cap && e < counts[sl] ? list[t] : kListHole;
+  bool act = i != kListHole, aes = false;
+  mq_pkt_desc d{};
+  const KeyRow* row = kt;
+  if (OPEN) {  // prepass_pick's checks; the tile kernels report the rest
+    if (act) {
+      d = desc[i];
+      act = d.key_id < n_rows && d.offset + (uint64_t)d.len <= arena_len && !(d.flags & MQ_PKT_NO_HP) &&
+            (uint64_t)d.pn_offset + 20 <= d.len;
+    }
+    if (act) {
+      row = kt + d.key_id;
+      const uint32_t su = row->suite;
+      aes = su == MQ_SUITE_AES128GCM;
+      act = aes || su == MQ_SUITE_CHACHA20;
+    }
+  } else {
+    act = act && status[i] == MQ_OK;
+    if (act) {
+      d = desc[i];
+      row = kt + d.key_id;
+      aes = row->suite == MQ_SUITE_AES128GCM;
+      const uint32_t P = d.len - ((uint32_t)d.pn_offset + d.pn_len) - 16;
+      // AES: the packets whose HP had no slot in their tile; ChaCha20: every packet
+      act = !(d.flags & MQ_PKT_NO_HP) && (!aes || 1 + ((P + 15) >> 4) < (uint32_t)kLanesPerPkt);
+    }
+  }
+  if (!__syncthreads_or(act)) return;
+  if (__syncthreads_or(act && aes)) {  // the S-box table only where AES lanes have work
+    build_t0(threadIdx.x, blockDim.x);
+    __syncthreads();
+  }
+  if (!act) return;
+  uint32_t w[5], m0, m1;
+  uint8_t b0;
+  prepass_header(arena, d, b0, w);
+  const uint32_t smp[4] = {w[1], w[2], w[3], w[4]};
+  if (aes) {
+    aes_hp_mask_words(smp, row, (uint32_t)(threadIdx.x & (kTReplicas - 1)) * 4, m0, m1);
+  } else {  // ChaChaHeaderProtection::mask (rustcrypto.rs:197-220)
+    uint32_t hk[8], blk[16];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) hk[q] = row->hp[q];
+    chacha20_block(hk, smp[0], smp[1], smp[2], smp[3], blk);
+    m0 = blk[0];
+    m1 = blk[1];
+  }
+  if (OPEN) hpm[i] = prepass_decode_words(b0, w[0], d, m0, m1);
+  else seal_apply_hp(arena, d, b0, w[0], m0, m1);
+}
+
+hipError_t mq_launch_mixed_hp(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena, uint64_t arena_len,
+                              const mq_pkt_desc* desc, const uint32_t* list, uint32_t cap, const uint32_t* counts,
+                              const uint8_t* status, uint2* hpm, hipStream_t s) {
+  const uint32_t blocks = (uint32_t)((2ull * cap + 255) / 256);
+  if (blocks == 0) return hipSuccess;
+  if (open)
+    hipLaunchKernelGGL(mq_mixed_hp_kernel<true>, dim3(blocks), dim3(256), 0, s, kt, n_rows, arena, arena_len, desc, list,
+                       cap, counts, status, hpm);
+  else
+    hipLaunchKernelGGL(mq_mixed_hp_kernel<false>, dim3(blocks), dim3(256), 0, s, kt, n_rows, arena, arena_len, desc,
+                       list, cap, counts, status, hpm);
   return hipGetLastError();
 }
 

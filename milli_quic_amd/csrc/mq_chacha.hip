@@ -6,9 +6,9 @@
 // src/connection/recv.rs:340-421,953-1025 (receive) compose them.
 //
 // Per tile (8 packets, one octet of lanes per packet; see mq_tile.h):
-//   seal: keystream block ctr on lane ctr % 8 (ctr 0 = Poly1305 one-time key) XORed into LDS,
-//         HP block in the first free slot -> interleaved Poly1305 over AAD||pad||CT||pad||lens
-//         -> tag -> header mask applied
+//   seal: keystream block ctr on lane ctr % 8 (ctr 0 = Poly1305 one-time key) XORed into LDS
+//         (blocks >= 16 through the workgroup's keystream pool) -> interleaved Poly1305 over
+//         AAD||pad||CT||pad||lens -> tag; the header mask comes from mq_chacha_seal_hp_kernel
 //   open: HP mask -> unmask byte 0 / PN -> decode_pn -> nonce -> first keystream block (lane 0:
 //         one-time key) -> Poly1305 over the untouched ciphertext -> tag check -> only then the
 //         keystream XOR (held first block + the rest); failed packets are never stored.
@@ -158,35 +158,21 @@ __device__ __forceinline__ void load_key8(const uint32_t* src, uint32_t (&k)[8])
   k[0] = a.x; k[1] = a.y; k[2] = a.z; k[3] = a.w; k[4] = b.x; k[5] = b.y; k[6] = b.z; k[7] = b.w;
 }
 
-// Seal: the HP block (slot nblk) lies in an iteration the packet's keystream runs anyway — not in
-// iteration 0 (no ciphertext sample yet) and not alone in an extra iteration (nblk % 8 == 0)
-__device__ __forceinline__ bool cc_hp_in_slot(uint32_t nblk) { return nblk > (uint32_t)kLanesPerPkt && (nblk % kLanesPerPkt) != 0; }
-
-// RFC 9001 §5.4.1: apply the 5-byte mask to byte 0 (low 4 / 5 bits) and the PN bytes.
-template <class S>
-__device__ __forceinline__ void apply_hp(const S& sp, typename S::off_t pkt, const mq_pkt_desc& d,
-                                         uint32_t m0, uint32_t m1) {
-  const uint8_t fb = (d.flags & MQ_PKT_LONG_HEADER) ? 0x0f : 0x1f;
-  sp.st8(pkt, sp.ld8(pkt) ^ ((uint8_t)m0 & fb));
-  const uint32_t mk = (m0 >> 8) | (m1 << 24);  // mask[1..4]
-  for (uint32_t b = 0; b < d.pn_len; ++b)
-    sp.st8(pkt + d.pn_offset + b, sp.ld8(pkt + d.pn_offset + b) ^ (uint8_t)(mk >> (8 * b)));
-}
-
-// ---- open: keystream pool of a workgroup (kCcOpenWaves waves, one staged tile each) ----------
-// Opening a 1200-B packet takes 20 ChaCha20 blocks (one-time key and 19 keystream; the HP mask
-// comes from the pre-pass), but an octet runs 24 slots in three iterations, so 1/6 of the rounds
-// went idle. Each wave now runs iterations 0 and 1 of its own packets; every later keystream
-// block (slot >= 16) goes to the workgroup's pool, which all its lanes work off together between
-// two barriers once the MACs have read the ciphertext: 4 waves x 8 packets x 4 blocks = 128
+// ---- keystream pool of a workgroup (kCcWaves waves, one staged tile each) ---------------------
+// A 1200-B packet takes 20 ChaCha20 blocks (one-time key and 19 keystream; the header-protection
+// block runs in a one-packet-per-lane pass: the open pre-pass before, the seal post-pass after),
+// but an octet runs 24 slots in three iterations, so 1/6 of the rounds went idle. Each wave runs
+// iterations 0 and 1 of its own packets; every later keystream block (slot >= 16) goes to the
+// workgroup's pool, which all its lanes work off together between two barriers (open: once the
+// MACs have read the ciphertext; seal: before the MACs): 4 waves x 8 packets x 4 blocks = 128
 // blocks, two wave-iterations for the four instead of a 4/8-full third one each. (Measured at 2,
-// 4 and 8 waves: 8 in lockstep lose most of the gain to staging waits that no longer overlap. For
-// seal the HP block fills the idle slot for free; a pool would have to move HP to a post-pass,
-// which costs more than the pool saves.)
-#ifndef MQ_CC_OPEN_WAVES
-#define MQ_CC_OPEN_WAVES 4
+// 4 and 8 waves: 8 in lockstep lose most of the gain to staging waits that no longer overlap.
+// Seal with the HP block kept in the tile measured no gain: 21 blocks = 2.625 iterations per
+// tile leave a 3-iteration wave in every workgroup, profiles/r02_ab_chacha_seal_pool_b_rejected.txt.)
+#ifndef MQ_CC_WAVES
+#define MQ_CC_WAVES 4
 #endif
-constexpr int kCcOpenWaves = MQ_CC_OPEN_WAVES;
+constexpr int kCcWaves = MQ_CC_WAVES;
 constexpr uint32_t kCcPoolSlot = 2 * kLanesPerPkt;  // first pooled slot (iterations 0 and 1 are the wave's)
 
 // this packet's 32-B pool record in its wave's scratch: [0] pooled blocks, [1] payload LDS
@@ -201,7 +187,7 @@ struct CcPool {
 
 template <bool SINGLE>
 __device__ __forceinline__ void cc_pool_run(const CcPool& pool) {
-  constexpr uint32_t kQ = kPktsPerTile * kCcOpenWaves;  // packets of the workgroup
+  constexpr uint32_t kQ = kPktsPerTile * kCcWaves;  // packets of the workgroup
   static_assert(kQ <= kWave, "one packet per lane in the pool scan");
   const int lane = threadIdx.x & (kWave - 1);
   const uint32_t w = threadIdx.x >> 6;
@@ -212,7 +198,7 @@ __device__ __forceinline__ void cc_pool_run(const CcPool& pool) {
   const uint32_t incl = wave_incl_scan(nq), excl = incl - nq;
   const uint32_t T = lane_u32(incl, kWave - 1);
   const LdsSpace sp{pool.wg};
-  for (uint32_t e0 = kWave * w; e0 < T; e0 += kWave * kCcOpenWaves) {  // wave-uniform
+  for (uint32_t e0 = kWave * w; e0 < T; e0 += kWave * kCcWaves) {  // wave-uniform
     const uint32_t e = e0 + (uint32_t)lane;
     uint32_t q = 0;  // the packet of entry e: the last q with excl[q] <= e
 #pragma unroll
@@ -275,13 +261,13 @@ struct ChaChaPolicy {
     hp_mask_words(smp, row, m0, m1);
   }
 
-  // send composite (transmit.rs:625-755): seal, then header protection from the sample.
-  // Keystream block ctr of the packet runs on lane ctr % 8 in iteration ctr / 8 (ctr 0 = the
-  // Poly1305 key); the HP block runs in the first free slot after ctr 1 (whose ciphertext holds
-  // the sample) unless the sample reaches into the tag (tiny payloads: a separate phase).
-  template <class S, class G>
-  static __device__ __forceinline__ void seal(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j, G& stg,
-                                              bool short_post) {
+  // send composite (transmit.rs:625-755), AEAD part: keystream block ctr of the packet runs on
+  // lane ctr % 8 in iteration ctr / 8 (ctr 0 = the Poly1305 key); with the pool, blocks >= 16 run
+  // in the workgroup's pool before the MACs. Header protection follows in
+  // mq_chacha_seal_hp_kernel (the sample is ciphertext, so it needs the sealed packet).
+  template <bool SINGLE, class S, class G>
+  static __device__ __forceinline__ void seal(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j,
+                                              G& stg, const CcPool& pool) {
     const mq_pkt_desc& d = c.d;
     uint32_t key[8];
     load_key8(row->key, key);
@@ -289,43 +275,21 @@ struct ChaChaPolicy {
     const uint32_t P = c.act ? d.len - aad_len - 16 : 0u;
     const typename S::off_t pay = pkt + aad_len;
     // DirectionalKeys::nonce (src/crypto/mod.rs:66-74): iv ^ (0^32 || BE64(pn))
-    const uint32_t pn_hi = bswap32((uint32_t)(c.pn >> 32)), pn_lo = bswap32((uint32_t)c.pn);
-    uint32_t n0 = row->iv[0], n1 = row->iv[1] ^ pn_hi, n2 = row->iv[2] ^ pn_lo;
+    uint32_t n0 = row->iv[0], n1 = row->iv[1] ^ bswap32((uint32_t)(c.pn >> 32)), n2 = row->iv[2] ^ bswap32((uint32_t)c.pn);
 #pragma unroll
     for (int k = 0; k < 8; ++k) pin(key[k]);
     pin(n0); pin(n1); pin(n2);
     stg.issue();  // packet bytes stream into LDS while the first keystream block is computed
     const uint32_t nblk = 1 + (P + 63) / 64;  // block 0 = Poly1305 key, 1.. = keystream
-    const bool hp_on = c.act && !(d.flags & MQ_PKT_NO_HP);
-    // short_post (wave-uniform): packets whose HP block has no free slot in the iterations their
-    // keystream needs get it from mq_chacha_seal_hp_kernel afterwards
-    const bool hp_defer = short_post && hp_on && !cc_hp_in_slot(nblk);
-    const bool hp_post = hp_on && !hp_defer && 20 > P + d.pn_len;  // sample reaches into the tag
-    const bool hp_slot = hp_on && !hp_defer && !hp_post;
-    uint32_t hp_it = nblk / kLanesPerPkt, hp_lane = nblk % kLanesPerPkt;
-    if (hp_it == 0) { hp_it = 1; hp_lane = 0; }
-    const uint32_t iters = max((nblk + kLanesPerPkt - 1) / kLanesPerPkt, hp_slot ? hp_it + 1 : 0u);
-    const uint32_t Imax = wave_max_u32(c.act ? iters : 0u);
-    uint32_t m0 = 0, m1 = 0;
-    bool have_mask = false;
+    const uint32_t kst = pool.on ? min(nblk, kCcPoolSlot) : nblk;  // blocks of this wave's own slots
+    const uint32_t Imax = wave_max_u32(c.act ? (kst + kLanesPerPkt - 1) / kLanesPerPkt : 0u);
     for (uint32_t it = 0; it < Imax; ++it) {
       const uint32_t ctr = (uint32_t)j + kLanesPerPkt * it;
-      const bool a = c.act && ctr < nblk;
-      const bool is_hp = hp_slot && it == hp_it && (uint32_t)j == hp_lane;
+      const bool a = c.act && ctr < kst;
       uint32_t w[17];
       if (it > 0) load_block(sp, pay, a ? ctr : 0u, w);  // LDS reads in flight during the block function
-      uint32_t cc = ctr;
-      const bool hp_iter = wave_any(is_hp);
-      if (hp_iter) {  // the HP lane runs block(hp_key, sample) in this slot: swap its inputs in place
-        uint32_t smp[4], hk[8];
-        load_words<4>(sp, pkt + (c.act ? d.pn_offset + 4u : 0u), smp);
-        load_key8(row->hp, hk);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) key[k] = is_hp ? hk[k] : key[k];
-        if (is_hp) { cc = smp[0]; n0 = smp[1]; n1 = smp[2]; n2 = smp[3]; }
-      }
       uint32_t ks[16];
-      chacha20_block(key, cc, n0, n1, n2, ks);
+      chacha20_block(key, ctr, n0, n1, n2, ks);
       if (it == 0) {
         stg.complete();
         MQ_STAMP(c.tile, 2);
@@ -341,30 +305,27 @@ struct ChaChaPolicy {
       } else if (a) {
         store_block(sp, pay, ctr, P, ks, w);
       }
-      if (is_hp) { m0 = ks[0]; m1 = ks[1]; have_mask = true; }
-      if (hp_iter && it + 1 < Imax) {  // restore the HP lane's AEAD inputs
-        uint32_t kr[8];
-        load_key8(row->key, kr);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) key[k] = is_hp ? kr[k] : key[k];
-        if (is_hp) { n0 = row->iv[0]; n1 = row->iv[1] ^ pn_hi; n2 = row->iv[2] ^ pn_lo; }
-      }
-      wave_sync();  // this iteration's ciphertext (the HP sample) is visible to the next
+      wave_sync();
     }
     if (Imax == 0) stg.complete();
+    if (j == 0) {  // pool record
+      const uint32_t np = pool.on && c.act && nblk > kCcPoolSlot ? nblk - kCcPoolSlot : 0u;
+      pool.rec[0] = np;
+      if (np) {
+        pool.rec[1] = (pool.base + (uint32_t)pay) | P << 17;
+        pool.rec[3] = d.key_id;
+        pool.rec[4] = n0; pool.rec[5] = n1; pool.rec[6] = n2;
+      }
+    }
+    __syncthreads();  // every wave's records
+    cc_pool_run<SINGLE>(pool);
+    __syncthreads();  // every pooled block is in place before any MAC reads it
     MQ_STAMP(c.tile, 3);
     uint32_t tag[4];
     poly_tag(sp, pkt, pay, aad_len, P, c.otk, j, c.act, tag);
     if (c.act && j == 0) store_words<4>(sp, pay + P, tag);
     wave_sync();
     MQ_STAMP(c.tile, 4);
-    if (wave_any(hp_post)) {  // rare: sample includes tag bytes
-      uint32_t t0, t1;
-      hp_mask(sp, pkt + (c.act ? d.pn_offset + 4u : 0u), row, t0, t1);
-      if (hp_post && j == 0) { m0 = t0; m1 = t1; have_mask = true; }
-    }
-    if (have_mask) apply_hp(sp, pkt, d, m0, m1);  // after the MAC read the unprotected header
-    MQ_STAMP(c.tile, 5);
   }
 
   // receive composite (recv.rs:340-421 / 953-1025): HP removal, decode_pn, open.
@@ -459,11 +420,10 @@ struct ChaChaPolicy {
 
 using namespace mq;
 
-// Tile kernels: one tile per wave, each with its private 10 KiB LDS image. Seal runs one wave per
-// workgroup (its HP block fills an otherwise idle slot, so a pool would gain nothing); open runs
-// kCcOpenWaves-wave workgroups sharing the keystream pool above between two barriers. Every wave
-// of an open workgroup runs both barriers: waves past the batch with an empty record,
-// direct-path tiles (images over the budget) with nothing pooled. (A persistent grid walking
+// Tile kernels: one tile per wave, each with its private 10 KiB LDS image, kCcWaves-wave
+// workgroups sharing the keystream pool above between two barriers. Every wave of a workgroup
+// runs both barriers: waves past the batch with an empty record, direct-path tiles (images over
+// the budget) with nothing pooled. (A persistent grid walking
 // tiles, as the AES kernels use, measured 10 % slower here: identical waves stay in phase, so
 // their staging waits line up.) The "1" variants are launched when the key table has a single
 // row (every valid packet on row 0): key material then lives in SGPRs.
@@ -472,10 +432,10 @@ __device__ __forceinline__ void chacha_tile(const KeyRow* __restrict__ kt, uint3
                                             uint64_t arena_len, const mq_pkt_desc* __restrict__ desc, uint32_t n,
                                             const uint32_t* __restrict__ index, const uint32_t* __restrict__ n_dev,
                                             uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,
-                                            const uint2* __restrict__ hpm, bool short_post) {
-  constexpr uint32_t W = OPEN ? kCcOpenWaves : 1;
+                                            const uint2* __restrict__ hpm) {
+  constexpr uint32_t W = kCcWaves;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const uint32_t w = W > 1 ? threadIdx.x >> 6 : 0u;
+  const uint32_t w = threadIdx.x >> 6;
   uint8_t* wsm = smem + w * kLdsBytes;
   const int lane = threadIdx.x & (kWave - 1), p = lane / kLanesPerPkt, j = lane % kLanesPerPkt;
   const uint32_t tile_id = blockIdx.x * W + w;
@@ -485,8 +445,8 @@ __device__ __forceinline__ void chacha_tile(const KeyRow* __restrict__ kt, uint3
   if (!tile_ctx<MQ_SUITE_CHACHA20, OPEN, SINGLE>(tile_id, kt, n_rows, arena_len, desc, n, index, n_dev, hpm,
                                                  TilePrefetch{false, 0u, 0u}, c, row)) {
     // past the batch (list capacities exceed the count): a whole workgroup leaves at once, a
-    // wave of a live open workgroup only joins its barriers and pool
-    if (W == 1 || blockIdx.x * W * kPktsPerTile >= (n_dev ? *n_dev : n)) return;  // workgroup-uniform
+    // wave of a live workgroup only joins its barriers and pool
+    if (blockIdx.x * W * kPktsPerTile >= (n_dev ? *n_dev : n)) return;  // workgroup-uniform
     if (j == 0) pool.rec[0] = 0;
     __syncthreads();
     cc_pool_run<SINGLE>(pool);
@@ -505,13 +465,13 @@ __device__ __forceinline__ void chacha_tile(const KeyRow* __restrict__ kt, uint3
   const uint32_t total = lane_u32(incl, kWave - 1);
   if (total * 16u <= kDataBudget) {
     pl.slot = incl - nch;
-    pool.on = W > 1;
+    pool.on = true;
     DmaStager stg{wsm, arena, arena_len, lane, j, pl};
     LdsSpace sp{wsm};
     MQ_STAMP(tile_id, 1);
     const uint32_t pkt = pl.slot * 16u + pl.head();
     if (OPEN) ChaChaPolicy::template open<SINGLE, LdsSpace>(sp, pkt, c, row, j, false, stg, pool);
-    else ChaChaPolicy::template seal<LdsSpace>(sp, pkt, c, row, j, stg, short_post);
+    else ChaChaPolicy::template seal<SINGLE, LdsSpace>(sp, pkt, c, row, j, stg, pool);
     MQ_STAMP(tile_id, 6);
     wave_sync();
     stage_out(wsm, arena, lane, c.act, pl);
@@ -520,25 +480,24 @@ __device__ __forceinline__ void chacha_tile(const KeyRow* __restrict__ kt, uint3
     GlobalSpace sp{arena, arena_len};
     NoStager stg;
     if (OPEN) ChaChaPolicy::template open<SINGLE, GlobalSpace>(sp, off, c, row, j, true, stg, pool);
-    else ChaChaPolicy::template seal<GlobalSpace>(sp, off, c, row, j, stg, short_post);
+    else ChaChaPolicy::template seal<SINGLE, GlobalSpace>(sp, off, c, row, j, stg, pool);
   }
   tile_status<OPEN>(c, j, status, pn_out);
 }
 
 #define MQ_CHACHA_KERNELS(NAME_SEAL, NAME_OPEN, SINGLE)                                                   \
-  extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void NAME_SEAL(    \
+  extern "C" __global__ __launch_bounds__(64 * kCcWaves) __attribute__((amdgpu_waves_per_eu(4))) void NAME_SEAL( \
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
-      const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint32_t short_post) {            \
-    chacha_tile<false, SINGLE>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr, nullptr, \
-                               short_post != 0);                                                          \
+      const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status) {                                 \
+    chacha_tile<false, SINGLE>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr, nullptr); \
   }                                                                                                       \
-  extern "C" __global__ __launch_bounds__(64 * kCcOpenWaves) __attribute__((amdgpu_waves_per_eu(4))) void NAME_OPEN( \
+  extern "C" __global__ __launch_bounds__(64 * kCcWaves) __attribute__((amdgpu_waves_per_eu(4))) void NAME_OPEN( \
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
       const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,    \
       const uint2* __restrict__ hpm) {                                                                    \
-    chacha_tile<true, SINGLE>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm, false); \
+    chacha_tile<true, SINGLE>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm); \
   }
 MQ_CHACHA_KERNELS(mq_chacha_seal_kernel, mq_chacha_open_kernel, false)
 MQ_CHACHA_KERNELS(mq_chacha_seal1_kernel, mq_chacha_open1_kernel, true)
@@ -594,11 +553,10 @@ __global__ __launch_bounds__(256) void mq_chacha_open_hp_kernel(
   }
 }
 
-// Seal post-pass (list mode): header protection of the sealed packets whose HP block had no free
-// slot in their tile (short packets: nblk <= 8 or a multiple of 8, incl. samples reaching into the
-// tag) — transmit.rs:713-719 with ChaChaHeaderProtection::mask (rustcrypto.rs:197-220), one
-// packet per lane: sample = the 16 bytes at pn_offset + 4 of the sealed packet, mask applied to
-// byte 0 (low 4 / 5 bits) and the PN bytes (RFC 9001 §5.4.1).
+// Seal post-pass: header protection of every sealed packet — transmit.rs:713-719 with
+// ChaChaHeaderProtection::mask (rustcrypto.rs:197-220), one packet per lane: sample = the 16
+// bytes at pn_offset + 4 of the sealed packet (ciphertext, into the tag for tiny payloads), mask
+// applied to byte 0 (low 4 / 5 bits) and the PN bytes (RFC 9001 §5.4.1).
 __global__ __launch_bounds__(256) void mq_chacha_seal_hp_kernel(
     const KeyRow* __restrict__ kt, uint8_t* __restrict__ arena, const mq_pkt_desc* __restrict__ desc, uint32_t n,
     const uint32_t* __restrict__ index, const uint32_t* __restrict__ n_dev, const uint8_t* __restrict__ status) {
@@ -608,8 +566,7 @@ __global__ __launch_bounds__(256) void mq_chacha_seal_hp_kernel(
   const uint32_t i = index ? index[t] : t;
   if (i == kListHole || status[i] != MQ_OK) return;
   const mq_pkt_desc d = desc[i];
-  const uint32_t P = d.len - ((uint32_t)d.pn_offset + d.pn_len) - 16, nblk = 1 + (P + 63) / 64;
-  if ((d.flags & MQ_PKT_NO_HP) || cc_hp_in_slot(nblk)) return;  // records are NO_HP
+  if (d.flags & MQ_PKT_NO_HP) return;  // records and plain AEAD rows
   uint32_t w[5], m0, m1;
   uint8_t b0;
   prepass_header(arena, d, b0, w);  // inside the packet (validated: pn_offset + 20 <= len)
@@ -622,10 +579,10 @@ __global__ __launch_bounds__(256) void mq_chacha_seal_hp_kernel(
 hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena,
                             uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
                             const uint32_t* index, const uint32_t* n_dev, uint8_t* status,
-                            uint64_t* pn_out, uint2* hpm, hipStream_t s) {
+                            uint64_t* pn_out, uint2* hpm, bool own_hp, hipStream_t s) {
   const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
   if (tiles == 0) return hipSuccess;
-  if (open && hpm) {
+  if (open && hpm && own_hp) {  // !own_hp: mq_launch_mixed_hp covers both suites' lists
     hipLaunchKernelGGL(mq_chacha_open_hp_kernel<true>, dim3((n + 255) / 256), dim3(256), 0, s, kt, n_rows, arena,
                        arena_len, desc, n, index, n_dev, hpm);
     const hipError_t e = hipGetLastError();
@@ -633,15 +590,13 @@ hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_
   }
   if (open)
     hipLaunchKernelGGL(n_rows == 1 ? mq_chacha_open1_kernel : mq_chacha_open_kernel,
-                       dim3((tiles + kCcOpenWaves - 1) / kCcOpenWaves), dim3(kWave * kCcOpenWaves), kLdsBytes * kCcOpenWaves, s, kt,
+                       dim3((tiles + kCcWaves - 1) / kCcWaves), dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kt,
                        n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm);
   if (open) return hipGetLastError();
-  // list mode (mixed batches: length-sorted tiles, the short classes at the end) defers the HP
-  // blocks that would cost their tile an extra iteration to the one-packet-per-lane post-pass
-  const uint32_t short_post = index ? 1u : 0u;
-  hipLaunchKernelGGL(n_rows == 1 ? mq_chacha_seal1_kernel : mq_chacha_seal_kernel, dim3(tiles), dim3(kWave), kLdsBytes,
-                     s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, short_post);
-  if (short_post) {
+  hipLaunchKernelGGL(n_rows == 1 ? mq_chacha_seal1_kernel : mq_chacha_seal_kernel,
+                     dim3((tiles + kCcWaves - 1) / kCcWaves), dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kt,
+                     n_rows, arena, arena_len, desc, n, index, n_dev, status);
+  if (own_hp) {  // !own_hp: mq_launch_mixed_hp covers both suites' lists, or the rows are NO_HP
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(mq_chacha_seal_hp_kernel, dim3((n + 255) / 256), dim3(256), 0, s, kt, arena, desc, n, index,

@@ -22,13 +22,16 @@ using mq::KeyRow;
 hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena,
                             uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
                             const uint32_t* index, const uint32_t* n_dev, uint8_t* status,
-                            uint64_t* pn_out, uint2* hpm, hipStream_t s);
+                            uint64_t* pn_out, uint2* hpm, bool own_hp, hipStream_t s);
 hipError_t mq_launch_chacha_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t* key_ids,
                                const uint8_t* samples, uint8_t* masks, uint32_t n, hipStream_t s);
 hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena,
                          uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
                          const uint32_t* index, const uint32_t* n_dev, uint8_t* status,
-                         uint64_t* pn_out, uint2* hpm, hipStream_t s);
+                         uint64_t* pn_out, uint2* hpm, bool own_hp, hipStream_t s);
+hipError_t mq_launch_mixed_hp(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena, uint64_t arena_len,
+                              const mq_pkt_desc* desc, const uint32_t* list, uint32_t cap, const uint32_t* counts,
+                              const uint8_t* status, uint2* hpm, hipStream_t s);
 hipError_t mq_launch_aes_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t* key_ids,
                             const uint8_t* samples, uint8_t* masks, uint32_t n, hipStream_t s);
 hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_desc* desc, uint32_t n,
@@ -385,10 +388,11 @@ int run_one(Scratch& sc, const KeyRow& row, const uint8_t* aad, uint32_t aad_len
   const mq_pkt_desc* dd = (const mq_pkt_desc*)(sc.dev + Scratch::kDesc);
   uint8_t* st = sc.dev + Scratch::kStatus;
   uint64_t* pn = (uint64_t*)(sc.dev + Scratch::kPn);
-  // the arena is the whole scratch buffer; the packet sits at offset kHdr
+  // the arena is the whole scratch buffer; the packet sits at offset kHdr. NO_HP: no header
+  // protection pass to launch (own_hp false)
   hipError_t e = row.suite == MQ_SUITE_CHACHA20
-                     ? mq_launch_chacha(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, st, pn, nullptr, sc.stream)
-                     : mq_launch_aes(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, st, pn, nullptr, sc.stream);
+                     ? mq_launch_chacha(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, st, pn, nullptr, false, sc.stream)
+                     : mq_launch_aes(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, st, pn, nullptr, false, sc.stream);
   if (e != hipSuccess) return MQ_ERR_HIP;
   // status and the transformed packet in one read-back (the status sits before the packet)
   if ((rc = sc.finish(Scratch::kStatus, Scratch::kHdr - Scratch::kStatus + pkt_len)) != MQ_OK) return rc;
@@ -679,9 +683,10 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
   // open with a workspace: header-protection masks come from the one-lane-per-packet pre-pass
   uint2* hpm = (open && ws) ? (uint2*)ws : nullptr;
   if (suite_hint == MQ_SUITE_CHACHA20) {
-    e = mq_launch_chacha(open, kt->dev, kt->rows, arena, arena_len, desc, n, nullptr, nullptr, status, pn_out, hpm, s);
+    e = mq_launch_chacha(open, kt->dev, kt->rows, arena, arena_len, desc, n, nullptr, nullptr, status, pn_out, hpm, true,
+                         s);
   } else if (suite_hint == MQ_SUITE_AES128GCM && (kt->rows == 1 || !ws || n > (1u << 30))) {
-    e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, n, nullptr, nullptr, status, pn_out, hpm, s);
+    e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, n, nullptr, nullptr, status, pn_out, hpm, true, s);
   } else if (suite_hint == MQ_SUITE_MIXED || suite_hint == MQ_SUITE_AES128GCM) {
     // the two index lists (2 x mq_partition_list_cap(n) entries, holes included) are addressed
     // with 32-bit positions: up to 2^30 packets per mixed batch. An AES batch over several key
@@ -699,14 +704,21 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
     // list mode: the grids cover the list capacity; the kernels read the real lengths from counts
     const uint32_t cap = mq_partition_list_cap(n);
     e = mq_launch_partition(kt->dev, kt->rows, desc, n, list, hist, counts, s);
+    // mixed: one header-protection pass covers both lists (before the tiles for open, after
+    // both suites' tiles for seal); an AES-hinted batch keeps the per-launch passes
+    const bool own = aes_only;
+    if (e == hipSuccess && !own && open && hpm)
+      e = mq_launch_mixed_hp(true, kt->dev, kt->rows, arena, arena_len, desc, list, cap, counts, status, hpm, s);
     if (e == hipSuccess)
-      e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list, counts, status, pn_out, hpm, s);
+      e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list, counts, status, pn_out, hpm, own, s);
     if (e == hipSuccess && aes_only)
       e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list + cap, counts + 1, status, pn_out,
-                        hpm, s);
+                        hpm, own, s);
     else if (e == hipSuccess)
       e = mq_launch_chacha(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list + cap, counts + 1, status,
-                           pn_out, hpm, s);
+                           pn_out, hpm, own, s);
+    if (e == hipSuccess && !own && !open)
+      e = mq_launch_mixed_hp(false, kt->dev, kt->rows, arena, arena_len, desc, list, cap, counts, status, nullptr, s);
   } else {
     return MQ_ERR_INVALID_ARG;
   }
