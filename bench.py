@@ -16,8 +16,8 @@ failure counts and tag checksums; rank 0 checks the checksum of a fixed sample o
 against the CPU oracle (the checker, outside the timed region).
 
   value  = sum over ranks of wire bytes x 2 / max-over-ranks(t_seal + t_open) / 2^30   [GiB/s]
-  roofline.achieved = algorithmic bytes of one seal launch (2 x L per packet: read + write) /
-                      its average duration, from HIP events on the launch stream
+  roofline.achieved = algorithmic bytes of one seal (2 x L per packet: read + write) / the seal
+                      composite's average duration (tile kernel + HP pass), HIP events on its stream
   cpu_baseline = the C oracle (oracle/, "port") on a bounded sample (1 core, the box's CPU share,
                  all cores); cpu_openssl = OpenSSL EVP running the same composites
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config b|c|e] [--packets P] [--keys K]
@@ -295,25 +295,34 @@ def end_to_end(torch, batch, kt, w, sd, od, dev, chunks=8, reps=3):
 
 
 # ---- roofline bookkeeping ---------------------------------------------------------------------
-KERNELS = {"b": "mq_chacha_seal_kernel", "c": "mq_aes_seal_kernel", "e": None}
+# The seal composite of a single-suite batch: the tile kernel, then the header-protection pass
+# (ChaCha20: every packet's mask; AES: the packets with no free slot in their tile). The "1" tile
+# kernel variant (key material in SGPRs) runs when the key table has a single row (launchers in
+# mq_chacha.hip / mq_aes.hip). seal_ms (HIP events around mq_batch_seal) spans both.
+KERNELS = {"b": ("mq_chacha_seal_kernel", "mq_chacha_seal_hp_kernel"),
+           "c": ("mq_aes_seal_kernel", "mq_aes_seal_hp_kernel"), "e": None}
 
 
-def seal_kernel(cfg, n_rows):
-    """The seal kernel a single-suite batch launches: the "1" variant (key material in SGPRs)
-    when the key table has a single row (launchers in mq_chacha.hip / mq_aes.hip)."""
-    k = KERNELS.get(cfg)
-    return k.replace("_seal_kernel", "_seal1_kernel") if k and n_rows == 1 else k
+def seal_kernels(cfg, n_rows):
+    ks = KERNELS.get(cfg)
+    if not ks:
+        return None
+    tile, hp = ks
+    return (tile.replace("_seal_kernel", "_seal1_kernel") if n_rows == 1 else tile), hp
 
 
-def load_traffic(cfg, kern):
-    """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC summary
+def load_traffic(cfg, kerns):
+    """HBM bytes per seal composite (sum over its kernels) from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic_<cfg>.json, written by tools/pmc_summary.py: FETCH_SIZE x 2 + WRITE_SIZE),
     measured at the default 2^20 packets per GPU (reported only for that size)."""
     path = os.path.join(ROOT, "profiles", f"pmc_traffic_{cfg}.json")
     try:
         with open(path) as f:
-            d = json.load(f)
-        return int(d["kernels"][kern]["hbm_bytes_per_launch"]) if kern else None
+            d = json.load(f)["kernels"]
+        if not kerns:
+            return None
+        by_name = {k.split("(")[0]: v for k, v in d.items()}
+        return int(sum(by_name[k]["hbm_bytes_per_launch"] for k in kerns))
     except (OSError, ValueError, KeyError, TypeError):
         return None
 
@@ -404,13 +413,14 @@ def main():
     if rank == 0:
         algo_bytes = 2.0 * wire  # per launch: read + write of every wire byte
         achieved = algo_bytes / (seal_ms * 1e-3) / 1e9
-        kern = seal_kernel(args.config, len(w.keys))
+        kerns = seal_kernels(args.config, len(w.keys))
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": load_traffic(args.config, kern) if (w.n == 1 << 20 and args.keys == 1) else None,
+                "traffic": load_traffic(args.config, kerns) if (w.n == 1 << 20 and args.keys == 1) else None,
                 # north_star's "HBM-read roofline" fraction: wire bytes read per seal ÷ 8 TB/s
                 "read_frac": round(wire / (seal_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                "kernel": kern or "seal batch (partition + AES + ChaCha kernels)",
+                "kernel": ("seal composite: " + " + ".join(kerns)) if kerns
+                          else "seal batch (partition + AES + ChaCha kernels + HP pass)",
                 "seal_ms": round(seal_ms, 4), "open_ms": round(open_ms, 4),
                 "open_frac": round(algo_bytes / (open_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "algorithmic_bytes_per_launch": int(algo_bytes)}

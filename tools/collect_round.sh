@@ -8,6 +8,8 @@ cp $O/latency.json profiles/${T}_latency_per_packet.json
 cp $O/ossl_scaling.txt profiles/${T}_ossl_scaling.txt
 cp $O/pmc_b.txt profiles/${T}_pmc_b.txt; cp $O/pmc_c.txt profiles/${T}_pmc_c.txt
 cp $O/pmc_traffic_b.json profiles/${T}_pmc_traffic_b.json; cp $O/pmc_traffic_c.json profiles/${T}_pmc_traffic_c.json
+# the PMC traffic bench.py quotes as roofline.traffic
+cp $O/pmc_traffic_b.json profiles/pmc_traffic_b.json; cp $O/pmc_traffic_c.json profiles/pmc_traffic_c.json
 cp $O/tests.log profiles/${T}_gpu_tests.log
 for c in b c e; do cp $O/prof_$c/run_kernel_stats.csv profiles/${T}_kernel_stats_$c.csv; done
 ls profiles/${T}_* | wc -l
