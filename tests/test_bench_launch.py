@@ -49,3 +49,17 @@ def test_sample_indices_and_shard_positions():
             got.append(local + rank * n)
         assert (np.concatenate(got) == g).all()
     assert len(shard.sample_indices(8 << 20)) == 4096
+
+
+def test_roofline_seal_composite_traffic():
+    """roofline.kernel / traffic name the seal composite the bench's event time covers: the tile
+    kernel ("1" variant for a one-row key table) plus the header-protection pass; the PMC traffic
+    is the sum of both kernels' per-launch HBM bytes from profiles/pmc_traffic_<cfg>.json."""
+    assert bench.seal_kernels("b", 1) == ("mq_chacha_seal1_kernel", "mq_chacha_seal_hp_kernel")
+    assert bench.seal_kernels("c", 1024) == ("mq_aes_seal_kernel", "mq_aes_seal_hp_kernel")
+    assert bench.seal_kernels("e", 4098) is None
+    for cfg in ("b", "c"):
+        ks = bench.seal_kernels(cfg, 1)
+        with open(os.path.join(HERE, "..", "profiles", f"pmc_traffic_{cfg}.json")) as f:
+            d = {k.split("(")[0]: v["hbm_bytes_per_launch"] for k, v in json.load(f)["kernels"].items()}
+        assert bench.load_traffic(cfg, ks) == int(sum(d[k] for k in ks))
