@@ -24,11 +24,11 @@
 // majority key does. With no majority the vote's candidate is just some key: results are the
 // same either way, only the tile composition changes.
 //
-// Launches: fill + sampled vote (mq_part_init_kernel); per-block class histograms
-// (class-major) and, keyed, per-(row, class) counts (global atomics, one per distinct bin per
-// wave); one workgroup for the exclusive scan of the histograms and, keyed, the scan of the
-// per-row counts into bin bases; scatter. (r02: five launches with a full vote pass took ~126 us per
-// mixed 2^20-packet partition.)
+// Launches: fill + sliced sample vote (mq_part_init_kernel); per-block class histograms
+// (class-major) and, keyed, per-(row, class) counts (one global atomic per packet); one workgroup
+// for the exclusive scan of the histograms and, keyed, the scan of the per-row counts into bin
+// bases; scatter. (r02 start: eight operations with a full vote pass, ~126 us per mixed
+// 2^20-packet partition.)
 #include "mq_tile.h"
 
 using namespace mq;
@@ -75,49 +75,6 @@ __device__ __forceinline__ uint32_t part_class(uint32_t hot, const PartItem& x) 
 __device__ __forceinline__ uint32_t key_bin(const PartItem& x) {
   return x.key * kKeyClasses + (kKeyClasses - 1 - min(x.len >> 7, kKeyClasses - 1));
 }
-// Per distinct bin among the wave's lanes with `pend`, one atomicAdd of its lane count on
-// ctr[bin] — all issued by one instruction: the wave sorts its (bin, lane) pairs (bitonic, 21
-// steps), so equal bins form runs whose first lane adds the run length. With `claim`, every
-// pending lane gets the old value plus its rank in its run, as the list position of descriptor
-// `i` (the lane that receives it need not be the lane that holds it: position and index travel
-// together), returned through pos / idx (pos = 0xFFFFFFFF: nothing for this lane).
-template <bool CLAIM>
-__device__ __forceinline__ void wave_bin_add(uint32_t* ctr, uint32_t bin, bool pend, uint32_t i, uint32_t& pos,
-                                             uint32_t& idx) {
-  const int lane = threadIdx.x & 63;
-  constexpr uint32_t kNone = 0xFFFFFFFFu;
-  // key: bin (< 2^26) above the lane; idle lanes sort last
-  uint32_t k = pend ? (bin << 6 | (uint32_t)lane) : kNone;
-#pragma unroll
-  for (int sz = 2; sz <= 64; sz <<= 1) {
-#pragma unroll
-    for (int st = sz >> 1; st >= 1; st >>= 1) {
-      const uint32_t o = (uint32_t)__shfl_xor((int)k, st, kWave);
-      const bool up = (lane & sz) == 0, low = (lane & st) == 0;
-      k = (low == up) ? min(k, o) : max(k, o);
-    }
-  }
-  const bool valid = k != kNone;
-  const uint32_t b = k >> 6;
-  const uint32_t prev = (uint32_t)__shfl_up((int)k, 1, kWave) >> 6;
-  const bool head = lane == 0 || b != prev || !valid;  // idle lanes end the last run
-  const uint64_t heads = __ballot(head);
-  const uint64_t upto = ~0ull >> (63 - lane);  // lanes 0..lane
-  const int start = 63 - __clzll((long long)(heads & upto));
-  const uint64_t after = heads & ~upto;
-  const int end = after ? __ffsll((unsigned long long)after) - 1 : 64;
-  uint32_t base = 0;
-  if (valid && head) {
-    if (CLAIM) base = atomicAdd(&ctr[b], (uint32_t)(end - lane));
-    else atomicAdd(&ctr[b], (uint32_t)(end - lane));
-  }
-  if (CLAIM) {
-    base = (uint32_t)__shfl((int)base, start, kWave);
-    pos = valid ? base + (uint32_t)(lane - start) : kNone;
-    idx = (uint32_t)__shfl((int)i, (int)(k & 63u), kWave);  // descriptor of the sorted pair's lane
-  }
-}
-
 // Boyer-Moore majority pairs (candidate, count); combining any partition of the input in any
 // order keeps the majority element if there is one
 __device__ __forceinline__ uint2 vote_join(uint2 a, uint2 b) {
@@ -164,35 +121,41 @@ uint32_t mq_partition_list_cap(uint32_t n) {
 }
 
 // The batch's hot AES key: Boyer-Moore vote over a fixed sample of kVoteSample descriptors
-// (evenly spaced), one workgroup. The hot key only shapes tiles; any candidate gives the same
-// results.
-constexpr uint32_t kVoteSample = 4096;
-__device__ __forceinline__ uint32_t sampled_hot(const KeyRow* __restrict__ kt, uint32_t n_rows,
-                                                const mq_pkt_desc* __restrict__ desc, uint32_t n) {
-  constexpr int kPer = kVoteSample / kPartThreads;
+// (evenly spaced), in kVoteSlices slices of 256 — init blocks 0 .. V-1 vote one slice each
+// (votes[s]), and every count block folds the V slice votes the same way (lane 0's result),
+// so no launch and no single workgroup carries it. The hot key only shapes tiles; any candidate
+// gives the same results.
+constexpr uint32_t kVoteSample = 4096, kVoteSlice = 256, kVoteSlices = kVoteSample / kVoteSlice;
+__device__ __forceinline__ uint2 vote_slice(const KeyRow* __restrict__ kt, uint32_t n_rows,
+                                            const mq_pkt_desc* __restrict__ desc, uint32_t n, uint32_t s) {
   const uint32_t S = min(n, kVoteSample), stride = n / S;
-  uint32_t key[kPer];
-#pragma unroll
-  for (int q = 0; q < kPer; ++q) {
-    const uint32_t k = threadIdx.x + kPartThreads * q;
-    key[q] = k < S ? desc[k * stride].key_id : 0xFFFFFFFFu;
-  }
+  const uint32_t k = s * kVoteSlice + threadIdx.x;
   uint2 v = make_uint2(kNoKey, 0u);
+  if (threadIdx.x < kVoteSlice && k < S) {
+    const uint32_t key = desc[k * stride].key_id;
+    if (key < n_rows && kt[key].suite == MQ_SUITE_AES128GCM) v = make_uint2(key, 1u);
+  }
+  return block_vote(v);
+}
+// fold of the slice votes (every lane of a wave computes it; the result is lane 0's)
+__device__ __forceinline__ uint32_t fold_votes(const uint2* __restrict__ votes, uint32_t nv) {
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  uint2 v = lane < nv ? votes[lane] : make_uint2(kNoKey, 0u);
 #pragma unroll
-  for (int q = 0; q < kPer; ++q)
-    if (key[q] < n_rows && kt[key[q]].suite == MQ_SUITE_AES128GCM) v = vote_join(v, make_uint2(key[q], 1u));
-  v = block_vote(v);
-  return v.y ? v.x : kNoKey;
+  for (int d = kWave / 2; d > 0; d >>= 1)
+    v = vote_join(v, make_uint2((uint32_t)__shfl_xor((int)v.x, d, kWave), (uint32_t)__shfl_xor((int)v.y, d, kWave)));
+  const uint32_t x = __builtin_amdgcn_readfirstlane(v.x), y = __builtin_amdgcn_readfirstlane(v.y);
+  return y ? x : kNoKey;
 }
 // First launch: fills the lists with holes and zeroes the keyed bins (grid-stride, 16-B stores);
-// block 0 also runs the sampled vote, so it costs no launch of its own.
+// blocks 0 .. nv-1 also vote a sample slice each.
 extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_init_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_pkt_desc* __restrict__ desc, uint32_t n,
-    uint32_t* __restrict__ hot_p, uint4* __restrict__ list, uint32_t list_q, uint4* __restrict__ bins,
+    uint2* __restrict__ votes, uint32_t nv, uint4* __restrict__ list, uint32_t list_q, uint4* __restrict__ bins,
     uint32_t bins_q) {
-  if (blockIdx.x == 0) {  // block-uniform
-    const uint32_t hot = sampled_hot(kt, n_rows, desc, n);
-    if (threadIdx.x == 0) *hot_p = hot;
+  if (blockIdx.x < nv) {  // block-uniform
+    const uint2 v = vote_slice(kt, n_rows, desc, n, blockIdx.x);
+    if (threadIdx.x == 0) votes[blockIdx.x] = v;
   }
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < list_q; q += stride)
@@ -204,21 +167,24 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_init_kernel(
 // non-majority AES packets are counted per (row, class) bin instead.
 extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_count_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_pkt_desc* __restrict__ desc, uint32_t n,
-    uint32_t nblocks, const uint32_t* __restrict__ hot_p, uint32_t* __restrict__ hist, uint32_t* __restrict__ bins) {
+    uint32_t nblocks, const uint2* __restrict__ votes, uint32_t nv, uint32_t* __restrict__ hot_p,
+    uint32_t* __restrict__ hist, uint32_t* __restrict__ bins) {
   __shared__ uint32_t s_cnt[kClasses];
   PartItem it[kPartItems];
   part_fetch(kt, n_rows, desc, n, it);
   if (threadIdx.x < kClasses) s_cnt[threadIdx.x] = 0;
-  const uint32_t hot = *hot_p;
+  const uint32_t hot = fold_votes(votes, nv);  // the same in every wave of every block
+  if (blockIdx.x == 0 && threadIdx.x == 0) *hot_p = hot;  // for the scatter
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < kPartItems; ++k) {
     const uint32_t i = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
     const bool in = i < n;
     const uint32_t c = in ? part_class(hot, it[k]) : 0u;
-    const bool keyed = bins && in && c / kLenClasses == 1;  // wave-uniform branch below
-    uint32_t pos, idx;
-    if (bins && __ballot(keyed)) wave_bin_add<false>(bins, keyed ? key_bin(it[k]) : 0u, keyed, i, pos, idx);
+    const bool keyed = bins && in && c / kLenClasses == 1;
+    // keyed bins: one global atomic per packet (the bins of a wave's lanes are mostly distinct:
+    // packets of many keys; equal ones serialise inside the instruction)
+    if (keyed) atomicAdd(&bins[key_bin(it[k])], 1u);
     if (in && !keyed) atomicAdd(&s_cnt[c], 1u);
   }
   __syncthreads();
@@ -376,11 +342,7 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_scatter_kerne
     const uint32_t i = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
     const uint32_t c = i < n ? part_class(hot, it[k]) : 0u;
     const bool keyed = bins && i < n && c / kLenClasses == 1;
-    if (bins && __ballot(keyed)) {
-      uint32_t pos, idx;
-      wave_bin_add<true>(bins, keyed ? key_bin(it[k]) : 0u, keyed, i, pos, idx);
-      if (pos != 0xFFFFFFFFu) list[pos] = idx;
-    }
+    if (keyed) list[atomicAdd(&bins[key_bin(it[k])], 1u)] = i;  // position inside the bin: any order
     const bool in = i < n && !keyed;
     // lanes of this wave with the same class (7 ballots), rank among them = peers below
     uint64_t peers = __ballot(in);
@@ -403,13 +365,16 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_scatter_kerne
 }
 
 // keyed layout bins: one counter per (row, class), within a budget of 2 per packet (at least
-// 64 Ki) and below 2^26 (wave_bin_add's sort keys), and only when the keyed list (at most 7
-// holes per row) fits the list capacity
+// 64 Ki) and below 2^26, and only when the keyed list (at most 7 holes per row) fits the list
+// capacity
 static size_t key_bins(uint32_t n) { return 2 * (size_t)n > 65536 ? 2 * (size_t)n : 65536; }
 static bool keyed_layout(uint32_t n, uint32_t n_rows) {
   return (size_t)n_rows * kKeyClasses <= key_bins(n) && (size_t)n_rows * kKeyClasses < (1u << 26) &&
          (uint64_t)n + kPktsPerTile * kLenClasses + (uint64_t)(kPktsPerTile - 1) * n_rows <= mq_partition_list_cap(n);
 }
+
+// meta: counts[0..1] | hot row | pad | seg[kClasses] | slice votes (kVoteSlices pairs)
+constexpr uint32_t kMetaWords = 4 + kClasses + 2 * kVoteSlices;
 
 // list (2 x cap entries) | class histograms (kClasses per block) |
 // meta (2 totals, hot row, pad, kClasses segment starts) | keyed bins, 256-B aligned pieces
@@ -420,15 +385,20 @@ hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_d
   const uint32_t nblocks = (n + kPartBlock - 1) / kPartBlock;
   if (nblocks == 0) return hipMemsetAsync(counts, 0, 2 * sizeof(uint32_t), s);
   const uint32_t cap = mq_partition_list_cap(n);
-  uint32_t* hot = counts + 2;  // meta: counts[0..1] | hot row | pad | seg[kClasses]
+  uint32_t* hot = counts + 2;  // meta (kMetaWords): counts[0..1] | hot row | pad | seg | votes
   uint32_t* seg = counts + 4;
-  uint32_t* bins = keyed_layout(n, n_rows) ? (uint32_t*)((uint8_t*)counts + part_align(sizeof(uint32_t) * (4 + kClasses)))
+  uint2* votes = (uint2*)(counts + 4 + kClasses);
+  uint32_t* bins = keyed_layout(n, n_rows) ? (uint32_t*)((uint8_t*)counts + part_align(sizeof(uint32_t) * kMetaWords))
                                            : nullptr;
   const uint32_t list_q = cap / 2, bins_q = bins ? kKeyClasses / 4 * n_rows : 0u;  // 16-B words
-  hipLaunchKernelGGL(mq_part_init_kernel, dim3(min(256u, (list_q + bins_q + kPartThreads - 1) / kPartThreads)),
-                     dim3(kPartThreads), 0, s, kt, n_rows, desc, n, hot, (uint4*)list, list_q, (uint4*)bins, bins_q);
+  const uint32_t init_blocks = max(1u, min(256u, (list_q + bins_q + kPartThreads - 1) / kPartThreads));
+  const uint32_t nv = min(kVoteSlices, init_blocks);
+  const uint32_t S = min(n, kVoteSample), used = (S + kVoteSlice - 1) / kVoteSlice;  // slices with samples
+  const uint32_t grid = max(init_blocks, used);
+  hipLaunchKernelGGL(mq_part_init_kernel, dim3(grid), dim3(kPartThreads), 0, s, kt, n_rows, desc, n, votes,
+                     max(nv, used), (uint4*)list, list_q, (uint4*)bins, bins_q);
   hipLaunchKernelGGL(mq_part_count_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, kt, n_rows, desc, n,
-                     nblocks, hot, hist, bins);
+                     nblocks, votes, max(nv, used), hot, hist, bins);
   hipLaunchKernelGGL(mq_part_scan_kernel, dim3(1), dim3(64 * kScanWaves), 0, s, hist, nblocks, cap, counts, seg,
                      bins, n_rows);
   hipLaunchKernelGGL(mq_part_scatter_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, kt, n_rows, desc, n,
@@ -439,7 +409,7 @@ hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_d
 size_t mq_partition_workspace(uint32_t n) {
   const size_t nblocks = (n + kPartBlock - 1) / kPartBlock;
   return part_align(sizeof(uint32_t) * 2 * (size_t)mq_partition_list_cap(n)) +
-         part_align(sizeof(uint32_t) * kClasses * nblocks) + part_align(sizeof(uint32_t) * (4 + kClasses)) +
+         part_align(sizeof(uint32_t) * kClasses * nblocks) + part_align(sizeof(uint32_t) * kMetaWords) +
          part_align(sizeof(uint32_t) * key_bins(n));
 }
 
