@@ -41,8 +41,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)  # ~0.2-0.3 s timed: long enough for SMI samplers
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="b", choices=["b", "c", "e"])
     ap.add_argument("--packets", type=int, default=1 << 20, help="packets per GPU")
     ap.add_argument("--keys", type=int, default=1, help="configs b/c: key rows, key_id = g mod K (SURVEY §8d)")
