@@ -489,13 +489,15 @@ __device__ __forceinline__ void aes_stream_tiles(const KeyRow* __restrict__ kt, 
                                                  const mq_pkt_desc* __restrict__ desc, uint32_t n,
                                                  const uint32_t* __restrict__ index,
                                                  const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status,
-                                                 uint64_t* __restrict__ pn_out, const uint2* __restrict__ hpm) {
+                                                 uint64_t* __restrict__ pn_out, const uint2* __restrict__ hpm,
+                                                 uint32_t skip) {
   const uint32_t w = wave_id();
   const int lane = (int)(threadIdx.x & (kWave - 1)), j = lane & (kLanesPerPkt - 1);
-  constexpr uint32_t W = aes_waves(SINGLE);
+  constexpr uint32_t W = aes_waves(SINGLE), C = SINGLE ? 1u : kAesChunk;
   uint32_t wt_kid = 0xFFFFFFFFu;  // multi-key: the row whose half table and key schedules the wave holds
-  for_tiles<OPEN, SINGLE ? 1u : kAesChunk>(blockIdx.x * W + w, gridDim.x * W, desc, n, index, n_dev, hpm,
+  for_tiles<OPEN, C>(blockIdx.x * W + w + (C == 1 ? skip : 0u), gridDim.x * W, desc, n, index, n_dev, hpm,
                   [&](uint32_t t, const TilePrefetch& pf) __attribute__((always_inline)) {
+    if (C != 1 && t < skip) return;
     PktCtx c;
     const KeyRow* row;
     if (!tile_ctx<MQ_SUITE_AES128GCM, OPEN, SINGLE>(t, kt, n_rows, arena_len, desc, n, index, n_dev, hpm, pf, c,
@@ -551,22 +553,46 @@ __device__ __forceinline__ void aes_stream_tiles(const KeyRow* __restrict__ kt, 
   });
 }
 
+// hot (partition lists only, else null): hot[0] = the hot key's row, hot[1] = the entries of its
+// segment at the front of the list (whole tiles). A single-key kernel then runs that segment with
+// the hot row as its one-row table; the multi-key kernel starts after it.
+template <bool SINGLE>
+__device__ __forceinline__ bool aes_hot_split(const uint32_t* __restrict__ hot, const KeyRow* __restrict__& kt,
+                                              const uint32_t* __restrict__& n_dev, uint32_t& skip) {
+  skip = 0;
+  if (!hot) return true;
+  const uint32_t entries = hot[1];
+  if (SINGLE) {
+    if (entries == 0) return false;  // workgroup-uniform, before any barrier; hot[0] may be no row
+    kt += hot[0];
+    n_dev = hot + 1;
+  } else {
+    skip = entries / kPktsPerTile;
+  }
+  return true;
+}
+
 #define MQ_AES_KERNELS(NAME_SEAL, NAME_OPEN, SINGLE)                                                      \
   extern "C" __global__ __launch_bounds__(64 * aes_waves(SINGLE)) void NAME_SEAL(                           \
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
-      const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status) {                                 \
+      const uint32_t* __restrict__ n_dev, const uint32_t* __restrict__ hot, uint8_t* __restrict__ status) { \
+    uint32_t skip;                                                                                        \
+    if (!aes_hot_split<SINGLE>(hot, kt, n_dev, skip)) return;                                             \
     aes_tables<SINGLE>(kt);                                                                               \
     aes_stream_tiles<SINGLE, false>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr,  \
-                                    nullptr);                                                             \
+                                    nullptr, skip);                                                       \
   }                                                                                                       \
   extern "C" __global__ __launch_bounds__(64 * aes_waves(SINGLE)) void NAME_OPEN(                           \
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
-      const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,    \
-      const uint2* __restrict__ hpm) {                                                                    \
+      const uint32_t* __restrict__ n_dev, const uint32_t* __restrict__ hot, uint8_t* __restrict__ status, \
+      uint64_t* __restrict__ pn_out, const uint2* __restrict__ hpm) {                                     \
+    uint32_t skip;                                                                                        \
+    if (!aes_hot_split<SINGLE>(hot, kt, n_dev, skip)) return;                                             \
     aes_tables<SINGLE>(kt);                                                                               \
-    aes_stream_tiles<SINGLE, true>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm); \
+    aes_stream_tiles<SINGLE, true>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm, \
+                                   skip);                                                                 \
   }
 MQ_AES_KERNELS(mq_aes_seal_kernel, mq_aes_open_kernel, false)
 MQ_AES_KERNELS(mq_aes_seal1_kernel, mq_aes_open1_kernel, true)
@@ -677,10 +703,14 @@ static uint32_t aes_grid(uint32_t tiles, uint32_t waves) {
 
 hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena, uint64_t arena_len,
                          const mq_pkt_desc* desc, uint32_t n, const uint32_t* index, const uint32_t* n_dev,
-                         uint8_t* status, uint64_t* pn_out, uint2* hpm, bool own_hp, hipStream_t s) {
+                         const uint32_t* hot, uint8_t* status, uint64_t* pn_out, uint2* hpm, bool own_hp,
+                         hipStream_t s) {
   const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
   if (tiles == 0) return hipSuccess;
   const uint32_t waves = aes_waves(n_rows == 1), blocks = aes_grid(tiles, waves);
+  // a partition list over several rows: the hot key's segment on a single-key kernel first
+  hot = (hot && index && n_rows > 1) ? hot : nullptr;
+  const uint32_t hot_blocks = hot ? aes_grid(tiles, aes_waves(true)) : 0u;
   if (open && hpm && own_hp) {  // !own_hp: mq_launch_mixed_hp covers both suites' lists
     hipLaunchKernelGGL(mq_aes_open_hp_kernel<true>, dim3((n + 255) / 256), dim3(256), 0, s, kt, n_rows, arena,
                        arena_len, desc, n, index, n_dev, hpm);
@@ -688,12 +718,18 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
     if (e != hipSuccess) return e;
   }
   if (open) {
+    if (hot)
+      hipLaunchKernelGGL(mq_aes_open1_kernel, dim3(hot_blocks), dim3(64 * aes_waves(true)), 0, s, kt, n_rows, arena,
+                         arena_len, desc, n, index, n_dev, hot, status, pn_out, hpm);
     hipLaunchKernelGGL(n_rows == 1 ? mq_aes_open1_kernel : mq_aes_open_kernel, dim3(blocks), dim3(64 * waves),
-                       0, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm);
+                       0, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, hot, status, pn_out, hpm);
     return hipGetLastError();
   }
+  if (hot)
+    hipLaunchKernelGGL(mq_aes_seal1_kernel, dim3(hot_blocks), dim3(64 * aes_waves(true)), 0, s, kt, n_rows, arena,
+                       arena_len, desc, n, index, n_dev, hot, status);
   hipLaunchKernelGGL(n_rows == 1 ? mq_aes_seal1_kernel : mq_aes_seal_kernel, dim3(blocks), dim3(64 * waves),
-                     0, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status);
+                     0, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, hot, status);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess || !own_hp) return e;
   hipLaunchKernelGGL(mq_aes_seal_hp_kernel, dim3((n + 255) / 256), dim3(256), 0, s, kt, arena, arena_len, desc, n,

@@ -27,8 +27,8 @@ hipError_t mq_launch_chacha_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t
                                const uint8_t* samples, uint8_t* masks, uint32_t n, hipStream_t s);
 hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena,
                          uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
-                         const uint32_t* index, const uint32_t* n_dev, uint8_t* status,
-                         uint64_t* pn_out, uint2* hpm, bool own_hp, hipStream_t s);
+                         const uint32_t* index, const uint32_t* n_dev, const uint32_t* hot,
+                         uint8_t* status, uint64_t* pn_out, uint2* hpm, bool own_hp, hipStream_t s);
 hipError_t mq_launch_mixed_hp(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena, uint64_t arena_len,
                               const mq_pkt_desc* desc, const uint32_t* list, uint32_t cap, const uint32_t* counts,
                               const uint8_t* status, uint2* hpm, hipStream_t s);
@@ -392,7 +392,8 @@ int run_one(Scratch& sc, const KeyRow& row, const uint8_t* aad, uint32_t aad_len
   // protection pass to launch (own_hp false)
   hipError_t e = row.suite == MQ_SUITE_CHACHA20
                      ? mq_launch_chacha(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, st, pn, nullptr, false, sc.stream)
-                     : mq_launch_aes(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, st, pn, nullptr, false, sc.stream);
+                     : mq_launch_aes(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, nullptr, st, pn, nullptr, false,
+                                     sc.stream);
   if (e != hipSuccess) return MQ_ERR_HIP;
   // status and the transformed packet in one read-back (the status sits before the packet)
   if ((rc = sc.finish(Scratch::kStatus, Scratch::kHdr - Scratch::kStatus + pkt_len)) != MQ_OK) return rc;
@@ -686,7 +687,8 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
     e = mq_launch_chacha(open, kt->dev, kt->rows, arena, arena_len, desc, n, nullptr, nullptr, status, pn_out, hpm, true,
                          s);
   } else if (suite_hint == MQ_SUITE_AES128GCM && (kt->rows == 1 || !ws || n > (1u << 30))) {
-    e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, n, nullptr, nullptr, status, pn_out, hpm, true, s);
+    e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, n, nullptr, nullptr, nullptr, status, pn_out,
+                      hpm, true, s);
   } else if (suite_hint == MQ_SUITE_MIXED || suite_hint == MQ_SUITE_AES128GCM) {
     // the two index lists (2 x mq_partition_list_cap(n) entries, holes included) are addressed
     // with 32-bit positions: up to 2^30 packets per mixed batch. An AES batch over several key
@@ -707,12 +709,15 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
     // mixed: one header-protection pass covers both lists (before the tiles for open, after
     // both suites' tiles for seal); an AES-hinted batch keeps the per-launch passes
     const bool own = aes_only;
+    // counts + 2: the hot key's row and segment length (list 0's front), which the AES launch runs
+    // on its single-key kernel
     if (e == hipSuccess && !own && open && hpm)
       e = mq_launch_mixed_hp(true, kt->dev, kt->rows, arena, arena_len, desc, list, cap, counts, status, hpm, s);
     if (e == hipSuccess)
-      e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list, counts, status, pn_out, hpm, own, s);
+      e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list, counts, counts + 2, status,
+                        pn_out, hpm, own, s);
     if (e == hipSuccess && aes_only)
-      e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list + cap, counts + 1, status, pn_out,
+      e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list + cap, counts + 1, nullptr, status, pn_out,
                         hpm, own, s);
     else if (e == hipSuccess)
       e = mq_launch_chacha(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list + cap, counts + 1, status,

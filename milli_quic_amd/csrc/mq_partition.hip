@@ -194,7 +194,8 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_count_kernel(
 // Single workgroup: per class, the exclusive scan of its per-block counts (in place: the rank of
 // the block's first packet inside the class); then the class segments (whole tiles) are laid out
 // list by list (groups 0 and 1: list 0, group 2: list 1 at `cap`): seg[c] = first list entry of
-// class c, counts[s] = entries of list s, holes included.
+// class c, counts[s] = entries of list s, holes included; counts[3] = entries of the hot key's
+// classes (the front of list 0, whole tiles).
 // Latency-bound work (a few thousand counts): each wave owns kClasses / 16 classes and issues
 // all their loads before any scan (4 consecutive blocks per lane per 256-block chunk), so the
 // kernel waits on memory once instead of once per class (r01: 26 us per partition, rocprof).
@@ -253,7 +254,9 @@ extern "C" __global__ __launch_bounds__(64 * kScanWaves) void mq_part_scan_kerne
     const uint32_t ent = in ? kPktsPerTile * ((s_tot[c] + ppt - 1) / ppt) : 0u;
     const uint32_t incl = wave_incl_scan(ent), e = lane_u32(incl, kWave - 1);
     if (in) seg[c] = s * cap + incl - ent;
+    const uint32_t hot_e = lane_u32(incl, kLenClasses - 1);  // list 0: the hot key's classes first
     if (lane == 0) {
+      if (s == 0) counts[3] = hot_e;
       // mq_partition_list_cap bounds e; the clamp only keeps a broken bound from running a suite
       // kernel over the other list
       counts[s] = min(e, cap);
@@ -373,19 +376,19 @@ static bool keyed_layout(uint32_t n, uint32_t n_rows) {
          (uint64_t)n + kPktsPerTile * kLenClasses + (uint64_t)(kPktsPerTile - 1) * n_rows <= mq_partition_list_cap(n);
 }
 
-// meta: counts[0..1] | hot row | pad | seg[kClasses] | slice votes (kVoteSlices pairs)
+// meta: counts[0..1] | hot row | hot segment entries | seg[kClasses] | slice votes (kVoteSlices pairs)
 constexpr uint32_t kMetaWords = 4 + kClasses + 2 * kVoteSlices;
 
 // list (2 x cap entries) | class histograms (kClasses per block) |
-// meta (2 totals, hot row, pad, kClasses segment starts) | keyed bins, 256-B aligned pieces
+// meta (2 totals, hot row, hot segment entries, kClasses segment starts) | keyed bins, 256-B aligned pieces
 static size_t part_align(size_t b) { return (b + 255) & ~(size_t)255; }
 
 hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_desc* desc, uint32_t n,
                                uint32_t* list, uint32_t* hist, uint32_t* counts, hipStream_t s) {
   const uint32_t nblocks = (n + kPartBlock - 1) / kPartBlock;
-  if (nblocks == 0) return hipMemsetAsync(counts, 0, 2 * sizeof(uint32_t), s);
+  if (nblocks == 0) return hipMemsetAsync(counts, 0, 4 * sizeof(uint32_t), s);
   const uint32_t cap = mq_partition_list_cap(n);
-  uint32_t* hot = counts + 2;  // meta (kMetaWords): counts[0..1] | hot row | pad | seg | votes
+  uint32_t* hot = counts + 2;  // meta (kMetaWords): counts[0..1] | hot row | hot entries | seg | votes
   uint32_t* seg = counts + 4;
   uint2* votes = (uint2*)(counts + 4 + kClasses);
   uint32_t* bins = keyed_layout(n, n_rows) ? (uint32_t*)((uint8_t*)counts + part_align(sizeof(uint32_t) * kMetaWords))
