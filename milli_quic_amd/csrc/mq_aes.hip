@@ -445,7 +445,8 @@ using namespace mq;
 constexpr int aes_waves(bool single) { return single ? 16 : (int)kAesMultiWaves; }
 // multi-key kernels: consecutive tiles per wave (for_tiles chunks). Measured on configs E and C
 // with 1024 keys: chunks of 4 or 8 tiles (a key's tiles sharing one half-table build) lose more
-// to load imbalance than they save, so 1.
+// to load imbalance than they save, so 1. Re-measured with the hot key split off (E's Initial
+// packets only): chunks of 2 / 4 give E +2.0 % / -0.2 %, 1024-key C -0.3 % / -0.9 %; kept at 1.
 #ifndef MQ_AES_CHUNK
 #define MQ_AES_CHUNK 1
 #endif
@@ -495,9 +496,8 @@ __device__ __forceinline__ void aes_stream_tiles(const KeyRow* __restrict__ kt, 
   const int lane = (int)(threadIdx.x & (kWave - 1)), j = lane & (kLanesPerPkt - 1);
   constexpr uint32_t W = aes_waves(SINGLE), C = SINGLE ? 1u : kAesChunk;
   uint32_t wt_kid = 0xFFFFFFFFu;  // multi-key: the row whose half table and key schedules the wave holds
-  for_tiles<OPEN, C>(blockIdx.x * W + w + (C == 1 ? skip : 0u), gridDim.x * W, desc, n, index, n_dev, hpm,
+  for_tiles<OPEN, C>(blockIdx.x * W + w, gridDim.x * W, desc, n, index, n_dev, hpm,
                   [&](uint32_t t, const TilePrefetch& pf) __attribute__((always_inline)) {
-    if (C != 1 && t < skip) return;
     PktCtx c;
     const KeyRow* row;
     if (!tile_ctx<MQ_SUITE_AES128GCM, OPEN, SINGLE>(t, kt, n_rows, arena_len, desc, n, index, n_dev, hpm, pf, c,
@@ -550,7 +550,7 @@ __device__ __forceinline__ void aes_stream_tiles(const KeyRow* __restrict__ kt, 
     }
     MQ_STAMP(t, 7);
     tile_status<OPEN>(c, j, status, pn_out);
-  });
+  }, skip);
 }
 
 // hot (partition lists only, else null): hot[0] = the hot key's row, hot[1] = the entries of its

@@ -479,19 +479,20 @@ __device__ __forceinline__ void run_tile(uint8_t* smem, uint32_t tile_id, const 
 // further ahead still (list entry, then descriptor: two dependent loads off the critical path).
 // Tiles are taken in chunks of C consecutive ones — chunks first, first + stride, ... — so that
 // a multi-key wave meets a key's consecutive tiles (the partition lays them out together) in a
-// row. A device-side count without an index list runs unprefetched.
+// row. Tiles below `base` are not this launch's (chunks count from it). A device-side count
+// without an index list runs unprefetched.
 template <bool OPEN, uint32_t C = 1, class F>
 __device__ __forceinline__ void for_tiles(uint32_t first, uint32_t stride, const mq_pkt_desc* __restrict__ desc,
                                           uint32_t n, const uint32_t* __restrict__ index,
                                           const uint32_t* __restrict__ n_dev, const uint2* __restrict__ hpm,
-                                          F&& body) {
+                                          F&& body, uint32_t base = 0) {
   const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
   if (n_dev && !index) {
-    for (uint32_t t = first; t < tiles; t += stride) body(t, TilePrefetch{false, 0u, 0u, 0u});
+    for (uint32_t t = base + first; t < tiles; t += stride) body(t, TilePrefetch{false, 0u, 0u, 0u});
     return;
   }
   const uint32_t lane = threadIdx.x & (kWave - 1), p = lane / kLanesPerPkt, j = lane % kLanesPerPkt;
-  auto next = [&](uint32_t t) { return (t + 1) % C != 0 ? t + 1 : t + 1 - C + stride * C; };
+  auto next = [&](uint32_t t) { return (t - base + 1) % C != 0 ? t + 1 : t + 1 - C + stride * C; };
   auto idx_of = [&](uint32_t t) -> uint32_t {  // packet p's descriptor index (list: a load)
     const uint32_t e = t * kPktsPerTile + p;
     if (t >= tiles || e >= n) return kListHole;
@@ -502,7 +503,7 @@ __device__ __forceinline__ void for_tiles(uint32_t first, uint32_t stride, const
     dw = ok ? reinterpret_cast<const uint32_t*>(desc)[(size_t)ix * 8 + j] : 0u;
     hm = (OPEN && hpm && ok && j < 2) ? reinterpret_cast<const uint32_t*>(hpm)[(size_t)ix * 2 + j] : 0u;
   };
-  uint32_t t = first * C, t1 = next(t);
+  uint32_t t = base + first * C, t1 = next(t);
   uint32_t ix0 = idx_of(t), ix1 = idx_of(t1), dw, hm;
   fetch(ix0, dw, hm);
   while (t < tiles) {
