@@ -563,7 +563,9 @@ __device__ __forceinline__ bool aes_hot_split(const uint32_t* __restrict__ hot, 
   if (!hot) return true;
   const uint32_t entries = hot[1];
   if (SINGLE) {
-    if (entries == 0) return false;  // workgroup-uniform, before any barrier; hot[0] may be no row
+    // workgroup-uniform, before any barrier: no segment (hot[0] may be no row), or no tile for
+    // this workgroup (a small segment: skip the table builds)
+    if (blockIdx.x * (aes_waves(true) * kPktsPerTile) >= entries) return false;
     kt += hot[0];
     n_dev = hot + 1;
   } else {
@@ -701,6 +703,29 @@ static uint32_t aes_grid(uint32_t tiles, uint32_t waves) {
   return wgs < (uint32_t)(cus * per_cu) ? wgs : (uint32_t)(cus * per_cu);
 }
 
+// The hot segment's kernel on a side stream of the calling thread, forked from and joined back
+// to the caller's stream: each CU then moves from one tile kernel to the other as its own
+// workgroup ends, not after the other kernel's last one.
+#ifndef MQ_AES_HOT_FORK
+#define MQ_AES_HOT_FORK 0
+#endif
+struct SideStream {
+  hipStream_t st = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  bool ok = false;
+};
+static SideStream* side_stream() {
+  static thread_local SideStream ss;
+  static thread_local bool tried = false;
+  if (!tried) {
+    tried = true;
+    ss.ok = hipStreamCreateWithFlags(&ss.st, hipStreamNonBlocking) == hipSuccess &&
+            hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) == hipSuccess;
+  }
+  return ss.ok ? &ss : nullptr;
+}
+
 hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena, uint64_t arena_len,
                          const mq_pkt_desc* desc, uint32_t n, const uint32_t* index, const uint32_t* n_dev,
                          const uint32_t* hot, uint8_t* status, uint64_t* pn_out, uint2* hpm, bool own_hp,
@@ -717,21 +742,34 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
+  SideStream* ss = (hot && MQ_AES_HOT_FORK) ? side_stream() : nullptr;
+  hipStream_t hs = s;
+  if (ss) {
+    hipError_t e = hipEventRecord(ss->fork, s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(ss->st, ss->fork, 0);
+    if (e != hipSuccess) return e;
+    hs = ss->st;
+  }
   if (open) {
     if (hot)
-      hipLaunchKernelGGL(mq_aes_open1_kernel, dim3(hot_blocks), dim3(64 * aes_waves(true)), 0, s, kt, n_rows, arena,
-                         arena_len, desc, n, index, n_dev, hot, status, pn_out, hpm);
+      hipLaunchKernelGGL(mq_aes_open1_kernel, dim3(hot_blocks), dim3(64 * aes_waves(true)), 0, hs, kt, n_rows,
+                         arena, arena_len, desc, n, index, n_dev, hot, status, pn_out, hpm);
     hipLaunchKernelGGL(n_rows == 1 ? mq_aes_open1_kernel : mq_aes_open_kernel, dim3(blocks), dim3(64 * waves),
                        0, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, hot, status, pn_out, hpm);
-    return hipGetLastError();
+  } else {
+    if (hot)
+      hipLaunchKernelGGL(mq_aes_seal1_kernel, dim3(hot_blocks), dim3(64 * aes_waves(true)), 0, hs, kt, n_rows,
+                         arena, arena_len, desc, n, index, n_dev, hot, status);
+    hipLaunchKernelGGL(n_rows == 1 ? mq_aes_seal1_kernel : mq_aes_seal_kernel, dim3(blocks), dim3(64 * waves),
+                       0, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, hot, status);
   }
-  if (hot)
-    hipLaunchKernelGGL(mq_aes_seal1_kernel, dim3(hot_blocks), dim3(64 * aes_waves(true)), 0, s, kt, n_rows, arena,
-                       arena_len, desc, n, index, n_dev, hot, status);
-  hipLaunchKernelGGL(n_rows == 1 ? mq_aes_seal1_kernel : mq_aes_seal_kernel, dim3(blocks), dim3(64 * waves),
-                     0, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, hot, status);
-  const hipError_t e = hipGetLastError();
-  if (e != hipSuccess || !own_hp) return e;
+  hipError_t e = hipGetLastError();
+  if (ss) {  // join even after a failed launch, so the side stream never runs ahead of s
+    const hipError_t ej = hipEventRecord(ss->join, hs);
+    const hipError_t ew = ej == hipSuccess ? hipStreamWaitEvent(s, ss->join, 0) : ej;
+    if (e == hipSuccess) e = ew;
+  }
+  if (e != hipSuccess || open || !own_hp) return e;
   hipLaunchKernelGGL(mq_aes_seal_hp_kernel, dim3((n + 255) / 256), dim3(256), 0, s, kt, arena, arena_len, desc, n,
                      index, n_dev, status);
   return hipGetLastError();
