@@ -707,7 +707,7 @@ static uint32_t aes_grid(uint32_t tiles, uint32_t waves) {
 // to the caller's stream: each CU then moves from one tile kernel to the other as its own
 // workgroup ends, not after the other kernel's last one.
 #ifndef MQ_AES_HOT_FORK
-#define MQ_AES_HOT_FORK 0
+#define MQ_AES_HOT_FORK 1
 #endif
 struct SideStream {
   hipStream_t st = nullptr;
