@@ -126,6 +126,39 @@ def sample_for_rank(cfg, n, rank, world):
     return g, mine - rank * n
 
 
+def parity_check(cfg, w, g_sample, keys, fails, csum, s_csum, pn_ok, dist=None, device=None):
+    """Whole-job parity after the timed region (the checker, CPU oracle). Configs b/c hold ONE global
+    batch: the ranks all-reduce the checksum of the tags at the fixed global sample and rank 0's
+    oracle seals exactly those packets. Config e: every rank holds its own seeded batch, so every
+    rank checks its own sample against the oracle and the ranks all-reduce the verdicts. Returns
+    the parity record (identical on every rank)."""
+    from milli_quic_amd import shard
+    world = dist.get_world_size() if dist is not None and dist.is_initialized() else 1
+    rank = dist.get_rank() if world > 1 else 0
+    own_bad, o_fail, o_csum = 0, 0, None
+    if cfg == "e":  # this rank's own batch
+        o_fail, o_csum = oracle_sample_checksum(cfg, w, g_sample, keys)
+        own_bad = int(o_fail != 0 or o_csum != s_csum)
+    fails_all, csum_all, s_csum_all, pn_bad, bad_ranks = shard.reduce_sums(
+        [fails, csum, s_csum, 0 if pn_ok else 1, own_bad], dist, device)
+    if cfg != "e":
+        o_fail, o_csum = oracle_sample_checksum(cfg, w, g_sample, keys) if rank == 0 else (0, None)
+        bad0 = int(rank == 0 and not (o_fail == 0 and o_csum == s_csum_all))
+        match = shard.reduce_sums([bad0], dist, device)[0] == 0  # rank 0's verdict on every rank
+        scope = f"global batch of {world * w.n}"
+    else:
+        match = bad_ranks == 0
+        scope = f"each rank's own batch, checked by that rank ({world} ranks)"
+    rec = {"failures": fails_all, "pn_mismatch_ranks": pn_bad, "tag_checksum": csum_all,
+           "sample_packets": int(len(g_sample)) * (world if cfg == "e" else 1),
+           "sample_tag_checksum": s_csum_all, "oracle_sample_tag_checksum": o_csum, "sample_scope": scope,
+           "ranks_mismatching_oracle": bad_ranks if cfg == "e" else None,
+           "match": bool(match and fails_all == 0 and pn_bad == 0)}
+    if cfg == "e":
+        rec["oracle_sample_tag_checksum"] = None  # per rank; see ranks_mismatching_oracle
+    return rec
+
+
 def oracle_sample_checksum(cfg, w, g, keys):
     """CPU oracle (the checker) on the sampled global indices: the tag checksum the GPU run must
     reproduce. Config e: rank 0's own batch."""
@@ -402,7 +435,8 @@ def main():
     ls = torch.from_numpy(local_sample.astype(np.int64)).to(dev)
     csum = shard.tag_checksum_torch(arena, offs_t, lens_t)
     s_csum = shard.tag_checksum_torch(arena, offs_t[ls], lens_t[ls])
-    fails_all, csum_all, s_csum_all, pn_bad = shard.reduce_sums([fails, csum, s_csum, 0 if pn_ok else 1], dd, dev)
+    parity = parity_check(args.config, w, g_sample, keys, fails, csum, s_csum, pn_ok, dd, dev)
+    fails_all = parity["failures"]
 
     wire = w.wire_bytes
     tot = shard.reduce_totals(elapsed, wire, 0, dd, dev)
@@ -424,13 +458,6 @@ def main():
                 "seal_ms": round(seal_ms, 4), "open_ms": round(open_ms, 4),
                 "open_frac": round(algo_bytes / (open_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "algorithmic_bytes_per_launch": int(algo_bytes)}
-        # the checker (CPU oracle) on the fixed sample of global indices, outside the timed region
-        o_fail, o_csum = oracle_sample_checksum(args.config, w, g_sample, keys)
-        parity = {"failures": fails_all, "pn_mismatch_ranks": pn_bad, "tag_checksum": csum_all,
-                  "sample_packets": int(len(g_sample)), "sample_tag_checksum": s_csum_all,
-                  "oracle_sample_tag_checksum": o_csum,
-                  "sample_scope": "rank 0's batch" if args.config == "e" else f"global batch of {world * args.packets}",
-                  "match": bool(o_fail == 0 and o_csum == s_csum_all and fails_all == 0 and pn_bad == 0)}
         cpu = ossl = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(w, args.cpu_sample, args.cpu_seconds)
@@ -444,7 +471,9 @@ def main():
                              f"ChaCha20-Poly1305 batch sharded across {world} GPUs")
         out = {
             "metric": "GiB/s device-resident AEAD seal+open, 1M×1200B QUIC packets, 1/2/4/8 GPU",
-            "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            # a run whose results differ from the oracle has no throughput (exit status 1 below)
+            "value": round(value, 2) if parity["match"] else None,
+            "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
             "config": {"workload": workload_name, "packets_per_gpu": w.n, "key_rows": len(w.keys),
@@ -464,6 +493,8 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if not parity["match"]:
+        sys.exit(1)
 
 
 if __name__ == "__main__":

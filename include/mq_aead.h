@@ -186,8 +186,26 @@ typedef struct mq_hp_ctx mq_hp_ctx;         /* one HeaderProtection instance    
 typedef struct mq_keytable mq_keytable;     /* device-resident table of expanded keys            */
 
 /* ---- library / device ---------------------------------------------------------------------- */
+/* Devices. Every object is bound to the device it was created on: key tables (mq_keytable_create)
+ * and AEAD / HP contexts (mq_aead_new, mq_hp_new) are created on the calling thread's device —
+ * the one it selected with mq_device_init, else its current HIP device — and every later call on
+ * them runs on THAT device, whichever thread makes it (a batch call's stream and buffers must
+ * belong to the key table's device). The library never changes a thread's current HIP device,
+ * except in mq_device_init, so one host thread can drive several GPUs, one key table (and stream)
+ * per GPU, and threads on different GPUs never see each other's choice. */
 const char* mq_version(void);
-int mq_device_init(int device);            /* selects the HIP device used by this thread         */
+/* Selects (and makes current) the HIP device this thread creates objects on: MQ_OK, or
+ * MQ_ERR_NO_DEVICE (no such device / not a gfx950; the thread's previous selection stays). */
+int mq_device_init(int device);
+/* The device this thread creates objects on (its selection, else its current HIP device), or -1
+ * when that is not a usable gfx950. */
+int mq_device_current(void);
+/* The device a key table lives on (-1 for NULL). */
+int mq_keytable_device(const mq_keytable* kt);
+/* Mixed / multi-key batches run some tile kernels on side streams forked from and joined back
+ * to the caller's stream (one set per device and caller stream, at most 64 sets, least recently
+ * used dropped). Call before destroying a stream that such batches used, to free its set now. */
+void mq_stream_release(void* stream);
 const char* mq_status_str(int status);
 
 /* ---- CryptoProvider::aead / Aead (per packet, host buffers; runs the HIP kernels) ----------- */
@@ -316,9 +334,11 @@ int mq_batch_protect(const mq_keytable* kt, const mq_conn_send* conns, uint32_t 
  * *n_pkts is the number of packets the datagrams split into, which can EXCEED max_pkts: only the
  * first max_pkts (in arrival order) are processed and recorded; the rest are neither opened nor
  * reflected in conns — resubmit their datagrams (or size max_pkts from *n_pkts).
- * A packet that opened under keys other than the ones the sequential reference would have chosen
+ * A packet that opened under inputs other than the ones the sequential reference would have chosen
  * (possible only when an earlier packet of its connection failed where the batch speculated it
- * would open) reports MQ_ERR_CRYPTO, as the reference would; its bytes then hold the plaintext. */
+ * would open, e.g. a PN decoded against a largest PN the reference never reached) reports
+ * MQ_ERR_CRYPTO, as the reference would, and is sealed again under the inputs that opened it, so
+ * its bytes are exactly as received — like every packet that fails. */
 size_t mq_batch_recv_workspace_size(uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_conns);
 int mq_batch_recv(const mq_keytable* kt, mq_conn_recv* conns, uint32_t n_conns, uint8_t* arena,
                   uint64_t arena_len, const mq_dgram* dgrams, uint32_t n_dgrams, mq_recv_pkt* pkts,

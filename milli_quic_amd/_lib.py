@@ -9,7 +9,9 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmq_aead.so")
+# MQ_ASAN=1 (tools/asan_cpu_tests.sh, CPU only): the build whose host code carries AddressSanitizer +
+# UBSan (`make -C milli_quic_amd/csrc asan`); the kernels are the same
+LIB_PATH = os.path.join(_HERE, "asan" if os.environ.get("MQ_ASAN") == "1" else "", "libmq_aead.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "mq_aead.h")
 
 MQ_OK = 0
@@ -78,6 +80,9 @@ _u64 = ctypes.c_uint64
 SIGNATURES = {
     "mq_version": (ctypes.c_char_p, []),
     "mq_device_init": (ctypes.c_int, [ctypes.c_int]),
+    "mq_device_current": (ctypes.c_int, []),
+    "mq_keytable_device": (ctypes.c_int, [_vp]),
+    "mq_stream_release": (None, [_vp]),
     "mq_status_str": (ctypes.c_char_p, [ctypes.c_int]),
     "mq_aead_new": (ctypes.c_int, [_u32, _vp, _sz, ctypes.POINTER(_vp)]),
     "mq_aead_free": (None, [_vp]),

@@ -686,70 +686,40 @@ __global__ __launch_bounds__(256) void mq_aes_seal_hp_kernel(
 }
 
 // Persistent grid: one workgroup per CU (152 KiB of LDS each), capped by the tile count.
-static uint32_t aes_grid(uint32_t tiles, uint32_t waves) {
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0, v = 0;
-    (void)hipGetDevice(&dev);
-    cus = hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0 ? v : 256;
-  }
-  static int per_cu = -1;
-  if (per_cu < 0) {  // diagnostic override: workgroups per CU of the grid (0 = one tile per wave)
+static uint32_t aes_grid(uint32_t tiles, uint32_t waves, int cus) {
+  static const int per_cu = [] {  // diagnostic override: workgroups per CU of the grid (0 = one tile per wave)
     const char* e = getenv("MQ_AES_WGS_PER_CU");
-    per_cu = e ? max(atoi(e), 0) : 1;
-  }
+    return e ? max(atoi(e), 0) : 1;
+  }();
+  if (cus <= 0) cus = 256;
   const uint32_t wgs = (tiles + waves - 1) / waves;
   if (per_cu == 0) return wgs;
   return wgs < (uint32_t)(cus * per_cu) ? wgs : (uint32_t)(cus * per_cu);
 }
 
-// The hot segment's kernel on a side stream of the calling thread, forked from and joined back
-// to the caller's stream: each CU then moves from one tile kernel to the other as its own
-// workgroup ends, not after the other kernel's last one.
-#ifndef MQ_AES_HOT_FORK
-#define MQ_AES_HOT_FORK 1
-#endif
-struct SideStream {
-  hipStream_t st = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-  bool ok = false;
-};
-static SideStream* side_stream() {
-  static thread_local SideStream ss;
-  static thread_local bool tried = false;
-  if (!tried) {
-    tried = true;
-    ss.ok = hipStreamCreateWithFlags(&ss.st, hipStreamNonBlocking) == hipSuccess &&
-            hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) == hipSuccess &&
-            hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) == hipSuccess;
-  }
-  return ss.ok ? &ss : nullptr;
-}
-
+// hs: the stream of the hot segment's kernel — a side stream forked from s by the caller
+// (mq_host.cpp, one per device and caller stream), so each CU moves from one tile kernel to the
+// other as its own workgroup ends, not after the other kernel's last one; s when not forked.
+// cus: the device's compute units (the persistent grid).
 hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena, uint64_t arena_len,
                          const mq_pkt_desc* desc, uint32_t n, const uint32_t* index, const uint32_t* n_dev,
                          const uint32_t* hot, uint8_t* status, uint64_t* pn_out, uint2* hpm, bool own_hp,
-                         hipStream_t s) {
+                         hipStream_t s, hipStream_t hs, int cus) {
   const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
   if (tiles == 0) return hipSuccess;
-  const uint32_t waves = aes_waves(n_rows == 1), blocks = aes_grid(tiles, waves);
+  const uint32_t waves = aes_waves(n_rows == 1), blocks = aes_grid(tiles, waves, cus);
   // a partition list over several rows: the hot key's segment on a single-key kernel first
   hot = (hot && index && n_rows > 1) ? hot : nullptr;
-  const uint32_t hot_blocks = hot ? aes_grid(tiles, aes_waves(true)) : 0u;
+  const uint32_t hot_blocks = hot ? aes_grid(tiles, aes_waves(true), cus) : 0u;
   if (open && hpm && own_hp) {  // !own_hp: mq_launch_mixed_hp covers both suites' lists
     hipLaunchKernelGGL(mq_aes_open_hp_kernel<true>, dim3((n + 255) / 256), dim3(256), 0, s, kt, n_rows, arena,
                        arena_len, desc, n, index, n_dev, hpm);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  SideStream* ss = (hot && MQ_AES_HOT_FORK) ? side_stream() : nullptr;
-  hipStream_t hs = s;
-  if (ss) {
-    hipError_t e = hipEventRecord(ss->fork, s);
-    if (e == hipSuccess) e = hipStreamWaitEvent(ss->st, ss->fork, 0);
-    if (e != hipSuccess) return e;
-    hs = ss->st;
-  }
+  if (!hot) hs = s;
+  // the launch's own HP passes run on s: a forked hot kernel would race them
+  if (own_hp && hs != s) return hipErrorInvalidValue;
   if (open) {
     if (hot)
       hipLaunchKernelGGL(mq_aes_open1_kernel, dim3(hot_blocks), dim3(64 * aes_waves(true)), 0, hs, kt, n_rows,
@@ -763,12 +733,7 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
     hipLaunchKernelGGL(n_rows == 1 ? mq_aes_seal1_kernel : mq_aes_seal_kernel, dim3(blocks), dim3(64 * waves),
                        0, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, hot, status);
   }
-  hipError_t e = hipGetLastError();
-  if (ss) {  // join even after a failed launch, so the side stream never runs ahead of s
-    const hipError_t ej = hipEventRecord(ss->join, hs);
-    const hipError_t ew = ej == hipSuccess ? hipStreamWaitEvent(s, ss->join, 0) : ej;
-    if (e == hipSuccess) e = ew;
-  }
+  const hipError_t e = hipGetLastError();
   if (e != hipSuccess || open || !own_hp) return e;
   hipLaunchKernelGGL(mq_aes_seal_hp_kernel, dim3((n + 255) / 256), dim3(256), 0, s, kt, arena, arena_len, desc, n,
                      index, n_dev, status);

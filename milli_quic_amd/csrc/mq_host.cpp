@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "mq_device.h"
+#include "mq_runtime.h"
 
 using mq::KeyRow;
 
@@ -28,7 +29,8 @@ hipError_t mq_launch_chacha_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t
 hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena,
                          uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
                          const uint32_t* index, const uint32_t* n_dev, const uint32_t* hot,
-                         uint8_t* status, uint64_t* pn_out, uint2* hpm, bool own_hp, hipStream_t s);
+                         uint8_t* status, uint64_t* pn_out, uint2* hpm, bool own_hp, hipStream_t s,
+                         hipStream_t hot_stream, int cus);
 hipError_t mq_launch_mixed_hp(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena, uint64_t arena_len,
                               const mq_pkt_desc* desc, const uint32_t* list, uint32_t cap, const uint32_t* counts,
                               const uint8_t* status, uint2* hpm, hipStream_t s);
@@ -69,29 +71,61 @@ void mq_stamps_set_aes(uint64_t* p);
 namespace {
 
 // ---------------------------------------------------------------------------------------------
-// device selection
-std::mutex g_dev_mu;
-int g_dev_state = 0;  // 0 unknown, 1 ok, -1 unusable
-int g_dev = 0;
+// device selection (per thread) and side streams (per device and caller stream): mq_runtime.h
+struct HipBackend {
+  typedef hipStream_t Stream;
+  typedef hipEvent_t Event;
+  static int count() {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+  }
+  static bool usable(int dev) {
+    hipDeviceProp_t prop;
+    return hipGetDeviceProperties(&prop, dev) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+  }
+  static int cus(int dev) {
+    int v = 0;
+    return hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess ? v : 0;
+  }
+  static int get() {
+    int d = -1;
+    return hipGetDevice(&d) == hipSuccess ? d : -1;
+  }
+  static bool set(int dev) { return hipSetDevice(dev) == hipSuccess; }
+  static bool stream_create(Stream* s) { return hipStreamCreateWithFlags(s, hipStreamNonBlocking) == hipSuccess; }
+  static void stream_destroy(Stream s) {
+    (void)hipStreamSynchronize(s);
+    (void)hipStreamDestroy(s);
+  }
+  static bool event_create(Event* e) { return hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess; }
+  static void event_destroy(Event e) { (void)hipEventDestroy(e); }
+  static bool record(Event e, Stream s) { return hipEventRecord(e, s) == hipSuccess; }
+  static bool wait(Stream s, Event e) { return hipStreamWaitEvent(s, e, 0) == hipSuccess; }
+};
+typedef mq::DeviceRegistry<HipBackend> Devices;
+typedef Devices::Guard DeviceGuard;
+// Constructed on first use and never destroyed: side streams and device state may be touched from
+// other libraries' static destructors, after which the HIP runtime may already be gone.
+Devices& devices() {
+  static Devices* d = new Devices();
+  return *d;
+}
+mq::SideStreams<HipBackend>& side_streams() {
+  static auto* s = new mq::SideStreams<HipBackend>(64);
+  return *s;
+}
 
-int ensure_device() {
-  std::lock_guard<std::mutex> lk(g_dev_mu);
-  if (g_dev_state == 1) {
-    (void)hipSetDevice(g_dev);
-    return MQ_OK;
-  }
-  if (g_dev_state == -1) return MQ_ERR_NO_DEVICE;
-  int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess || n <= g_dev) { g_dev_state = -1; return MQ_ERR_NO_DEVICE; }
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, g_dev) != hipSuccess ||
-      std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
-    g_dev_state = -1;
-    return MQ_ERR_NO_DEVICE;
-  }
-  if (hipSetDevice(g_dev) != hipSuccess) { g_dev_state = -1; return MQ_ERR_NO_DEVICE; }
-  g_dev_state = 1;
-  return MQ_OK;
+// The device a new object (key table, AEAD / HP context) is created on: the thread's selection,
+// else its current HIP device; -1 (MQ_ERR_NO_DEVICE) when that is not a gfx950.
+int creation_device() { return devices().current(); }
+
+// Forked tile kernels: MQ_FORK=0 runs every kernel of a batch on the caller's stream (diagnostic)
+bool fork_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("MQ_FORK");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -300,6 +334,7 @@ void hmac_sha256(const uint8_t* key, size_t key_len, const uint8_t* m1, size_t l
 // one stream sync, no copies. MQ_PER_PACKET_COPY=1 selects the copy path instead (a device mirror,
 // H2D before and D2H after the kernel), kept for comparison (tools/bench_latency.py).
 struct Scratch {
+  int device = -1;          // the owning context's device (every call runs there)
   hipStream_t stream = nullptr;
   uint8_t* dev = nullptr;   // what the kernel addresses: device mirror, or the mapped host buffer
   uint8_t* host = nullptr;  // pinned host buffer
@@ -350,6 +385,8 @@ struct Scratch {
     return hipStreamSynchronize(stream) == hipSuccess ? MQ_OK : MQ_ERR_HIP;
   }
   ~Scratch() {
+    if (!stream && !host) return;
+    DeviceGuard g(device);
     release();
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -359,12 +396,13 @@ struct Scratch {
 // body = `body_len` bytes of buf (plaintext for seal, ciphertext || tag for open), staged straight
 // into the pinned scratch (no heap allocation per call); `pkt_len` = aad_len + body_len (+ 16 on
 // seal: the tag area). Descriptor in NO_HP mode with pn = 0 (the caller's nonce sits in row.iv).
-// On MQ_OK the transformed body (`out_len` bytes) is copied back into buf.
+// On MQ_OK the transformed body (`out_len` bytes) is copied back into buf. Runs on the scratch's
+// (its context's) device.
 int run_one(Scratch& sc, const KeyRow& row, const uint8_t* aad, uint32_t aad_len, uint8_t* buf,
             uint32_t body_len, uint32_t pkt_len, uint32_t out_len, bool open) {
-  int rc = ensure_device();
-  if (rc) return rc;
-  rc = sc.ensure(pkt_len);
+  DeviceGuard g(sc.device);
+  if (!g.ok()) return MQ_ERR_NO_DEVICE;
+  int rc = sc.ensure(pkt_len);
   if (rc) return rc;
   std::memcpy(sc.host, &row, sizeof row);
   mq_pkt_desc d;
@@ -393,7 +431,7 @@ int run_one(Scratch& sc, const KeyRow& row, const uint8_t* aad, uint32_t aad_len
   hipError_t e = row.suite == MQ_SUITE_CHACHA20
                      ? mq_launch_chacha(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, st, pn, nullptr, false, sc.stream)
                      : mq_launch_aes(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, nullptr, st, pn, nullptr, false,
-                                     sc.stream);
+                                     sc.stream, sc.stream, devices().cus(sc.device));
   if (e != hipSuccess) return MQ_ERR_HIP;
   // status and the transformed packet in one read-back (the status sits before the packet)
   if ((rc = sc.finish(Scratch::kStatus, Scratch::kHdr - Scratch::kStatus + pkt_len)) != MQ_OK) return rc;
@@ -419,20 +457,20 @@ struct mq_hp_ctx {
 struct mq_keytable {
   KeyRow* dev = nullptr;
   uint32_t rows = 0;
+  int device = -1;  // where the rows live; every batch call on this table runs there
 };
 
 extern "C" {
 
-const char* mq_version(void) { return "mq_aead 0.1.0 (gfx950)"; }
+const char* mq_version(void) { return "mq_aead 0.2.0 (gfx950)"; }
 
-int mq_device_init(int device) {
-  {
-    std::lock_guard<std::mutex> lk(g_dev_mu);
-    g_dev = device;
-    g_dev_state = 0;
-  }
-  return ensure_device();
-}
+int mq_device_init(int device) { return devices().select(device) ? MQ_OK : MQ_ERR_NO_DEVICE; }
+
+int mq_device_current(void) { return devices().current(); }
+
+int mq_keytable_device(const mq_keytable* kt) { return kt ? kt->device : -1; }
+
+void mq_stream_release(void* stream) { side_streams().release((hipStream_t)stream); }
 
 const char* mq_status_str(int status) {
   switch (status) {
@@ -455,13 +493,14 @@ int mq_aead_new(uint32_t suite, const uint8_t* key, size_t key_len, mq_aead_ctx*
   if (!out) return MQ_ERR_INVALID_ARG;
   *out = nullptr;
   if (!suite_key_len(suite) || !key || key_len != suite_key_len(suite)) return MQ_ERR_CRYPTO;
-  const int rc = ensure_device();
-  if (rc) return rc;
+  const int dev = creation_device();
+  if (dev < 0) return MQ_ERR_NO_DEVICE;
   mq_key_material km;
   std::memset(&km, 0, sizeof km);
   km.suite = suite;
   std::memcpy(km.key, key, key_len);
   mq_aead_ctx* c = new mq_aead_ctx();
+  c->sc.device = dev;
   c->suite = suite;
   build_row(km, c->row);
   *out = c;
@@ -514,14 +553,15 @@ int mq_hp_new(uint32_t suite, const uint8_t* key, size_t key_len, mq_hp_ctx** ou
   *out = nullptr;
   const size_t want = suite == MQ_SUITE_AES128GCM ? 16 : suite == MQ_SUITE_CHACHA20 ? 32 : 0;
   if (!want || !key || key_len != want) return MQ_ERR_CRYPTO;  // rustcrypto.rs:247-249,280-282
-  const int rc = ensure_device();
-  if (rc) return rc;
+  const int dev = creation_device();
+  if (dev < 0) return MQ_ERR_NO_DEVICE;
   mq_key_material km;
   std::memset(&km, 0, sizeof km);
   km.suite = suite;
   std::memcpy(km.hp, key, key_len);
   if (suite == MQ_SUITE_AES128GCM) std::memset(km.key, 0, 16);
   mq_hp_ctx* c = new mq_hp_ctx();
+  c->sc.device = dev;
   c->suite = suite;
   build_row(km, c->row);
   *out = c;
@@ -532,11 +572,11 @@ void mq_hp_free(mq_hp_ctx* ctx) { delete ctx; }
 
 int mq_hp_mask(const mq_hp_ctx* ctx, const uint8_t* sample, size_t sample_len, uint8_t mask[5]) {
   if (!ctx || !mask || !sample || sample_len < 16) return MQ_ERR_INVALID_ARG;
-  int rc = ensure_device();
-  if (rc) return rc;
   std::lock_guard<std::mutex> lk(ctx->sc.mu);
   Scratch& sc = ctx->sc;
-  rc = sc.ensure(64);
+  DeviceGuard g(sc.device);
+  if (!g.ok()) return MQ_ERR_NO_DEVICE;
+  int rc = sc.ensure(64);
   if (rc) return rc;
   // layout: row | key id (4) @kDesc | sample 16 @kSample | mask 5 @kStatus
   std::memcpy(sc.host, &ctx->row, sizeof(KeyRow));
@@ -630,15 +670,18 @@ int mq_derive_next_secret(const uint8_t* secret, size_t secret_len, uint8_t next
 int mq_keytable_create(const mq_key_material* rows, uint32_t n_rows, mq_keytable** out) {
   if (!out || (!rows && n_rows)) return MQ_ERR_INVALID_ARG;
   *out = nullptr;
-  int rc = ensure_device();
-  if (rc) return rc;
+  const int dev = creation_device();
+  if (dev < 0) return MQ_ERR_NO_DEVICE;
+  DeviceGuard g(dev);
+  if (!g.ok()) return MQ_ERR_NO_DEVICE;
   mq_keytable* kt = new mq_keytable();
   kt->rows = n_rows;
+  kt->device = dev;
   if (hipMalloc(&kt->dev, sizeof(KeyRow) * (n_rows ? n_rows : 1)) != hipSuccess) {
     delete kt;
     return MQ_ERR_HIP;
   }
-  rc = mq_keytable_update(kt, 0, rows, n_rows);
+  int rc = mq_keytable_update(kt, 0, rows, n_rows);
   if (rc) {
     mq_keytable_free(kt);
     return rc;
@@ -653,6 +696,8 @@ int mq_keytable_update(mq_keytable* kt, uint32_t first_row, const mq_key_materia
   std::vector<KeyRow> host(n_rows);
   for (uint32_t i = 0; i < n_rows; ++i)
     if (!build_row(rows[i], host[i])) std::memset(&host[i], 0, sizeof(KeyRow));  // suite 0: rejected per packet
+  DeviceGuard g(kt->device);
+  if (!g.ok()) return MQ_ERR_NO_DEVICE;
   if (hipMemcpy(kt->dev + first_row, host.data(), sizeof(KeyRow) * n_rows, hipMemcpyHostToDevice) != hipSuccess)
     return MQ_ERR_HIP;
   return MQ_OK;
@@ -662,7 +707,10 @@ uint32_t mq_keytable_rows(const mq_keytable* kt) { return kt ? kt->rows : 0; }
 
 void mq_keytable_free(mq_keytable* kt) {
   if (!kt) return;
-  if (kt->dev) (void)hipFree(kt->dev);
+  if (kt->dev) {
+    DeviceGuard g(kt->device);
+    (void)hipFree(kt->dev);
+  }
   delete kt;
 }
 
@@ -675,9 +723,10 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
                  uint32_t suite_hint, void* workspace, void* stream) {
   if (!kt || (n && (!arena || !desc || !status))) return MQ_ERR_INVALID_ARG;
   if (((uintptr_t)arena & 15) != 0) return MQ_ERR_INVALID_ARG;  // 16-B staging chunks
-  int rc = ensure_device();
-  if (rc) return rc;
+  DeviceGuard g(kt->device);  // the table's device; `stream` must belong to it
+  if (!g.ok()) return MQ_ERR_NO_DEVICE;
   if (n == 0) return MQ_OK;
+  const int cus = devices().cus(kt->device);
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
   uint8_t* ws = (uint8_t*)workspace;
@@ -688,7 +737,7 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
                          s);
   } else if (suite_hint == MQ_SUITE_AES128GCM && (kt->rows == 1 || !ws || n > (1u << 30))) {
     e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, n, nullptr, nullptr, nullptr, status, pn_out,
-                      hpm, true, s);
+                      hpm, true, s, s, cus);
   } else if (suite_hint == MQ_SUITE_MIXED || suite_hint == MQ_SUITE_AES128GCM) {
     // the two index lists (2 x mq_partition_list_cap(n) entries, holes included) are addressed
     // with 32-bit positions: up to 2^30 packets per mixed batch. An AES batch over several key
@@ -706,23 +755,29 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
     // list mode: the grids cover the list capacity; the kernels read the real lengths from counts
     const uint32_t cap = mq_partition_list_cap(n);
     e = mq_launch_partition(kt->dev, kt->rows, desc, n, list, hist, counts, s);
-    // mixed: one header-protection pass covers both lists (before the tiles for open, after
-    // both suites' tiles for seal); an AES-hinted batch keeps the per-launch passes
-    const bool own = aes_only;
-    // counts + 2: the hot key's row and segment length (list 0's front), which the AES launch runs
-    // on its single-key kernel
-    if (e == hipSuccess && !own && open && hpm)
+    // one header-protection pass covers both lists, before the tiles for open and after every
+    // tile kernel for seal (the AES tiles mask their long packets themselves)
+    if (e == hipSuccess && open && hpm)
       e = mq_launch_mixed_hp(true, kt->dev, kt->rows, arena, arena_len, desc, list, cap, counts, status, hpm, s);
-    if (e == hipSuccess)
-      e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list, counts, counts + 2, status,
-                        pn_out, hpm, own, s);
+    if (e != hipSuccess) return MQ_ERR_HIP;
+    // The tile kernels of the lists run concurrently: the hot AES key's segment (counts + 2: its
+    // row and segment length, list 0's front; single-key kernel) on side stream 0, the other AES
+    // keys' tiles on s, list 1 (ChaCha20, or the AES hint's leftovers) on side stream 1 — each CU
+    // moves on to the next kernel's workgroups as its own finish, instead of idling at every
+    // kernel's tail. Side streams are per (device, caller stream): mq_runtime.h.
+    auto fork = fork_enabled() ? side_streams().fork(kt->device, s, 2) : mq::SideStreams<HipBackend>::Fork();
+    hipStream_t s_hot = fork ? fork.side(0) : s, s_list1 = fork ? fork.side(1) : s;
+    e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list, counts, counts + 2, status, pn_out,
+                      hpm, false, s, s_hot, cus);
     if (e == hipSuccess && aes_only)
-      e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list + cap, counts + 1, nullptr, status, pn_out,
-                        hpm, own, s);
+      e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list + cap, counts + 1, nullptr, status,
+                        pn_out, hpm, false, s_list1, s_list1, cus);
     else if (e == hipSuccess)
       e = mq_launch_chacha(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list + cap, counts + 1, status,
-                           pn_out, hpm, own, s);
-    if (e == hipSuccess && !own && !open)
+                           pn_out, hpm, false, s_list1);
+    // join even after a failed launch, so no side stream runs ahead of s
+    if (!fork.join() && e == hipSuccess) e = hipErrorUnknown;
+    if (e == hipSuccess && !open)
       e = mq_launch_mixed_hp(false, kt->dev, kt->rows, arena, arena_len, desc, list, cap, counts, status, nullptr, s);
   } else {
     return MQ_ERR_INVALID_ARG;
@@ -795,8 +850,8 @@ int mq_batch_derive_initial(mq_keytable* kt, uint32_t first_row, const uint8_t* 
                             uint32_t n, mq_key_material* km_out, uint8_t* status, void* stream) {
   if (!kt || (n && (!dcids || !dcid_lens || !status))) return MQ_ERR_INVALID_ARG;
   if ((uint64_t)first_row + 2ull * n > kt->rows) return MQ_ERR_INVALID_ARG;
-  const int rc = ensure_device();
-  if (rc) return rc;
+  DeviceGuard g(kt->device);
+  if (!g.ok()) return MQ_ERR_NO_DEVICE;
   return mq_launch_derive_initial(derive_consts(), dcids, dcid_lens, n, kt->dev + first_row, km_out, status,
                                   (hipStream_t)stream) == hipSuccess
              ? MQ_OK
@@ -815,8 +870,8 @@ int mq_batch_protect(const mq_keytable* kt, const mq_conn_send* conns, uint32_t 
   if (!kt || (n && (!conns || !frames || !out || !req || !status || !pkt_len || !workspace)))
     return MQ_ERR_INVALID_ARG;
   if (((uintptr_t)out & 15) != 0) return MQ_ERR_INVALID_ARG;
-  const int rc = ensure_device();
-  if (rc) return rc;
+  DeviceGuard g(kt->device);
+  if (!g.ok()) return MQ_ERR_NO_DEVICE;
   if (n == 0) return MQ_OK;
   hipStream_t s = (hipStream_t)stream;
   uint8_t* ws = (uint8_t*)workspace;
@@ -843,8 +898,8 @@ int mq_batch_recv(const mq_keytable* kt, mq_conn_recv* conns, uint32_t n_conns, 
       (max_pkts && !pkts))
     return MQ_ERR_INVALID_ARG;
   if (((uintptr_t)arena & 15) != 0) return MQ_ERR_INVALID_ARG;
-  const int rc = ensure_device();
-  if (rc) return rc;
+  DeviceGuard g(kt->device);
+  if (!g.ok()) return MQ_ERR_NO_DEVICE;
   hipStream_t s = (hipStream_t)stream;
   const size_t open_ws = mq_batch_workspace_size(max_pkts);
   mq::MQRecvPass p;
@@ -867,7 +922,11 @@ int mq_batch_recv(const mq_keytable* kt, mq_conn_recv* conns, uint32_t n_conns, 
                      round + 1 == kRounds, s) != hipSuccess)
       return MQ_ERR_HIP;
   }
-  return MQ_OK;
+  // Re-seal pass: a packet that opened under the speculation's inputs but fails under the
+  // reference's (MQ_ERR_CRYPTO) holds plaintext; the final walk left its opening key row and PN in
+  // d1 (every other entry has no key row and is skipped), and sealing it again under them restores
+  // its bytes as received. Statuses land in the st1 scratch.
+  return batch(false, kt, arena, arena_len, p.d1, max_pkts, p.st1, nullptr, MQ_SUITE_MIXED, p.open_ws, stream);
 }
 
 // ---- TLS 1.3 records (tcp_tls/record.rs:88-143, connection.rs:546-600) -----------------------
@@ -919,8 +978,8 @@ int mq_batch_open_records(const mq_keytable* kt, uint8_t* arena, uint64_t arena_
 int mq_batch_hp_mask(const mq_keytable* kt, const uint32_t* key_ids, const uint8_t* samples,
                      uint8_t* masks, uint32_t n, void* stream) {
   if (!kt || (n && (!key_ids || !samples || !masks))) return MQ_ERR_INVALID_ARG;
-  int rc = ensure_device();
-  if (rc) return rc;
+  DeviceGuard g(kt->device);
+  if (!g.ok()) return MQ_ERR_NO_DEVICE;
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = mq_launch_chacha_hp(kt->dev, kt->rows, key_ids, samples, masks, n, s);
   if (e == hipSuccess) e = mq_launch_aes_hp(kt->dev, kt->rows, key_ids, samples, masks, n, s);
@@ -931,9 +990,10 @@ int mq_batch_time_seal_open(const mq_keytable* kt, uint8_t* arena, uint64_t aren
                             const mq_pkt_desc* desc, uint32_t n, uint8_t* status, uint64_t* pn_out,
                             uint32_t suite_hint, void* workspace, void* stream, int iters,
                             float* seal_ms, float* open_ms) {
-  if (iters <= 0 || !seal_ms || !open_ms) return MQ_ERR_INVALID_ARG;
-  int rc = ensure_device();
-  if (rc) return rc;
+  if (!kt || iters <= 0 || !seal_ms || !open_ms) return MQ_ERR_INVALID_ARG;
+  DeviceGuard g(kt->device);
+  if (!g.ok()) return MQ_ERR_NO_DEVICE;
+  int rc = MQ_OK;
   hipStream_t s = (hipStream_t)stream;
   std::vector<hipEvent_t> ev(2 * iters + 1, nullptr);
   auto destroy = [&] {

@@ -362,8 +362,18 @@ extern "C" __global__ __launch_bounds__(64) void mq_recv_walk_kernel(
         } else if (t.pn == p.pn && opened == p.retry) {
           st = MQ_OK;
           gen = 0;
-        } else {  // the reference's keys fail on it: Error::Crypto (bytes hold the plaintext)
+        } else {
+          // the reference's keys fail on it: Error::Crypto. It opened under the speculation's
+          // inputs, so its bytes hold plaintext; the final walk hands it to the re-seal pass
+          // (mq_host.cpp) with the key row and PN that opened it, which brings back ciphertext,
+          // tag and masked header exactly as received — the reference never touches the
+          // datagram of a failed packet (it opens a 2048-B copy, recv.rs:356-361)
           st = MQ_ERR_CRYPTO;
+          if (final_walk) {
+            a.key_id = opened;
+            a.pn = t.pn;
+            a.pn_len = t.pn_len;
+          }
         }
       } else if (same) {  // failed with exactly the reference's inputs
         st = MQ_ERR_CRYPTO;

@@ -11,15 +11,18 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "build", "liborc.so")
-OSSL_LIB = os.path.join(HERE, "build", "libossl.so")
+# MQ_ASAN=1 (tools/asan_cpu_tests.sh): the AddressSanitizer + UBSan builds of `make asan`
+_BUILD = os.path.join(HERE, "build", "asan") if os.environ.get("MQ_ASAN") == "1" else os.path.join(HERE, "build")
+LIB = os.path.join(_BUILD, "liborc.so")
+OSSL_LIB = os.path.join(_BUILD, "libossl.so")
 
 _lib = None
 _ossl = None
 
 
 def build():
-    subprocess.run(["make", "-C", HERE, "-s"], check=True)
+    subprocess.run(["make", "-C", HERE, "-s"] + (["asan"] if _BUILD != os.path.join(HERE, "build") else []),
+                   check=True)
 
 
 def load():

@@ -38,15 +38,21 @@ def main():
     ls = torch.from_numpy(local.astype(np.int64))
     csum = shard.tag_checksum_torch(arena, offs, lens)
     s_csum = shard.tag_checksum_torch(arena, offs[ls], lens[ls])
-    fails_all, csum_all, s_csum_all = shard.reduce_sums([fails, csum, s_csum], dd)
+    if os.environ.get("MQ_TEST_CORRUPT_RANK") == str(rank):  # a wrong result on one rank
+        s_csum += 1
+    pn_ok = bool((pn == w.pns).all())
+    parity = bench.parity_check(args.config, w, g, keys, fails, csum, s_csum, pn_ok, dd)
     tot = shard.reduce_totals(0.25 * (rank + 1), w.wire_bytes, 0, dd)
     if rank == 0:
         o_fail, o_csum = bench.oracle_sample_checksum(args.config, w, g, keys)
         with open(os.environ["MQ_TEST_OUT"], "w") as f:
-            json.dump({"world": world, "fails": fails_all, "csum": csum_all, "sample_csum": s_csum_all,
-                       "oracle_sample_csum": o_csum, "oracle_fail": o_fail, "n_sample": int(len(g)),
+            json.dump({"world": world, "fails": parity["failures"], "csum": parity["tag_checksum"],
+                       "sample_csum": parity["sample_tag_checksum"], "oracle_sample_csum": o_csum,
+                       "oracle_fail": o_fail, "n_sample": int(len(g)), "parity": parity,
                        "elapsed": tot.elapsed, "wire": tot.wire_bytes, "key_rows": len(w.keys),
                        "first_pn": int(w.pns[0])}, f)
+    with open(os.environ["MQ_TEST_OUT"] + f".match{rank}", "w") as f:
+        f.write("1" if parity["match"] else "0")
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

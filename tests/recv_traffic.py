@@ -116,3 +116,42 @@ def assemble(orc, keys, conns, scripts, seed=1, extras=True):
     for o, b in blobs:
         arena[o:o + len(b)] = np.frombuffer(b, dtype=np.uint8)
     return arena, dgrams
+
+
+def build_pn_jump(orc, suites=(_lib.MQ_SUITE_CHACHA20, _lib.MQ_SUITE_AES128GCM), seed=7):
+    """ADVICE r02 (mq_recv.hip walk): per connection, a packet X with a large PN jump arrives
+    corrupted, and the sender, believing X acknowledged, encodes the next two packets' PNs in one
+    byte against it. The sequential reference never advances its largest PN past X, so it decodes
+    those PNs wrongly and fails them (Error::Crypto, datagram untouched); the batch's speculation
+    (X opens) decodes them right and opens them. A later packet with a long PN opens for both.
+    Returns keys, conns, arena, dgrams (one packet per datagram)."""
+    rng = np.random.default_rng(seed)
+    keys = [_lib.KeyMaterial()]
+    conns = np.zeros(len(suites), dtype=recv.CONN_DTYPE)
+    order = []
+    for c, suite in enumerate(suites):
+        dcid = rng.bytes(8)
+        row = len(keys)
+        keys.append(key_material(suite, rng.bytes(32)))
+        conns[c]["app_row"] = [0, row, 0]
+        conns[c]["dcid_len"] = 8
+        conns[c]["flags"] = recv.HAS_APP
+        # (pn, the sender's largest acknowledged pn, tampered)
+        for pn, la, tamper in ((1, 0, False), (1000, 1, False), (41000, 1000, True), (41005, 41000, False),
+                               (41006, 41005, False), (41100, 1000, False), (41101, 41100, False)):
+            p = protect_one(orc, keys, dcid, 2, row, 0, pn, la, rng.bytes(int(rng.integers(20, 200))), False)
+            if tamper:
+                b = bytearray(p)
+                b[-20] ^= 0x10
+                p = bytes(b)
+            order.append((c, p))
+    dgrams = np.zeros(len(order), dtype=recv.DGRAM_DTYPE)
+    pos, blobs = 0, []
+    for i, (c, blob) in enumerate(order):
+        dgrams[i]["offset"], dgrams[i]["len"], dgrams[i]["conn"] = pos, len(blob), c
+        blobs.append((pos, blob))
+        pos += len(blob) + 3
+    arena = np.zeros(pos + 64, dtype=np.uint8)
+    for o, b in blobs:
+        arena[o:o + len(b)] = np.frombuffer(b, dtype=np.uint8)
+    return keys, conns, arena, dgrams

@@ -37,6 +37,32 @@ def test_launch_two_ranks_sharded_global_batch(tmp_path, orc, keys):
     assert (st == 0).all()
     assert r["csum"] == shard.tag_checksum(w.arena, w.seal_desc)
     assert r["wire"] == 2 * n * 1200 and r["elapsed"] == 0.5  # summed bytes, max of elapsed
+    assert r["parity"]["match"] and all((tmp_path / f"r0.json.match{k}").read_text() == "1" for k in (0, 1))
+
+
+@pytest.mark.parametrize("corrupt", [None, 1])
+def test_launch_two_ranks_config_e(tmp_path, orc, corrupt):
+    # config E ranks hold independent seeded batches; each rank checks its own sample
+    # against the oracle, so a correct 2-rank run matches and a wrong result on rank 1 does not
+    out = tmp_path / "r0.json"
+    os.environ["MQ_TEST_OUT"] = str(out)
+    if corrupt is None:
+        os.environ.pop("MQ_TEST_CORRUPT_RANK", None)
+    else:
+        os.environ["MQ_TEST_CORRUPT_RANK"] = str(corrupt)
+    try:
+        rc = bench.launch_ranks(2, ["--gpus", "2", "--packets", "700", "--config", "e"],
+                                script=os.path.join(HERE, "dist_bench_worker.py"))
+    finally:
+        os.environ.pop("MQ_TEST_CORRUPT_RANK", None)
+    assert rc == 0
+    r = json.loads(out.read_text())
+    assert r["world"] == 2 and r["fails"] == 0
+    p = r["parity"]
+    assert p["ranks_mismatching_oracle"] == (0 if corrupt is None else 1)
+    assert p["match"] == (corrupt is None)
+    # every rank reaches the same verdict
+    assert {(tmp_path / f"r0.json.match{k}").read_text() for k in (0, 1)} == {"1" if corrupt is None else "0"}
 
 
 def test_sample_indices_and_shard_positions():

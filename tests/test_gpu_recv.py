@@ -9,7 +9,7 @@ torch = pytest.importorskip("torch")
 from milli_quic_amd import recv  # noqa: E402
 from milli_quic_amd.batch import KeyTable  # noqa: E402
 
-from recv_traffic import assemble, build_traffic  # noqa: E402
+from recv_traffic import assemble, build_pn_jump, build_traffic  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -63,3 +63,25 @@ def test_recv_max_pkts_truncates(orc):
     o_pk, o_n = orc.batch_recv(keys, conns.copy(), arena.copy(), dgrams, 1 << 12)
     g_pk, g_n, _, _ = gpu_recv(keys, conns, arena, dgrams, 7)  # only the first 7 records are kept
     assert g_n == o_n and len(g_pk) == 7
+
+
+def test_recv_speculation_opened_reference_fails(orc):
+    # packets that open only under the batch's speculation (a PN decoded against a
+    # corrupted packet's PN the reference never accepts) are MQ_ERR_CRYPTO, as in the reference,
+    # and are re-sealed under the inputs that opened them: every arena byte equals the oracle's,
+    # whose failed packets are never touched
+    keys, conns, arena, dgrams = build_pn_jump(orc)
+    oc, oa = conns.copy(), arena.copy()
+    o_pk, o_n = orc.batch_recv(keys, oc, oa, dgrams, 1 << 10)
+    st = o_pk["status"][:o_n]
+    assert list(st[:7]) == [0, 0, 1, 1, 1, 0, 0] and list(st[7:14]) == [0, 0, 1, 1, 1, 0, 0]
+    g_pk, g_n, gc, ga = gpu_recv(keys, conns, arena, dgrams, 1 << 10)
+    assert g_n == o_n
+    for f in recv.PKT_DTYPE.names:
+        assert (g_pk[f] == o_pk[f][:o_n]).all(), (f, g_pk[f], o_pk[f][:o_n])
+    assert gc.tobytes() == oc.tobytes()
+    assert ga.tobytes() == oa.tobytes()
+    # the failed packets' bytes are exactly as received
+    for k in np.nonzero(st != 0)[0]:
+        o, L = int(g_pk["offset"][k]), int(g_pk["len"][k])
+        assert ga[o:o + L].tobytes() == arena[o:o + L].tobytes()
