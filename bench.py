@@ -328,11 +328,12 @@ def end_to_end(torch, batch, kt, w, sd, od, dev, chunks=8, reps=3):
 
 
 # ---- roofline bookkeeping ---------------------------------------------------------------------
-# The seal composite of a single-suite batch: the tile kernel, then the header-protection pass
-# (ChaCha20: every packet's mask; AES: the packets with no free slot in their tile). The "1" tile
-# kernel variant (key material in SGPRs) runs when the key table has a single row (launchers in
-# mq_chacha.hip / mq_aes.hip). seal_ms (HIP events around mq_batch_seal) spans both.
-KERNELS = {"b": ("mq_chacha_seal_kernel", "mq_chacha_seal_hp_kernel"),
+# The seal composite of a single-suite batch: the tile kernel (ChaCha20: header protection
+# included, r03), then for AES the header-protection pass of the packets with no free slot in their
+# tile. The "1" tile kernel variant (key material in SGPRs) runs when the key table has a single
+# row (launchers in mq_chacha.hip / mq_aes.hip). seal_ms (HIP events around mq_batch_seal) spans
+# the composite.
+KERNELS = {"b": ("mq_chacha_seal_kernel",),
            "c": ("mq_aes_seal_kernel", "mq_aes_seal_hp_kernel"), "e": None}
 
 
@@ -340,8 +341,8 @@ def seal_kernels(cfg, n_rows):
     ks = KERNELS.get(cfg)
     if not ks:
         return None
-    tile, hp = ks
-    return (tile.replace("_seal_kernel", "_seal1_kernel") if n_rows == 1 else tile), hp
+    tile = ks[0].replace("_seal_kernel", "_seal1_kernel") if n_rows == 1 else ks[0]
+    return (tile,) + tuple(ks[1:])
 
 
 def load_traffic(cfg, kerns):

@@ -743,8 +743,8 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
 // Mixed batches: the open pre-pass (OPEN) or the seal HP post-pass of BOTH partition lists in one
 // launch (list 0 = list[0, counts[0]), list 1 = list[cap, cap + counts[1])), one packet per lane,
 // either suite per lane — the two passes' memory latencies overlap instead of adding up. Seal:
-// the packets whose HP had no slot in their tile (AES: fewer than 7 CTR blocks; ChaCha20: all),
-// as mq_aes_seal_hp_kernel / mq_chacha_seal_hp_kernel do per list.
+// the AES packets whose HP had no slot in their tile (fewer than 7 CTR blocks), as
+// mq_aes_seal_hp_kernel does per list; the ChaCha20 tiles mask their packets themselves.
 template <bool OPEN>
 __global__ __launch_bounds__(256) void mq_mixed_hp_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
@@ -775,8 +775,8 @@ __global__ __launch_bounds__(256) void mq_mixed_hp_kernel(
       row = kt + d.key_id;
       aes = row->suite == MQ_SUITE_AES128GCM;
       const uint32_t P = d.len - ((uint32_t)d.pn_offset + d.pn_len) - 16;
-      // AES: the packets whose HP had no slot in their tile; ChaCha20: every packet
-      act = !(d.flags & MQ_PKT_NO_HP) && (!aes || 1 + ((P + 15) >> 4) < (uint32_t)kLanesPerPkt);
+      // the AES packets whose HP had no slot in their tile (ChaCha20 tiles mask every packet)
+      act = aes && !(d.flags & MQ_PKT_NO_HP) && 1 + ((P + 15) >> 4) < (uint32_t)kLanesPerPkt;
     }
   }
   if (!__syncthreads_or(act)) return;

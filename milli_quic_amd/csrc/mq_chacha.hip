@@ -7,8 +7,8 @@
 //
 // Per tile (8 packets, one octet of lanes per packet; see mq_tile.h):
 //   seal: keystream block ctr on lane ctr % 8 (ctr 0 = Poly1305 one-time key) XORed into LDS
-//         (blocks >= 16 through the workgroup's keystream pool) -> interleaved Poly1305 over
-//         AAD||pad||CT||pad||lens -> tag; the header mask comes from mq_chacha_seal_hp_kernel
+//         (blocks >= 16 and the header-protection block through the workgroup's keystream pool)
+//         -> interleaved Poly1305 over AAD||pad||CT||pad||lens -> tag -> header mask applied
 //   open: HP mask -> unmask byte 0 / PN -> decode_pn -> nonce -> first keystream block (lane 0:
 //         one-time key) -> Poly1305 over the untouched ciphertext -> tag check -> only then the
 //         keystream XOR (held first block + the rest); failed packets are never stored.
@@ -175,8 +175,17 @@ __device__ __forceinline__ void load_key8(const uint32_t* src, uint32_t (&k)[8])
 constexpr int kCcWaves = MQ_CC_WAVES;
 constexpr uint32_t kCcPoolSlot = 2 * kLanesPerPkt;  // first pooled slot (iterations 0 and 1 are the wave's)
 
-// this packet's 32-B pool record in its wave's scratch: [0] pooled blocks, [1] payload LDS
-// offset (workgroup) | P << 17, [3] key row, [4..6] nonce words
+// Seal also pools every packet's header-protection block (RFC 9001 §5.4.4: ChaCha20 under the HP
+// key, counter and nonce from the 16-B ciphertext sample at pn_offset + 4), as the packet's last
+// pool entry: the sample is ciphertext of keystream block 1, in place after iteration 0, and the
+// pool's second wave-iteration is otherwise idle for waves 2-3 of a 1200-B workgroup (128 keystream
+// blocks + 32 HP blocks = 160 entries < 3 x 64), so the mask costs no extra time and no pass over
+// the batch (r02 ran it as a post-pass kernel: 63 us and 0.23 GB per 2^20 packets). The mask waits
+// in the record until the MAC has read the unprotected header; octet lane 0 then applies it.
+//
+// this packet's 32-B pool record in its wave's scratch: [0] pooled keystream blocks | the PN
+// length << 8 when the header-protection block is pooled too, [1] payload LDS offset (workgroup)
+// | P << 17, [2] / [7] mask words 0 / 1 (written by the pool), [3] key row, [4..6] nonce words
 struct CcPool {
   bool on;              // wave-uniform: staged tile whose slots >= 16 go to the pool
   uint8_t* wg;          // the workgroup's LDS
@@ -191,10 +200,11 @@ __device__ __forceinline__ void cc_pool_run(const CcPool& pool) {
   static_assert(kQ <= kWave, "one packet per lane in the pool scan");
   const int lane = threadIdx.x & (kWave - 1);
   const uint32_t w = threadIdx.x >> 6;
-  auto rec = [&](uint32_t q) -> const uint32_t* {
-    return (const uint32_t*)(pool.wg + (q >> 3) * kLdsBytes + kDataBudget + 32u * (q & 7));
+  auto rec = [&](uint32_t q) -> uint32_t* {
+    return (uint32_t*)(pool.wg + (q >> 3) * kLdsBytes + kDataBudget + 32u * (q & 7));
   };
-  const uint32_t nq = (uint32_t)lane < kQ ? rec((uint32_t)lane)[0] : 0u;  // lane q: packet q
+  const uint32_t r0l = (uint32_t)lane < kQ ? rec((uint32_t)lane)[0] : 0u;  // lane q: packet q
+  const uint32_t nq = (r0l & 0xffu) + ((r0l >> 8) ? 1u : 0u);
   const uint32_t incl = wave_incl_scan(nq), excl = incl - nq;
   const uint32_t T = lane_u32(incl, kWave - 1);
   const LdsSpace sp{pool.wg};
@@ -208,18 +218,46 @@ __device__ __forceinline__ void cc_pool_run(const CcPool& pool) {
     }
     const uint32_t eq = (uint32_t)__shfl((int)excl, (int)q, kWave);
     const bool act = e < T;
-    const uint32_t* r = rec(q);
-    const uint32_t r1 = r[1], pay = r1 & 0x1ffffu, P = r1 >> 17;
-    const uint32_t cb = kCcPoolSlot + (e - eq), o = 64u * (cb - 1);
+    uint32_t* r = rec(q);
+    const uint32_t r0 = r[0], r1 = r[1], pay = r1 & 0x1ffffu, P = r1 >> 17;
+    const uint32_t idx = e - eq, pn_len = r0 >> 8;
+    const bool hp = act && idx == (r0 & 0xffu);  // the packet's last entry: its HP block
+    const uint32_t cb = kCcPoolSlot + idx, o = 64u * (cb - 1);
     const KeyRow* row = SINGLE || !act ? pool.kt : pool.kt + r[3];  // an idle lane's record may be stale
     uint32_t key[8];
-    load_key8(row->key, key);
-    uint32_t raw[17];
-    load_raw<16>(sp, act ? pay + o : 0u, raw);  // in flight during the rounds
+    if (SINGLE) {  // both keys wave-uniform (SGPRs); pick per lane
+      uint32_t kd[8], kh[8];
+      load_key8(row->key, kd);
+      load_key8(row->hp, kh);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) key[k] = hp ? kh[k] : kd[k];
+    } else {
+      load_key8(hp ? row->hp : row->key, key);
+    }
+    uint32_t raw[17], smp[4];
+    load_raw<16>(sp, act && !hp ? pay + o : 0u, raw);  // in flight during the rounds
+    // the sample: 16 bytes at pn_offset + 4 = payload - pn_len + 4 (ciphertext of block 1)
+    load_words<4>(sp, hp ? pay + 4u - pn_len : 0u, smp);
     uint32_t ks[16];
-    chacha20_block(key, cb, r[4], r[5], r[6], ks);
-    if (act) xor_words<16>(sp, pay + o, ks, (int)min(64u, P - o), raw);
+    chacha20_block(key, hp ? smp[0] : cb, hp ? smp[1] : r[4], hp ? smp[2] : r[5], hp ? smp[3] : r[6], ks);
+    if (hp) {
+      r[2] = ks[0];
+      r[7] = ks[1];
+    } else if (act) {
+      xor_words<16>(sp, pay + o, ks, (int)min(64u, P - o), raw);
+    }
   }
+}
+
+// RFC 9001 §5.4.1: XOR the mask into the first byte (low 4 / 5 bits) and the PN bytes of a sealed
+// packet whose MAC has been computed (octet lane 0)
+template <class S>
+__device__ __forceinline__ void apply_hp(const S& sp, typename S::off_t pkt, const mq_pkt_desc& d, uint32_t m0,
+                                         uint32_t m1) {
+  sp.st8(pkt, (uint8_t)(sp.ld8(pkt) ^ ((uint8_t)m0 & ((d.flags & MQ_PKT_LONG_HEADER) ? 0x0f : 0x1f))));
+  const uint32_t mk = (m0 >> 8) | (m1 << 24);
+  for (uint32_t b = 0; b < d.pn_len; ++b)
+    sp.st8(pkt + d.pn_offset + b, (uint8_t)(sp.ld8(pkt + d.pn_offset + b) ^ (uint8_t)(mk >> (8 * b))));
 }
 
 struct ChaChaPolicy {
@@ -308,10 +346,15 @@ struct ChaChaPolicy {
       wave_sync();
     }
     if (Imax == 0) stg.complete();
-    if (j == 0) {  // pool record
+    const bool hp = c.act && !(d.flags & MQ_PKT_NO_HP);  // records and plain AEAD rows have none
+    // the pool takes the HP block when the sample (payload bytes [4 - pn_len, 20 - pn_len)) is all
+    // ciphertext; for tiny payloads it reaches into the tag, which only the MAC below produces
+    const bool hp_pool = pool.on && hp && P + d.pn_len >= 20u;
+    if (j == 0) {  // pool record: keystream blocks >= 16 and the HP block
       const uint32_t np = pool.on && c.act && nblk > kCcPoolSlot ? nblk - kCcPoolSlot : 0u;
-      pool.rec[0] = np;
-      if (np) {
+      const uint32_t hpn = hp_pool ? (uint32_t)d.pn_len : 0u;  // 1..4 (validated)
+      pool.rec[0] = np | hpn << 8;
+      if (np || hpn) {
         pool.rec[1] = (pool.base + (uint32_t)pay) | P << 17;
         pool.rec[3] = d.key_id;
         pool.rec[4] = n0; pool.rec[5] = n1; pool.rec[6] = n2;
@@ -319,11 +362,28 @@ struct ChaChaPolicy {
     }
     __syncthreads();  // every wave's records
     cc_pool_run<SINGLE>(pool);
-    __syncthreads();  // every pooled block is in place before any MAC reads it
+    __syncthreads();  // every pooled block (and mask) is in place before any MAC reads it
     MQ_STAMP(c.tile, 3);
     uint32_t tag[4];
     poly_tag(sp, pkt, pay, aad_len, P, c.otk, j, c.act, tag);
     if (c.act && j == 0) store_words<4>(sp, pay + P, tag);
+    // header protection (transmit.rs:713-738), now that the MAC has read the unprotected header
+    uint32_t m0 = 0, m1 = 0;
+    if (hp_pool) {
+      m0 = pool.rec[2];
+      m1 = pool.rec[7];
+    }
+    const bool late = hp && !hp_pool;  // direct path, or a sample that reaches into the tag
+    if (wave_any(late)) {  // this wave computes those masks itself
+      wave_sync();  // ciphertext and tags are in place
+      uint32_t a0, a1;
+      hp_mask(sp, pkt + d.pn_offset + 4, row, a0, a1);
+      if (late) {
+        m0 = a0;
+        m1 = a1;
+      }
+    }
+    if (hp && j == 0) apply_hp(sp, pkt, d, m0, m1);
     wave_sync();
     MQ_STAMP(c.tile, 4);
   }
@@ -396,7 +456,7 @@ struct ChaChaPolicy {
       chacha20_block(key, ctr, n0, n1, n2, ks);
       if (a) store_block(sp, pay, ctr, P, ks, w);
     }
-    if (j == 0) {  // pool record: only verified packets are decrypted
+    if (j == 0) {  // pool record: only verified packets are decrypted (no HP block on open)
       const uint32_t np = pool.on && c.act && nblk > kCcPoolSlot ? nblk - kCcPoolSlot : 0u;
       pool.rec[0] = np;
       if (np) {
@@ -553,28 +613,6 @@ __global__ __launch_bounds__(256) void mq_chacha_open_hp_kernel(
   }
 }
 
-// Seal post-pass: header protection of every sealed packet — transmit.rs:713-719 with
-// ChaChaHeaderProtection::mask (rustcrypto.rs:197-220), one packet per lane: sample = the 16
-// bytes at pn_offset + 4 of the sealed packet (ciphertext, into the tag for tiny payloads), mask
-// applied to byte 0 (low 4 / 5 bits) and the PN bytes (RFC 9001 §5.4.1).
-__global__ __launch_bounds__(256) void mq_chacha_seal_hp_kernel(
-    const KeyRow* __restrict__ kt, uint8_t* __restrict__ arena, const mq_pkt_desc* __restrict__ desc, uint32_t n,
-    const uint32_t* __restrict__ index, const uint32_t* __restrict__ n_dev, const uint8_t* __restrict__ status) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t count = n_dev ? *n_dev : n;
-  if (t >= count) return;
-  const uint32_t i = index ? index[t] : t;
-  if (i == kListHole || status[i] != MQ_OK) return;
-  const mq_pkt_desc d = desc[i];
-  if (d.flags & MQ_PKT_NO_HP) return;  // records and plain AEAD rows
-  uint32_t w[5], m0, m1;
-  uint8_t b0;
-  prepass_header(arena, d, b0, w);  // inside the packet (validated: pn_offset + 20 <= len)
-  const uint32_t smp[4] = {w[1], w[2], w[3], w[4]};
-  ChaChaPolicy::hp_mask_words(smp, kt + d.key_id, m0, m1);
-  seal_apply_hp(arena, d, b0, w[0], m0, m1);
-}
-
 // ---- host-side launchers (called from mq_host.cpp) -------------------------------------------
 hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena,
                             uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
@@ -593,15 +631,10 @@ hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_
                        dim3((tiles + kCcWaves - 1) / kCcWaves), dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kt,
                        n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm);
   if (open) return hipGetLastError();
+  // seal: header protection runs inside the tile kernel (the pool's HP blocks, cc_pool_run)
   hipLaunchKernelGGL(n_rows == 1 ? mq_chacha_seal1_kernel : mq_chacha_seal_kernel,
                      dim3((tiles + kCcWaves - 1) / kCcWaves), dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kt,
                      n_rows, arena, arena_len, desc, n, index, n_dev, status);
-  if (own_hp) {  // !own_hp: mq_launch_mixed_hp covers both suites' lists, or the rows are NO_HP
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(mq_chacha_seal_hp_kernel, dim3((n + 255) / 256), dim3(256), 0, s, kt, arena, desc, n, index,
-                       n_dev, status);
-  }
   return hipGetLastError();
 }
 

@@ -760,13 +760,15 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
     if (e == hipSuccess && open && hpm)
       e = mq_launch_mixed_hp(true, kt->dev, kt->rows, arena, arena_len, desc, list, cap, counts, status, hpm, s);
     if (e != hipSuccess) return MQ_ERR_HIP;
-    // The tile kernels of the lists run concurrently: the hot AES key's segment (counts + 2: its
-    // row and segment length, list 0's front; single-key kernel) on side stream 0, the other AES
-    // keys' tiles on s, list 1 (ChaCha20, or the AES hint's leftovers) on side stream 1 — each CU
-    // moves on to the next kernel's workgroups as its own finish, instead of idling at every
-    // kernel's tail. Side streams are per (device, caller stream): mq_runtime.h.
-    auto fork = fork_enabled() ? side_streams().fork(kt->device, s, 2) : mq::SideStreams<HipBackend>::Fork();
-    hipStream_t s_hot = fork ? fork.side(0) : s, s_list1 = fork ? fork.side(1) : s;
+    // The hot AES key's segment (counts + 2: its row and segment length, list 0's front;
+    // single-key kernel) runs on a side stream beside the other AES keys' tiles on s: each CU moves
+    // on to the other kernel's workgroups as its own finish (r02: E 2.794 -> 2.749 ms). List 1
+    // (ChaCha20, or the AES hint's leftovers) follows on s: forked as well it cost E 15 % (r03a:
+    // 1.346 -> 1.562 ms seal), because its 40-KiB workgroups take CUs that the persistent AES
+    // grids (one 152-KiB workgroup per CU) then wait for. Side streams are per (device, caller
+    // stream): mq_runtime.h.
+    auto fork = fork_enabled() ? side_streams().fork(kt->device, s, 1) : mq::SideStreams<HipBackend>::Fork();
+    hipStream_t s_hot = fork ? fork.side(0) : s, s_list1 = s;
     e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list, counts, counts + 2, status, pn_out,
                       hpm, false, s, s_hot, cus);
     if (e == hipSuccess && aes_only)

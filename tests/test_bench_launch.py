@@ -79,9 +79,11 @@ def test_sample_indices_and_shard_positions():
 
 def test_roofline_seal_composite_traffic():
     """roofline.kernel / traffic name the seal composite the bench's event time covers: the tile
-    kernel ("1" variant for a one-row key table) plus the header-protection pass; the PMC traffic
-    is the sum of both kernels' per-launch HBM bytes from profiles/pmc_traffic_<cfg>.json."""
-    assert bench.seal_kernels("b", 1) == ("mq_chacha_seal1_kernel", "mq_chacha_seal_hp_kernel")
+    kernel ("1" variant for a one-row key table), plus for AES the header-protection pass of short
+    packets; the PMC traffic is the sum of those kernels' per-launch HBM bytes from
+    profiles/pmc_traffic_<cfg>.json."""
+    assert bench.seal_kernels("b", 1) == ("mq_chacha_seal1_kernel",)  # HP inside the tile (r03)
+    assert bench.seal_kernels("b", 1024) == ("mq_chacha_seal_kernel",)
     assert bench.seal_kernels("c", 1024) == ("mq_aes_seal_kernel", "mq_aes_seal_hp_kernel")
     assert bench.seal_kernels("e", 4098) is None
     for cfg in ("b", "c"):

@@ -6,6 +6,9 @@ export TMPDIR=/tmp
 O=gpurun_out/r03a
 mkdir -p $O
 step() { echo "== $1 $(date +%T)"; }
+step ubench8
+timeout -k 10 120 ./tools/ubench/ubench8 > $O/ubench8.txt 2>&1 || { cat $O/ubench8.txt; exit 1; }
+cat $O/ubench8.txt
 step tests
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
