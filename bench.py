@@ -333,16 +333,29 @@ def end_to_end(torch, batch, kt, w, sd, od, dev, chunks=8, reps=3):
 # tile. The "1" tile kernel variant (key material in SGPRs) runs when the key table has a single
 # row (launchers in mq_chacha.hip / mq_aes.hip). seal_ms (HIP events around mq_batch_seal) spans
 # the composite.
+# Config E's seal is the whole mixed batch: the four partition launches, the hot AES key's
+# single-key kernel beside the multi-key one, the ChaCha20 list and the HP pass of short AES
+# packets.
 KERNELS = {"b": ("mq_chacha_seal_kernel",),
-           "c": ("mq_aes_seal_kernel", "mq_aes_seal_hp_kernel"), "e": None}
+           "c": ("mq_aes_seal_kernel", "mq_aes_seal_hp_kernel"),
+           "e": ("mq_part_init_kernel", "mq_part_count_kernel", "mq_part_scan_kernel", "mq_part_scatter_kernel",
+                 "mq_aes_seal1_kernel", "mq_aes_seal_kernel", "mq_chacha_seal_kernel", "mq_mixed_hp_kernel<false>")}
 
 
 def seal_kernels(cfg, n_rows):
     ks = KERNELS.get(cfg)
     if not ks:
         return None
+    if cfg == "e":
+        return ks
     tile = ks[0].replace("_seal_kernel", "_seal1_kernel") if n_rows == 1 else ks[0]
     return (tile,) + tuple(ks[1:])
+
+
+def kernel_key(name):
+    """rocprofv3 kernel name -> the name KERNELS uses (argument list and 'void ' dropped)."""
+    k = name.split("(")[0]
+    return k[5:] if k.startswith("void ") else k
 
 
 def load_traffic(cfg, kerns):
@@ -355,7 +368,7 @@ def load_traffic(cfg, kerns):
             d = json.load(f)["kernels"]
         if not kerns:
             return None
-        by_name = {k.split("(")[0]: v for k, v in d.items()}
+        by_name = {kernel_key(k): v for k, v in d.items()}
         return int(sum(by_name[k]["hbm_bytes_per_launch"] for k in kerns))
     except (OSError, ValueError, KeyError, TypeError):
         return None
@@ -454,8 +467,7 @@ def main():
                 "traffic": load_traffic(args.config, kerns) if (w.n == 1 << 20 and args.keys == 1) else None,
                 # north_star's "HBM-read roofline" fraction: wire bytes read per seal ÷ 8 TB/s
                 "read_frac": round(wire / (seal_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                "kernel": ("seal composite: " + " + ".join(kerns)) if kerns
-                          else "seal batch (partition + AES + ChaCha kernels + HP pass)",
+                "kernel": ("seal composite: " if args.config != "e" else "seal batch: ") + " + ".join(kerns),
                 "seal_ms": round(seal_ms, 4), "open_ms": round(open_ms, 4),
                 "open_frac": round(algo_bytes / (open_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "algorithmic_bytes_per_launch": int(algo_bytes)}

@@ -740,20 +740,18 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
   return hipGetLastError();
 }
 
-// Mixed batches: the open pre-pass (OPEN) or the seal HP post-pass of BOTH partition lists in one
-// launch (list 0 = list[0, counts[0]), list 1 = list[cap, cap + counts[1])), one packet per lane,
-// either suite per lane — the two passes' memory latencies overlap instead of adding up. Seal:
-// the AES packets whose HP had no slot in their tile (fewer than 7 CTR blocks), as
-// mq_aes_seal_hp_kernel does per list; the ChaCha20 tiles mask their packets themselves.
+// Mixed batches: the open pre-pass (OPEN) or the seal HP post-pass over every descriptor of the
+// batch in DESCRIPTOR order, one packet per lane, either suite per lane. (r02 walked the two
+// partition lists: their order scatters the descriptor, status and header reads over the arena,
+// 0.34 / 0.17 GB per 2^20-packet config-E launch where the descriptors alone are 34 MB, r03b PMC.)
+// Seal: the AES packets whose HP had no slot in their tile (fewer than 7 CTR blocks), as
+// mq_aes_seal_hp_kernel does for flat batches; the ChaCha20 tiles mask their packets themselves.
 template <bool OPEN>
 __global__ __launch_bounds__(256) void mq_mixed_hp_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
-    const mq_pkt_desc* __restrict__ desc, const uint32_t* __restrict__ list, uint32_t cap,
-    const uint32_t* __restrict__ counts, const uint8_t* __restrict__ status, uint2* __restrict__ hpm) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t sl = t >= cap ? 1u : 0u, e = t - sl * cap;
-  uint32_t i = t < 2 * cap && e < counts[sl] ? list[t] : kListHole;
-  bool act = i != kListHole, aes = false;
+    const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint8_t* __restrict__ status, uint2* __restrict__ hpm) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  bool act = i < n, aes = false;
   mq_pkt_desc d{};
   const KeyRow* row = kt;
   if (OPEN) {  // prepass_pick's checks; the tile kernels report the rest
@@ -772,11 +770,13 @@ __global__ __launch_bounds__(256) void mq_mixed_hp_kernel(
     act = act && status[i] == MQ_OK;
     if (act) {
       d = desc[i];
+      act = !(d.flags & MQ_PKT_NO_HP) && d.key_id < n_rows;
+    }
+    if (act) {
       row = kt + d.key_id;
       aes = row->suite == MQ_SUITE_AES128GCM;
       const uint32_t P = d.len - ((uint32_t)d.pn_offset + d.pn_len) - 16;
-      // the AES packets whose HP had no slot in their tile (ChaCha20 tiles mask every packet)
-      act = aes && !(d.flags & MQ_PKT_NO_HP) && 1 + ((P + 15) >> 4) < (uint32_t)kLanesPerPkt;
+      act = aes && 1 + ((P + 15) >> 4) < (uint32_t)kLanesPerPkt;
     }
   }
   if (!__syncthreads_or(act)) return;
@@ -804,16 +804,15 @@ __global__ __launch_bounds__(256) void mq_mixed_hp_kernel(
 }
 
 hipError_t mq_launch_mixed_hp(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena, uint64_t arena_len,
-                              const mq_pkt_desc* desc, const uint32_t* list, uint32_t cap, const uint32_t* counts,
-                              const uint8_t* status, uint2* hpm, hipStream_t s) {
-  const uint32_t blocks = (uint32_t)((2ull * cap + 255) / 256);
+                              const mq_pkt_desc* desc, uint32_t n, const uint8_t* status, uint2* hpm, hipStream_t s) {
+  const uint32_t blocks = (n + 255) / 256;
   if (blocks == 0) return hipSuccess;
   if (open)
-    hipLaunchKernelGGL(mq_mixed_hp_kernel<true>, dim3(blocks), dim3(256), 0, s, kt, n_rows, arena, arena_len, desc, list,
-                       cap, counts, status, hpm);
+    hipLaunchKernelGGL(mq_mixed_hp_kernel<true>, dim3(blocks), dim3(256), 0, s, kt, n_rows, arena, arena_len, desc, n,
+                       status, hpm);
   else
     hipLaunchKernelGGL(mq_mixed_hp_kernel<false>, dim3(blocks), dim3(256), 0, s, kt, n_rows, arena, arena_len, desc,
-                       list, cap, counts, status, hpm);
+                       n, status, hpm);
   return hipGetLastError();
 }
 

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "mq_device.h"
+#include "mq_resident.h"
 #include "mq_runtime.h"
 
 using mq::KeyRow;
@@ -32,8 +33,7 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
                          uint8_t* status, uint64_t* pn_out, uint2* hpm, bool own_hp, hipStream_t s,
                          hipStream_t hot_stream, int cus);
 hipError_t mq_launch_mixed_hp(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena, uint64_t arena_len,
-                              const mq_pkt_desc* desc, const uint32_t* list, uint32_t cap, const uint32_t* counts,
-                              const uint8_t* status, uint2* hpm, hipStream_t s);
+                              const mq_pkt_desc* desc, uint32_t n, const uint8_t* status, uint2* hpm, hipStream_t s);
 hipError_t mq_launch_aes_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t* key_ids,
                             const uint8_t* samples, uint8_t* masks, uint32_t n, hipStream_t s);
 hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_desc* desc, uint32_t n,
@@ -63,6 +63,8 @@ hipError_t mq_recv_outcomes(uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_con
                             size_t open_ws_bytes, hipStream_t s);
 hipError_t mq_launch_record_inner(const uint8_t* arena, uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
                                   uint8_t* status, uint64_t* info, hipStream_t s);
+int mq_resident_call(int dev, const mq::ResReq& q, const uint8_t* aad, const uint8_t* body, uint8_t* out,
+                     size_t out_off, size_t out_len, int* status, uint32_t* mask);
 #ifdef MQ_STAMPS
 void mq_stamps_set_chacha(uint64_t* p);
 void mq_stamps_set_aes(uint64_t* p);
@@ -440,6 +442,37 @@ int run_one(Scratch& sc, const KeyRow& row, const uint8_t* aad, uint32_t aad_len
   return status;
 }
 
+// Per-packet calls go to the device's resident kernel (mq_resident.hip: no launch per call) unless
+// MQ_RESIDENT=0 or the packet exceeds its buffer; then run_one's batch of one.
+bool resident_enabled(size_t bytes) {
+  const char* e = std::getenv("MQ_RESIDENT");  // per call: tests and tools/bench_latency.py switch it
+  return !(e && e[0] == '0') && bytes <= mq::kResMaxPkt;
+}
+
+// The resident request image of a context: suite and key material (and for AES-128-GCM the GHASH
+// powers H^1..H^64 of its 64-lane Horner), filled once at creation.
+mq::ResReq* res_image(const KeyRow& row, bool aead) {
+  mq::ResReq* q = new mq::ResReq();
+  std::memset(q, 0, sizeof *q);
+  q->suite = row.suite;
+  std::memcpy(q->key, row.key, sizeof q->key);
+  std::memcpy(q->hp, row.hp, sizeof q->hp);
+  std::memcpy(q->aes_rk, row.aes_rk, sizeof q->aes_rk);
+  std::memcpy(q->hp_rk, row.hp_rk, sizeof q->hp_rk);
+  if (aead && row.suite == MQ_SUITE_AES128GCM) {
+    uint8_t h[16], x[16], zero[16] = {0};
+    aes_encrypt(row.aes_rk, zero, h);  // H = E_K(0^128)
+    std::memcpy(x, h, 16);
+    for (int p = 0; p < 64; ++p) {
+      for (int w = 0; w < 4; ++w) q->Hpow[p][w] = be32(x + 4 * w);
+      uint8_t y[16];
+      gf128_mul(x, h, y);
+      std::memcpy(x, y, 16);
+    }
+  }
+  return q;
+}
+
 }  // namespace
 
 // =============================================================================================
@@ -448,11 +481,15 @@ struct mq_aead_ctx {
   uint32_t suite;
   KeyRow row;  // key schedule, H powers; iv is overwritten by the per-call nonce
   mutable Scratch sc;
+  mq::ResReq* res = nullptr;  // resident request image (mutated per call under sc.mu)
+  ~mq_aead_ctx() { delete res; }
 };
 struct mq_hp_ctx {
   uint32_t suite;
   KeyRow row;
   mutable Scratch sc;
+  mq::ResReq* res = nullptr;
+  ~mq_hp_ctx() { delete res; }
 };
 struct mq_keytable {
   KeyRow* dev = nullptr;
@@ -503,6 +540,7 @@ int mq_aead_new(uint32_t suite, const uint8_t* key, size_t key_len, mq_aead_ctx*
   c->sc.device = dev;
   c->suite = suite;
   build_row(km, c->row);
+  c->res = res_image(c->row, true);
   *out = c;
   return MQ_OK;
 }
@@ -521,6 +559,21 @@ int mq_aead_seal_in_place(const mq_aead_ctx* ctx, const uint8_t* nonce, size_t n
   }
   if ((aad_len && !aad) || !buf || aad_len > 0xffff || aad_len + total > 0xffffffffu) return MQ_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(ctx->sc.mu);
+  if (resident_enabled(aad_len + total)) {
+    DeviceGuard g(ctx->sc.device);
+    if (!g.ok()) return MQ_ERR_NO_DEVICE;
+    mq::ResReq& q = *ctx->res;
+    q.op = mq::kResSeal;
+    q.aad_len = (uint32_t)aad_len;
+    q.body_len = (uint32_t)payload_len;
+    for (int i = 0; i < 3; ++i) q.nonce[i] = le32(nonce + 4 * i);
+    int st = MQ_ERR_HIP;
+    const int rc = mq_resident_call(ctx->sc.device, q, aad, buf, buf, aad_len, total, &st, nullptr);
+    if (rc) return rc;
+    if (st) return st;
+    if (out_len) *out_len = total;
+    return MQ_OK;
+  }
   KeyRow row = ctx->row;
   for (int i = 0; i < 3; ++i) row.iv[i] = le32(nonce + 4 * i);
   const int rc = run_one(ctx->sc, row, aad, (uint32_t)aad_len, buf, (uint32_t)payload_len,
@@ -539,6 +592,21 @@ int mq_aead_open_in_place(const mq_aead_ctx* ctx, const uint8_t* nonce, size_t n
   if (ct_len > buf_len) return MQ_ERR_INVALID_ARG;      // the reference panics (:83,154)
   if ((aad_len && !aad) || !buf || aad_len > 0xffff || aad_len + ct_len > 0xffffffffu) return MQ_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(ctx->sc.mu);
+  if (resident_enabled(aad_len + ct_len)) {
+    DeviceGuard g(ctx->sc.device);
+    if (!g.ok()) return MQ_ERR_NO_DEVICE;
+    mq::ResReq& q = *ctx->res;
+    q.op = mq::kResOpen;
+    q.aad_len = (uint32_t)aad_len;
+    q.body_len = (uint32_t)ct_len;
+    for (int i = 0; i < 3; ++i) q.nonce[i] = le32(nonce + 4 * i);
+    int st = MQ_ERR_HIP;
+    const int rc = mq_resident_call(ctx->sc.device, q, aad, buf, buf, aad_len, ct_len - 16, &st, nullptr);
+    if (rc) return rc;
+    if (st) return st;  // buffer untouched on failure
+    if (out_len) *out_len = ct_len - 16;
+    return MQ_OK;
+  }
   KeyRow row = ctx->row;
   for (int i = 0; i < 3; ++i) row.iv[i] = le32(nonce + 4 * i);
   const int rc = run_one(ctx->sc, row, aad, (uint32_t)aad_len, buf, (uint32_t)ct_len, (uint32_t)(aad_len + ct_len),
@@ -564,6 +632,7 @@ int mq_hp_new(uint32_t suite, const uint8_t* key, size_t key_len, mq_hp_ctx** ou
   c->sc.device = dev;
   c->suite = suite;
   build_row(km, c->row);
+  c->res = res_image(c->row, false);
   *out = c;
   return MQ_OK;
 }
@@ -576,6 +645,20 @@ int mq_hp_mask(const mq_hp_ctx* ctx, const uint8_t* sample, size_t sample_len, u
   Scratch& sc = ctx->sc;
   DeviceGuard g(sc.device);
   if (!g.ok()) return MQ_ERR_NO_DEVICE;
+  if (resident_enabled(0)) {
+    mq::ResReq& q = *ctx->res;
+    q.op = mq::kResHp;
+    q.aad_len = q.body_len = 0;
+    for (int i = 0; i < 4; ++i) q.sample[i] = le32(sample + 4 * i);
+    int st = MQ_ERR_HIP;
+    uint32_t m[2] = {0, 0};
+    const int rc = mq_resident_call(sc.device, q, nullptr, nullptr, nullptr, 0, 0, &st, m);
+    if (rc) return rc;
+    if (st) return st;
+    for (int b = 0; b < 4; ++b) mask[b] = (uint8_t)(m[0] >> (8 * b));
+    mask[4] = (uint8_t)m[1];
+    return MQ_OK;
+  }
   int rc = sc.ensure(64);
   if (rc) return rc;
   // layout: row | key id (4) @kDesc | sample 16 @kSample | mask 5 @kStatus
@@ -758,7 +841,7 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
     // one header-protection pass covers both lists, before the tiles for open and after every
     // tile kernel for seal (the AES tiles mask their long packets themselves)
     if (e == hipSuccess && open && hpm)
-      e = mq_launch_mixed_hp(true, kt->dev, kt->rows, arena, arena_len, desc, list, cap, counts, status, hpm, s);
+      e = mq_launch_mixed_hp(true, kt->dev, kt->rows, arena, arena_len, desc, n, status, hpm, s);
     if (e != hipSuccess) return MQ_ERR_HIP;
     // The hot AES key's segment (counts + 2: its row and segment length, list 0's front;
     // single-key kernel) runs on a side stream beside the other AES keys' tiles on s: each CU moves
@@ -780,7 +863,7 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
     // join even after a failed launch, so no side stream runs ahead of s
     if (!fork.join() && e == hipSuccess) e = hipErrorUnknown;
     if (e == hipSuccess && !open)
-      e = mq_launch_mixed_hp(false, kt->dev, kt->rows, arena, arena_len, desc, list, cap, counts, status, nullptr, s);
+      e = mq_launch_mixed_hp(false, kt->dev, kt->rows, arena, arena_len, desc, n, status, nullptr, s);
   } else {
     return MQ_ERR_INVALID_ARG;
   }

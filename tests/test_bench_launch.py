@@ -85,7 +85,8 @@ def test_roofline_seal_composite_traffic():
     assert bench.seal_kernels("b", 1) == ("mq_chacha_seal1_kernel",)  # HP inside the tile (r03)
     assert bench.seal_kernels("b", 1024) == ("mq_chacha_seal_kernel",)
     assert bench.seal_kernels("c", 1024) == ("mq_aes_seal_kernel", "mq_aes_seal_hp_kernel")
-    assert bench.seal_kernels("e", 4098) is None
+    assert bench.seal_kernels("e", 4098)[-1] == "mq_mixed_hp_kernel<false>"
+    assert bench.kernel_key("void mq_mixed_hp_kernel<false>(mq::KeyRow const*, unsigned int)") == "mq_mixed_hp_kernel<false>"
     for cfg in ("b", "c"):
         ks = bench.seal_kernels(cfg, 1)
         with open(os.path.join(HERE, "..", "profiles", f"pmc_traffic_{cfg}.json")) as f:

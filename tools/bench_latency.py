@@ -1,13 +1,15 @@
 #!/usr/bin/env python3
-"""Per-packet latency of the drop-in trait path: microseconds per call of
-mq_aead_seal_in_place / mq_aead_open_in_place / mq_hp_mask on one 1200-B packet (13-B AAD,
+"""Per-packet latency of the drop-in trait path: microseconds per call
+of mq_aead_seal_in_place / mq_aead_open_in_place / mq_hp_mask on one 1200-B packet (13-B AAD,
 1171-B payload), called through ctypes exactly as the reference calls Aead / HeaderProtection
-once per packet (transmit.rs:713-719, recv.rs:416-421). Each call is a batch of one: the packet
-is staged in a pinned scratch that the kernel reads and writes over PCIe (zero-copy, default),
-or — MQ_PER_PACKET_COPY=1, timed as "copy" — copied H2D before and D2H after the kernel; then
-the stream is synchronised. Prints one JSON line (median and p99 over `--calls` calls, after
-warm-up), for both suites and both modes. The batch API is the throughput path; this measures
-the correctness shim."""
+once per packet (transmit.rs:713-719, recv.rs:416-421). Modes:
+  resident   (default since r03) the device's resident wave serves the call from a mailbox in
+             pinned host memory: no kernel launch (mq_resident.hip);
+  zero_copy  (MQ_RESIDENT=0) a batch of one: one kernel launch on a pinned scratch mapped into the
+             device, then a stream sync;
+  copy       (MQ_RESIDENT=0 MQ_PER_PACKET_COPY=1) the same with H2D / D2H copies around it.
+Prints one JSON line (median and p99 over `--calls` calls, after warm-up), both suites, all modes.
+The batch API is the throughput path."""
 import argparse
 import ctypes
 import json
@@ -28,9 +30,11 @@ def main():
     lib = _lib.load()
     assert lib.mq_device_init(0) == 0
     out = {"unit": "us per call", "packet": "1200 B (13 B AAD, 1171 B payload, 16 B tag)", "calls": args.calls}
-    for mode in ("zero_copy", "copy"):
+    for mode in ("resident", "zero_copy", "copy"):
+        os.environ["MQ_RESIDENT"] = "1" if mode == "resident" else "0"
         os.environ["MQ_PER_PACKET_COPY"] = "1" if mode == "copy" else "0"
         out[mode] = measure(lib, _lib, args.calls)
+    os.environ.pop("MQ_RESIDENT", None)
     print(json.dumps(out), flush=True)
 
 

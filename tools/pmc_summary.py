@@ -26,7 +26,8 @@ def load(d):
         with open(f) as fh:
             per = defaultdict(float)  # (dispatch, kernel, counter) -> sum
             for r in csv.DictReader(fh):
-                k = r["Kernel_Name"]
+                k = r["Kernel_Name"].split("(")[0]
+                k = k[5:] if k.startswith("void ") else k  # templated kernels: "void mq_...<..>(...)"
                 if not k.startswith("mq_"):
                     continue
                 per[(r["Dispatch_Id"], k, r["Counter_Name"])] += float(r["Counter_Value"])
