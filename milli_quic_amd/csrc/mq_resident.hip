@@ -77,15 +77,21 @@ __device__ void res_poly(uint32_t aad_len, uint32_t pay, uint32_t ct_len, const 
   const LdsSpace sp{s_pkt};
   const P26 r = p26_from_words(otk[0] & 0x0fffffffu, otk[1] & 0x0ffffffcu, otk[2] & 0x0ffffffcu,
                                otk[3] & 0x0ffffffcu, 0);
-  // ladder: e = r^(2^s); v = r^(1 + lane) from the bits of lane; r^64 = e after 6 squarings
-  P26 e = r, v = r;
+  // powers by a prefix product over the lanes: after step s lane j holds r^(min(j, 2^(s+1) - 1) + 1)
+  // (6 multiplies, not 6 squarings + 6 conditional multiplies); r^64 = lane 63's r^64
+  P26 v = r;
 #pragma unroll 1
   for (int s = 0; s < 6; ++s) {
+    P26 u;
+#pragma unroll
+    for (int l = 0; l < 5; ++l) u.l[l] = (uint32_t)__shfl((int)v.l[l], max(lane - (1 << s), 0), 64);
     P26 t = v;
-    p26_mul(t, p26_mult(e));
-    if ((lane >> s) & 1) v = t;
-    p26_mul(e, p26_mult(e));
+    p26_mul(t, p26_mult(u));
+    if (lane >= (1 << s)) v = t;
   }
+  P26 e;
+#pragma unroll
+  for (int l = 0; l < 5; ++l) e.l[l] = (uint32_t)__builtin_amdgcn_readlane((int)v.l[l], 63);
   const P26m m64 = p26_mult(e);
   P26 last;
 #pragma unroll
@@ -343,7 +349,7 @@ extern "C" __global__ __launch_bounds__(64) void mq_resident_kernel(ResArea* are
         t_last = now;
         continue;
       }
-      __builtin_amdgcn_s_sleep(8);
+      __builtin_amdgcn_s_sleep(1);  // the poll itself is a PCIe round trip (~1 us)
       continue;
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the request written before seq
