@@ -328,28 +328,25 @@ def end_to_end(torch, batch, kt, w, sd, od, dev, chunks=8, reps=3):
 
 
 # ---- roofline bookkeeping ---------------------------------------------------------------------
-# The seal composite of a single-suite batch: the tile kernel (ChaCha20: header protection
-# included, r03), then for AES the header-protection pass of the packets with no free slot in their
-# tile. The "1" tile kernel variant (key material in SGPRs) runs when the key table has a single
-# row (launchers in mq_chacha.hip / mq_aes.hip). seal_ms (HIP events around mq_batch_seal) spans
-# the composite.
-# Config E's seal is the whole mixed batch: the four partition launches, the hot AES key's
-# single-key kernel beside the multi-key one, the ChaCha20 list and the HP pass of short AES
-# packets.
-KERNELS = {"b": ("mq_chacha_seal_kernel",),
-           "c": ("mq_aes_seal_kernel", "mq_aes_seal_hp_kernel"),
-           "e": ("mq_part_init_kernel", "mq_part_count_kernel", "mq_part_scan_kernel", "mq_part_scatter_kernel",
-                 "mq_aes_seal1_kernel", "mq_aes_seal_kernel", "mq_chacha_seal_kernel", "mq_mixed_hp_kernel<false>")}
+# The seal composite of a single-suite, single-key batch is its tile kernel (the "1" variant: key
+# material in SGPRs, n_rows == 1); the tiles apply header protection themselves (ChaCha20 and AES,
+# r03), so no pass follows. seal_ms (HIP events around mq_batch_seal) spans the composite.
+# A mixed batch (config E) or a multi-key AES batch goes through the partition (four launches),
+# then list 0's AES tiles — the hot key's segment on the single-key kernel beside the multi-key
+# kernel — then list 1 (ChaCha20, or the AES hint's leftovers on the multi-key kernel again).
+# mq_host.cpp batch() makes the same launches.
+PARTITION = ("mq_part_init_kernel", "mq_part_count_kernel", "mq_part_scan_kernel", "mq_part_scatter_kernel")
+AES_LIST0 = ("mq_aes_seal1_kernel", "mq_aes_seal_kernel")
 
 
 def seal_kernels(cfg, n_rows):
-    ks = KERNELS.get(cfg)
-    if not ks:
-        return None
+    if cfg == "b":
+        return ("mq_chacha_seal1_kernel",) if n_rows == 1 else ("mq_chacha_seal_kernel",)
+    if cfg == "c":
+        return ("mq_aes_seal1_kernel",) if n_rows == 1 else PARTITION + AES_LIST0 + ("mq_aes_seal_kernel",)
     if cfg == "e":
-        return ks
-    tile = ks[0].replace("_seal_kernel", "_seal1_kernel") if n_rows == 1 else ks[0]
-    return (tile,) + tuple(ks[1:])
+        return PARTITION + AES_LIST0 + ("mq_chacha_seal_kernel",)
+    return None
 
 
 def kernel_key(name):

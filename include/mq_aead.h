@@ -206,6 +206,12 @@ int mq_keytable_device(const mq_keytable* kt);
  * to the caller's stream (one set per device and caller stream, at most 64 sets, least recently
  * used dropped). Call before destroying a stream that such batches used, to free its set now. */
 void mq_stream_release(void* stream);
+/* Diagnostic: device-side phases (ns) of the last per-packet call served by device dev's resident
+ * workgroup — the poll round trip that saw it, request + first 2 KiB loaded, rest loaded, first
+ * half of the work (seal: cipher, open: MAC), second half, written back — then three host-side
+ * ones: request written, waiting for `done` (0 if the call relaunched the server), result copied.
+ * Writes min(n, 9) values and returns that count; 0 before any resident call. */
+int mq_resident_phases(int device, uint32_t* ns, int n);
 const char* mq_status_str(int status);
 
 /* ---- CryptoProvider::aead / Aead (per packet, host buffers; runs the HIP kernels) ----------- */

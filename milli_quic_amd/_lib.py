@@ -83,6 +83,7 @@ SIGNATURES = {
     "mq_device_current": (ctypes.c_int, []),
     "mq_keytable_device": (ctypes.c_int, [_vp]),
     "mq_stream_release": (None, [_vp]),
+    "mq_resident_phases": (ctypes.c_int, [ctypes.c_int, _vp, ctypes.c_int]),
     "mq_status_str": (ctypes.c_char_p, [ctypes.c_int]),
     "mq_aead_new": (ctypes.c_int, [_u32, _vp, _sz, ctypes.POINTER(_vp)]),
     "mq_aead_free": (None, [_vp]),

@@ -173,13 +173,12 @@ struct AesStream {
     return m8;
   }
 
-  // send composite (transmit.rs:625-755): seal, then header protection from the sample
   // send composite (transmit.rs:625-755): seal, then header protection from the sample. For
   // packets of at least 7 CTR blocks (nblk >= 8) the HP block runs in slot nblk — a free slot of
   // the last iteration, after iteration 0 produced the sample — with the HP key through its LDS
-  // pointer; shorter packets get theirs from mq_aes_seal_hp_kernel afterwards (an extra iteration
-  // for them cost more than that pass). key: the AEAD key source (SGPRs in single-key kernels,
-  // LDS otherwise); kl: this packet's LDS key schedules. CACHED: every counter of the wave's
+  // pointer; shorter packets get theirs from one extra AES block of the wave after the tag (r03:
+  // it replaced a post-pass over the whole batch). key: the AEAD key source (SGPRs in single-key
+  // kernels, LDS otherwise); kl: this packet's LDS key schedules. CACHED: every counter of the wave's
   // packets < 256 (aes128_ctr1).
   template <bool CACHED, class K>
   static __device__ __forceinline__ void seal(uint8_t* __restrict__ arena, PktCtx& c, const KeyRow* row, int j, const K& key,
@@ -196,7 +195,7 @@ struct AesStream {
     k.A = (k.aad_len + 15) >> 4;
     k.nblk = 1 + ((k.P + 15) >> 4);
     k.hp = k.act && !(d.flags & MQ_PKT_NO_HP);
-    const bool hp_slot = k.hp && k.nblk >= (uint32_t)kLanesPerPkt;  // else mq_aes_seal_hp_kernel
+    const bool hp_slot = k.hp && k.nblk >= (uint32_t)kLanesPerPkt;  // else after the tag
     const int it_lo = -(int)wave_max_u32(k.act ? (k.A + 6) / 8 : 0u);
     const int it_hi = (int)wave_max_u32(k.act ? k.nblk / 8 + 1 : 0u);
     nonce_be(row, c.pn, k.nb);
@@ -295,6 +294,21 @@ struct AesStream {
     uint32_t tag[4];
     finish(acc, row, j, k, ej0, tag);
     if (k.act && j == 0) st16(arena + k.pay + k.P, tag);
+    // packets of fewer than 7 CTR blocks (no free slot for the HP block; a sample that may reach
+    // into the tag): one more AES block for the wave once ciphertext and tag are stored — length-
+    // sorted batches put such packets in a few tiles of their own
+    const bool late = k.hp && !hp_slot;
+    if (wave_any(late)) {
+      wave_sync();  // this wave's ciphertext and tag stores before its sample loads
+      uint32_t s[4] = {0, 0, 0, 0};
+      if (late) {
+        u4w(ld16(arena + k.pkt + d.pn_offset + 4), s);  // inside the packet (pn_offset + 20 <= len)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s[q] = bswap32(s[q]);
+      }
+      aes128_enc(RkLds{kl + 44}, L, s);
+      if (late && j == 0) { m0 = bswap32(s[0]); m1 = s[1] >> 24; have_mask = true; }
+    }
     if (have_mask) {  // after the MAC read the unprotected header (RFC 9001 §5.4.1)
       uint8_t* h = arena + k.pkt;
       h[0] ^= (uint8_t)m0 & ((d.flags & MQ_PKT_LONG_HEADER) ? 0x0f : 0x1f);
@@ -652,39 +666,6 @@ __global__ __launch_bounds__(256) void mq_aes_open_hp_kernel(
   }
 }
 
-// Seal post-pass: header protection of the sealed packets shorter than 7 CTR blocks (their HP
-// block has no free slot in the tile; transmit.rs:713-719 with AesHeaderProtection::mask,
-// rustcrypto.rs:175-186), one packet per lane: sample = the 16 bytes at pn_offset + 4
-// (ciphertext, reaching into the tag for tiny payloads), mask applied to byte 0 (low 4 / 5 bits)
-// and the PN bytes (RFC 9001 §5.4.1).
-__global__ __launch_bounds__(256) void mq_aes_seal_hp_kernel(
-    const KeyRow* __restrict__ kt, uint8_t* __restrict__ arena, uint64_t arena_len,
-    const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,
-    const uint32_t* __restrict__ n_dev, const uint8_t* __restrict__ status) {
-  const uint32_t count = n_dev ? *n_dev : n;
-  if (blockIdx.x * blockDim.x >= count) return;  // list mode: grids cover the list capacity
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t i = t < count ? (index ? index[t] : t) : kListHole;
-  bool need = i != kListHole && status[i] == MQ_OK;
-  mq_pkt_desc d{};
-  if (need) {
-    d = desc[i];
-    const uint32_t P = d.len - ((uint32_t)d.pn_offset + d.pn_len) - 16, nblk = 1 + ((P + 15) >> 4);
-    need = !(d.flags & MQ_PKT_NO_HP) && nblk < (uint32_t)kLanesPerPkt;  // records are NO_HP
-  }
-  // the S-box table only for blocks with work (1200-B batches have none)
-  if (!__syncthreads_or(need)) return;
-  build_t0(threadIdx.x, blockDim.x);
-  __syncthreads();
-  if (!need) return;
-  uint32_t w[5], m0, m1;
-  uint8_t b0;
-  prepass_header(arena, d, b0, w);  // inside the packet (validated: pn_offset + 20 <= len)
-  const uint32_t smp[4] = {w[1], w[2], w[3], w[4]};
-  aes_hp_mask_words(smp, kt + d.key_id, (uint32_t)(threadIdx.x & (kTReplicas - 1)) * 4, m0, m1);
-  seal_apply_hp(arena, d, b0, w[0], m0, m1);
-}
-
 // Persistent grid: one workgroup per CU (152 KiB of LDS each), capped by the tile count.
 static uint32_t aes_grid(uint32_t tiles, uint32_t waves, int cus) {
   static const int per_cu = [] {  // diagnostic override: workgroups per CU of the grid (0 = one tile per wave)
@@ -733,51 +714,31 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
     hipLaunchKernelGGL(n_rows == 1 ? mq_aes_seal1_kernel : mq_aes_seal_kernel, dim3(blocks), dim3(64 * waves),
                        0, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, hot, status);
   }
-  const hipError_t e = hipGetLastError();
-  if (e != hipSuccess || open || !own_hp) return e;
-  hipLaunchKernelGGL(mq_aes_seal_hp_kernel, dim3((n + 255) / 256), dim3(256), 0, s, kt, arena, arena_len, desc, n,
-                     index, n_dev, status);
   return hipGetLastError();
 }
 
-// Mixed batches: the open pre-pass (OPEN) or the seal HP post-pass over every descriptor of the
-// batch in DESCRIPTOR order, one packet per lane, either suite per lane. (r02 walked the two
-// partition lists: their order scatters the descriptor, status and header reads over the arena,
-// 0.34 / 0.17 GB per 2^20-packet config-E launch where the descriptors alone are 34 MB, r03b PMC.)
-// Seal: the AES packets whose HP had no slot in their tile (fewer than 7 CTR blocks), as
-// mq_aes_seal_hp_kernel does for flat batches; the ChaCha20 tiles mask their packets themselves.
-template <bool OPEN>
+// Mixed batches: the open pre-pass over every descriptor of the batch in DESCRIPTOR order, one
+// packet per lane, either suite per lane. (r02 walked the two partition lists: their order
+// scatters the descriptor and header reads over the arena, 0.34 GB per 2^20-packet config-E
+// launch where the descriptors alone are 34 MB, r03b PMC.) Seal needs no pass: both suites' tiles
+// mask their own packets (r03).
 __global__ __launch_bounds__(256) void mq_mixed_hp_kernel(
-    const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
-    const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint8_t* __restrict__ status, uint2* __restrict__ hpm) {
+    const KeyRow* __restrict__ kt, uint32_t n_rows, const uint8_t* __restrict__ arena, uint64_t arena_len,
+    const mq_pkt_desc* __restrict__ desc, uint32_t n, uint2* __restrict__ hpm) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   bool act = i < n, aes = false;
   mq_pkt_desc d{};
   const KeyRow* row = kt;
-  if (OPEN) {  // prepass_pick's checks; the tile kernels report the rest
-    if (act) {
-      d = desc[i];
-      act = d.key_id < n_rows && d.offset + (uint64_t)d.len <= arena_len && !(d.flags & MQ_PKT_NO_HP) &&
-            (uint64_t)d.pn_offset + 20 <= d.len;
-    }
-    if (act) {
-      row = kt + d.key_id;
-      const uint32_t su = row->suite;
-      aes = su == MQ_SUITE_AES128GCM;
-      act = aes || su == MQ_SUITE_CHACHA20;
-    }
-  } else {
-    act = act && status[i] == MQ_OK;
-    if (act) {
-      d = desc[i];
-      act = !(d.flags & MQ_PKT_NO_HP) && d.key_id < n_rows;
-    }
-    if (act) {
-      row = kt + d.key_id;
-      aes = row->suite == MQ_SUITE_AES128GCM;
-      const uint32_t P = d.len - ((uint32_t)d.pn_offset + d.pn_len) - 16;
-      act = aes && 1 + ((P + 15) >> 4) < (uint32_t)kLanesPerPkt;
-    }
+  if (act) {  // prepass_pick's checks; the tile kernels report the rest
+    d = desc[i];
+    act = d.key_id < n_rows && d.offset + (uint64_t)d.len <= arena_len && !(d.flags & MQ_PKT_NO_HP) &&
+          (uint64_t)d.pn_offset + 20 <= d.len;
+  }
+  if (act) {
+    row = kt + d.key_id;
+    const uint32_t su = row->suite;
+    aes = su == MQ_SUITE_AES128GCM;
+    act = aes || su == MQ_SUITE_CHACHA20;
   }
   if (!__syncthreads_or(act)) return;
   if (__syncthreads_or(act && aes)) {  // the S-box table only where AES lanes have work
@@ -799,20 +760,14 @@ __global__ __launch_bounds__(256) void mq_mixed_hp_kernel(
     m0 = blk[0];
     m1 = blk[1];
   }
-  if (OPEN) hpm[i] = prepass_decode_words(b0, w[0], d, m0, m1);
-  else seal_apply_hp(arena, d, b0, w[0], m0, m1);
+  hpm[i] = prepass_decode_words(b0, w[0], d, m0, m1);
 }
 
-hipError_t mq_launch_mixed_hp(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena, uint64_t arena_len,
-                              const mq_pkt_desc* desc, uint32_t n, const uint8_t* status, uint2* hpm, hipStream_t s) {
+hipError_t mq_launch_mixed_open_hp(const KeyRow* kt, uint32_t n_rows, const uint8_t* arena, uint64_t arena_len,
+                                   const mq_pkt_desc* desc, uint32_t n, uint2* hpm, hipStream_t s) {
   const uint32_t blocks = (n + 255) / 256;
   if (blocks == 0) return hipSuccess;
-  if (open)
-    hipLaunchKernelGGL(mq_mixed_hp_kernel<true>, dim3(blocks), dim3(256), 0, s, kt, n_rows, arena, arena_len, desc, n,
-                       status, hpm);
-  else
-    hipLaunchKernelGGL(mq_mixed_hp_kernel<false>, dim3(blocks), dim3(256), 0, s, kt, n_rows, arena, arena_len, desc,
-                       n, status, hpm);
+  hipLaunchKernelGGL(mq_mixed_hp_kernel, dim3(blocks), dim3(256), 0, s, kt, n_rows, arena, arena_len, desc, n, hpm);
   return hipGetLastError();
 }
 

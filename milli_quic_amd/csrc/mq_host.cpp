@@ -32,8 +32,8 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
                          const uint32_t* index, const uint32_t* n_dev, const uint32_t* hot,
                          uint8_t* status, uint64_t* pn_out, uint2* hpm, bool own_hp, hipStream_t s,
                          hipStream_t hot_stream, int cus);
-hipError_t mq_launch_mixed_hp(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena, uint64_t arena_len,
-                              const mq_pkt_desc* desc, uint32_t n, const uint8_t* status, uint2* hpm, hipStream_t s);
+hipError_t mq_launch_mixed_open_hp(const KeyRow* kt, uint32_t n_rows, const uint8_t* arena, uint64_t arena_len,
+                                   const mq_pkt_desc* desc, uint32_t n, uint2* hpm, hipStream_t s);
 hipError_t mq_launch_aes_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t* key_ids,
                             const uint8_t* samples, uint8_t* masks, uint32_t n, hipStream_t s);
 hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_desc* desc, uint32_t n,
@@ -129,6 +129,7 @@ bool fork_enabled() {
   }();
   return on;
 }
+
 
 // ---------------------------------------------------------------------------------------------
 // AES-128 key expansion / block encryption (FIPS-197), host side: the reference computes the
@@ -446,7 +447,7 @@ int run_one(Scratch& sc, const KeyRow& row, const uint8_t* aad, uint32_t aad_len
 // MQ_RESIDENT=0 or the packet exceeds its buffer; then run_one's batch of one.
 bool resident_enabled(size_t bytes) {
   const char* e = std::getenv("MQ_RESIDENT");  // per call: tests and tools/bench_latency.py switch it
-  return !(e && e[0] == '0') && bytes <= mq::kResMaxPkt;
+  return !(e && e[0] == '0') && bytes + 31 <= mq::kResMaxPkt;  // + the body's alignment pad and the tag
 }
 
 // The resident request image of a context: suite and key material (and for AES-128-GCM the GHASH
@@ -568,7 +569,7 @@ int mq_aead_seal_in_place(const mq_aead_ctx* ctx, const uint8_t* nonce, size_t n
     q.body_len = (uint32_t)payload_len;
     for (int i = 0; i < 3; ++i) q.nonce[i] = le32(nonce + 4 * i);
     int st = MQ_ERR_HIP;
-    const int rc = mq_resident_call(ctx->sc.device, q, aad, buf, buf, aad_len, total, &st, nullptr);
+    const int rc = mq_resident_call(ctx->sc.device, q, aad, buf, buf, 0, total, &st, nullptr);
     if (rc) return rc;
     if (st) return st;
     if (out_len) *out_len = total;
@@ -601,7 +602,7 @@ int mq_aead_open_in_place(const mq_aead_ctx* ctx, const uint8_t* nonce, size_t n
     q.body_len = (uint32_t)ct_len;
     for (int i = 0; i < 3; ++i) q.nonce[i] = le32(nonce + 4 * i);
     int st = MQ_ERR_HIP;
-    const int rc = mq_resident_call(ctx->sc.device, q, aad, buf, buf, aad_len, ct_len - 16, &st, nullptr);
+    const int rc = mq_resident_call(ctx->sc.device, q, aad, buf, buf, 0, ct_len - 16, &st, nullptr);
     if (rc) return rc;
     if (st) return st;  // buffer untouched on failure
     if (out_len) *out_len = ct_len - 16;
@@ -838,10 +839,11 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
     // list mode: the grids cover the list capacity; the kernels read the real lengths from counts
     const uint32_t cap = mq_partition_list_cap(n);
     e = mq_launch_partition(kt->dev, kt->rows, desc, n, list, hist, counts, s);
-    // one header-protection pass covers both lists, before the tiles for open and after every
-    // tile kernel for seal (the AES tiles mask their long packets themselves)
-    if (e == hipSuccess && open && hpm)
-      e = mq_launch_mixed_hp(true, kt->dev, kt->rows, arena, arena_len, desc, n, status, hpm, s);
+    // open: one header-protection pre-pass over the whole batch in descriptor order, both suites,
+    // before the tiles (seal needs none: the tiles mask their own packets). r03f ran it on a side
+    // stream beside the partition: no gain (E open 1.279 -> 1.280 ms), its blocks delayed the
+    // partition's single-workgroup scan (27 -> 85 us)
+    if (e == hipSuccess && open && hpm) e = mq_launch_mixed_open_hp(kt->dev, kt->rows, arena, arena_len, desc, n, hpm, s);
     if (e != hipSuccess) return MQ_ERR_HIP;
     // The hot AES key's segment (counts + 2: its row and segment length, list 0's front;
     // single-key kernel) runs on a side stream beside the other AES keys' tiles on s: each CU moves
@@ -862,8 +864,6 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
                            pn_out, hpm, false, s_list1);
     // join even after a failed launch, so no side stream runs ahead of s
     if (!fork.join() && e == hipSuccess) e = hipErrorUnknown;
-    if (e == hipSuccess && !open)
-      e = mq_launch_mixed_hp(false, kt->dev, kt->rows, arena, arena_len, desc, n, status, nullptr, s);
   } else {
     return MQ_ERR_INVALID_ARG;
   }

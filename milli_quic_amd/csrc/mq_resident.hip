@@ -46,11 +46,17 @@ __device__ __forceinline__ void st_sys_sc(uint32_t* p, uint32_t v) {
 }
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
-// LDS of the resident wave: the request, the packet, scratch
+// The resident workgroup: kResWaves waves, one per SIMD. Wave 0 polls; the others wait at the
+// workgroup barrier (no issue slots) and join for the copies and the keystream.
+constexpr int kResWaves = 4, kResThreads = 64 * kResWaves;
+
+// LDS: the request, the packet, the open keystream, scratch
 constexpr uint32_t kResReqWords = sizeof(ResReq) / 4;
 __shared__ __attribute__((aligned(16))) uint32_t s_req[kResReqWords];
 __shared__ __attribute__((aligned(16))) uint8_t s_pkt[kResMaxPkt + 64];
-__shared__ __attribute__((aligned(16))) uint32_t s_scr[16];  // one-time key / E_K(J0)
+__shared__ __attribute__((aligned(16))) uint32_t s_ks[kResMaxPkt / 4];  // open: keystream until the tag verifies
+__shared__ __attribute__((aligned(16))) uint32_t s_scr[16];  // one-time key / E_K(J0); [12]: verdict
+__shared__ uint32_t s_cmd[2];                                // wave 0 -> all: leave?, seq
 #define REQ (*(const ResReq*)s_req)
 
 // 64-bit lane sums of Poly1305 limbs -> the accumulator mod 2^130 - 5 in 26-bit limbs
@@ -71,32 +77,94 @@ __device__ __forceinline__ P26 p26_from_sums(const uint64_t (&s)[5]) {
   return h;
 }
 
-// Poly1305 of AAD||pad||C||pad||lens over the LDS packet (aad at 0, ciphertext at pay), 64 lanes
-__device__ void res_poly(uint32_t aad_len, uint32_t pay, uint32_t ct_len, const uint32_t* otk, int lane,
-                         uint32_t (&tag)[4]) {
-  const LdsSpace sp{s_pkt};
-  const P26 r = p26_from_words(otk[0] & 0x0fffffffu, otk[1] & 0x0ffffffcu, otk[2] & 0x0ffffffcu,
-                               otk[3] & 0x0ffffffcu, 0);
-  // powers by a prefix product over the lanes: after step s lane j holds r^(min(j, 2^(s+1) - 1) + 1)
-  // (6 multiplies, not 6 squarings + 6 conditional multiplies); r^64 = lane 63's r^64
-  P26 v = r;
-#pragma unroll 1
-  for (int s = 0; s < 6; ++s) {
-    P26 u;
+// 64-bit sum / 32-bit XOR over the 64 lanes of a wave by DPP (quad_perm, half- and row-mirror
+// within each row of 16, then the four row results by readlane): ALU latency per step, where a
+// __shfl_xor ladder waits on LDS six times
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp64(uint64_t x) {
+  return ((uint64_t)dpp32<CTRL>((uint32_t)(x >> 32)) << 32) | dpp32<CTRL>((uint32_t)x);
+}
+__device__ __forceinline__ uint64_t rdl64(uint64_t x, int l) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(x >> 32), l) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)x, l);
+}
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t x) {
+  x += dpp64<0xB1>(x);   // quad_perm [1,0,3,2]
+  x += dpp64<0x4E>(x);   // quad_perm [2,3,0,1]
+  x += dpp64<0x141>(x);  // row_half_mirror
+  x += dpp64<0x140>(x);  // row_mirror: every lane holds its row's sum
+  return rdl64(x, 0) + rdl64(x, 16) + rdl64(x, 32) + rdl64(x, 48);
+}
+__device__ __forceinline__ uint32_t wave_xor_u32(uint32_t x) {
+  x ^= dpp32<0xB1>(x);
+  x ^= dpp32<0x4E>(x);
+  x ^= dpp32<0x141>(x);
+  x ^= dpp32<0x140>(x);
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, 0) ^ (uint32_t)__builtin_amdgcn_readlane((int)x, 16) ^
+         (uint32_t)__builtin_amdgcn_readlane((int)x, 32) ^ (uint32_t)__builtin_amdgcn_readlane((int)x, 48);
+}
+
+// h = h * m mod 2^130 - 5 for ONE wave's latency: the five column sums are independent chains
+// of v_mad_u64_u32 and the carries follow, where p26_mul (the tile kernels' throughput form)
+// starts each column from the previous column's carry — a 25-multiply dependent chain. Same
+// bounds (column sums < 2^58).
+__device__ __forceinline__ void p26_mul_lat(P26& h, const P26m& m) {
+  const uint64_t h0 = h.l[0], h1 = h.l[1], h2 = h.l[2], h3 = h.l[3], h4 = h.l[4];
+  const uint64_t c0 = h0 * m.r[0] + h1 * m.s[3] + h2 * m.s[2] + h3 * m.s[1] + h4 * m.s[0];
+  const uint64_t c1 = h0 * m.r[1] + h1 * m.r[0] + h2 * m.s[3] + h3 * m.s[2] + h4 * m.s[1];
+  const uint64_t c2 = h0 * m.r[2] + h1 * m.r[1] + h2 * m.r[0] + h3 * m.s[3] + h4 * m.s[2];
+  const uint64_t c3 = h0 * m.r[3] + h1 * m.r[2] + h2 * m.r[1] + h3 * m.r[0] + h4 * m.s[3];
+  const uint64_t c4 = h0 * m.r[4] + h1 * m.r[3] + h2 * m.r[2] + h3 * m.r[1] + h4 * m.r[0];
+  const uint64_t d1 = c1 + (c0 >> 26), d2 = c2 + (d1 >> 26), d3 = c3 + (d2 >> 26), d4 = c4 + (d3 >> 26);
+  const uint32_t k4 = (uint32_t)(d4 >> 26);
+  const uint64_t t = (uint64_t)((uint32_t)c0 & 0x3ffffff) + (uint64_t)k4 * 5u;
+  h.l[0] = (uint32_t)t & 0x3ffffff;
+  h.l[1] = ((uint32_t)d1 & 0x3ffffff) + (uint32_t)(t >> 26);
+  h.l[2] = (uint32_t)d2 & 0x3ffffff;
+  h.l[3] = (uint32_t)d3 & 0x3ffffff;
+  h.l[4] = (uint32_t)d4 & 0x3ffffff;
+}
+
+// Poly1305 as a 64-way interleaved Horner on ONE wave (wave 0): the powers first (they need only
+// the one-time key, so they run while the other waves make the keystream), then the blocks.
+// Lane j takes the blocks whose last multiplier is r^(j + 1) (blocks 64k + 63 - j - z), so the
+// powers are the inclusive prefix product of r over the lanes: row_shr 1, 2, 4, 8 inside each
+// row of 16, then row_bcast15 / row_bcast31 across rows (DPP; lanes without a source multiply by
+// one), six multiplies with no LDS round trip.
+struct PolyPow { P26m m64, mj; };  // multiplier between rounds (r^64), lane j's last (r^(j + 1))
+template <int CTRL, int ROWS>
+__device__ __forceinline__ P26 p26_dpp(const P26& v) {
+  P26 u;
 #pragma unroll
-    for (int l = 0; l < 5; ++l) u.l[l] = (uint32_t)__shfl((int)v.l[l], max(lane - (1 << s), 0), 64);
-    P26 t = v;
-    p26_mul(t, p26_mult(u));
-    if (lane >= (1 << s)) v = t;
-  }
+  for (int l = 0; l < 5; ++l)
+    u.l[l] = (uint32_t)__builtin_amdgcn_update_dpp(l == 0 ? 1 : 0, (int)v.l[l], CTRL, ROWS, 0xf, false);
+  return u;
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void p26_scan_step(P26& v) {
+  p26_mul_lat(v, p26_mult(p26_dpp<CTRL, ROWS>(v)));
+}
+__device__ __forceinline__ PolyPow poly_powers(const uint32_t (&otk)[8]) {
+  P26 v = p26_from_words(otk[0] & 0x0fffffffu, otk[1] & 0x0ffffffcu, otk[2] & 0x0ffffffcu, otk[3] & 0x0ffffffcu, 0);
+  p26_scan_step<0x111, 0xf>(v);  // row_shr:1
+  p26_scan_step<0x112, 0xf>(v);  // row_shr:2
+  p26_scan_step<0x114, 0xf>(v);  // row_shr:4
+  p26_scan_step<0x118, 0xf>(v);  // row_shr:8 -> r^(j % 16 + 1)
+  p26_scan_step<0x142, 0xa>(v);  // row_bcast:15 into rows 1, 3
+  p26_scan_step<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3 -> r^(j + 1)
   P26 e;
 #pragma unroll
   for (int l = 0; l < 5; ++l) e.l[l] = (uint32_t)__builtin_amdgcn_readlane((int)v.l[l], 63);
-  const P26m m64 = p26_mult(e);
-  P26 last;
-#pragma unroll
-  for (int l = 0; l < 5; ++l) last.l[l] = (uint32_t)__shfl((int)v.l[l], 63 - lane, 64);  // r^(64 - lane)
-  const P26m ml = p26_mult(last);
+  return PolyPow{p26_mult(e), p26_mult(v)};
+}
+// the tag of AAD||pad||C||pad||lens over the LDS packet (aad at 0, ciphertext at the aligned pay)
+__device__ __forceinline__ void poly_tag(uint32_t aad_len, uint32_t pay, uint32_t ct_len, const PolyPow& pw,
+                                         const uint32_t (&otk)[8], int lane, uint32_t (&tag)[4]) {
+  const LdsSpace sp{s_pkt};
   const uint32_t A = (aad_len + 15) >> 4, T = (ct_len + 15) >> 4, nb = A + T + 1;
   const uint32_t K = (nb + 63) / 64;
   const int z = (int)(64 * K) - (int)nb;
@@ -105,7 +173,7 @@ __device__ void res_poly(uint32_t aad_len, uint32_t pay, uint32_t ct_len, const 
   for (int l = 0; l < 5; ++l) acc.l[l] = 0;
 #pragma unroll 1
   for (uint32_t k = 0; k < K; ++k) {
-    const int i = (int)(64 * k) + lane - z;
+    const int i = (int)(64 * k) + 63 - lane - z;
     uint32_t m[4] = {0, 0, 0, 0};
     uint32_t hib = 1;
     if (i < 0) {
@@ -127,182 +195,204 @@ __device__ void res_poly(uint32_t aad_len, uint32_t pay, uint32_t ct_len, const 
     const P26 x = p26_from_words(m[0], m[1], m[2], m[3], hib);
 #pragma unroll
     for (int l = 0; l < 5; ++l) acc.l[l] += x.l[l];
-    p26_mul(acc, k + 1 < K ? m64 : ml);
+    p26_mul_lat(acc, k + 1 < K ? pw.m64 : pw.mj);
   }
   uint64_t s[5];
 #pragma unroll
-  for (int l = 0; l < 5; ++l) {
-    uint64_t x = acc.l[l];
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
-    s[l] = x;
-  }
+  for (int l = 0; l < 5; ++l) s[l] = wave_sum_u64(acc.l[l]);
   const uint32_t sk[4] = {otk[4], otk[5], otk[6], otk[7]};
   p26_finish(p26_from_sums(s), sk, tag);
 }
 
-// ChaCha20-Poly1305 seal / open of the LDS packet (aad at 0, body at aad_len); returns MQ_*
-__device__ int res_chacha(bool open, uint32_t aad_len, uint32_t body_len, int lane) {
-  const LdsSpace sp{s_pkt};
+// ChaCha20 block on a quad of lanes (RFC 8439 §2.3): lane q of the quad holds column q of the
+// state (words q, 4 + q, 8 + q, 12 + q), so a column round is one quarter-round per lane and a
+// diagonal round one quarter-round after rotating rows 1..3 by 1..3 lanes (quad_perm DPP) — a
+// quarter of the dependent chain of a block on one lane. ks[k] = keystream word 4k + q.
+__device__ __forceinline__ void chacha20_block4(const uint32_t (&key)[8], uint32_t ctr, uint32_t n0, uint32_t n1,
+                                                uint32_t n2, int q, uint32_t (&ks)[4]) {
+  const uint32_t c0 = q == 0 ? 0x61707865u : q == 1 ? 0x3320646eu : q == 2 ? 0x79622d32u : 0x6b206574u;
+  const uint32_t k0 = q == 0 ? key[0] : q == 1 ? key[1] : q == 2 ? key[2] : key[3];
+  const uint32_t k1 = q == 0 ? key[4] : q == 1 ? key[5] : q == 2 ? key[6] : key[7];
+  const uint32_t d0 = q == 0 ? ctr : q == 1 ? n0 : q == 2 ? n1 : n2;
+  uint32_t a = c0, b = k0, c = k1, d = d0;
+#pragma unroll 2
+  for (int i = 0; i < 10; ++i) {
+    MQ_QR(a, b, c, d)
+    // diagonals: lane q takes b of lane q+1, c of q+2, d of q+3 (quad_perm [1,2,3,0], [2,3,0,1], [3,0,1,2])
+    b = dpp32<0x39>(b); c = dpp32<0x4E>(c); d = dpp32<0x93>(d);
+    MQ_QR(a, b, c, d)
+    b = dpp32<0x93>(b); c = dpp32<0x4E>(c); d = dpp32<0x39>(d);
+  }
+  ks[0] = a + c0; ks[1] = b + k0; ks[2] = c + k1; ks[3] = d + d0;
+}
+
+// ChaCha20-Poly1305 seal / open of the LDS packet (aad at 0, body at the aligned pay). Wave 0
+// makes the Poly1305 key (block 0, on its quads) and the MAC's powers of r while waves 1..3 make
+// keystream blocks 1.. (one per quad, 48 per pass); then wave 0 runs the MAC. Seal XORs the
+// keystream in place before the MAC; open keeps it in s_ks, verifies, and applies it only if the
+// tag matched. Returns MQ_* (workgroup-uniform).
+__device__ int res_chacha(bool open, uint32_t aad_len, uint32_t pay, uint32_t body_len, int tid, uint64_t& t_mid) {
   uint32_t key[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) key[k] = REQ.key[k];
   const uint32_t n0 = REQ.nonce[0], n1 = REQ.nonce[1], n2 = REQ.nonce[2];
-  const uint32_t P = open ? body_len - 16 : body_len, pay = aad_len;
-  const uint32_t nblk = 1 + (P + 63) / 64;  // block 0: the Poly1305 key
-  auto xor_blocks = [&](bool with_otk) {
-#pragma unroll 1
-    for (uint32_t b0 = 0; b0 < nblk; b0 += 64) {
-      const uint32_t b = b0 + (uint32_t)lane;
-      uint32_t raw[17];
-      load_raw<16>(sp, b >= 1 && b < nblk ? pay + 64 * (b - 1) : 0u, raw);
-      uint32_t ks[16];
-      chacha20_block(key, b, n0, n1, n2, ks);
-      if (b == 0 && with_otk) {
+  const uint32_t P = open ? body_len - 16 : body_len;
+  const uint32_t nblk = 1 + (P + 63) / 64;
+  const int q = tid & 3;
+  uint32_t* pw = (uint32_t*)(s_pkt + pay);
+  uint32_t otk[8];
+  PolyPow pp;
+  if (tid < 64) {
+    uint32_t ks[4];
+    chacha20_block4(key, 0, n0, n1, n2, q, ks);
+    if (tid < 4) { s_scr[q] = ks[0]; s_scr[4 + q] = ks[1]; }
+    wave_sync();
 #pragma unroll
-        for (int q = 0; q < 8; ++q) s_scr[q] = ks[q];
-      } else if (b >= 1 && b < nblk) {
-        xor_words<16>(sp, pay + 64 * (b - 1), ks, (int)min(64u, P - 64 * (b - 1)), raw);
+    for (int k = 0; k < 8; ++k) otk[k] = s_scr[k];
+    pp = poly_powers(otk);
+    if (open) {  // the ciphertext is in place: the MAC need not wait for the keystream
+      uint32_t tag[4], got[4];
+      poly_tag(aad_len, pay, P, pp, otk, tid, tag);
+      load_words<4>(LdsSpace{s_pkt}, pay + P, got);
+      if (tid == 0) s_scr[12] = (tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) | (tag[3] ^ got[3]);
+    }
+  } else {
+    constexpr uint32_t kQuads = (kResThreads - 64) / 4;
+#pragma unroll 1
+    for (uint32_t b0 = 1; b0 < nblk; b0 += kQuads) {
+      const uint32_t b = b0 + (uint32_t)((tid - 64) >> 2);
+      uint32_t ks[4];
+      chacha20_block4(key, b, n0, n1, n2, q, ks);
+      if (b < nblk) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t o = 64 * (b - 1) + 16 * k + 4 * q;  // payload byte offset of word 4k + q
+          if (o < P) {
+            if (open) s_ks[o / 4] = ks[k];
+            else pw[o / 4] ^= ks[k] & byte_mask((int)(P - o), 0);
+          }
+        }
       }
     }
-    wave_sync();
-  };
-  uint32_t tag[4];
+  }
+  __syncthreads();
+  t_mid = wall_clock64();
   if (!open) {
-    xor_blocks(true);
-    uint32_t otk[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) otk[q] = s_scr[q];
-    res_poly(aad_len, pay, P, otk, lane, tag);
-    if (lane == 0) store_words<4>(sp, pay + P, tag);
-    wave_sync();
+    if (tid < 64) {  // the write-back that follows is wave 0's too: no barrier after the tag
+      uint32_t tag[4];
+      poly_tag(aad_len, pay, P, pp, otk, tid, tag);
+      if (tid == 0) store_words<4>(LdsSpace{s_pkt}, pay + P, tag);
+    }
     return MQ_OK;
   }
-  if (lane == 0) {  // the one-time key only: the MAC reads the untouched ciphertext
-    uint32_t ks[16];
-    chacha20_block(key, 0, n0, n1, n2, ks);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) s_scr[q] = ks[q];
-  }
-  wave_sync();
-  uint32_t otk[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) otk[q] = s_scr[q];
-  res_poly(aad_len, pay, P, otk, lane, tag);
-  uint32_t got[4];
-  load_words<4>(sp, pay + P, got);
-  const uint32_t diff = uni((tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) | (tag[3] ^ got[3]));
-  if (diff) return MQ_ERR_CRYPTO;  // rustcrypto.rs:156-163; nothing decrypted
-  wave_sync();
-  xor_blocks(false);
+  if (s_scr[12]) return MQ_ERR_CRYPTO;  // rustcrypto.rs:156-163; nothing decrypted
+  for (uint32_t w = (uint32_t)tid; 4 * w < P; w += kResThreads) pw[w] ^= s_ks[w] & byte_mask((int)(P - 4 * w), 0);
+  __syncthreads();
   return MQ_OK;
 }
 
-// AES-128-GCM seal / open of the LDS packet
-__device__ int res_aes(bool open, uint32_t aad_len, uint32_t body_len, int lane) {
+// GHASH(AAD || C || lens) on ONE wave (lane j: blocks 64k + j - z, multiplier H^64, final
+// H^(64 - j), lanes XOR-reduced), reflected basis (mq_aes.h); tag = that ^ E_K(J0)
+__device__ __forceinline__ void ghash_tag(uint32_t aad_len, uint32_t pay, uint32_t P, const GfOp& m64,
+                                          const GfOp& ml, const uint32_t (&ej0)[4], int lane, uint32_t (&tag)[4]) {
   const LdsSpace sp{s_pkt};
+  const uint32_t A = (aad_len + 15) >> 4, T = (P + 15) >> 4, nb = A + T + 1;
+  const uint32_t K = (nb + 63) / 64;
+  const int z = (int)(64 * K) - (int)nb;
+  uint32_t acc[4] = {0, 0, 0, 0};
+#pragma unroll 1
+  for (uint32_t k = 0; k < K; ++k) {
+    const int i = (int)(64 * k) + lane - z;
+    uint32_t m[4] = {0, 0, 0, 0};
+    if (i >= 0 && i < (int)A) {
+      load_words<4>(sp, 16u * (uint32_t)i, m);
+      const int rem = (int)aad_len - 16 * i;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) m[w] = refl(m[w] & byte_mask(rem, w));
+    } else if (i >= (int)A && i < (int)(A + T)) {
+      const uint32_t o = 16u * (uint32_t)(i - (int)A);
+      load_words<4>(sp, pay + o, m);
+      const int rem = (int)(P - o);
+#pragma unroll
+      for (int w = 0; w < 4; ++w) m[w] = refl(m[w] & byte_mask(rem, w));
+    } else if (i == (int)(A + T)) {
+      const uint64_t ab = (uint64_t)aad_len * 8, cb = (uint64_t)P * 8;
+      m[0] = brev((uint32_t)(ab >> 32)); m[1] = brev((uint32_t)ab);
+      m[2] = brev((uint32_t)(cb >> 32)); m[3] = brev((uint32_t)cb);
+    }
+#pragma unroll
+    for (int w = 0; w < 4; ++w) acc[w] ^= m[w];
+    gf_mul(acc, k + 1 < K ? m64 : ml);
+  }
+#pragma unroll
+  for (int w = 0; w < 4; ++w) tag[w] = bswap32(brev(wave_xor_u32(acc[w]))) ^ ej0[w];
+}
+
+// AES-128-GCM seal / open of the LDS packet: wave 0 makes E_K(J0) and the GHASH multipliers
+// (H^64, and H^(64 - lane) from the request's powers) while waves 1..3 run the CTR blocks (one per
+// thread, 192 per pass); then wave 0 runs GHASH. Open verifies before it decrypts.
+__device__ int res_aes(bool open, uint32_t aad_len, uint32_t pay, uint32_t body_len, int tid, uint64_t& t_mid) {
   const TwLane L = tw_lane();
   const RkLds key{REQ.aes_rk};
   const uint32_t nb0 = bswap32(REQ.nonce[0]), nb1 = bswap32(REQ.nonce[1]), nb2 = bswap32(REQ.nonce[2]);
-  const uint32_t P = open ? body_len - 16 : body_len, pay = aad_len;
+  const uint32_t P = open ? body_len - 16 : body_len;
   const uint32_t nblk = 1 + (P + 15) / 16;  // slot 0: E_K(J0), slot b >= 1: CTR block with counter b + 1
-  auto ctr_pass = [&](bool with_j0) {
-#pragma unroll 1
-    for (uint32_t b0 = 0; b0 < nblk; b0 += 64) {
-      const uint32_t b = b0 + (uint32_t)lane;
-      uint32_t s[4] = {nb0, nb1, nb2, b == 0 ? 1u : b + 1};
-      aes128_enc(key, L, s);
-      uint32_t ks[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) ks[q] = bswap32(s[q]);
-      if (b == 0 && with_j0) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) s_scr[8 + q] = ks[q];
-      } else if (b >= 1 && b < nblk) {
-        uint32_t raw[5];
-        const uint32_t o = pay + 16 * (b - 1);
-        load_raw<4>(sp, o, raw);
-        xor_words<4>(sp, o, ks, (int)min(16u, P - 16 * (b - 1)), raw);
-      }
-    }
-    wave_sync();
-  };
-  // GHASH(AAD || C || lens) in the reflected basis (mq_aes.h), lane j: blocks 64k + j - z
-  auto ghash = [&](uint32_t (&g)[4]) {
-    const uint32_t A = (aad_len + 15) >> 4, T = (P + 15) >> 4, nb = A + T + 1;
-    const uint32_t K = (nb + 63) / 64;
-    const int z = (int)(64 * K) - (int)nb;
-    uint32_t h[4];
-#pragma unroll
-    for (int w = 0; w < 4; ++w) h[w] = brev(REQ.Hpow[63][w]);
-    const GfOp m64 = gf_prepare(h);
-    uint32_t acc[4] = {0, 0, 0, 0};
-#pragma unroll 1
-    for (uint32_t k = 0; k < K; ++k) {
-      const int i = (int)(64 * k) + lane - z;
-      uint32_t m[4] = {0, 0, 0, 0};
-      if (i >= 0 && i < (int)A) {
-        load_words<4>(sp, 16u * (uint32_t)i, m);
-        const int rem = (int)aad_len - 16 * i;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) m[w] = refl(m[w] & byte_mask(rem, w));
-      } else if (i >= (int)A && i < (int)(A + T)) {
-        const uint32_t o = 16u * (uint32_t)(i - (int)A);
-        load_words<4>(sp, pay + o, m);
-        const int rem = (int)(P - o);
-#pragma unroll
-        for (int w = 0; w < 4; ++w) m[w] = refl(m[w] & byte_mask(rem, w));
-      } else if (i == (int)(A + T)) {
-        const uint64_t ab = (uint64_t)aad_len * 8, cb = (uint64_t)P * 8;
-        m[0] = brev((uint32_t)(ab >> 32)); m[1] = brev((uint32_t)ab);
-        m[2] = brev((uint32_t)(cb >> 32)); m[3] = brev((uint32_t)cb);
-      }
-#pragma unroll
-      for (int w = 0; w < 4; ++w) acc[w] ^= m[w];
-      if (k + 1 < K) gf_mul(acc, m64);
-    }
-    uint32_t hl[4];  // H^(64 - lane)
-#pragma unroll
-    for (int w = 0; w < 4; ++w) hl[w] = brev(REQ.Hpow[63 - lane][w]);
-    gf_mul(acc, gf_prepare(hl));
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      uint32_t x = acc[w];
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) x ^= (uint32_t)__shfl_xor((int)x, d, 64);
-      g[w] = x;
-    }
-  };
-  uint32_t g[4], tag[4];
-  if (!open) {
-    ctr_pass(true);
-    ghash(g);
-#pragma unroll
-    for (int w = 0; w < 4; ++w) tag[w] = bswap32(brev(g[w])) ^ s_scr[8 + w];
-    if (lane == 0) store_words<4>(sp, pay + P, tag);
-    wave_sync();
-    return MQ_OK;
-  }
-  if (lane == 0) {  // E_K(J0) only: GHASH reads the untouched ciphertext
+  uint32_t* pw = (uint32_t*)(s_pkt + pay);
+  GfOp m64, ml;
+  uint32_t ej0[4];
+  if (tid < 64) {
     uint32_t s[4] = {nb0, nb1, nb2, 1u};
     aes128_enc(key, L, s);
+    uint32_t h[4], hl[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) s_scr[8 + q] = bswap32(s[q]);
+    for (int w = 0; w < 4; ++w) {
+      ej0[w] = bswap32(s[w]);
+      h[w] = brev(REQ.Hpow[63][w]);
+      hl[w] = brev(REQ.Hpow[63 - tid][w]);
+    }
+    m64 = gf_prepare(h);
+    ml = gf_prepare(hl);
+    if (open) {  // the ciphertext is in place: GHASH need not wait for the keystream
+      uint32_t tag[4], got[4];
+      ghash_tag(aad_len, pay, P, m64, ml, ej0, tid, tag);
+      load_words<4>(LdsSpace{s_pkt}, pay + P, got);
+      if (tid == 0) s_scr[12] = (tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) | (tag[3] ^ got[3]);
+    }
+  } else {
+#pragma unroll 1
+    for (uint32_t b0 = 1; b0 < nblk; b0 += kResThreads - 64) {
+      const uint32_t b = b0 + (uint32_t)(tid - 64);
+      uint32_t s[4] = {nb0, nb1, nb2, b + 1};
+      aes128_enc(key, L, s);
+      if (b < nblk) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t o = 16 * (b - 1) + 4 * k;
+          if (o < P) {
+            if (open) s_ks[o / 4] = bswap32(s[k]);
+            else pw[o / 4] ^= bswap32(s[k]) & byte_mask((int)(P - o), 0);
+          }
+        }
+      }
+    }
   }
-  wave_sync();
-  ghash(g);
-  uint32_t got[4];
-  load_words<4>(sp, pay + P, got);
-  uint32_t diff = 0;
-#pragma unroll
-  for (int w = 0; w < 4; ++w) diff |= (bswap32(brev(g[w])) ^ s_scr[8 + w]) ^ got[w];
-  if (uni(diff)) return MQ_ERR_CRYPTO;  // rustcrypto.rs:85-91; nothing decrypted
-  wave_sync();
-  ctr_pass(false);
+  __syncthreads();
+  t_mid = wall_clock64();
+  if (!open) {
+    if (tid < 64) {  // the write-back that follows is wave 0's too: no barrier after the tag
+      uint32_t tag[4];
+      ghash_tag(aad_len, pay, P, m64, ml, ej0, tid, tag);
+      if (tid == 0) store_words<4>(LdsSpace{s_pkt}, pay + P, tag);
+    }
+    return MQ_OK;
+  }
+  if (s_scr[12]) return MQ_ERR_CRYPTO;  // rustcrypto.rs:85-91; nothing decrypted
+  for (uint32_t w = (uint32_t)tid; 4 * w < P; w += kResThreads) pw[w] ^= s_ks[w] & byte_mask((int)(P - 4 * w), 0);
+  __syncthreads();
   return MQ_OK;
 }
 
-__device__ void res_hp(uint32_t suite, int lane, uint32_t& m0, uint32_t& m1) {
+__device__ void res_hp(uint32_t suite, uint32_t& m0, uint32_t& m1) {
   const uint32_t smp[4] = {REQ.sample[0], REQ.sample[1], REQ.sample[2], REQ.sample[3]};
   if (suite == MQ_SUITE_CHACHA20) {  // rustcrypto.rs:197-220
     uint32_t hk[8], blk[16];
@@ -317,103 +407,157 @@ __device__ void res_hp(uint32_t suite, int lane, uint32_t& m0, uint32_t& m1) {
     m0 = bswap32(s[0]);
     m1 = s[1] >> 24;
   }
-  (void)lane;
 }
 
 }  // namespace mq
 
 using namespace mq;
 
-extern "C" __global__ __launch_bounds__(64) void mq_resident_kernel(ResArea* area, uint64_t idle_ticks,
-                                                                    uint64_t life_ticks) {
-  const int lane = (int)threadIdx.x;
+extern "C" __global__ __launch_bounds__(kResThreads) void mq_resident_kernel(ResArea* area, uint64_t idle_ticks,
+                                                                             uint64_t life_ticks) {
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const bool w0 = tid < 64;
   ResCtl* ctl = &area->ctl;
-  build_tw(lane, 64);  // the wide AES T-table, once per kernel
-  wave_sync();
+  build_tw(tid, kResThreads);  // the wide AES T-table, once per kernel
+  __syncthreads();
   uint32_t done = uni(ld_sys(&ctl->done));
   const uint64_t t0 = wall_clock64();
-  uint64_t t_last = t0;
+  uint64_t t_last = t0, tp = t0, t_seen = t0;
   for (;;) {
-    // seq and stop in one 8-B system-scope load: one PCIe round trip per poll
-    const uint64_t ss = __hip_atomic_load((const uint64_t*)&ctl->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    const uint32_t seq = uni((uint32_t)ss);
-    if (uni((uint32_t)(ss >> 32))) break;
-    if (seq == done) {
-      const uint64_t now = wall_clock64();
-      if (now - t_last > idle_ticks || now - t0 > life_ticks) {
-        // claim the exit, then look once more: a request posted meanwhile is served first
-        if (lane == 0) st_sys_sc(&ctl->state, kResExiting);
-        wave_sync();
-        if (uni(ld_sys_sc(&ctl->seq)) == done) break;
-        if (lane == 0) st_sys_sc(&ctl->state, kResRunning);
-        t_last = now;
-        continue;
+    if (w0) {  // wave 0 polls; waves 1..3 wait at the barrier below
+      // seq and stop in one 8-B system-scope load, kResPolls of them in flight (a new one issued
+      // as the oldest returns, so a request is seen about one PCIe round trip after the host
+      // posts it, not up to two). Reads may be served out of order, so a poll can return an older
+      // seq than the last one: a request is new iff seq - done > 0 (wrapping).
+      auto poll = [&]() {
+        return __hip_atomic_load((const uint64_t*)&ctl->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      };
+      uint32_t leave = 0, seq = done;
+      bool got = false;
+      // 0: keep polling; 1: serve seq / leave (see `leave`)
+      auto check = [&](uint64_t ss) -> bool {
+        seq = uni((uint32_t)ss);
+        t_seen = wall_clock64();
+        if (uni((uint32_t)(ss >> 32))) { leave = 1; return true; }
+        if ((int32_t)(seq - done) > 0) return true;
+        const uint64_t now = wall_clock64();
+        if (now - t_last > idle_ticks || now - t0 > life_ticks) {
+          // claim the exit, then look once more: a request posted meanwhile is served first
+          if (lane == 0) st_sys_sc(&ctl->state, kResExiting);
+          wave_sync();
+          seq = uni(ld_sys_sc(&ctl->seq));
+          if ((int32_t)(seq - done) <= 0) { leave = 1; return true; }
+          if (lane == 0) st_sys_sc(&ctl->state, kResRunning);
+          t_last = now;
+          return true;
+        }
+        return false;
+      };
+      tp = wall_clock64();
+      uint64_t pa = poll();
+      __builtin_amdgcn_s_sleep(8);
+      uint64_t pb = poll();
+      __builtin_amdgcn_s_sleep(8);
+      uint64_t pc = poll();
+      __builtin_amdgcn_s_sleep(8);
+      uint64_t pd = poll();
+      while (!got) {  // unrolled by the number of polls in flight: each keeps its register
+        if ((got = check(pa))) break;
+        tp = wall_clock64(); pa = poll();
+        if ((got = check(pb))) break;
+        tp = wall_clock64(); pb = poll();
+        if ((got = check(pc))) break;
+        tp = wall_clock64(); pc = poll();
+        if ((got = check(pd))) break;
+        tp = wall_clock64(); pd = poll();
       }
-      __builtin_amdgcn_s_sleep(1);  // the poll itself is a PCIe round trip (~1 us)
-      continue;
+      if (lane == 0) { s_cmd[0] = leave; s_cmd[1] = seq; }
+      // system scope, once for the workgroup (the barrier below orders the other waves' loads
+      // after it): the request written before seq
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the request written before seq
-    // One round trip: the request (two 16-B loads per lane) and the packet's first 2 KiB (two
+    __syncthreads();
+    if (s_cmd[0]) break;
+    const uint32_t seq = s_cmd[1];
+    // One round trip: the request (one 16-B load per thread) and the packet's first 2 KiB (one
     // more), all in flight together; a longer packet's rest follows below. Vector loads with
     // per-lane addresses after the acquire fence (never the scalar cache).
     constexpr uint32_t kReq16 = sizeof(ResReq) / 16, kFirst16 = 128;
+    static_assert(kReq16 <= (uint32_t)kResThreads && kFirst16 <= (uint32_t)kResThreads, "one load of each per thread");
     const uint4* rq4 = (const uint4*)&area->req;
     const uint4* src = (const uint4*)area->data;
     const uint4 z4 = make_uint4(0, 0, 0, 0);
-    const uint4 q0 = (uint32_t)lane < kReq16 ? rq4[lane] : z4, q1 = (uint32_t)lane + 64 < kReq16 ? rq4[lane + 64] : z4;
-    const uint4 d0 = src[lane], d1 = src[lane + 64];
-    if ((uint32_t)lane < kReq16) ((uint4*)s_req)[lane] = q0;
-    if ((uint32_t)lane + 64 < kReq16) ((uint4*)s_req)[lane + 64] = q1;
-    ((uint4*)s_pkt)[lane] = d0;
-    ((uint4*)s_pkt)[lane + 64] = d1;
-    wave_sync();
+    const uint4 q0 = (uint32_t)tid < kReq16 ? rq4[tid] : z4;
+    const uint4 d0 = (uint32_t)tid < kFirst16 ? src[tid] : z4;
+    if ((uint32_t)tid < kReq16) ((uint4*)s_req)[tid] = q0;
+    if ((uint32_t)tid < kFirst16) ((uint4*)s_pkt)[tid] = d0;
+    __syncthreads();
+    const uint64_t t_req = wall_clock64();
     const uint32_t op = uni(REQ.op), suite = uni(REQ.suite), aad_len = uni(REQ.aad_len), body_len = uni(REQ.body_len);
-    const uint32_t tot = op == kResHp ? 0u : aad_len + body_len + (op == kResSeal ? 16u : 0u);
+    const uint32_t pay = uni(REQ.pay_off);
+    const uint32_t tot = op == kResHp ? 0u : pay + body_len + (op == kResSeal ? 16u : 0u);
     const uint32_t nch = (tot + 15) / 16;
+    const bool bad = op != kResHp && (pay < aad_len || pay > aad_len + 15 || (pay & 15) || tot > kResMaxPkt ||
+                                      (op == kResOpen && body_len < 16));
 #pragma unroll 1
-    for (uint32_t c0 = kFirst16; c0 < nch; c0 += 256) {  // the rest: 4 loads in flight per lane
+    for (uint32_t c0 = kFirst16; !bad && c0 < nch; c0 += 4 * kResThreads) {  // the rest: 4 loads per thread
       uint4 v[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const uint32_t c = c0 + 64 * u + (uint32_t)lane;
+        const uint32_t c = c0 + kResThreads * u + (uint32_t)tid;
         v[u] = c < nch ? src[c] : make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const uint32_t c = c0 + 64 * u + (uint32_t)lane;
+        const uint32_t c = c0 + kResThreads * u + (uint32_t)tid;
         if (c < nch) *(uint4*)(s_pkt + 16 * c) = v[u];
       }
     }
-    wave_sync();
+    __syncthreads();
+    const uint64_t t_rest = wall_clock64();
+    uint64_t t_mid = t_rest;
     int st = MQ_OK;
     uint32_t m0 = 0, m1 = 0;
     if (op == kResHp) {
-      res_hp(suite, lane, m0, m1);
-    } else if (tot > kResMaxPkt || (op == kResOpen && body_len < 16)) {
+      if (w0) res_hp(suite, m0, m1);
+    } else if (bad) {
       st = MQ_ERR_INVALID_ARG;  // the host checks these; never trust the mailbox
     } else if (suite == MQ_SUITE_CHACHA20) {
-      st = res_chacha(op == kResOpen, aad_len, body_len, lane);
+      st = res_chacha(op == kResOpen, aad_len, pay, body_len, tid, t_mid);
     } else if (suite == MQ_SUITE_AES128GCM) {
-      st = res_aes(op == kResOpen, aad_len, body_len, lane);
+      st = res_aes(op == kResOpen, aad_len, pay, body_len, tid, t_mid);
     } else {
       st = MQ_ERR_INVALID_ARG;
     }
-    if (st == MQ_OK && op != kResHp) {  // the whole packet back (failed opens are not copied)
+    // The body back, by wave 0 alone (failed opens are not copied): its system-scope release
+    // fence then orders every store before `done`. Waves 1..3 go on to the next barrier, which
+    // wave 0 reaches only after this, so nothing overwrites the LDS packet meanwhile.
+    if (!w0) continue;
+    const uint64_t t_comp = wall_clock64();
+    if (st == MQ_OK && op != kResHp) {
       uint4* dst = (uint4*)area->data;
 #pragma unroll 1
-      for (uint32_t c = (uint32_t)lane; c < nch; c += 64) dst[c] = *(const uint4*)(s_pkt + 16 * c);
+      for (uint32_t c = pay / 16 + (uint32_t)lane; c < nch; c += 64) dst[c] = *(const uint4*)(s_pkt + 16 * c);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: results before done
-    if (lane == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: the results before done
+    const uint64_t t_wb = wall_clock64();
+    if (tid == 0) {
       st_sys(&ctl->status, (uint32_t)st);
       st_sys(&ctl->mask0, m0);
       st_sys(&ctl->mask1, m1);
+      static_assert(kResPhases == 6, "phase stamps");
+      st_sys(&ctl->phase[0], (uint32_t)(t_seen - tp));
+      st_sys(&ctl->phase[1], (uint32_t)(t_req - t_seen));
+      st_sys(&ctl->phase[2], (uint32_t)(t_rest - t_req));
+      st_sys(&ctl->phase[3], (uint32_t)(t_mid - t_rest));
+      st_sys(&ctl->phase[4], (uint32_t)(t_comp - t_mid));
+      st_sys(&ctl->phase[5], (uint32_t)(t_wb - t_comp));
       __hip_atomic_store(&ctl->done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     done = seq;
     t_last = wall_clock64();
   }
-  if (lane == 0) st_sys_sc(&ctl->state, kResExited);
+  if (tid == 0) st_sys_sc(&ctl->state, kResExited);
 }
 
 // ---- host ------------------------------------------------------------------------------------------
@@ -427,6 +571,8 @@ struct Resident {
   uint32_t seq = 0;
   bool launched = false;
   uint64_t idle = 0, life = 0;
+  int khz = 100000;  // wall-clock rate
+  uint32_t host_ns[3] = {0, 0, 0};  // last call: request written, waited for done, result copied
   std::mutex mu;
 };
 
@@ -458,10 +604,10 @@ uint32_t load_acq(const uint32_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIR
 }  // namespace
 
 // One call through the resident kernel of device `dev` (the caller holds a device guard on it).
-// `q` is the request with keys, nonce / sample, op, suite and lengths filled in; aad || body are
+// `q` is the request with keys, nonce / sample, op, suite and lengths filled in; aad and body are
 // the packet bytes. Returns MQ_OK when the call was served (*status = its result, out[0, out_len)
-// = data bytes [out_off, out_off + out_len) of the processed packet when *status is MQ_OK, mask =
-// the header-protection mask words), else an MQ_ERR_* of the transport.
+// = bytes [out_off, out_off + out_len) of the processed body when *status is MQ_OK, mask = the
+// header-protection mask words), else an MQ_ERR_* of the transport.
 int mq_resident_call(int dev, const ResReq& q, const uint8_t* aad, const uint8_t* body, uint8_t* out,
                      size_t out_off, size_t out_len, int* status, uint32_t* mask) {
   Resident* r = resident(dev);
@@ -477,20 +623,26 @@ int mq_resident_call(int dev, const ResReq& q, const uint8_t* aad, const uint8_t
       return MQ_ERR_HIP;
     int khz = 0;
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
+    r->khz = khz;
     const char* e = std::getenv("MQ_RESIDENT_IDLE_US");
     const uint64_t idle_us = e ? (uint64_t)std::strtoull(e, nullptr, 10) : 2000;  // 2 ms without a call
     r->idle = idle_us * (uint64_t)khz / 1000;
     r->life = 10ull * 1000 * (uint64_t)khz;  // 10 s, then leave at the next idle moment
   }
+  const auto h0 = std::chrono::steady_clock::now();
   ResArea* a = r->host;
+  const uint32_t pay = (q.aad_len + 15) & ~15u;  // the body 16-B aligned (mq_resident.h)
+  if (q.op != kResHp && (size_t)pay + q.body_len + 16 > kResMaxPkt) return MQ_ERR_INVALID_ARG;
   std::memcpy(&a->req, &q, sizeof q);
+  a->req.pay_off = pay;
   if (q.op != kResHp) {
     if (q.aad_len) std::memcpy(a->data, aad, q.aad_len);
-    if (q.body_len) std::memcpy(a->data + q.aad_len, body, q.body_len);
+    if (q.body_len) std::memcpy(a->data + pay, body, q.body_len);
   }
   const uint32_t seq = ++r->seq;
   __atomic_store_n(&a->ctl.seq, seq, __ATOMIC_SEQ_CST);
   const auto t0 = std::chrono::steady_clock::now();
+  bool relaunched = false;
   for (uint32_t spins = 0;; ++spins) {
     if (load_acq(&a->ctl.done) == seq) break;
     if (!r->launched || __atomic_load_n(&a->ctl.state, __ATOMIC_SEQ_CST) == kResExited) {
@@ -498,20 +650,43 @@ int mq_resident_call(int dev, const ResReq& q, const uint8_t* aad, const uint8_t
       if (load_acq(&a->ctl.done) == seq) break;  // served on its way out
       __atomic_store_n(&a->ctl.state, (uint32_t)kResRunning, __ATOMIC_SEQ_CST);
       __atomic_store_n(&a->ctl.stop, 0u, __ATOMIC_SEQ_CST);
-      hipLaunchKernelGGL(mq_resident_kernel, dim3(1), dim3(64), 0, r->stream, r->dptr, r->idle, r->life);
+      hipLaunchKernelGGL(mq_resident_kernel, dim3(1), dim3(kResThreads), 0, r->stream, r->dptr, r->idle, r->life);
       if (hipGetLastError() != hipSuccess) {
         __atomic_store_n(&a->ctl.state, (uint32_t)kResExited, __ATOMIC_SEQ_CST);
         return MQ_ERR_HIP;
       }
       r->launched = true;
+      relaunched = true;
     }
     if ((spins & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) return MQ_ERR_HIP;
   }
+  const auto t1 = std::chrono::steady_clock::now();
   *status = (int)__atomic_load_n(&a->ctl.status, __ATOMIC_ACQUIRE);
   if (mask) {
     mask[0] = a->ctl.mask0;
     mask[1] = a->ctl.mask1;
   }
-  if (*status == MQ_OK && out_len) std::memcpy(out, a->data + out_off, out_len);
+  if (*status == MQ_OK && out_len) std::memcpy(out, a->data + pay + out_off, out_len);
+  const auto t2 = std::chrono::steady_clock::now();
+  auto ns = [](std::chrono::steady_clock::duration d) {
+    return (uint32_t)std::chrono::duration_cast<std::chrono::nanoseconds>(d).count();
+  };
+  r->host_ns[0] = ns(t0 - h0);
+  r->host_ns[1] = relaunched ? 0u : ns(t1 - t0);
+  r->host_ns[2] = ns(t2 - t1);
   return MQ_OK;
+}
+
+// The device-side phases of device dev's last resident call in nanoseconds (ResCtl::phase);
+// returns the number written, 0 before any call.
+extern "C" int mq_resident_phases(int dev, uint32_t* ns, int n) {
+  if (dev < 0 || !ns || n <= 0) return 0;
+  Resident* r = resident(dev);
+  std::lock_guard<std::mutex> lk(r->mu);
+  if (!r->host || !r->seq) return 0;
+  int m = 0;
+  for (; m < n && m < kResPhases; ++m)
+    ns[m] = (uint32_t)((uint64_t)__atomic_load_n(&r->host->ctl.phase[m], __ATOMIC_ACQUIRE) * 1000000ull / (uint64_t)r->khz);
+  for (int k = 0; m < n && k < 3; ++k, ++m) ns[m] = r->host_ns[k];
+  return m;
 }

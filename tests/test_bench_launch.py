@@ -79,14 +79,16 @@ def test_sample_indices_and_shard_positions():
 
 def test_roofline_seal_composite_traffic():
     """roofline.kernel / traffic name the seal composite the bench's event time covers: the tile
-    kernel ("1" variant for a one-row key table), plus for AES the header-protection pass of short
-    packets; the PMC traffic is the sum of those kernels' per-launch HBM bytes from
+    kernel ("1" variant for a one-row key table; both suites' tiles apply header protection
+    themselves since r03), or for partitioned batches the partition launches and the tile kernels
+    mq_host.cpp picks; the PMC traffic is the sum of those kernels' per-launch HBM bytes from
     profiles/pmc_traffic_<cfg>.json."""
     assert bench.seal_kernels("b", 1) == ("mq_chacha_seal1_kernel",)  # HP inside the tile (r03)
     assert bench.seal_kernels("b", 1024) == ("mq_chacha_seal_kernel",)
-    assert bench.seal_kernels("c", 1024) == ("mq_aes_seal_kernel", "mq_aes_seal_hp_kernel")
-    assert bench.seal_kernels("e", 4098)[-1] == "mq_mixed_hp_kernel<false>"
-    assert bench.kernel_key("void mq_mixed_hp_kernel<false>(mq::KeyRow const*, unsigned int)") == "mq_mixed_hp_kernel<false>"
+    assert bench.seal_kernels("c", 1) == ("mq_aes_seal1_kernel",)
+    assert bench.seal_kernels("e", 4098) == bench.PARTITION + bench.AES_LIST0 + ("mq_chacha_seal_kernel",)
+    assert bench.seal_kernels("c", 1024) == bench.PARTITION + bench.AES_LIST0 + ("mq_aes_seal_kernel",)
+    assert bench.kernel_key("void mq_mixed_hp_kernel(mq::KeyRow const*, unsigned int)") == "mq_mixed_hp_kernel"
     for cfg in ("b", "c"):
         ks = bench.seal_kernels(cfg, 1)
         with open(os.path.join(HERE, "..", "profiles", f"pmc_traffic_{cfg}.json")) as f:

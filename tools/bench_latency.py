@@ -77,15 +77,28 @@ def measure(lib, _lib, calls):
             res[name] = {"median": round(float(np.median(t)) * 1e6, 2), "p99": round(float(np.quantile(t, 0.99)) * 1e6, 2)}
         # seal and open separately (open needs a sealed buffer: reseal before each timed open)
         ts, to = np.empty(calls), np.empty(calls)
+        ph = (ctypes.c_uint32 * 9)()
+        phs, pho = np.zeros((calls, 9)), np.zeros((calls, 9))
         for k in range(calls):
             t0 = time.perf_counter()
             assert seal() == 0
             t1 = time.perf_counter()
+            if lib.mq_resident_phases(0, ph, 9) == 9:  # outside the timed calls
+                phs[k] = list(ph)
+            t1b = time.perf_counter()
             assert open_() == 0
             t2 = time.perf_counter()
-            ts[k], to[k] = t1 - t0, t2 - t1
+            if lib.mq_resident_phases(0, ph, 9) == 9:
+                pho[k] = list(ph)
+            ts[k], to[k] = t1 - t0, t2 - t1b
         res["seal"] = {"median": round(float(np.median(ts)) * 1e6, 2), "p99": round(float(np.quantile(ts, 0.99)) * 1e6, 2)}
         res["open"] = {"median": round(float(np.median(to)) * 1e6, 2), "p99": round(float(np.quantile(to, 0.99)) * 1e6, 2)}
+        if os.environ.get("MQ_RESIDENT") == "1":  # device-side phases (mq_resident_phases), median us
+            names = ("poll_round_trip", "request_loaded", "rest_loaded", "first_half", "second_half", "written_back",
+                     "host_request_written", "host_wait_done", "host_copy_out")
+            res["phases_us"] = {
+                op: {n: round(float(np.median(a[:, i])) / 1e3, 2) for i, n in enumerate(names)}
+                for op, a in (("seal", phs), ("open", pho))}
         # ctypes call overhead alone (a call that returns at the argument checks)
         t = np.empty(calls)
         for k in range(calls):
