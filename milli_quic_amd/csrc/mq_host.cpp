@@ -8,6 +8,7 @@
 // MQ_ERR_NO_DEVICE.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -63,7 +64,7 @@ hipError_t mq_recv_outcomes(uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_con
                             size_t open_ws_bytes, hipStream_t s);
 hipError_t mq_launch_record_inner(const uint8_t* arena, uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
                                   uint8_t* status, uint64_t* info, hipStream_t s);
-int mq_resident_call(int dev, const mq::ResReq& q, const uint8_t* aad, const uint8_t* body, uint8_t* out,
+int mq_resident_call(int dev, const mq::ResReq& q, uint64_t uid, const uint8_t* aad, const uint8_t* body, uint8_t* out,
                      size_t out_off, size_t out_len, int* status, uint32_t* mask);
 #ifdef MQ_STAMPS
 void mq_stamps_set_chacha(uint64_t* p);
@@ -451,8 +452,11 @@ bool resident_enabled(size_t bytes) {
 }
 
 // The resident request image of a context: suite and key material (and for AES-128-GCM the GHASH
-// powers H^1..H^64 of its 64-lane Horner), filled once at creation.
-mq::ResReq* res_image(const KeyRow& row, bool aead) {
+// powers H^1..H^64 of its 64-lane Horner), filled once at creation; `uid` names the context to the
+// mailbox (its GHASH powers are copied there only when another context used it last).
+std::atomic<uint64_t> g_res_uid{0};
+mq::ResReq* res_image(const KeyRow& row, bool aead, uint64_t& uid) {
+  uid = ++g_res_uid;
   mq::ResReq* q = new mq::ResReq();
   std::memset(q, 0, sizeof *q);
   q->suite = row.suite;
@@ -483,6 +487,7 @@ struct mq_aead_ctx {
   KeyRow row;  // key schedule, H powers; iv is overwritten by the per-call nonce
   mutable Scratch sc;
   mq::ResReq* res = nullptr;  // resident request image (mutated per call under sc.mu)
+  uint64_t res_uid = 0;
   ~mq_aead_ctx() { delete res; }
 };
 struct mq_hp_ctx {
@@ -490,6 +495,7 @@ struct mq_hp_ctx {
   KeyRow row;
   mutable Scratch sc;
   mq::ResReq* res = nullptr;
+  uint64_t res_uid = 0;
   ~mq_hp_ctx() { delete res; }
 };
 struct mq_keytable {
@@ -541,7 +547,7 @@ int mq_aead_new(uint32_t suite, const uint8_t* key, size_t key_len, mq_aead_ctx*
   c->sc.device = dev;
   c->suite = suite;
   build_row(km, c->row);
-  c->res = res_image(c->row, true);
+  c->res = res_image(c->row, true, c->res_uid);
   *out = c;
   return MQ_OK;
 }
@@ -569,7 +575,7 @@ int mq_aead_seal_in_place(const mq_aead_ctx* ctx, const uint8_t* nonce, size_t n
     q.body_len = (uint32_t)payload_len;
     for (int i = 0; i < 3; ++i) q.nonce[i] = le32(nonce + 4 * i);
     int st = MQ_ERR_HIP;
-    const int rc = mq_resident_call(ctx->sc.device, q, aad, buf, buf, 0, total, &st, nullptr);
+    const int rc = mq_resident_call(ctx->sc.device, q, ctx->res_uid, aad, buf, buf, 0, total, &st, nullptr);
     if (rc) return rc;
     if (st) return st;
     if (out_len) *out_len = total;
@@ -602,7 +608,7 @@ int mq_aead_open_in_place(const mq_aead_ctx* ctx, const uint8_t* nonce, size_t n
     q.body_len = (uint32_t)ct_len;
     for (int i = 0; i < 3; ++i) q.nonce[i] = le32(nonce + 4 * i);
     int st = MQ_ERR_HIP;
-    const int rc = mq_resident_call(ctx->sc.device, q, aad, buf, buf, 0, ct_len - 16, &st, nullptr);
+    const int rc = mq_resident_call(ctx->sc.device, q, ctx->res_uid, aad, buf, buf, 0, ct_len - 16, &st, nullptr);
     if (rc) return rc;
     if (st) return st;  // buffer untouched on failure
     if (out_len) *out_len = ct_len - 16;
@@ -633,7 +639,7 @@ int mq_hp_new(uint32_t suite, const uint8_t* key, size_t key_len, mq_hp_ctx** ou
   c->sc.device = dev;
   c->suite = suite;
   build_row(km, c->row);
-  c->res = res_image(c->row, false);
+  c->res = res_image(c->row, false, c->res_uid);
   *out = c;
   return MQ_OK;
 }
@@ -653,7 +659,7 @@ int mq_hp_mask(const mq_hp_ctx* ctx, const uint8_t* sample, size_t sample_len, u
     for (int i = 0; i < 4; ++i) q.sample[i] = le32(sample + 4 * i);
     int st = MQ_ERR_HIP;
     uint32_t m[2] = {0, 0};
-    const int rc = mq_resident_call(sc.device, q, nullptr, nullptr, nullptr, 0, 0, &st, m);
+    const int rc = mq_resident_call(sc.device, q, ctx->res_uid, nullptr, nullptr, nullptr, 0, 0, &st, m);
     if (rc) return rc;
     if (st) return st;
     for (int b = 0; b < 4; ++b) mask[b] = (uint8_t)(m[0] >> (8 * b));

@@ -3,22 +3,27 @@
 // The reference's call sites are synchronous and per packet: Aead::seal_in_place
 // (transmit.rs:713-718), open_in_place (recv.rs:416-421) and HeaderProtection::mask
 // (transmit.rs:729, recv.rs:370) through rustcrypto.rs:38-220. Launching a kernel per call (r02:
-// a batch of one) costs 30-40 us; here one resident workgroup per device (one wave) polls a mailbox
-// in pinned host memory (mq_resident.h) and serves each call with all 64 lanes on ONE packet:
-//   ChaCha20-Poly1305: keystream block b on lane b (b = 0: the Poly1305 key), the MAC as a 64-way
-//     interleaved Horner (multiplier r^64, lane j's final multiplier r^(64-j) from a 6-step power
-//     ladder), lanes summed in 64-bit limbs;
-//   AES-128-GCM: CTR block b on lane b through the wide T-table (built once when the kernel starts),
-//     GHASH as a 64-way Horner with the bit-holed product (multiplier H^64, final H^(64-j); the
-//     host precomputes H^1 .. H^64 per context), lanes XOR-reduced;
-//   header protection: one block on lane 0.
-// The packet is copied host -> LDS once, processed in LDS, copied back; open verifies before it
-// decrypts (a failed packet is never written back). Memory ordering: the host writes the request
-// then `seq`; the wave polls `seq` with system-scope atomic loads (vector memory, never the scalar
-// cache), takes a system-scope acquire fence, reads the request with vector loads, and after the
-// results a system-scope release fence precedes `done`. The kernel leaves when the host asks (stop),
-// or after `idle` ticks without a request (or `life` ticks in all) — an exit claimed with a
-// Dekker-style handshake on `state` / `seq`, so a request posted meanwhile is either served or
+// a batch of one) costs 30-40 us; here one resident workgroup per device (4 waves, one per SIMD)
+// polls a mailbox in pinned host memory (mq_resident.h) and serves each call with all its lanes
+// on ONE packet:
+//   ChaCha20-Poly1305: keystream blocks on quads of lanes (a column per lane), the MAC as a 64-way
+//     interleaved Horner on wave 0 (multiplier r^64, lane j's final multiplier r^(j + 1) from a
+//     DPP prefix product), lanes summed in 64-bit limbs;
+//   AES-128-GCM: CTR block b on thread b through the wide T-table (built once when the kernel
+//     starts), GHASH on wave 0 as a 64-way Horner with the bit-holed product (multiplier H^64,
+//     final H^(64-j); the host precomputes H^1 .. H^64 per context), lanes XOR-reduced;
+//   header protection: one block on wave 0.
+// A request runs in two halves around the packet's arrival: the polling wave reads the request
+// header (key material, nonce, lengths — stamped slots, mq_resident.h) in its poll; the packet
+// then streams host -> LDS by LDS-DMA while the first half runs on the header alone (keystream or
+// CTR blocks, the one-time key and the powers of r, E_K(J0)); the second half (cipher XOR, MAC,
+// verdict) follows the packet. Open verifies before it decrypts (a failed packet is never written
+// back). Memory ordering: the host writes the packet, then the header slots, slot 0 last; the wave
+// polls with system-scope 8-B loads (vector memory, never the scalar cache) and takes a
+// system-scope acquire fence once the header is complete, before the packet's loads; after the
+// results a system-scope release fence precedes `done`. The kernel leaves when the host asks (stop
+// slot), or after `idle` ticks without a request (or `life` ticks in all) — an exit claimed with a
+// Dekker-style handshake on `state` / slot 0, so a request posted meanwhile is either served or
 // finds the kernel gone (the host then relaunches it).
 #include "mq_aes.h"
 #include "mq_resident.h"
@@ -32,9 +37,6 @@
 
 namespace mq {
 
-__device__ __forceinline__ uint32_t ld_sys(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 __device__ __forceinline__ uint32_t ld_sys_sc(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -50,14 +52,57 @@ __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_re
 // workgroup barrier (no issue slots) and join for the copies and the keystream.
 constexpr int kResWaves = 4, kResThreads = 64 * kResWaves;
 
-// LDS: the request, the packet, the open keystream, scratch
-constexpr uint32_t kResReqWords = sizeof(ResReq) / 4;
-__shared__ __attribute__((aligned(16))) uint32_t s_req[kResReqWords];
+// LDS: the request header, the packet, the open keystream, the GHASH powers, scratch
+__shared__ __attribute__((aligned(16))) uint32_t s_hdr[kResHdrSlots];
 __shared__ __attribute__((aligned(16))) uint8_t s_pkt[kResMaxPkt + 64];
 __shared__ __attribute__((aligned(16))) uint32_t s_ks[kResMaxPkt / 4];  // open: keystream until the tag verifies
-__shared__ __attribute__((aligned(16))) uint32_t s_scr[16];  // one-time key / E_K(J0); [12]: verdict
-__shared__ uint32_t s_cmd[2];                                // wave 0 -> all: leave?, seq
-#define REQ (*(const ResReq*)s_req)
+__shared__ __attribute__((aligned(16))) uint32_t s_hpow[64 * 4];        // AES: H^1 .. H^64 of the request
+__shared__ __attribute__((aligned(16))) uint32_t s_scr[16];             // [12]: open verdict
+__shared__ uint32_t s_cmd[2];                                           // wave 0 -> all: leave?, seq
+
+// Header polls: a ring of kResPolls polls in flight, each an LDS-DMA of the header slots (lane l
+// loads slots 2l, 2l + 1: 16 B, kPollLanes lanes) into its own 512-B LDS slot, reissued as soon as
+// it has been looked at, so host memory is sampled every ~RTT / kResPolls. Polls land in LDS, not
+// registers: no in-flight destination register can be copied or reused by the compiler, and each
+// look waits only for the oldest poll (vmcnt(kResPolls - 1): kResPolls - 1 later polls were issued
+// after it, other memory operations only make the wait longer). Polls may be served out of order;
+// each is judged on its own stamps.
+constexpr int kResPolls = 8;
+constexpr int kPollLanes = (int)(kHwStop + 2) / 2;  // slots 0 .. kHwStop (| kHwStop + 1)
+__shared__ __attribute__((aligned(16))) uint64_t s_ring[kResPolls][64];
+
+__device__ __forceinline__ void poll_issue(const ResArea* area, uint32_t k, int lane) {
+  if (lane < kPollLanes)
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)((const uint8_t*)area->hdr + 16 * lane),
+                                     (__attribute__((address_space(3))) void*)&s_ring[k][0], 16, 0,
+                                     17 /* sc0 sc1: system coherent */);
+}
+// this lane's slot of poll k (slots past kHwStop + 1 read as garbage: never looked at)
+__device__ __forceinline__ uint64_t poll_read(uint32_t k, int lane) {
+  static_assert(kResPolls == 8, "vmcnt(7) below");
+  uint64_t v;
+  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint64_t*)&s_ring[k][lane];
+  asm volatile("s_waitcnt vmcnt(7)\n\tds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+
+// Packet bytes host -> LDS: chunk c (16 B) of the mailbox's data area to s_pkt + 16c, by LDS-DMA
+// (global_load_lds_dwordx4: lane-linear LDS destination, one instruction per wave per 64
+// chunks); completes at the next fenced barrier (s_waitcnt vmcnt(0)).
+__device__ __forceinline__ void dma_chunks(const uint8_t* src, uint8_t* dst, uint32_t nch, int tid) {
+  const uint32_t w = (uint32_t)tid >> 6, lane = (uint32_t)tid & 63;
+  for (uint32_t b = 64 * w; b < nch; b += kResThreads)  // wave-uniform
+    if (b + lane < nch)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 16u * (b + lane)),
+                                       (__attribute__((address_space(3))) void*)(dst + 16u * b), 16, 0, 0);
+}
+
+// the octet of a keystream word from a quad of lanes (chacha20_block4) to all lanes: word k of
+// the block is ks[k >> 2] of quad lane k & 3 (wave 0's quad 0 holds block 0: the one-time key)
+__device__ __forceinline__ void otk_from_quad(const uint32_t (&ks)[4], uint32_t (&otk)[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) otk[k] = (uint32_t)__builtin_amdgcn_readlane((int)ks[k >> 2], k & 3);
+}
 
 // 64-bit lane sums of Poly1305 limbs -> the accumulator mod 2^130 - 5 in 26-bit limbs
 __device__ __forceinline__ P26 p26_from_sums(const uint64_t (&s)[5]) {
@@ -226,71 +271,6 @@ __device__ __forceinline__ void chacha20_block4(const uint32_t (&key)[8], uint32
   ks[0] = a + c0; ks[1] = b + k0; ks[2] = c + k1; ks[3] = d + d0;
 }
 
-// ChaCha20-Poly1305 seal / open of the LDS packet (aad at 0, body at the aligned pay). Wave 0
-// makes the Poly1305 key (block 0, on its quads) and the MAC's powers of r while waves 1..3 make
-// keystream blocks 1.. (one per quad, 48 per pass); then wave 0 runs the MAC. Seal XORs the
-// keystream in place before the MAC; open keeps it in s_ks, verifies, and applies it only if the
-// tag matched. Returns MQ_* (workgroup-uniform).
-__device__ int res_chacha(bool open, uint32_t aad_len, uint32_t pay, uint32_t body_len, int tid, uint64_t& t_mid) {
-  uint32_t key[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) key[k] = REQ.key[k];
-  const uint32_t n0 = REQ.nonce[0], n1 = REQ.nonce[1], n2 = REQ.nonce[2];
-  const uint32_t P = open ? body_len - 16 : body_len;
-  const uint32_t nblk = 1 + (P + 63) / 64;
-  const int q = tid & 3;
-  uint32_t* pw = (uint32_t*)(s_pkt + pay);
-  uint32_t otk[8];
-  PolyPow pp;
-  if (tid < 64) {
-    uint32_t ks[4];
-    chacha20_block4(key, 0, n0, n1, n2, q, ks);
-    if (tid < 4) { s_scr[q] = ks[0]; s_scr[4 + q] = ks[1]; }
-    wave_sync();
-#pragma unroll
-    for (int k = 0; k < 8; ++k) otk[k] = s_scr[k];
-    pp = poly_powers(otk);
-    if (open) {  // the ciphertext is in place: the MAC need not wait for the keystream
-      uint32_t tag[4], got[4];
-      poly_tag(aad_len, pay, P, pp, otk, tid, tag);
-      load_words<4>(LdsSpace{s_pkt}, pay + P, got);
-      if (tid == 0) s_scr[12] = (tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) | (tag[3] ^ got[3]);
-    }
-  } else {
-    constexpr uint32_t kQuads = (kResThreads - 64) / 4;
-#pragma unroll 1
-    for (uint32_t b0 = 1; b0 < nblk; b0 += kQuads) {
-      const uint32_t b = b0 + (uint32_t)((tid - 64) >> 2);
-      uint32_t ks[4];
-      chacha20_block4(key, b, n0, n1, n2, q, ks);
-      if (b < nblk) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint32_t o = 64 * (b - 1) + 16 * k + 4 * q;  // payload byte offset of word 4k + q
-          if (o < P) {
-            if (open) s_ks[o / 4] = ks[k];
-            else pw[o / 4] ^= ks[k] & byte_mask((int)(P - o), 0);
-          }
-        }
-      }
-    }
-  }
-  __syncthreads();
-  t_mid = wall_clock64();
-  if (!open) {
-    if (tid < 64) {  // the write-back that follows is wave 0's too: no barrier after the tag
-      uint32_t tag[4];
-      poly_tag(aad_len, pay, P, pp, otk, tid, tag);
-      if (tid == 0) store_words<4>(LdsSpace{s_pkt}, pay + P, tag);
-    }
-    return MQ_OK;
-  }
-  if (s_scr[12]) return MQ_ERR_CRYPTO;  // rustcrypto.rs:156-163; nothing decrypted
-  for (uint32_t w = (uint32_t)tid; 4 * w < P; w += kResThreads) pw[w] ^= s_ks[w] & byte_mask((int)(P - 4 * w), 0);
-  __syncthreads();
-  return MQ_OK;
-}
-
 // GHASH(AAD || C || lens) on ONE wave (lane j: blocks 64k + j - z, multiplier H^64, final
 // H^(64 - j), lanes XOR-reduced), reflected basis (mq_aes.h); tag = that ^ E_K(J0)
 __device__ __forceinline__ void ghash_tag(uint32_t aad_len, uint32_t pay, uint32_t P, const GfOp& m64,
@@ -328,82 +308,206 @@ __device__ __forceinline__ void ghash_tag(uint32_t aad_len, uint32_t pay, uint32
   for (int w = 0; w < 4; ++w) tag[w] = bswap32(brev(wave_xor_u32(acc[w]))) ^ ej0[w];
 }
 
-// AES-128-GCM seal / open of the LDS packet: wave 0 makes E_K(J0) and the GHASH multipliers
-// (H^64, and H^(64 - lane) from the request's powers) while waves 1..3 run the CTR blocks (one per
-// thread, 192 per pass); then wave 0 runs GHASH. Open verifies before it decrypts.
-__device__ int res_aes(bool open, uint32_t aad_len, uint32_t pay, uint32_t body_len, int tid, uint64_t& t_mid) {
-  const TwLane L = tw_lane();
-  const RkLds key{REQ.aes_rk};
-  const uint32_t nb0 = bswap32(REQ.nonce[0]), nb1 = bswap32(REQ.nonce[1]), nb2 = bswap32(REQ.nonce[2]);
+// Stamps of a request's phases on wave 0 (ResCtl::phase): first half done, packet landed, second
+// half done, decryption applied
+struct ResT { uint64_t half1, landed, half2, applied; };
+
+// ChaCha20-Poly1305 seal / open of the LDS packet (aad at 0, body at the aligned pay). First half
+// (header only, while the packet lands): wave 0 makes the Poly1305 key (block 0, on its quads) and
+// the MAC's powers of r; waves 1..3 make keystream blocks 1.. (one per quad, 48 per pass) — seal
+// keeps the first pass in registers, open writes every block to s_ks. Second half: seal XORs the
+// keystream in place (later passes too), then wave 0 runs the MAC; open runs the MAC over the
+// untouched ciphertext, verifies, and applies s_ks only if the tag matched. Returns MQ_*
+// (workgroup-uniform).
+__device__ int res_chacha(bool open, uint32_t aad_len, uint32_t pay, uint32_t body_len, int tid, ResT& t) {
+  uint32_t key[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) key[k] = s_hdr[kHwKey + k];
+  const uint32_t n0 = s_hdr[kHwNonce], n1 = s_hdr[kHwNonce + 1], n2 = s_hdr[kHwNonce + 2];
   const uint32_t P = open ? body_len - 16 : body_len;
-  const uint32_t nblk = 1 + (P + 15) / 16;  // slot 0: E_K(J0), slot b >= 1: CTR block with counter b + 1
+  const uint32_t nblk = 1 + (P + 63) / 64;
+  const int q = tid & 3;
   uint32_t* pw = (uint32_t*)(s_pkt + pay);
-  GfOp m64, ml;
-  uint32_t ej0[4];
+  constexpr uint32_t kQuads = (kResThreads - 64) / 4;
+  uint32_t otk[8], ks1[4];
+  PolyPow pp;
+  const uint32_t b1 = 1 + (uint32_t)((tid - 64) >> 2);  // waves 1..3: first-pass block
+  // payload word 4k + q of block b: keystream ks[k] (byte offset o < P)
+  auto put = [&](uint32_t b, const uint32_t (&ks)[4]) {
+    if (b >= nblk) return;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t o = 64 * (b - 1) + 16 * k + 4 * q;
+      if (o < P) {
+        if (open) s_ks[o / 4] = ks[k];
+        else pw[o / 4] ^= ks[k] & byte_mask((int)(P - o), 0);
+      }
+    }
+  };
   if (tid < 64) {
-    uint32_t s[4] = {nb0, nb1, nb2, 1u};
-    aes128_enc(key, L, s);
-    uint32_t h[4], hl[4];
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      ej0[w] = bswap32(s[w]);
-      h[w] = brev(REQ.Hpow[63][w]);
-      hl[w] = brev(REQ.Hpow[63 - tid][w]);
-    }
-    m64 = gf_prepare(h);
-    ml = gf_prepare(hl);
-    if (open) {  // the ciphertext is in place: GHASH need not wait for the keystream
-      uint32_t tag[4], got[4];
-      ghash_tag(aad_len, pay, P, m64, ml, ej0, tid, tag);
-      load_words<4>(LdsSpace{s_pkt}, pay + P, got);
-      if (tid == 0) s_scr[12] = (tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) | (tag[3] ^ got[3]);
-    }
+    uint32_t ks[4];
+    chacha20_block4(key, 0, n0, n1, n2, q, ks);
+    otk_from_quad(ks, otk);
+    pp = poly_powers(otk);
   } else {
+    chacha20_block4(key, b1, n0, n1, n2, q, ks1);
+    if (open) {
+      put(b1, ks1);
 #pragma unroll 1
-    for (uint32_t b0 = 1; b0 < nblk; b0 += kResThreads - 64) {
-      const uint32_t b = b0 + (uint32_t)(tid - 64);
-      uint32_t s[4] = {nb0, nb1, nb2, b + 1};
-      aes128_enc(key, L, s);
-      if (b < nblk) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint32_t o = 16 * (b - 1) + 4 * k;
-          if (o < P) {
-            if (open) s_ks[o / 4] = bswap32(s[k]);
-            else pw[o / 4] ^= bswap32(s[k]) & byte_mask((int)(P - o), 0);
-          }
-        }
+      for (uint32_t b0 = 1 + kQuads; b0 < nblk; b0 += kQuads) {
+        uint32_t ks[4];
+        const uint32_t b = b0 + (uint32_t)((tid - 64) >> 2);
+        chacha20_block4(key, b, n0, n1, n2, q, ks);
+        put(b, ks);
       }
     }
   }
-  __syncthreads();
-  t_mid = wall_clock64();
+  t.half1 = wall_clock64();
+  __syncthreads();  // the packet has landed (vmcnt(0)); open: s_ks complete
+  t.landed = wall_clock64();
   if (!open) {
+    if (tid >= 64) {
+      put(b1, ks1);
+#pragma unroll 1
+      for (uint32_t b0 = 1 + kQuads; b0 < nblk; b0 += kQuads) {
+        uint32_t ks[4];
+        const uint32_t b = b0 + (uint32_t)((tid - 64) >> 2);
+        chacha20_block4(key, b, n0, n1, n2, q, ks);
+        put(b, ks);
+      }
+    }
+    __syncthreads();  // the ciphertext is in place
+    if (tid < 64) {  // the write-back that follows is wave 0's too: no barrier after the tag
+      uint32_t tag[4];
+      poly_tag(aad_len, pay, P, pp, otk, tid, tag);
+      if (tid == 0) store_words<4>(LdsSpace{s_pkt}, pay + P, tag);
+    }
+    t.half2 = t.applied = wall_clock64();
+    return MQ_OK;
+  }
+  if (tid < 64) {
+    uint32_t tag[4], got[4];
+    poly_tag(aad_len, pay, P, pp, otk, tid, tag);
+    load_words<4>(LdsSpace{s_pkt}, pay + P, got);
+    if (tid == 0) s_scr[12] = (tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) | (tag[3] ^ got[3]);
+  }
+  __syncthreads();
+  t.half2 = wall_clock64();
+  if (s_scr[12]) return MQ_ERR_CRYPTO;  // rustcrypto.rs:156-163; nothing decrypted
+  for (uint32_t w = (uint32_t)tid; 4 * w < P; w += kResThreads) pw[w] ^= s_ks[w] & byte_mask((int)(P - 4 * w), 0);
+  __syncthreads();
+  t.applied = wall_clock64();
+  return MQ_OK;
+}
+
+// AES-128-GCM seal / open of the LDS packet. First half: wave 0 makes E_K(J0); waves 1..3 run CTR
+// blocks (one per thread, 192 per pass) — seal keeps the first pass in registers, open writes
+// every block to s_ks. Second half: wave 0 prepares the GHASH multipliers (H^64, and H^(64 - lane)
+// from the request's powers, which land with the packet); seal XORs the keystream in place, then
+// wave 0 runs GHASH; open runs GHASH over the ciphertext, verifies, then decrypts.
+__device__ int res_aes(bool open, uint32_t aad_len, uint32_t pay, uint32_t body_len, int tid, ResT& t) {
+  const TwLane L = tw_lane();
+  const RkLds key{s_hdr + kHwKey};
+  const uint32_t nb0 = bswap32(s_hdr[kHwNonce]), nb1 = bswap32(s_hdr[kHwNonce + 1]), nb2 = bswap32(s_hdr[kHwNonce + 2]);
+  const uint32_t P = open ? body_len - 16 : body_len;
+  const uint32_t nblk = 1 + (P + 15) / 16;  // slot 0: E_K(J0), slot b >= 1: CTR block with counter b + 1
+  uint32_t* pw = (uint32_t*)(s_pkt + pay);
+  constexpr uint32_t kBlk = kResThreads - 64;
+  uint32_t ej0[4], s1[4];
+  const uint32_t b1 = 1 + (uint32_t)(tid - 64);  // waves 1..3: first-pass block
+  auto put = [&](uint32_t b, const uint32_t (&s)[4]) {
+    if (b >= nblk) return;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t o = 16 * (b - 1) + 4 * k;
+      if (o < P) {
+        if (open) s_ks[o / 4] = bswap32(s[k]);
+        else pw[o / 4] ^= bswap32(s[k]) & byte_mask((int)(P - o), 0);
+      }
+    }
+  };
+  auto block = [&](uint32_t b, uint32_t (&s)[4]) {
+    s[0] = nb0; s[1] = nb1; s[2] = nb2; s[3] = b + 1;
+    aes128_enc(key, L, s);
+  };
+  if (tid < 64) {
+    uint32_t s[4] = {nb0, nb1, nb2, 1u};
+    aes128_enc(key, L, s);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) ej0[w] = bswap32(s[w]);
+  } else {
+    block(b1, s1);
+    if (open) {
+      put(b1, s1);
+#pragma unroll 1
+      for (uint32_t b0 = 1 + kBlk; b0 < nblk; b0 += kBlk) {
+        uint32_t s[4];
+        block(b0 + (uint32_t)(tid - 64), s);
+        put(b0 + (uint32_t)(tid - 64), s);
+      }
+    }
+  }
+  t.half1 = wall_clock64();
+  __syncthreads();  // the packet and the GHASH powers have landed; open: s_ks complete
+  t.landed = wall_clock64();
+  GfOp m64, ml;
+  if (tid < 64) {
+    uint32_t h[4], hl[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      h[w] = brev(s_hpow[4 * 63 + w]);
+      hl[w] = brev(s_hpow[4 * (63 - tid) + w]);
+    }
+    m64 = gf_prepare(h);
+    ml = gf_prepare(hl);
+  }
+  if (!open) {
+    if (tid >= 64) {
+      put(b1, s1);
+#pragma unroll 1
+      for (uint32_t b0 = 1 + kBlk; b0 < nblk; b0 += kBlk) {
+        uint32_t s[4];
+        block(b0 + (uint32_t)(tid - 64), s);
+        put(b0 + (uint32_t)(tid - 64), s);
+      }
+    }
+    __syncthreads();  // the ciphertext is in place
     if (tid < 64) {  // the write-back that follows is wave 0's too: no barrier after the tag
       uint32_t tag[4];
       ghash_tag(aad_len, pay, P, m64, ml, ej0, tid, tag);
       if (tid == 0) store_words<4>(LdsSpace{s_pkt}, pay + P, tag);
     }
+    t.half2 = t.applied = wall_clock64();
     return MQ_OK;
   }
+  if (tid < 64) {
+    uint32_t tag[4], got[4];
+    ghash_tag(aad_len, pay, P, m64, ml, ej0, tid, tag);
+    load_words<4>(LdsSpace{s_pkt}, pay + P, got);
+    if (tid == 0) s_scr[12] = (tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) | (tag[3] ^ got[3]);
+  }
+  __syncthreads();
+  t.half2 = wall_clock64();
   if (s_scr[12]) return MQ_ERR_CRYPTO;  // rustcrypto.rs:85-91; nothing decrypted
   for (uint32_t w = (uint32_t)tid; 4 * w < P; w += kResThreads) pw[w] ^= s_ks[w] & byte_mask((int)(P - 4 * w), 0);
   __syncthreads();
+  t.applied = wall_clock64();
   return MQ_OK;
 }
 
+// HeaderProtection::mask from the header alone (sample and HP key material), wave 0
 __device__ void res_hp(uint32_t suite, uint32_t& m0, uint32_t& m1) {
-  const uint32_t smp[4] = {REQ.sample[0], REQ.sample[1], REQ.sample[2], REQ.sample[3]};
+  const uint32_t smp[4] = {s_hdr[kHwSample], s_hdr[kHwSample + 1], s_hdr[kHwSample + 2], s_hdr[kHwSample + 3]};
   if (suite == MQ_SUITE_CHACHA20) {  // rustcrypto.rs:197-220
     uint32_t hk[8], blk[16];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) hk[k] = REQ.hp[k];
+    for (int k = 0; k < 8; ++k) hk[k] = s_hdr[kHwKey + k];
     chacha20_block(hk, smp[0], smp[1], smp[2], smp[3], blk);
     m0 = blk[0];
     m1 = blk[1] & 0xffu;
   } else {  // rustcrypto.rs:175-186
     uint32_t s[4] = {bswap32(smp[0]), bswap32(smp[1]), bswap32(smp[2]), bswap32(smp[3])};
-    aes128_enc(RkLds{REQ.hp_rk}, tw_lane(), s);
+    aes128_enc(RkLds{s_hdr + kHwKey}, tw_lane(), s);
     m0 = bswap32(s[0]);
     m1 = s[1] >> 24;
   }
@@ -420,143 +524,132 @@ extern "C" __global__ __launch_bounds__(kResThreads) void mq_resident_kernel(Res
   ResCtl* ctl = &area->ctl;
   build_tw(tid, kResThreads);  // the wide AES T-table, once per kernel
   __syncthreads();
-  uint32_t done = uni(ld_sys(&ctl->done));
+  uint32_t done = uni(ld_sys_sc(&ctl->done));
   const uint64_t t0 = wall_clock64();
-  uint64_t t_last = t0, tp = t0, t_seen = t0;
-  for (;;) {
-    if (w0) {  // wave 0 polls; waves 1..3 wait at the barrier below
-      // seq and stop in one 8-B system-scope load, kResPolls of them in flight (a new one issued
-      // as the oldest returns, so a request is seen about one PCIe round trip after the host
-      // posts it, not up to two). Reads may be served out of order, so a poll can return an older
-      // seq than the last one: a request is new iff seq - done > 0 (wrapping).
-      auto poll = [&]() {
-        return __hip_atomic_load((const uint64_t*)&ctl->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      };
-      uint32_t leave = 0, seq = done;
-      bool got = false;
-      // 0: keep polling; 1: serve seq / leave (see `leave`)
-      auto check = [&](uint64_t ss) -> bool {
-        seq = uni((uint32_t)ss);
-        t_seen = wall_clock64();
-        if (uni((uint32_t)(ss >> 32))) { leave = 1; return true; }
-        if ((int32_t)(seq - done) > 0) return true;
-        const uint64_t now = wall_clock64();
-        if (now - t_last > idle_ticks || now - t0 > life_ticks) {
-          // claim the exit, then look once more: a request posted meanwhile is served first
-          if (lane == 0) st_sys_sc(&ctl->state, kResExiting);
-          wave_sync();
-          seq = uni(ld_sys_sc(&ctl->seq));
-          if ((int32_t)(seq - done) <= 0) { leave = 1; return true; }
-          if (lane == 0) st_sys_sc(&ctl->state, kResRunning);
-          t_last = now;
-          return true;
-        }
-        return false;
-      };
-      tp = wall_clock64();
-      uint64_t pa = poll();
-      __builtin_amdgcn_s_sleep(8);
-      uint64_t pb = poll();
-      __builtin_amdgcn_s_sleep(8);
-      uint64_t pc = poll();
-      __builtin_amdgcn_s_sleep(8);
-      uint64_t pd = poll();
-      while (!got) {  // unrolled by the number of polls in flight: each keeps its register
-        if ((got = check(pa))) break;
-        tp = wall_clock64(); pa = poll();
-        if ((got = check(pb))) break;
-        tp = wall_clock64(); pb = poll();
-        if ((got = check(pc))) break;
-        tp = wall_clock64(); pc = poll();
-        if ((got = check(pd))) break;
-        tp = wall_clock64(); pd = poll();
-      }
-      if (lane == 0) { s_cmd[0] = leave; s_cmd[1] = seq; }
-      // system scope, once for the workgroup (the barrier below orders the other waves' loads
-      // after it): the request written before seq
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  uint64_t t_last = t0, t_seen = t0;
+  const bool w0u = wave_id() == 0;  // wave-uniform: a scalar branch around the poll loop
+  // wave 0's polls: kept in flight across loop iterations (and the request, see the end of the loop)
+  uint32_t pos = 0;  // the ring's oldest poll (wave 0)
+  if (w0u) {
+#pragma unroll
+    for (uint32_t k = 0; k < kResPolls; ++k) {
+      poll_issue(area, k, lane);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_sleep(10);  // ~0.3 us apart
+      __builtin_amdgcn_sched_barrier(0);
     }
-    __syncthreads();
+  }
+  for (;;) {
+    if (w0u) {  // wave 0 polls; waves 1..3 wait at the barrier below
+      // Request done + 1 is complete when every slot it uses carries that number (the host writes
+      // slot 0 last, so a complete header usually comes in the first poll that sees slot 0).
+      const uint32_t exp = done + 1;
+      uint32_t leave = 0;
+      uint64_t hv = 0;
+      // 0: nothing new, 1: request done + 1 (slot 0), 2: stop, 3: idle
+      auto test = [&](uint64_t v) -> uint32_t {
+        if (__builtin_amdgcn_readlane((int)(uint32_t)v, kHwStop)) return 2;
+        if ((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 0) == exp) return 1;
+        return 0;
+      };
+      for (;;) {
+        const uint64_t deadline = min(t_last + idle_ticks, t0 + life_ticks);
+        uint32_t r = 0;
+        do {
+          hv = poll_read(pos, lane);
+          r = test(hv);
+          poll_issue(area, pos, lane);
+          pos = (pos + 1) % kResPolls;
+          if (!r && wall_clock64() > deadline) r = 3;
+        } while (!r);
+        const uint64_t now = wall_clock64();
+        if (r == 2) { leave = 1; break; }
+        if (r == 1) {
+          const uint32_t n = res_hdr_words(((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)hv, 0) >> 8) & 0xffu);
+          if (!wave_any((uint32_t)lane < n && (uint32_t)(hv >> 32) != exp)) { t_seen = now; break; }
+          t_last = now;  // a request is being written: no idle exit meanwhile
+          continue;
+        }
+        // idle: claim the exit, then look once more; a request posted meanwhile is served first
+        if (lane == 0) st_sys_sc(&ctl->state, kResExiting);
+        wave_sync();
+        if (uni(ld_sys_sc((const uint32_t*)&area->hdr[0] + 1)) != exp) { leave = 1; break; }
+        if (lane == 0) st_sys_sc(&ctl->state, kResRunning);
+        t_last = now;
+      }
+      if (!leave) s_hdr[lane] = (uint32_t)hv;
+      if (lane == 0) { s_cmd[0] = leave; s_cmd[1] = exp; }
+      // The packet was written before the header; its loads are issued after this wave has seen the
+      // header (they cannot pass it). Invalidate the vector caches for them, without a fence: a
+      // system-scope acquire fence would wait for the ring's polls in flight (vmcnt(0)), up to a
+      // round trip.
+      asm volatile("buffer_inv sc0 sc1" ::: "memory");
+    }
+    // LDS-only barrier (the other waves' view of s_hdr / s_cmd): a __syncthreads() fence would also
+    // wait for wave 0's polls in flight
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (s_cmd[0]) break;
     const uint32_t seq = s_cmd[1];
-    // One round trip: the request (one 16-B load per thread) and the packet's first 2 KiB (one
-    // more), all in flight together; a longer packet's rest follows below. Vector loads with
-    // per-lane addresses after the acquire fence (never the scalar cache).
-    constexpr uint32_t kReq16 = sizeof(ResReq) / 16, kFirst16 = 128;
-    static_assert(kReq16 <= (uint32_t)kResThreads && kFirst16 <= (uint32_t)kResThreads, "one load of each per thread");
-    const uint4* rq4 = (const uint4*)&area->req;
-    const uint4* src = (const uint4*)area->data;
-    const uint4 z4 = make_uint4(0, 0, 0, 0);
-    const uint4 q0 = (uint32_t)tid < kReq16 ? rq4[tid] : z4;
-    const uint4 d0 = (uint32_t)tid < kFirst16 ? src[tid] : z4;
-    if ((uint32_t)tid < kReq16) ((uint4*)s_req)[tid] = q0;
-    if ((uint32_t)tid < kFirst16) ((uint4*)s_pkt)[tid] = d0;
-    __syncthreads();
-    const uint64_t t_req = wall_clock64();
-    const uint32_t op = uni(REQ.op), suite = uni(REQ.suite), aad_len = uni(REQ.aad_len), body_len = uni(REQ.body_len);
-    const uint32_t pay = uni(REQ.pay_off);
+    const uint64_t t_hdr = wall_clock64();
+    const uint32_t h0 = uni(s_hdr[kHwOp]), op = h0 & 0xffu, suite = (h0 >> 8) & 0xffu;
+    const uint32_t aad_len = uni(s_hdr[kHwAad]), body_len = uni(s_hdr[kHwBody]), pay = uni(s_hdr[kHwPay]);
     const uint32_t tot = op == kResHp ? 0u : pay + body_len + (op == kResSeal ? 16u : 0u);
     const uint32_t nch = (tot + 15) / 16;
-    const bool bad = op != kResHp && (pay < aad_len || pay > aad_len + 15 || (pay & 15) || tot > kResMaxPkt ||
-                                      (op == kResOpen && body_len < 16));
-#pragma unroll 1
-    for (uint32_t c0 = kFirst16; !bad && c0 < nch; c0 += 4 * kResThreads) {  // the rest: 4 loads per thread
-      uint4 v[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint32_t c = c0 + kResThreads * u + (uint32_t)tid;
-        v[u] = c < nch ? src[c] : make_uint4(0, 0, 0, 0);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint32_t c = c0 + kResThreads * u + (uint32_t)tid;
-        if (c < nch) *(uint4*)(s_pkt + 16 * c) = v[u];
-      }
+    const bool known = suite == MQ_SUITE_CHACHA20 || suite == MQ_SUITE_AES128GCM;
+    const bool bad = !known || op > kResHp ||
+                     (op != kResHp && (pay < aad_len || pay > aad_len + 15 || (pay & 15) || tot > kResMaxPkt ||
+                                       (op == kResOpen && body_len < 16)));
+    // the packet (and the GHASH powers) host -> LDS, landing during the first half
+    if (!bad && op != kResHp) {
+      dma_chunks(area->data, s_pkt, nch, tid);
+      if (suite == MQ_SUITE_AES128GCM) dma_chunks((const uint8_t*)area->Hpow, (uint8_t*)s_hpow, 64 * 4 * 4 / 16, tid);
     }
-    __syncthreads();
-    const uint64_t t_rest = wall_clock64();
-    uint64_t t_mid = t_rest;
+    ResT t{t_hdr, t_hdr, t_hdr, t_hdr};
     int st = MQ_OK;
     uint32_t m0 = 0, m1 = 0;
-    if (op == kResHp) {
-      if (w0) res_hp(suite, m0, m1);
-    } else if (bad) {
+    if (bad) {
       st = MQ_ERR_INVALID_ARG;  // the host checks these; never trust the mailbox
+    } else if (op == kResHp) {
+      if (w0) res_hp(suite, m0, m1);
+      t.half1 = t.landed = t.half2 = t.applied = wall_clock64();
     } else if (suite == MQ_SUITE_CHACHA20) {
-      st = res_chacha(op == kResOpen, aad_len, pay, body_len, tid, t_mid);
-    } else if (suite == MQ_SUITE_AES128GCM) {
-      st = res_aes(op == kResOpen, aad_len, pay, body_len, tid, t_mid);
+      st = res_chacha(op == kResOpen, aad_len, pay, body_len, tid, t);
     } else {
-      st = MQ_ERR_INVALID_ARG;
+      st = res_aes(op == kResOpen, aad_len, pay, body_len, tid, t);
     }
     // The body back, by wave 0 alone (failed opens are not copied): its system-scope release
     // fence then orders every store before `done`. Waves 1..3 go on to the next barrier, which
     // wave 0 reaches only after this, so nothing overwrites the LDS packet meanwhile.
     if (!w0) continue;
-    const uint64_t t_comp = wall_clock64();
     if (st == MQ_OK && op != kResHp) {
       uint4* dst = (uint4*)area->data;
 #pragma unroll 1
       for (uint32_t c = pay / 16 + (uint32_t)lane; c < nch; c += 64) dst[c] = *(const uint4*)(s_pkt + 16 * c);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: the results before done
     const uint64_t t_wb = wall_clock64();
-    if (tid == 0) {
-      st_sys(&ctl->status, (uint32_t)st);
-      st_sys(&ctl->mask0, m0);
-      st_sys(&ctl->mask1, m1);
+    if (tid == 0) {  // diagnostic stamps: they may land after `done`
       static_assert(kResPhases == 6, "phase stamps");
-      st_sys(&ctl->phase[0], (uint32_t)(t_seen - tp));
-      st_sys(&ctl->phase[1], (uint32_t)(t_req - t_seen));
-      st_sys(&ctl->phase[2], (uint32_t)(t_rest - t_req));
-      st_sys(&ctl->phase[3], (uint32_t)(t_mid - t_rest));
-      st_sys(&ctl->phase[4], (uint32_t)(t_comp - t_mid));
-      st_sys(&ctl->phase[5], (uint32_t)(t_wb - t_comp));
-      __hip_atomic_store(&ctl->done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      st_sys(&ctl->phase[0], (uint32_t)(t_hdr - t_seen));
+      st_sys(&ctl->phase[1], (uint32_t)(t.half1 - t_hdr));
+      st_sys(&ctl->phase[2], (uint32_t)(t.landed - t.half1));
+      st_sys(&ctl->phase[3], (uint32_t)(t.half2 - t.landed));
+      st_sys(&ctl->phase[4], (uint32_t)(t.applied - t.half2));
+      st_sys(&ctl->phase[5], (uint32_t)(t_wb - t.applied));
+    }
+    // system scope: the body before `done` — only when there is one: the fence waits for every
+    // load in flight too (vmcnt counts stores and loads on gfx950), and after a mask (no packet,
+    // no fenced barrier) the polls reissued at the hit are still in flight
+    if (st == MQ_OK && op != kResHp) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    if (tid == 0) {  // done, status and the mask in one 16-B store
+      typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+      const v4u out = {seq, (uint32_t)st, m0, m1};
+      asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(&ctl->done), "v"(out) : "memory");
     }
     done = seq;
     t_last = wall_clock64();
+
   }
+  __builtin_amdgcn_s_waitcnt(0);  // the ring's polls land before the wave ends
   if (tid == 0) st_sys_sc(&ctl->state, kResExited);
 }
 
@@ -569,6 +662,7 @@ struct Resident {
   ResArea* dptr = nullptr;
   hipStream_t stream = nullptr;
   uint32_t seq = 0;
+  uint64_t hpow_uid = 0;  // the context whose GHASH powers the mailbox holds (0: none)
   bool launched = false;
   uint64_t idle = 0, life = 0;
   int khz = 100000;  // wall-clock rate
@@ -581,7 +675,7 @@ std::vector<Resident*> g_res;  // per device; never freed (the kernel may outliv
 
 void stop_all() {  // atexit: ask every resident kernel to leave (plain stores, no HIP call)
   for (Resident* r : g_res)
-    if (r && r->host) __atomic_store_n(&r->host->ctl.stop, 1u, __ATOMIC_SEQ_CST);
+    if (r && r->host) __atomic_store_n(&r->host->hdr[kHwStop], (uint64_t)1, __ATOMIC_SEQ_CST);
 }
 
 Resident* resident(int dev) {
@@ -604,11 +698,12 @@ uint32_t load_acq(const uint32_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIR
 }  // namespace
 
 // One call through the resident kernel of device `dev` (the caller holds a device guard on it).
-// `q` is the request with keys, nonce / sample, op, suite and lengths filled in; aad and body are
-// the packet bytes. Returns MQ_OK when the call was served (*status = its result, out[0, out_len)
-// = bytes [out_off, out_off + out_len) of the processed body when *status is MQ_OK, mask = the
-// header-protection mask words), else an MQ_ERR_* of the transport.
-int mq_resident_call(int dev, const ResReq& q, const uint8_t* aad, const uint8_t* body, uint8_t* out,
+// `q` is the context's request image with op, lengths and nonce / sample filled in; `uid`
+// identifies the context (its GHASH powers are copied only when another context used the mailbox
+// last); aad and body are the packet bytes. Returns MQ_OK when the call was served (*status = its
+// result, out[0, out_len) = bytes [out_off, out_off + out_len) of the processed body when *status
+// is MQ_OK, mask = the header-protection mask words), else an MQ_ERR_* of the transport.
+int mq_resident_call(int dev, const ResReq& q, uint64_t uid, const uint8_t* aad, const uint8_t* body, uint8_t* out,
                      size_t out_off, size_t out_len, int* status, uint32_t* mask) {
   Resident* r = resident(dev);
   std::lock_guard<std::mutex> lk(r->mu);
@@ -632,15 +727,33 @@ int mq_resident_call(int dev, const ResReq& q, const uint8_t* aad, const uint8_t
   const auto h0 = std::chrono::steady_clock::now();
   ResArea* a = r->host;
   const uint32_t pay = (q.aad_len + 15) & ~15u;  // the body 16-B aligned (mq_resident.h)
-  if (q.op != kResHp && (size_t)pay + q.body_len + 16 > kResMaxPkt) return MQ_ERR_INVALID_ARG;
-  std::memcpy(&a->req, &q, sizeof q);
-  a->req.pay_off = pay;
-  if (q.op != kResHp) {
+  const bool aead = q.op != kResHp;
+  if (aead && (size_t)pay + q.body_len + 16 > kResMaxPkt) return MQ_ERR_INVALID_ARG;
+  // the packet, and for an AES-128-GCM AEAD call the context's GHASH powers, before the header
+  if (aead) {
     if (q.aad_len) std::memcpy(a->data, aad, q.aad_len);
     if (q.body_len) std::memcpy(a->data + pay, body, q.body_len);
+    if (q.suite == MQ_SUITE_AES128GCM && r->hpow_uid != uid) {
+      std::memcpy(a->Hpow, q.Hpow, sizeof a->Hpow);
+      r->hpow_uid = uid;
+    }
   }
+  uint32_t w[kResHdrSlots];
+  const uint32_t n = res_hdr_words(q.suite);
+  w[kHwOp] = q.op | q.suite << 8;
+  w[kHwAad] = q.aad_len;
+  w[kHwBody] = q.body_len;
+  w[kHwPay] = pay;
+  for (int i = 0; i < 3; ++i) w[kHwNonce + i] = q.nonce[i];
+  w[kHwNonce + 3] = 0;
+  for (int i = 0; i < 4; ++i) w[kHwSample + i] = q.sample[i];
+  if (q.suite == MQ_SUITE_AES128GCM) std::memcpy(w + kHwKey, aead ? q.aes_rk : q.hp_rk, 44 * 4);
+  else std::memcpy(w + kHwKey, aead ? q.key : q.hp, 8 * 4);
   const uint32_t seq = ++r->seq;
-  __atomic_store_n(&a->ctl.seq, seq, __ATOMIC_SEQ_CST);
+  // slots 1 .. n-1, then slot 0: each one 8-B store (never torn), stores in program order (x86-64)
+  for (uint32_t i = 1; i < n; ++i)
+    __atomic_store_n(&a->hdr[i], (uint64_t)w[i] | (uint64_t)seq << 32, __ATOMIC_RELAXED);
+  __atomic_store_n(&a->hdr[0], (uint64_t)w[0] | (uint64_t)seq << 32, __ATOMIC_SEQ_CST);
   const auto t0 = std::chrono::steady_clock::now();
   bool relaunched = false;
   for (uint32_t spins = 0;; ++spins) {
@@ -649,7 +762,7 @@ int mq_resident_call(int dev, const ResReq& q, const uint8_t* aad, const uint8_t
       if (r->launched && hipStreamSynchronize(r->stream) != hipSuccess) return MQ_ERR_HIP;  // it has left
       if (load_acq(&a->ctl.done) == seq) break;  // served on its way out
       __atomic_store_n(&a->ctl.state, (uint32_t)kResRunning, __ATOMIC_SEQ_CST);
-      __atomic_store_n(&a->ctl.stop, 0u, __ATOMIC_SEQ_CST);
+      __atomic_store_n(&a->hdr[kHwStop], (uint64_t)0, __ATOMIC_SEQ_CST);
       hipLaunchKernelGGL(mq_resident_kernel, dim3(1), dim3(kResThreads), 0, r->stream, r->dptr, r->idle, r->life);
       if (hipGetLastError() != hipSuccess) {
         __atomic_store_n(&a->ctl.state, (uint32_t)kResExited, __ATOMIC_SEQ_CST);
@@ -677,8 +790,9 @@ int mq_resident_call(int dev, const ResReq& q, const uint8_t* aad, const uint8_t
   return MQ_OK;
 }
 
-// The device-side phases of device dev's last resident call in nanoseconds (ResCtl::phase);
-// returns the number written, 0 before any call.
+// The device-side phases of device dev's last resident call in nanoseconds (ResCtl::phase), then
+// the host's (request written, waited for done, result copied); returns the number written, 0
+// before any call.
 extern "C" int mq_resident_phases(int dev, uint32_t* ns, int n) {
   if (dev < 0 || !ns || n <= 0) return 0;
   Resident* r = resident(dev);

@@ -94,7 +94,7 @@ def measure(lib, _lib, calls):
         res["seal"] = {"median": round(float(np.median(ts)) * 1e6, 2), "p99": round(float(np.quantile(ts, 0.99)) * 1e6, 2)}
         res["open"] = {"median": round(float(np.median(to)) * 1e6, 2), "p99": round(float(np.quantile(to, 0.99)) * 1e6, 2)}
         if os.environ.get("MQ_RESIDENT") == "1":  # device-side phases (mq_resident_phases), median us
-            names = ("poll_round_trip", "request_loaded", "rest_loaded", "first_half", "second_half", "written_back",
+            names = ("header_broadcast", "first_half", "packet_wait", "second_half", "decrypt_applied", "written_back",
                      "host_request_written", "host_wait_done", "host_copy_out")
             res["phases_us"] = {
                 op: {n: round(float(np.median(a[:, i])) / 1e3, 2) for i, n in enumerate(names)}
