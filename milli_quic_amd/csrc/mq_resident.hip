@@ -88,10 +88,12 @@ __device__ __forceinline__ uint64_t poll_read(uint32_t k, int lane) {
 
 // Packet bytes host -> LDS: chunk c (16 B) of the mailbox's data area to s_pkt + 16c, by LDS-DMA
 // (global_load_lds_dwordx4: lane-linear LDS destination, one instruction per wave per 64
-// chunks); completes at the next fenced barrier (s_waitcnt vmcnt(0)).
-__device__ __forceinline__ void dma_chunks(const uint8_t* src, uint8_t* dst, uint32_t nch, int tid) {
-  const uint32_t w = (uint32_t)tid >> 6, lane = (uint32_t)tid & 63;
-  for (uint32_t b = 64 * w; b < nch; b += kResThreads)  // wave-uniform
+// chunks) from waves 1..3 (wave 0's first half must not wait for them); completes at the next
+// fenced barrier (s_waitcnt vmcnt(0)).
+// (t: the thread's index among the loading threads, a multiple of 64 of them: kResThreads - 64)
+__device__ __forceinline__ void dma_chunks(const uint8_t* src, uint8_t* dst, uint32_t nch, int t) {
+  const uint32_t w = (uint32_t)t >> 6, lane = (uint32_t)t & 63;
+  for (uint32_t b = 64 * w; b < nch; b += kResThreads - 64)  // wave-uniform
     if (b + lane < nch)
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 16u * (b + lane)),
                                        (__attribute__((address_space(3))) void*)(dst + 16u * b), 16, 0, 0);
@@ -137,12 +139,15 @@ __device__ __forceinline__ uint64_t rdl64(uint64_t x, int l) {
   return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(x >> 32), l) << 32) |
          (uint32_t)__builtin_amdgcn_readlane((int)x, l);
 }
-__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t x) {
-  x += dpp64<0xB1>(x);   // quad_perm [1,0,3,2]
-  x += dpp64<0x4E>(x);   // quad_perm [2,3,0,1]
-  x += dpp64<0x141>(x);  // row_half_mirror
-  x += dpp64<0x140>(x);  // row_mirror: every lane holds its row's sum
-  return rdl64(x, 0) + rdl64(x, 16) + rdl64(x, 32) + rdl64(x, 48);
+// Sum over the wave of Poly1305 limbs (< 2^27 per lane): 32-bit DPP sums inside each row of 16
+// (< 2^31), the four row sums by readlane added in 64 bits
+__device__ __forceinline__ uint64_t wave_sum_limb(uint32_t x) {
+  x += dpp32<0xB1>(x);   // quad_perm [1,0,3,2]
+  x += dpp32<0x4E>(x);   // quad_perm [2,3,0,1]
+  x += dpp32<0x141>(x);  // row_half_mirror
+  x += dpp32<0x140>(x);  // row_mirror: every lane holds its row's sum
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)x, 0) + (uint32_t)__builtin_amdgcn_readlane((int)x, 16) +
+         (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)x, 32) + (uint32_t)__builtin_amdgcn_readlane((int)x, 48);
 }
 __device__ __forceinline__ uint32_t wave_xor_u32(uint32_t x) {
   x ^= dpp32<0xB1>(x);
@@ -207,8 +212,10 @@ __device__ __forceinline__ PolyPow poly_powers(const uint32_t (&otk)[8]) {
   return PolyPow{p26_mult(e), p26_mult(v)};
 }
 // the tag of AAD||pad||C||pad||lens over the LDS packet (aad at 0, ciphertext at the aligned pay)
+// (seal: ksw = the keystream words in s_ks, so the MAC reads plaintext ^ keystream without waiting
+// for the keystream pass over the packet; open: nullptr, the packet holds the ciphertext)
 __device__ __forceinline__ void poly_tag(uint32_t aad_len, uint32_t pay, uint32_t ct_len, const PolyPow& pw,
-                                         const uint32_t (&otk)[8], int lane, uint32_t (&tag)[4]) {
+                                         const uint32_t (&otk)[8], int lane, const uint32_t* ksw, uint32_t (&tag)[4]) {
   const LdsSpace sp{s_pkt};
   const uint32_t A = (aad_len + 15) >> 4, T = (ct_len + 15) >> 4, nb = A + T + 1;
   const uint32_t K = (nb + 63) / 64;
@@ -231,6 +238,10 @@ __device__ __forceinline__ void poly_tag(uint32_t aad_len, uint32_t pay, uint32_
     } else if (i < (int)(A + T)) {
       const uint32_t o = 16u * (uint32_t)(i - (int)A);
       load_words<4>(sp, pay + o, m);
+      if (ksw) {
+#pragma unroll
+        for (int w = 0; w < 4; ++w) m[w] ^= ksw[o / 4 + w];
+      }
       const int rem = (int)(ct_len - o);
 #pragma unroll
       for (int w = 0; w < 4; ++w) m[w] &= byte_mask(rem, w);
@@ -244,7 +255,7 @@ __device__ __forceinline__ void poly_tag(uint32_t aad_len, uint32_t pay, uint32_
   }
   uint64_t s[5];
 #pragma unroll
-  for (int l = 0; l < 5; ++l) s[l] = wave_sum_u64(acc.l[l]);
+  for (int l = 0; l < 5; ++l) s[l] = wave_sum_limb(acc.l[l]);
   const uint32_t sk[4] = {otk[4], otk[5], otk[6], otk[7]};
   p26_finish(p26_from_sums(s), sk, tag);
 }
@@ -273,8 +284,10 @@ __device__ __forceinline__ void chacha20_block4(const uint32_t (&key)[8], uint32
 
 // GHASH(AAD || C || lens) on ONE wave (lane j: blocks 64k + j - z, multiplier H^64, final
 // H^(64 - j), lanes XOR-reduced), reflected basis (mq_aes.h); tag = that ^ E_K(J0)
+// (ksw: as poly_tag)
 __device__ __forceinline__ void ghash_tag(uint32_t aad_len, uint32_t pay, uint32_t P, const GfOp& m64,
-                                          const GfOp& ml, const uint32_t (&ej0)[4], int lane, uint32_t (&tag)[4]) {
+                                          const GfOp& ml, const uint32_t (&ej0)[4], int lane, const uint32_t* ksw,
+                                          uint32_t (&tag)[4]) {
   const LdsSpace sp{s_pkt};
   const uint32_t A = (aad_len + 15) >> 4, T = (P + 15) >> 4, nb = A + T + 1;
   const uint32_t K = (nb + 63) / 64;
@@ -292,6 +305,10 @@ __device__ __forceinline__ void ghash_tag(uint32_t aad_len, uint32_t pay, uint32
     } else if (i >= (int)A && i < (int)(A + T)) {
       const uint32_t o = 16u * (uint32_t)(i - (int)A);
       load_words<4>(sp, pay + o, m);
+      if (ksw) {
+#pragma unroll
+        for (int w = 0; w < 4; ++w) m[w] ^= ksw[o / 4 + w];
+      }
       const int rem = (int)(P - o);
 #pragma unroll
       for (int w = 0; w < 4; ++w) m[w] = refl(m[w] & byte_mask(rem, w));
@@ -312,13 +329,17 @@ __device__ __forceinline__ void ghash_tag(uint32_t aad_len, uint32_t pay, uint32
 // half done, decryption applied
 struct ResT { uint64_t half1, landed, half2, applied; };
 
+// the keystream pass of a request (waves 1..3): pw ^= s_ks over the P payload bytes
+__device__ __forceinline__ void apply_ks(uint32_t* pw, uint32_t P, int t, int nt) {
+  for (uint32_t w = (uint32_t)t; 4 * w < P; w += (uint32_t)nt) pw[w] ^= s_ks[w] & byte_mask((int)(P - 4 * w), 0);
+}
+
 // ChaCha20-Poly1305 seal / open of the LDS packet (aad at 0, body at the aligned pay). First half
 // (header only, while the packet lands): wave 0 makes the Poly1305 key (block 0, on its quads) and
-// the MAC's powers of r; waves 1..3 make keystream blocks 1.. (one per quad, 48 per pass) — seal
-// keeps the first pass in registers, open writes every block to s_ks. Second half: seal XORs the
-// keystream in place (later passes too), then wave 0 runs the MAC; open runs the MAC over the
-// untouched ciphertext, verifies, and applies s_ks only if the tag matched. Returns MQ_*
-// (workgroup-uniform).
+// the MAC's powers of r; waves 1..3 write keystream blocks 1.. to s_ks (one per quad, 48 per pass).
+// Second half: seal runs the MAC (wave 0) over plaintext ^ s_ks and stores the tag, and its
+// write-back applies s_ks (no pass over the packet, no barrier); open runs the MAC over the untouched ciphertext, verifies,
+// and applies s_ks only if the tag matched. Returns MQ_* (workgroup-uniform).
 __device__ int res_chacha(bool open, uint32_t aad_len, uint32_t pay, uint32_t body_len, int tid, ResT& t) {
   uint32_t key[8];
 #pragma unroll
@@ -329,57 +350,35 @@ __device__ int res_chacha(bool open, uint32_t aad_len, uint32_t pay, uint32_t bo
   const int q = tid & 3;
   uint32_t* pw = (uint32_t*)(s_pkt + pay);
   constexpr uint32_t kQuads = (kResThreads - 64) / 4;
-  uint32_t otk[8], ks1[4];
+  uint32_t otk[8];
   PolyPow pp;
-  const uint32_t b1 = 1 + (uint32_t)((tid - 64) >> 2);  // waves 1..3: first-pass block
-  // payload word 4k + q of block b: keystream ks[k] (byte offset o < P)
-  auto put = [&](uint32_t b, const uint32_t (&ks)[4]) {
-    if (b >= nblk) return;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t o = 64 * (b - 1) + 16 * k + 4 * q;
-      if (o < P) {
-        if (open) s_ks[o / 4] = ks[k];
-        else pw[o / 4] ^= ks[k] & byte_mask((int)(P - o), 0);
-      }
-    }
-  };
   if (tid < 64) {
     uint32_t ks[4];
     chacha20_block4(key, 0, n0, n1, n2, q, ks);
     otk_from_quad(ks, otk);
     pp = poly_powers(otk);
   } else {
-    chacha20_block4(key, b1, n0, n1, n2, q, ks1);
-    if (open) {
-      put(b1, ks1);
 #pragma unroll 1
-      for (uint32_t b0 = 1 + kQuads; b0 < nblk; b0 += kQuads) {
-        uint32_t ks[4];
-        const uint32_t b = b0 + (uint32_t)((tid - 64) >> 2);
-        chacha20_block4(key, b, n0, n1, n2, q, ks);
-        put(b, ks);
+    for (uint32_t b0 = 1; b0 < nblk; b0 += kQuads) {
+      uint32_t ks[4];
+      const uint32_t b = b0 + (uint32_t)((tid - 64) >> 2);
+      chacha20_block4(key, b, n0, n1, n2, q, ks);
+      if (b < nblk) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t o = 64 * (b - 1) + 16 * k + 4 * q;  // payload byte offset of word 4k + q
+          if (o < P) s_ks[o / 4] = ks[k];
+        }
       }
     }
   }
   t.half1 = wall_clock64();
-  __syncthreads();  // the packet has landed (vmcnt(0)); open: s_ks complete
+  __syncthreads();  // the packet has landed (vmcnt(0)); s_ks complete
   t.landed = wall_clock64();
-  if (!open) {
-    if (tid >= 64) {
-      put(b1, ks1);
-#pragma unroll 1
-      for (uint32_t b0 = 1 + kQuads; b0 < nblk; b0 += kQuads) {
-        uint32_t ks[4];
-        const uint32_t b = b0 + (uint32_t)((tid - 64) >> 2);
-        chacha20_block4(key, b, n0, n1, n2, q, ks);
-        put(b, ks);
-      }
-    }
-    __syncthreads();  // the ciphertext is in place
-    if (tid < 64) {  // the write-back that follows is wave 0's too: no barrier after the tag
+  if (!open) {  // the packet keeps its plaintext: the write-back (wave 0) applies s_ks
+    if (tid < 64) {
       uint32_t tag[4];
-      poly_tag(aad_len, pay, P, pp, otk, tid, tag);
+      poly_tag(aad_len, pay, P, pp, otk, tid, s_ks, tag);
       if (tid == 0) store_words<4>(LdsSpace{s_pkt}, pay + P, tag);
     }
     t.half2 = t.applied = wall_clock64();
@@ -387,24 +386,22 @@ __device__ int res_chacha(bool open, uint32_t aad_len, uint32_t pay, uint32_t bo
   }
   if (tid < 64) {
     uint32_t tag[4], got[4];
-    poly_tag(aad_len, pay, P, pp, otk, tid, tag);
+    poly_tag(aad_len, pay, P, pp, otk, tid, nullptr, tag);
     load_words<4>(LdsSpace{s_pkt}, pay + P, got);
     if (tid == 0) s_scr[12] = (tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) | (tag[3] ^ got[3]);
   }
   __syncthreads();
   t.half2 = wall_clock64();
   if (s_scr[12]) return MQ_ERR_CRYPTO;  // rustcrypto.rs:156-163; nothing decrypted
-  for (uint32_t w = (uint32_t)tid; 4 * w < P; w += kResThreads) pw[w] ^= s_ks[w] & byte_mask((int)(P - 4 * w), 0);
+  apply_ks(pw, P, tid, kResThreads);
   __syncthreads();
   t.applied = wall_clock64();
   return MQ_OK;
 }
 
-// AES-128-GCM seal / open of the LDS packet. First half: wave 0 makes E_K(J0); waves 1..3 run CTR
-// blocks (one per thread, 192 per pass) — seal keeps the first pass in registers, open writes
-// every block to s_ks. Second half: wave 0 prepares the GHASH multipliers (H^64, and H^(64 - lane)
-// from the request's powers, which land with the packet); seal XORs the keystream in place, then
-// wave 0 runs GHASH; open runs GHASH over the ciphertext, verifies, then decrypts.
+// AES-128-GCM seal / open of the LDS packet. First half: wave 0 makes E_K(J0), then — once the
+// GHASH powers it loaded itself have landed — the GHASH multipliers (H^64, and H^(64 - lane));
+// waves 1..3 write CTR blocks (one per thread, 192 per pass) to s_ks. Second half: as res_chacha.
 __device__ int res_aes(bool open, uint32_t aad_len, uint32_t pay, uint32_t body_len, int tid, ResT& t) {
   const TwLane L = tw_lane();
   const RkLds key{s_hdr + kHwKey};
@@ -413,45 +410,15 @@ __device__ int res_aes(bool open, uint32_t aad_len, uint32_t pay, uint32_t body_
   const uint32_t nblk = 1 + (P + 15) / 16;  // slot 0: E_K(J0), slot b >= 1: CTR block with counter b + 1
   uint32_t* pw = (uint32_t*)(s_pkt + pay);
   constexpr uint32_t kBlk = kResThreads - 64;
-  uint32_t ej0[4], s1[4];
-  const uint32_t b1 = 1 + (uint32_t)(tid - 64);  // waves 1..3: first-pass block
-  auto put = [&](uint32_t b, const uint32_t (&s)[4]) {
-    if (b >= nblk) return;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t o = 16 * (b - 1) + 4 * k;
-      if (o < P) {
-        if (open) s_ks[o / 4] = bswap32(s[k]);
-        else pw[o / 4] ^= bswap32(s[k]) & byte_mask((int)(P - o), 0);
-      }
-    }
-  };
-  auto block = [&](uint32_t b, uint32_t (&s)[4]) {
-    s[0] = nb0; s[1] = nb1; s[2] = nb2; s[3] = b + 1;
-    aes128_enc(key, L, s);
-  };
+  uint32_t ej0[4];
+  GfOp m64, ml;
   if (tid < 64) {
     uint32_t s[4] = {nb0, nb1, nb2, 1u};
     aes128_enc(key, L, s);
 #pragma unroll
     for (int w = 0; w < 4; ++w) ej0[w] = bswap32(s[w]);
-  } else {
-    block(b1, s1);
-    if (open) {
-      put(b1, s1);
-#pragma unroll 1
-      for (uint32_t b0 = 1 + kBlk; b0 < nblk; b0 += kBlk) {
-        uint32_t s[4];
-        block(b0 + (uint32_t)(tid - 64), s);
-        put(b0 + (uint32_t)(tid - 64), s);
-      }
-    }
-  }
-  t.half1 = wall_clock64();
-  __syncthreads();  // the packet and the GHASH powers have landed; open: s_ks complete
-  t.landed = wall_clock64();
-  GfOp m64, ml;
-  if (tid < 64) {
+    // wave 0's only LDS-DMA is the GHASH powers (the packet is waves 1..3's): wait for it alone
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint32_t h[4], hl[4];
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
@@ -460,21 +427,28 @@ __device__ int res_aes(bool open, uint32_t aad_len, uint32_t pay, uint32_t body_
     }
     m64 = gf_prepare(h);
     ml = gf_prepare(hl);
-  }
-  if (!open) {
-    if (tid >= 64) {
-      put(b1, s1);
+  } else {
 #pragma unroll 1
-      for (uint32_t b0 = 1 + kBlk; b0 < nblk; b0 += kBlk) {
-        uint32_t s[4];
-        block(b0 + (uint32_t)(tid - 64), s);
-        put(b0 + (uint32_t)(tid - 64), s);
+    for (uint32_t b0 = 1; b0 < nblk; b0 += kBlk) {
+      const uint32_t b = b0 + (uint32_t)(tid - 64);
+      uint32_t s[4] = {nb0, nb1, nb2, b + 1};
+      aes128_enc(key, L, s);
+      if (b < nblk) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t o = 16 * (b - 1) + 4 * k;
+          if (o < P) s_ks[o / 4] = bswap32(s[k]);
+        }
       }
     }
-    __syncthreads();  // the ciphertext is in place
-    if (tid < 64) {  // the write-back that follows is wave 0's too: no barrier after the tag
+  }
+  t.half1 = wall_clock64();
+  __syncthreads();  // the packet has landed; s_ks complete
+  t.landed = wall_clock64();
+  if (!open) {  // the packet keeps its plaintext: the write-back (wave 0) applies s_ks
+    if (tid < 64) {
       uint32_t tag[4];
-      ghash_tag(aad_len, pay, P, m64, ml, ej0, tid, tag);
+      ghash_tag(aad_len, pay, P, m64, ml, ej0, tid, s_ks, tag);
       if (tid == 0) store_words<4>(LdsSpace{s_pkt}, pay + P, tag);
     }
     t.half2 = t.applied = wall_clock64();
@@ -482,14 +456,14 @@ __device__ int res_aes(bool open, uint32_t aad_len, uint32_t pay, uint32_t body_
   }
   if (tid < 64) {
     uint32_t tag[4], got[4];
-    ghash_tag(aad_len, pay, P, m64, ml, ej0, tid, tag);
+    ghash_tag(aad_len, pay, P, m64, ml, ej0, tid, nullptr, tag);
     load_words<4>(LdsSpace{s_pkt}, pay + P, got);
     if (tid == 0) s_scr[12] = (tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) | (tag[3] ^ got[3]);
   }
   __syncthreads();
   t.half2 = wall_clock64();
   if (s_scr[12]) return MQ_ERR_CRYPTO;  // rustcrypto.rs:85-91; nothing decrypted
-  for (uint32_t w = (uint32_t)tid; 4 * w < P; w += kResThreads) pw[w] ^= s_ks[w] & byte_mask((int)(P - 4 * w), 0);
+  apply_ks(pw, P, tid, kResThreads);
   __syncthreads();
   t.applied = wall_clock64();
   return MQ_OK;
@@ -601,8 +575,8 @@ extern "C" __global__ __launch_bounds__(kResThreads) void mq_resident_kernel(Res
                                        (op == kResOpen && body_len < 16)));
     // the packet (and the GHASH powers) host -> LDS, landing during the first half
     if (!bad && op != kResHp) {
-      dma_chunks(area->data, s_pkt, nch, tid);
-      if (suite == MQ_SUITE_AES128GCM) dma_chunks((const uint8_t*)area->Hpow, (uint8_t*)s_hpow, 64 * 4 * 4 / 16, tid);
+      if (!w0) dma_chunks(area->data, s_pkt, nch, tid - 64);  // waves 1..3: the packet
+      else if (suite == MQ_SUITE_AES128GCM) dma_chunks((const uint8_t*)area->Hpow, (uint8_t*)s_hpow, 64, tid);
     }
     ResT t{t_hdr, t_hdr, t_hdr, t_hdr};
     int st = MQ_OK;
@@ -623,8 +597,22 @@ extern "C" __global__ __launch_bounds__(kResThreads) void mq_resident_kernel(Res
     if (!w0) continue;
     if (st == MQ_OK && op != kResHp) {
       uint4* dst = (uint4*)area->data;
+      const uint32_t P = op == kResSeal ? body_len : 0u;  // seal: payload words still plaintext
 #pragma unroll 1
-      for (uint32_t c = pay / 16 + (uint32_t)lane; c < nch; c += 64) dst[c] = *(const uint4*)(s_pkt + 16 * c);
+      for (uint32_t c = pay / 16 + (uint32_t)lane; c < nch; c += 64) {
+        uint4 v = *(const uint4*)(s_pkt + 16 * c);
+        const uint32_t w0 = 4 * c - pay / 4;  // payload word of v.x (pay is 16-B aligned)
+        if (4 * w0 + 16 <= P) {  // a whole payload chunk
+          const uint4 k = *(const uint4*)(s_ks + w0);
+          v.x ^= k.x; v.y ^= k.y; v.z ^= k.z; v.w ^= k.w;
+        } else if (4 * w0 < P) {
+          v.x ^= s_ks[w0] & byte_mask((int)(P - 4 * w0), 0);
+          v.y ^= s_ks[w0 + 1] & byte_mask((int)(P - 4 * w0), 1);
+          v.z ^= s_ks[w0 + 2] & byte_mask((int)(P - 4 * w0), 2);
+          v.w ^= s_ks[w0 + 3] & byte_mask((int)(P - 4 * w0), 3);
+        }
+        dst[c] = v;
+      }
     }
     const uint64_t t_wb = wall_clock64();
     if (tid == 0) {  // diagnostic stamps: they may land after `done`
