@@ -272,60 +272,64 @@ extern "C" __global__ __launch_bounds__(64 * kScanWaves) void mq_part_scan_kerne
 // Keyed layout (the scan kernel's workgroup, after the class segments): each row's segment (its
 // bins' packets, whole tiles) follows the majority key's classes in list 0, which end on a tile
 // boundary at `base`; bins[b] becomes the list position of bin b's first packet (the scatter's
-// cursor) and counts[0] the list's entries.
-static_assert(64 * kScanWaves == 1024, "key scan: one row per thread of a 1024-thread workgroup");
+// cursor) and counts[0] the list's entries. Each thread takes kKeyRowsPerThread consecutive rows
+// (their bins are one contiguous 256-B read), so a 4096-row table is one pass of two barriers
+// (r02/r03 took one row per thread: five passes of three barriers for config E's 4098 rows).
+constexpr int kKeyRowsPerThread = 4;
+static_assert(64 * kScanWaves == 1024, "key scan: a 1024-thread workgroup");
 __device__ void key_scan(uint32_t* __restrict__ bins, uint32_t n_rows, uint32_t* __restrict__ counts, uint32_t base) {
-  constexpr int kKeyScanThreads = 64 * kScanWaves;
-  __shared__ uint32_t s_wave[kKeyScanThreads / kWave];
-  __shared__ uint32_t s_base;
+  constexpr int kThreads = 64 * kScanWaves, R = kKeyRowsPerThread;
+  __shared__ uint32_t s_wave[kScanWaves];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (threadIdx.x == 0) s_base = base;
-  __syncthreads();
-  auto fetch = [&](uint32_t r, uint4 (&v)[kKeyClasses / 4]) {
-    const uint4* src = (const uint4*)(bins + (size_t)r * kKeyClasses);
+  uint32_t run_base = base;  // entries of list 0 before this pass (the same in every thread)
+  for (uint32_t r0 = 0; r0 < n_rows; r0 += kThreads * R) {  // workgroup-uniform
+    const uint32_t rt = r0 + (uint32_t)threadIdx.x * R;  // this thread's first row
+    uint4 v[R][kKeyClasses / 4];
 #pragma unroll
-    for (int q = 0; q < (int)kKeyClasses / 4; ++q) v[q] = r < n_rows ? src[q] : make_uint4(0, 0, 0, 0);
-  };
-  uint4 nxt[kKeyClasses / 4];
-  fetch(threadIdx.x, nxt);
-  for (uint32_t r0 = 0; r0 < n_rows; r0 += kKeyScanThreads) {  // one row per thread
-    const uint32_t r = r0 + threadIdx.x;
-    uint32_t c[kKeyClasses], tot = 0;
+    for (int q = 0; q < R; ++q) {
+      const uint4* src = (const uint4*)(bins + (size_t)(rt + q) * kKeyClasses);
 #pragma unroll
-    for (int q = 0; q < (int)kKeyClasses / 4; ++q) {
-      const uint4 v = nxt[q];
-      c[4 * q] = v.x; c[4 * q + 1] = v.y; c[4 * q + 2] = v.z; c[4 * q + 3] = v.w;
-      tot += v.x + v.y + v.z + v.w;
+      for (int k = 0; k < (int)kKeyClasses / 4; ++k) v[q][k] = rt + q < n_rows ? src[k] : make_uint4(0, 0, 0, 0);
     }
-    fetch(r + kKeyScanThreads, nxt);  // the next round's row, in flight during this one
-    const uint32_t ent = (tot + kPktsPerTile - 1) & ~(kPktsPerTile - 1);
-    const uint32_t incl = wave_incl_scan(ent);
+    uint32_t ent[R], sum = 0;
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      uint32_t tot = 0;
+#pragma unroll
+      for (int k = 0; k < (int)kKeyClasses / 4; ++k) tot += v[q][k].x + v[q][k].y + v[q][k].z + v[q][k].w;
+      ent[q] = (tot + kPktsPerTile - 1) & ~(kPktsPerTile - 1);  // the row's segment: whole tiles
+      sum += ent[q];
+    }
+    const uint32_t incl = wave_incl_scan(sum);
     if (lane == 63) s_wave[wave] = incl;
     __syncthreads();
-    uint32_t before = s_base;
-    for (int q = 0; q < wave; ++q) before += s_wave[q];
-    uint32_t at = before + incl - ent;
-    if (r < n_rows) {
-      uint4* dst = (uint4*)(bins + (size_t)r * kKeyClasses);
+    uint32_t at = run_base + incl - sum, pass = 0;
 #pragma unroll
-      for (int q = 0; q < (int)kKeyClasses / 4; ++q) {
-        uint4 v;
-        v.x = at; at += c[4 * q];
-        v.y = at; at += c[4 * q + 1];
-        v.z = at; at += c[4 * q + 2];
-        v.w = at; at += c[4 * q + 3];
-        dst[q] = v;
+    for (int q = 0; q < kScanWaves; ++q) {
+      const uint32_t t = s_wave[q];
+      if (q < wave) at += t;
+      pass += t;
+    }
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      if (rt + q >= n_rows) break;
+      uint4* dst = (uint4*)(bins + (size_t)(rt + q) * kKeyClasses);
+      uint32_t p = at;
+#pragma unroll
+      for (int k = 0; k < (int)kKeyClasses / 4; ++k) {
+        uint4 o;
+        o.x = p; p += v[q][k].x;
+        o.y = p; p += v[q][k].y;
+        o.z = p; p += v[q][k].z;
+        o.w = p; p += v[q][k].w;
+        dst[k] = o;
       }
+      at += ent[q];
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      uint32_t t = 0;
-      for (int q = 0; q < kKeyScanThreads / kWave; ++q) t += s_wave[q];
-      s_base += t;
-    }
-    __syncthreads();
+    run_base += pass;
+    __syncthreads();  // s_wave is rewritten by the next pass
   }
-  if (threadIdx.x == 0) counts[0] = s_base;
+  if (threadIdx.x == 0) counts[0] = run_base;
 }
 
 extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_scatter_kernel(
