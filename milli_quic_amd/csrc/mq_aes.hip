@@ -470,10 +470,8 @@ constexpr uint32_t kAesChunk = MQ_AES_CHUNK;
 // workgroup)
 __shared__ __attribute__((aligned(16))) uint32_t g_aes_keys[kAesMultiWaves * kPktsPerTile * kRkSlotBytes / 4];
 
-template <bool SINGLE>
-__device__ __forceinline__ void aes_tables(const KeyRow* __restrict__ kt) {
-  build_tw(threadIdx.x, blockDim.x);
-  if (SINGLE) {
+// the key-dependent tables of a single-key workgroup (row kt[0]); ends with a barrier
+__device__ __forceinline__ void aes_key_tables(const KeyRow* __restrict__ kt) {
     if (threadIdx.x < kRkSlotBytes / 4) g_aes_keys[threadIdx.x] = kt[0].aes_rk[threadIdx.x];  // aes_rk || hp_rk
     const uint32_t w = wave_id();
     if (w < 8) {  // waves 0..7: the half table of H^(w + 1) for the tags' final multiplies
@@ -486,9 +484,13 @@ __device__ __forceinline__ void aes_tables(const KeyRow* __restrict__ kt) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) h8[q] = brev(kt[0].H[7][q]);
     build_gh(h8, threadIdx.x, blockDim.x);  // ends with a barrier
-  } else {
-    __syncthreads();
-  }
+}
+
+template <bool SINGLE>
+__device__ __forceinline__ void aes_tables(const KeyRow* __restrict__ kt) {
+  build_tw(threadIdx.x, blockDim.x);
+  if (SINGLE) aes_key_tables(kt);
+  else __syncthreads();
 }
 
 template <bool SINGLE, bool OPEN, int GH, bool CACHED, class K>
@@ -505,12 +507,13 @@ __device__ __forceinline__ void aes_stream_tiles(const KeyRow* __restrict__ kt, 
                                                  const uint32_t* __restrict__ index,
                                                  const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status,
                                                  uint64_t* __restrict__ pn_out, const uint2* __restrict__ hpm,
-                                                 uint32_t skip) {
+                                                 uint32_t skip, uint32_t first, uint32_t stride) {
   const uint32_t w = wave_id();
   const int lane = (int)(threadIdx.x & (kWave - 1)), j = lane & (kLanesPerPkt - 1);
   constexpr uint32_t W = aes_waves(SINGLE), C = SINGLE ? 1u : kAesChunk;
   uint32_t wt_kid = 0xFFFFFFFFu;  // multi-key: the row whose half table and key schedules the wave holds
-  for_tiles<OPEN, C>(blockIdx.x * W + w, gridDim.x * W, desc, n, index, n_dev, hpm,
+  (void)W;
+  for_tiles<OPEN, C>(first, stride, desc, n, index, n_dev, hpm,
                   [&](uint32_t t, const TilePrefetch& pf) __attribute__((always_inline)) {
     PktCtx c;
     const KeyRow* row;
@@ -597,7 +600,8 @@ __device__ __forceinline__ bool aes_hot_split(const uint32_t* __restrict__ hot, 
     if (!aes_hot_split<SINGLE>(hot, kt, n_dev, skip)) return;                                             \
     aes_tables<SINGLE>(kt);                                                                               \
     aes_stream_tiles<SINGLE, false>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr,  \
-                                    nullptr, skip);                                                       \
+                                    nullptr, skip, blockIdx.x * aes_waves(SINGLE) + wave_id(),            \
+                                    gridDim.x * aes_waves(SINGLE));                                       \
   }                                                                                                       \
   extern "C" __global__ __launch_bounds__(64 * aes_waves(SINGLE)) void NAME_OPEN(                           \
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
@@ -608,10 +612,64 @@ __device__ __forceinline__ bool aes_hot_split(const uint32_t* __restrict__ hot, 
     if (!aes_hot_split<SINGLE>(hot, kt, n_dev, skip)) return;                                             \
     aes_tables<SINGLE>(kt);                                                                               \
     aes_stream_tiles<SINGLE, true>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm, \
-                                   skip);                                                                 \
+                                   skip, blockIdx.x * aes_waves(SINGLE) + wave_id(),                      \
+                                   gridDim.x * aes_waves(SINGLE));                                        \
   }
 MQ_AES_KERNELS(mq_aes_seal_kernel, mq_aes_open_kernel, false)
 MQ_AES_KERNELS(mq_aes_seal1_kernel, mq_aes_open1_kernel, true)
+
+// Key-segmented single-key kernels (r03): for a partition list in the keyed layout whose keys carry
+// many packets each (config C with 1024 keys: 128 tiles per key), every key's segment runs at
+// single-key speed — one persistent workgroup per CU walks segments (the hot key's classes at the
+// list's front, then row r's segment, hot[] and rowseg[] from the partition), rebuilding only the
+// key-dependent tables (round keys, the GHASH table of H^8, the half tables of H^1..H^8: a few us)
+// between them, its 16 waves striding the segment's tiles. The 12-wave multi-key kernel pays for
+// key changes per tile instead (per-lane key set-up, the bit-holed final multiply: 1024-key C 21 %
+// slower than one key on the same packets, profiles/r03p_scatter_probe.json).
+template <bool OPEN>
+__device__ __forceinline__ void aes_seg_tiles(const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena,
+                                              uint64_t arena_len, const mq_pkt_desc* __restrict__ desc,
+                                              const uint32_t* __restrict__ list, const uint32_t* __restrict__ hot,
+                                              const uint32_t* __restrict__ rowseg, uint8_t* __restrict__ status,
+                                              uint64_t* __restrict__ pn_out, const uint2* __restrict__ hpm) {
+  constexpr uint32_t W = aes_waves(true);
+  build_tw(threadIdx.x, blockDim.x);  // key-independent: once
+  const uint32_t w = wave_id();
+  for (uint32_t sg = blockIdx.x; sg <= n_rows; sg += gridDim.x) {  // segment 0: the hot key; 1 + r: row r
+    uint32_t row, first, ent;
+    if (sg == 0) {
+      row = hot[0];
+      first = 0;
+      ent = hot[1];
+    } else {
+      row = sg - 1;
+      first = rowseg[2 * row];
+      ent = rowseg[2 * row + 1];
+    }
+    row = __builtin_amdgcn_readfirstlane(row);
+    first = __builtin_amdgcn_readfirstlane(first);
+    ent = __builtin_amdgcn_readfirstlane(ent);
+    if (row >= n_rows || ent == 0) continue;  // workgroup-uniform
+    __syncthreads();  // every wave is done with the previous segment's tables
+    const KeyRow* ks = kt + row;  // the segment's row as a one-row table (validation uses n_rows)
+    aes_key_tables(ks);  // ends with a barrier
+    aes_stream_tiles<true, OPEN>(ks, n_rows, arena, arena_len, desc, first + ent, list, nullptr, status, pn_out, hpm,
+                                 first / kPktsPerTile, w, W);
+  }
+}
+extern "C" __global__ __launch_bounds__(64 * aes_waves(true)) void mq_aes_seals_kernel(
+    const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
+    const mq_pkt_desc* __restrict__ desc, const uint32_t* __restrict__ list, const uint32_t* __restrict__ hot,
+    const uint32_t* __restrict__ rowseg, uint8_t* __restrict__ status) {
+  aes_seg_tiles<false>(kt, n_rows, arena, arena_len, desc, list, hot, rowseg, status, nullptr, nullptr);
+}
+extern "C" __global__ __launch_bounds__(64 * aes_waves(true)) void mq_aes_opens_kernel(
+    const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
+    const mq_pkt_desc* __restrict__ desc, const uint32_t* __restrict__ list, const uint32_t* __restrict__ hot,
+    const uint32_t* __restrict__ rowseg, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,
+    const uint2* __restrict__ hpm) {
+  aes_seg_tiles<true>(kt, n_rows, arena, arena_len, desc, list, hot, rowseg, status, pn_out, hpm);
+}
 
 extern "C" __global__ __launch_bounds__(256) void mq_aes_hp_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, const uint32_t* __restrict__ key_ids,
@@ -682,12 +740,24 @@ static uint32_t aes_grid(uint32_t tiles, uint32_t waves, int cus) {
 // (mq_host.cpp, one per device and caller stream), so each CU moves from one tile kernel to the
 // other as its own workgroup ends, not after the other kernel's last one; s when not forked.
 // cus: the device's compute units (the persistent grid).
+// rowseg (a keyed partition list, mq_partition_rowseg): the key-segmented kernels run the whole
+// list (hot key included) instead of the hot split + multi-key kernel.
 hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena, uint64_t arena_len,
                          const mq_pkt_desc* desc, uint32_t n, const uint32_t* index, const uint32_t* n_dev,
                          const uint32_t* hot, uint8_t* status, uint64_t* pn_out, uint2* hpm, bool own_hp,
-                         hipStream_t s, hipStream_t hs, int cus) {
+                         hipStream_t s, hipStream_t hs, int cus, const uint32_t* rowseg) {
   const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
   if (tiles == 0) return hipSuccess;
+  if (rowseg && index && hot && n_rows > 1 && !own_hp) {
+    const uint32_t blocks = (uint32_t)(cus > 0 ? cus : 256);
+    if (open)
+      hipLaunchKernelGGL(mq_aes_opens_kernel, dim3(blocks), dim3(64 * aes_waves(true)), 0, s, kt, n_rows, arena,
+                         arena_len, desc, index, hot, rowseg, status, pn_out, hpm);
+    else
+      hipLaunchKernelGGL(mq_aes_seals_kernel, dim3(blocks), dim3(64 * aes_waves(true)), 0, s, kt, n_rows, arena,
+                         arena_len, desc, index, hot, rowseg, status);
+    return hipGetLastError();
+  }
   const uint32_t waves = aes_waves(n_rows == 1), blocks = aes_grid(tiles, waves, cus);
   // a partition list over several rows: the hot key's segment on a single-key kernel first
   hot = (hot && index && n_rows > 1) ? hot : nullptr;

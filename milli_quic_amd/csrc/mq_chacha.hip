@@ -16,6 +16,16 @@
 
 namespace mq {
 
+// Byte stride between the LDS images of a packet's consecutive keystream blocks: 64. The
+// MQ_PROF_SKIP & 128 diagnostic build (never the product) uses 68 — a 17-dword stride, so the
+// eight lanes of a packet hit eight distinct LDS banks — computing garbage with the same
+// instructions: its time minus the product's is what the keystream XOR's bank conflicts cost.
+#if MQ_PROF_SKIP & 128
+constexpr uint32_t kKsStride = 68;
+#else
+constexpr uint32_t kKsStride = 64;
+#endif
+
 // Interleaved Poly1305 of the AEAD MAC input for the octet's packet (RFC 8439 §2.8: AAD||pad16||
 // CT||pad16||LE64(len AAD)||LE64(len CT)): lane j takes MAC blocks 8k + j, Horner with r^8, one
 // final multiply by r^(8-j), then the octet sum. Every lane of the octet returns the same tag.
@@ -222,7 +232,7 @@ __device__ __forceinline__ void cc_pool_run(const CcPool& pool) {
     const uint32_t r0 = r[0], r1 = r[1], pay = r1 & 0x1ffffu, P = r1 >> 17;
     const uint32_t idx = e - eq, pn_len = r0 >> 8;
     const bool hp = act && idx == (r0 & 0xffu);  // the packet's last entry: its HP block
-    const uint32_t cb = kCcPoolSlot + idx, o = 64u * (cb - 1);
+    const uint32_t cb = kCcPoolSlot + idx, o = kKsStride * (cb - 1);
     const KeyRow* row = SINGLE || !act ? pool.kt : pool.kt + r[3];  // an idle lane's record may be stale
     uint32_t key[8];
     if (SINGLE) {  // both keys wave-uniform (SGPRs); pick per lane
@@ -267,12 +277,12 @@ struct ChaChaPolicy {
   template <class S>
   static __device__ __forceinline__ void load_block(const S& sp, typename S::off_t pay, uint32_t ctr,
                                                     uint32_t (&raw)[17]) {
-    load_raw<16>(sp, pay + 64 * (ctr > 0 ? ctr - 1 : 0), raw);
+    load_raw<16>(sp, pay + kKsStride * (ctr > 0 ? ctr - 1 : 0), raw);
   }
   template <class S>
   static __device__ __forceinline__ void store_block(const S& sp, typename S::off_t pay, uint32_t ctr, uint32_t P,
                                                      const uint32_t (&ks)[16], const uint32_t (&raw)[17]) {
-    const uint32_t o = 64 * (ctr - 1);
+    const uint32_t o = kKsStride * (ctr - 1);
     xor_words<16>(sp, pay + o, ks, (int)min(64u, P - o), raw);
   }
 

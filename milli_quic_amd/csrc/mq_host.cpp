@@ -32,7 +32,8 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
                          uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
                          const uint32_t* index, const uint32_t* n_dev, const uint32_t* hot,
                          uint8_t* status, uint64_t* pn_out, uint2* hpm, bool own_hp, hipStream_t s,
-                         hipStream_t hot_stream, int cus);
+                         hipStream_t hot_stream, int cus, const uint32_t* rowseg = nullptr);
+const uint32_t* mq_partition_rowseg(uint32_t n, uint32_t n_rows, const uint32_t* counts);
 hipError_t mq_launch_mixed_open_hp(const KeyRow* kt, uint32_t n_rows, const uint8_t* arena, uint64_t arena_len,
                                    const mq_pkt_desc* desc, uint32_t n, uint2* hpm, hipStream_t s);
 hipError_t mq_launch_aes_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t* key_ids,
@@ -858,10 +859,17 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
     // 1.346 -> 1.562 ms seal), because its 40-KiB workgroups take CUs that the persistent AES
     // grids (one 152-KiB workgroup per CU) then wait for. Side streams are per (device, caller
     // stream): mq_runtime.h.
-    auto fork = fork_enabled() ? side_streams().fork(kt->device, s, 1) : mq::SideStreams<HipBackend>::Fork();
+    // Keys with many packets each (on average >= kSegPackets per row, keyed layout): the
+    // key-segmented single-key kernels run list 0 whole, no fork (mq_aes.hip aes_seg_tiles)
+    constexpr uint32_t kSegPackets = 512;
+    const char* seg_env = std::getenv("MQ_AES_SEG");  // diagnostic: 0 = never
+    const uint32_t* rowseg = (seg_env && seg_env[0] == '0') || (uint64_t)n < (uint64_t)kSegPackets * kt->rows
+                                 ? nullptr
+                                 : mq_partition_rowseg(n, kt->rows, counts);
+    auto fork = fork_enabled() && !rowseg ? side_streams().fork(kt->device, s, 1) : mq::SideStreams<HipBackend>::Fork();
     hipStream_t s_hot = fork ? fork.side(0) : s, s_list1 = s;
     e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list, counts, counts + 2, status, pn_out,
-                      hpm, false, s, s_hot, cus);
+                      hpm, false, s, s_hot, cus, rowseg);
     if (e == hipSuccess && aes_only)
       e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list + cap, counts + 1, nullptr, status,
                         pn_out, hpm, false, s_list1, s_list1, cus);

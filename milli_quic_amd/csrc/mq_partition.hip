@@ -201,14 +201,16 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_count_kernel(
 // kernel waits on memory once instead of once per class (r01: 26 us per partition, rocprof).
 constexpr int kScanWaves = 16, kClassesPerWave = kClasses / kScanWaves;
 static_assert(kClasses % kScanWaves == 0, "classes per scan wave");
-__device__ void key_scan(uint32_t* __restrict__ bins, uint32_t n_rows, uint32_t* __restrict__ counts, uint32_t base);
+__device__ void key_scan(uint32_t* __restrict__ bins, uint32_t n_rows, uint32_t* __restrict__ counts, uint32_t base,
+                         uint32_t* __restrict__ rowseg);
 
 extern "C" __global__ __launch_bounds__(64 * kScanWaves) void mq_part_scan_kernel(uint32_t* __restrict__ hist,
                                                                                  uint32_t nblocks, uint32_t cap,
                                                                                  uint32_t* __restrict__ counts,
                                                                                  uint32_t* __restrict__ seg,
                                                                                  uint32_t* __restrict__ bins,
-                                                                                 uint32_t n_rows) {
+                                                                                 uint32_t n_rows,
+                                                                                 uint32_t* __restrict__ rowseg) {
   __shared__ uint32_t s_list0;
   __shared__ uint32_t s_tot[kClasses];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -265,19 +267,21 @@ extern "C" __global__ __launch_bounds__(64 * kScanWaves) void mq_part_scan_kerne
   }
   if (bins) {  // keyed layout: the other AES keys' segments follow (workgroup-uniform)
     __syncthreads();
-    key_scan(bins, n_rows, counts, s_list0);
+    key_scan(bins, n_rows, counts, s_list0, rowseg);
   }
 }
 
 // Keyed layout (the scan kernel's workgroup, after the class segments): each row's segment (its
 // bins' packets, whole tiles) follows the majority key's classes in list 0, which end on a tile
 // boundary at `base`; bins[b] becomes the list position of bin b's first packet (the scatter's
-// cursor) and counts[0] the list's entries. Each thread takes kKeyRowsPerThread consecutive rows
+// cursor), rowseg[2r], rowseg[2r + 1] = row r's segment (first entry, entries including the tile
+// padding) and counts[0] the list's entries. Each thread takes kKeyRowsPerThread consecutive rows
 // (their bins are one contiguous 256-B read), so a 4096-row table is one pass of two barriers
 // (r02/r03 took one row per thread: five passes of three barriers for config E's 4098 rows).
 constexpr int kKeyRowsPerThread = 4;
 static_assert(64 * kScanWaves == 1024, "key scan: a 1024-thread workgroup");
-__device__ void key_scan(uint32_t* __restrict__ bins, uint32_t n_rows, uint32_t* __restrict__ counts, uint32_t base) {
+__device__ void key_scan(uint32_t* __restrict__ bins, uint32_t n_rows, uint32_t* __restrict__ counts, uint32_t base,
+                         uint32_t* __restrict__ rowseg) {
   constexpr int kThreads = 64 * kScanWaves, R = kKeyRowsPerThread;
   __shared__ uint32_t s_wave[kScanWaves];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -313,6 +317,8 @@ __device__ void key_scan(uint32_t* __restrict__ bins, uint32_t n_rows, uint32_t*
 #pragma unroll
     for (int q = 0; q < R; ++q) {
       if (rt + q >= n_rows) break;
+      // the row's segment of list 0 (the key-segmented AES kernels walk these)
+      *(uint2*)(rowseg + 2 * (size_t)(rt + q)) = make_uint2(at, ent[q]);
       uint4* dst = (uint4*)(bins + (size_t)(rt + q) * kKeyClasses);
       uint32_t p = at;
 #pragma unroll
@@ -387,6 +393,14 @@ constexpr uint32_t kMetaWords = 4 + kClasses + 2 * kVoteSlices;
 // meta (2 totals, hot row, hot segment entries, kClasses segment starts) | keyed bins, 256-B aligned pieces
 static size_t part_align(size_t b) { return (b + 255) & ~(size_t)255; }
 
+// The per-row segments of a keyed partition (rowseg, 2 words per row after the keyed bins), or
+// null when mq_launch_partition(n, n_rows) does not lay the list out keyed. counts: the
+// partition's meta (as passed to mq_launch_partition).
+const uint32_t* mq_partition_rowseg(uint32_t n, uint32_t n_rows, const uint32_t* counts) {
+  if (!keyed_layout(n, n_rows)) return nullptr;
+  return (const uint32_t*)((const uint8_t*)counts + part_align(sizeof(uint32_t) * kMetaWords)) + key_bins(n);
+}
+
 hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_desc* desc, uint32_t n,
                                uint32_t* list, uint32_t* hist, uint32_t* counts, hipStream_t s) {
   const uint32_t nblocks = (n + kPartBlock - 1) / kPartBlock;
@@ -407,7 +421,7 @@ hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_d
   hipLaunchKernelGGL(mq_part_count_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, kt, n_rows, desc, n,
                      nblocks, votes, max(nv, used), hot, hist, bins);
   hipLaunchKernelGGL(mq_part_scan_kernel, dim3(1), dim3(64 * kScanWaves), 0, s, hist, nblocks, cap, counts, seg,
-                     bins, n_rows);
+                     bins, n_rows, bins ? bins + key_bins(n) : nullptr);
   hipLaunchKernelGGL(mq_part_scatter_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, kt, n_rows, desc, n,
                      nblocks, hot, hist, seg, list, bins);
   return hipGetLastError();
@@ -417,7 +431,7 @@ size_t mq_partition_workspace(uint32_t n) {
   const size_t nblocks = (n + kPartBlock - 1) / kPartBlock;
   return part_align(sizeof(uint32_t) * 2 * (size_t)mq_partition_list_cap(n)) +
          part_align(sizeof(uint32_t) * kClasses * nblocks) + part_align(sizeof(uint32_t) * kMetaWords) +
-         part_align(sizeof(uint32_t) * key_bins(n));
+         part_align(sizeof(uint32_t) * (key_bins(n) + key_bins(n) / 8));  // keyed bins + rowseg
 }
 
 // offsets of the pieces inside the partition workspace

@@ -2,7 +2,8 @@
 
 Times seal and open of one workload with the product library and with each variant that skips
 one phase (1 ChaCha rounds, 2 MAC, 4 LDS->HBM store, 8 HBM->LDS staging, 16 AES rounds, 12 both
-copies, 32 every tile on the direct path); the difference is what that phase costs.
+copies, 32 every tile on the direct path; 128: the ChaCha keystream XOR with a conflict-free
+68-B block stride); the difference is what that phase costs.
 MQ_PROF_DIR names the variants' directory (default milli_quic_amd/prof, which gpurun does not ship:
 copy them under tools/ab_libs/ for a GPU run). Diagnostic only: variants compute garbage.
 Usage: python tools/phase_cost.py [b|c|e|bk|ck] [packets]   (bk, ck: 1024 key rows)
@@ -58,7 +59,7 @@ def main():
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
     libs = [("product", os.path.join(ROOT, "milli_quic_amd", "libmq_aead.so"))]
     names = {1: "no chacha rounds", 2: "no MAC", 4: "no store", 8: "no staging", 16: "no AES rounds",
-             12: "no store+staging", 32: "all direct"}
+             12: "no store+staging", 32: "all direct", 128: "ks stride 68"}
     for m, nm in names.items():
         p = os.path.join(BUILD, f"prof_{m}.so")
         if os.path.exists(p):
