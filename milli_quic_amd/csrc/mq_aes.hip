@@ -591,13 +591,24 @@ __device__ __forceinline__ bool aes_hot_split(const uint32_t* __restrict__ hot, 
   return true;
 }
 
+// workgroup-uniform, before any table is built: whether this workgroup of a persistent grid has
+// a tile (a partition list's device count may be small or zero — an AES batch's leftover list is
+// usually empty, and 256 workgroups building their tables for nothing cost ~35 us)
+template <bool SINGLE>
+__device__ __forceinline__ bool aes_wg_has_work(uint32_t n, const uint32_t* __restrict__ n_dev, uint32_t skip) {
+  const uint32_t count = n_dev ? *n_dev : n;
+  const uint32_t tiles = (count + kPktsPerTile - 1) / kPktsPerTile;
+  const uint32_t c = SINGLE ? 1u : kAesChunk;
+  return skip + blockIdx.x * aes_waves(SINGLE) * c < tiles;
+}
+
 #define MQ_AES_KERNELS(NAME_SEAL, NAME_OPEN, SINGLE)                                                      \
   extern "C" __global__ __launch_bounds__(64 * aes_waves(SINGLE)) void NAME_SEAL(                           \
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
       const uint32_t* __restrict__ n_dev, const uint32_t* __restrict__ hot, uint8_t* __restrict__ status) { \
     uint32_t skip;                                                                                        \
-    if (!aes_hot_split<SINGLE>(hot, kt, n_dev, skip)) return;                                             \
+    if (!aes_hot_split<SINGLE>(hot, kt, n_dev, skip) || !aes_wg_has_work<SINGLE>(n, n_dev, skip)) return;   \
     aes_tables<SINGLE>(kt);                                                                               \
     aes_stream_tiles<SINGLE, false>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr,  \
                                     nullptr, skip, blockIdx.x * aes_waves(SINGLE) + wave_id(),            \
@@ -609,7 +620,7 @@ __device__ __forceinline__ bool aes_hot_split(const uint32_t* __restrict__ hot, 
       const uint32_t* __restrict__ n_dev, const uint32_t* __restrict__ hot, uint8_t* __restrict__ status, \
       uint64_t* __restrict__ pn_out, const uint2* __restrict__ hpm) {                                     \
     uint32_t skip;                                                                                        \
-    if (!aes_hot_split<SINGLE>(hot, kt, n_dev, skip)) return;                                             \
+    if (!aes_hot_split<SINGLE>(hot, kt, n_dev, skip) || !aes_wg_has_work<SINGLE>(n, n_dev, skip)) return;   \
     aes_tables<SINGLE>(kt);                                                                               \
     aes_stream_tiles<SINGLE, true>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm, \
                                    skip, blockIdx.x * aes_waves(SINGLE) + wave_id(),                      \

@@ -176,16 +176,31 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_count_kernel(
   const uint32_t hot = fold_votes(votes, nv);  // the same in every wave of every block
   if (blockIdx.x == 0 && threadIdx.x == 0) *hot_p = hot;  // for the scatter
   __syncthreads();
+  uint32_t kb[kPartItems];
+  bool kd[kPartItems];
 #pragma unroll
   for (int k = 0; k < kPartItems; ++k) {
     const uint32_t i = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
     const bool in = i < n;
     const uint32_t c = in ? part_class(hot, it[k]) : 0u;
-    const bool keyed = bins && in && c / kLenClasses == 1;
-    // keyed bins: one global atomic per packet (the bins of a wave's lanes are mostly distinct:
-    // packets of many keys; equal ones serialise inside the instruction)
-    if (keyed) atomicAdd(&bins[key_bin(it[k])], 1u);
-    if (in && !keyed) atomicAdd(&s_cnt[c], 1u);
+    kd[k] = bins && in && c / kLenClasses == 1;
+    kb[k] = kd[k] ? key_bin(it[k]) : 0u;
+    if (in && !kd[k]) atomicAdd(&s_cnt[c], 1u);
+  }
+  // keyed bins: one global atomic per distinct bin of the thread's items (a thread's items are
+  // kPartThreads descriptors apart: with keys assigned round-robin over 1024 rows, as in config C
+  // with 1024 keys, all four share a bin — 4x fewer atomics on the 1024 hot addresses)
+#pragma unroll
+  for (int k = 0; k < kPartItems; ++k) {
+    bool first = kd[k];
+    uint32_t cnt = 1;
+#pragma unroll
+    for (int j = 0; j < kPartItems; ++j) {
+      const bool same = kd[j] && kb[j] == kb[k];
+      if (j < k && same) first = false;
+      if (j > k && same) ++cnt;
+    }
+    if (first) atomicAdd(&bins[kb[k]], cnt);
   }
   __syncthreads();
   if (threadIdx.x < kClasses) hist[(size_t)threadIdx.x * nblocks + blockIdx.x] = s_cnt[threadIdx.x];
@@ -350,12 +365,40 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_scatter_kerne
   if (threadIdx.x < kClasses) s_rank[threadIdx.x] = hist[(size_t)threadIdx.x * nblocks + blockIdx.x];
   __syncthreads();
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  // keyed bins: the thread's items of one bin claim their positions with one atomic (as counted)
+  uint32_t kb[kPartItems], kpos[kPartItems];
+  bool kd[kPartItems];
 #pragma unroll
   for (int k = 0; k < kPartItems; ++k) {
     const uint32_t i = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
     const uint32_t c = i < n ? part_class(hot, it[k]) : 0u;
-    const bool keyed = bins && i < n && c / kLenClasses == 1;
-    if (keyed) list[atomicAdd(&bins[key_bin(it[k])], 1u)] = i;  // position inside the bin: any order
+    kd[k] = bins && i < n && c / kLenClasses == 1;
+    kb[k] = kd[k] ? key_bin(it[k]) : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < kPartItems; ++k) {
+    int lead = k;
+    uint32_t cnt = 1, rank = 0;
+#pragma unroll
+    for (int j = 0; j < kPartItems; ++j) {
+      const bool same = kd[j] && kb[j] == kb[k];
+      if (j < k && same) { rank += 1; lead = lead == k ? j : lead; }
+      if (j > k && same) ++cnt;
+    }
+    uint32_t base = 0;
+    if (kd[k] && lead == k) base = atomicAdd(&bins[kb[k]], cnt);
+    // a follower takes the leader's position (its base: the leader comes first in k order) + rank
+#pragma unroll
+    for (int j = 0; j < kPartItems; ++j)
+      if (j == lead && j < k) base = kpos[j];
+    kpos[k] = kd[k] ? base + rank : 0u;
+    if (kd[k]) list[kpos[k]] = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;  // any order in a bin
+  }
+#pragma unroll
+  for (int k = 0; k < kPartItems; ++k) {
+    const uint32_t i = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
+    const uint32_t c = i < n ? part_class(hot, it[k]) : 0u;
+    const bool keyed = kd[k];
     const bool in = i < n && !keyed;
     // lanes of this wave with the same class (7 ballots), rank among them = peers below
     uint64_t peers = __ballot(in);
