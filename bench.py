@@ -348,11 +348,15 @@ PARTITION = ("mq_part_init_kernel", "mq_part_count_kernel", "mq_part_scan_kernel
 AES_LIST0 = ("mq_aes_seal1_kernel", "mq_aes_seal_kernel")
 
 
-def seal_kernels(cfg, n_rows):
+def seal_kernels(cfg, n_rows, n=1 << 20):
     if cfg == "b":
         return ("mq_chacha_seal1_kernel",) if n_rows == 1 else ("mq_chacha_seal_kernel",)
     if cfg == "c":
-        return ("mq_aes_seal1_kernel",) if n_rows == 1 else PARTITION + AES_LIST0 + ("mq_aes_seal_kernel",)
+        if n_rows == 1:
+            return ("mq_aes_seal1_kernel",)
+        if n >= 512 * n_rows:  # mq_host.cpp: keys with >= 512 packets each: the key-segmented kernel
+            return PARTITION + ("mq_aes_seals_kernel", "mq_aes_seal_kernel")
+        return PARTITION + AES_LIST0 + ("mq_aes_seal_kernel",)
     if cfg == "e":
         return PARTITION + AES_LIST0 + ("mq_chacha_seal_kernel",)
     return None
@@ -364,11 +368,11 @@ def kernel_key(name):
     return k[5:] if k.startswith("void ") else k
 
 
-def load_traffic(cfg, kerns):
+def load_traffic(cfg, kerns, keys=1):
     """HBM bytes per seal composite (sum over its kernels) from the committed rocprofv3 PMC summary
-    (profiles/pmc_traffic_<cfg>.json, written by tools/pmc_summary.py: FETCH_SIZE x 2 + WRITE_SIZE),
-    measured at the default 2^20 packets per GPU (reported only for that size)."""
-    path = os.path.join(ROOT, "profiles", f"pmc_traffic_{cfg}.json")
+    (profiles/pmc_traffic_<cfg>[_k<keys>].json, written by tools/pmc_summary.py: FETCH_SIZE x 2 +
+    WRITE_SIZE), measured at the default 2^20 packets per GPU (reported only for that size)."""
+    path = os.path.join(ROOT, "profiles", f"pmc_traffic_{cfg}.json" if keys == 1 else f"pmc_traffic_{cfg}_k{keys}.json")
     try:
         with open(path) as f:
             d = json.load(f)["kernels"]
@@ -467,10 +471,10 @@ def main():
     if rank == 0:
         algo_bytes = 2.0 * wire  # per launch: read + write of every wire byte
         achieved = algo_bytes / (seal_ms * 1e-3) / 1e9
-        kerns = seal_kernels(args.config, len(w.keys))
+        kerns = seal_kernels(args.config, len(w.keys), w.n)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": load_traffic(args.config, kerns) if (w.n == 1 << 20 and args.keys == 1) else None,
+                "traffic": load_traffic(args.config, kerns, args.keys) if w.n == 1 << 20 else None,
                 # north_star's "HBM-read roofline" fraction: wire bytes read per seal ÷ 8 TB/s
                 "read_frac": round(wire / (seal_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "kernel": ("seal composite: " if args.config != "e" else "seal batch: ") + " + ".join(kerns),

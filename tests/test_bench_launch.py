@@ -87,7 +87,10 @@ def test_roofline_seal_composite_traffic():
     assert bench.seal_kernels("b", 1024) == ("mq_chacha_seal_kernel",)
     assert bench.seal_kernels("c", 1) == ("mq_aes_seal1_kernel",)
     assert bench.seal_kernels("e", 4098) == bench.PARTITION + bench.AES_LIST0 + ("mq_chacha_seal_kernel",)
-    assert bench.seal_kernels("c", 1024) == bench.PARTITION + bench.AES_LIST0 + ("mq_aes_seal_kernel",)
+    # 1024 keys over 2^20 packets (>= 512 per row): the key-segmented kernel runs list 0 (r03);
+    # 4096 keys: the hot split and the multi-key kernel
+    assert bench.seal_kernels("c", 1024) == bench.PARTITION + ("mq_aes_seals_kernel", "mq_aes_seal_kernel")
+    assert bench.seal_kernels("c", 4096) == bench.PARTITION + bench.AES_LIST0 + ("mq_aes_seal_kernel",)
     assert bench.kernel_key("void mq_mixed_hp_kernel(mq::KeyRow const*, unsigned int)") == "mq_mixed_hp_kernel"
     for cfg in ("b", "c"):
         ks = bench.seal_kernels(cfg, 1)

@@ -1,6 +1,6 @@
 """Minimal profiling driver: `reps` seal+open passes of one workload (for rocprofv3 runs).
 
-Usage: python tools/prof_driver.py [b|c|e] [packets] [reps]
+Usage: python tools/prof_driver.py [b|c|e|ck] [packets] [reps]   (ck: config C with 1024 keys)
 """
 import os
 import sys
@@ -18,7 +18,8 @@ def main():
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
     reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
     assert _lib.load().mq_device_init(0) == 0
-    w = {"b": workload.config_b, "c": workload.config_c, "e": workload.config_e}[cfg](n)
+    w = {"b": workload.config_b, "c": workload.config_c, "e": workload.config_e,
+         "ck": lambda m: workload.config_c(m, n_keys=1024)}[cfg](n)
     dev = torch.device("cuda", 0)
     kt = KeyTable(w.keys)
     arena = torch.from_numpy(w.arena).to(dev)
