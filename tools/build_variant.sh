@@ -12,7 +12,7 @@ O=$C/build/var_$NAME
 mkdir -p $O $ROOT/tools/ab_libs
 HIPFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result -Wno-align-mismatch"
 OBJS=""
-for f in mq_chacha.hip mq_aes.hip mq_partition.hip mq_record.hip mq_derive.hip mq_send.hip mq_recv.hip mq_host.cpp; do
+for f in mq_chacha.hip mq_aes.hip mq_partition.hip mq_record.hip mq_derive.hip mq_send.hip mq_recv.hip mq_resident.hip mq_host.cpp; do
   if [[ " $SRCS " == *" $f "* ]]; then
     /opt/rocm/bin/hipcc $HIPFLAGS $FLAGS -c $C/$f -o $O/$f.o
     OBJS="$OBJS $O/$f.o"
