@@ -802,36 +802,61 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
 // packet per lane, either suite per lane. (r02 walked the two partition lists: their order
 // scatters the descriptor and header reads over the arena, 0.34 GB per 2^20-packet config-E
 // launch where the descriptors alone are 34 MB, r03b PMC.) Seal needs no pass: both suites' tiles
-// mask their own packets (r03).
+// mask their own packets (r03). The block's AES packets go to its first threads and its ChaCha20
+// packets to the next ones, so only the wave on the boundary runs both suites' code (in
+// descriptor order a mixed batch puts both suites in nearly every wave, and a wave paid for the
+// AES block and the ChaCha20 block).
+__device__ __forceinline__ bool mixed_hp_pick(const KeyRow* __restrict__ kt, uint32_t n_rows, uint64_t arena_len,
+                                              const mq_pkt_desc* __restrict__ desc, uint32_t n, uint32_t i,
+                                              mq_pkt_desc& d, bool& aes) {
+  aes = false;
+  if (i >= n) return false;
+  d = desc[i];  // prepass_pick's checks; the tile kernels report the rest
+  if (!(d.key_id < n_rows && d.offset + (uint64_t)d.len <= arena_len && !(d.flags & MQ_PKT_NO_HP) &&
+        (uint64_t)d.pn_offset + 20 <= d.len))
+    return false;
+  const uint32_t su = kt[d.key_id].suite;
+  aes = su == MQ_SUITE_AES128GCM;
+  return aes || su == MQ_SUITE_CHACHA20;
+}
+
 __global__ __launch_bounds__(256) void mq_mixed_hp_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, const uint8_t* __restrict__ arena, uint64_t arena_len,
     const mq_pkt_desc* __restrict__ desc, uint32_t n, uint2* __restrict__ hpm) {
+  __shared__ uint32_t s_item[256];
+  __shared__ uint32_t s_wcnt[2][4];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  bool act = i < n, aes = false;
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x >> 6;
   mq_pkt_desc d{};
-  const KeyRow* row = kt;
-  if (act) {  // prepass_pick's checks; the tile kernels report the rest
-    d = desc[i];
-    act = d.key_id < n_rows && d.offset + (uint64_t)d.len <= arena_len && !(d.flags & MQ_PKT_NO_HP) &&
-          (uint64_t)d.pn_offset + 20 <= d.len;
+  bool aes;
+  const bool act = mixed_hp_pick(kt, n_rows, arena_len, desc, n, i, d, aes);
+  // compaction: AES packets to threads [0, nA), ChaCha20 packets to [nA, nA + nC)
+  const uint64_t ba = __ballot(act && aes), bc = __ballot(act && !aes);
+  const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  if (lane == 0) { s_wcnt[0][w] = (uint32_t)__popcll(ba); s_wcnt[1][w] = (uint32_t)__popcll(bc); }
+  __syncthreads();
+  uint32_t nA = 0, nC = 0, preA = 0, preC = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (q < w) { preA += s_wcnt[0][q]; preC += s_wcnt[1][q]; }
+    nA += s_wcnt[0][q];
+    nC += s_wcnt[1][q];
   }
-  if (act) {
-    row = kt + d.key_id;
-    const uint32_t su = row->suite;
-    aes = su == MQ_SUITE_AES128GCM;
-    act = aes || su == MQ_SUITE_CHACHA20;
-  }
-  if (!__syncthreads_or(act)) return;
-  if (__syncthreads_or(act && aes)) {  // the S-box table only where AES lanes have work
-    build_t0(threadIdx.x, blockDim.x);
-    __syncthreads();
-  }
-  if (!act) return;
-  uint32_t w[5], m0, m1;
+  if (nA + nC == 0) return;  // block-uniform
+  if (act) s_item[aes ? preA + (uint32_t)__popcll(ba & below) : nA + preC + (uint32_t)__popcll(bc & below)] = i;
+  if (nA) build_t0(threadIdx.x, blockDim.x);  // the S-box table only where AES lanes have work
+  __syncthreads();
+  const uint32_t t = threadIdx.x;
+  if (t >= nA + nC) return;
+  const uint32_t item = s_item[t];
+  const bool a = t < nA;
+  if (item != i) d = desc[item];  // the moved packets' descriptors (cached: this block just read them)
+  const KeyRow* row = kt + d.key_id;
+  uint32_t wd[5], m0, m1;
   uint8_t b0;
-  prepass_header(arena, d, b0, w);
-  const uint32_t smp[4] = {w[1], w[2], w[3], w[4]};
-  if (aes) {
+  prepass_header(arena, d, b0, wd);
+  const uint32_t smp[4] = {wd[1], wd[2], wd[3], wd[4]};
+  if (a) {
     aes_hp_mask_words(smp, row, (uint32_t)(threadIdx.x & (kTReplicas - 1)) * 4, m0, m1);
   } else {  // ChaChaHeaderProtection::mask (rustcrypto.rs:197-220)
     uint32_t hk[8], blk[16];
@@ -841,7 +866,7 @@ __global__ __launch_bounds__(256) void mq_mixed_hp_kernel(
     m0 = blk[0];
     m1 = blk[1];
   }
-  hpm[i] = prepass_decode_words(b0, w[0], d, m0, m1);
+  hpm[item] = prepass_decode_words(b0, wd[0], d, m0, m1);
 }
 
 hipError_t mq_launch_mixed_open_hp(const KeyRow* kt, uint32_t n_rows, const uint8_t* arena, uint64_t arena_len,

@@ -183,7 +183,11 @@ __device__ __forceinline__ void load_key8(const uint32_t* src, uint32_t (&k)[8])
 #define MQ_CC_WAVES 4
 #endif
 constexpr int kCcWaves = MQ_CC_WAVES;
-constexpr uint32_t kCcPoolSlot = 2 * kLanesPerPkt;  // first pooled slot (iterations 0 and 1 are the wave's)
+#ifndef MQ_CC_POOL_ITERS
+#define MQ_CC_POOL_ITERS 2
+#endif
+constexpr uint32_t kCcOwnIters = MQ_CC_POOL_ITERS;  // a wave's own iterations before the pool
+constexpr uint32_t kCcPoolSlot = kCcOwnIters * kLanesPerPkt;  // first pooled slot
 
 // Seal also pools every packet's header-protection block (RFC 9001 §5.4.4: ChaCha20 under the HP
 // key, counter and nonce from the 16-B ciphertext sample at pn_offset + 4), as the packet's last
@@ -456,7 +460,7 @@ struct ChaChaPolicy {
       load_block(sp, pay, ctr0, w);
       store_block(sp, pay, ctr0, P, ks0, w);
     }
-    const uint32_t Cown = pool.on ? min(Cmax, 2u) : Cmax;  // later slots: the workgroup's pool
+    const uint32_t Cown = pool.on ? min(Cmax, kCcOwnIters) : Cmax;  // later slots: the workgroup's pool
     for (uint32_t it = 1; it < Cown; ++it) {
       const uint32_t ctr = (uint32_t)j + kLanesPerPkt * it;
       const bool a = c.act && ctr < nblk;

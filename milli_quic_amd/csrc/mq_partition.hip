@@ -292,7 +292,8 @@ extern "C" __global__ __launch_bounds__(64 * kScanWaves) void mq_part_scan_kerne
 // cursor), rowseg[2r], rowseg[2r + 1] = row r's segment (first entry, entries including the tile
 // padding) and counts[0] the list's entries. Each thread takes kKeyRowsPerThread consecutive rows
 // (their bins are one contiguous 256-B read), so a 4096-row table is one pass of two barriers
-// (r02/r03 took one row per thread: five passes of three barriers for config E's 4098 rows).
+// (r02/r03 took one row per thread: five passes of three barriers for config E's 4098 rows). Five
+// rows per thread (one pass for E's 4098) spill at 128 VGPRs and measured 34 -> 45 us (r03y).
 constexpr int kKeyRowsPerThread = 4;
 static_assert(64 * kScanWaves == 1024, "key scan: a 1024-thread workgroup");
 __device__ void key_scan(uint32_t* __restrict__ bins, uint32_t n_rows, uint32_t* __restrict__ counts, uint32_t base,
