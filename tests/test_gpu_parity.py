@@ -395,6 +395,27 @@ def test_full_size_roundtrip(orc, cfg):
     assert v.tobytes() == w.arena.reshape(w.n, 1200)[:, :1184].tobytes()
 
 
+@pytest.mark.parametrize("cfg", ["b", "c", "ck", "e"])
+def test_full_size_byte_exact(orc, cfg):
+    # BASELINE configs[1], configs[2] (also with 1024 keys, key_id = g mod 1024: the key-segmented
+    # AES kernels) and configs[4] at the bench's full 2^20 packets, every byte of the arena, every
+    # status and PN against the oracle (16 threads), sealed and then opened — not a sample.
+    w = {"b": lambda: workload.config_b(1 << 20), "c": lambda: workload.config_c(1 << 20),
+         "ck": lambda: workload.config_c(1 << 20, n_keys=1024), "e": lambda: workload.config_e(1 << 20)}[cfg]()
+    g_out, g_st, _ = gpu_run(w.keys, w.arena, w.seal_desc, w.suite_hint)
+    o_out = w.arena.copy()
+    o_st = orc.batch_seal(w.keys, o_out, w.seal_desc, w.suite_hint, threads=16)
+    assert (o_st == 0).all() and (g_st == o_st).all()
+    assert np.array_equal(g_out, o_out)
+    del o_out
+    g_back, g_st, g_pn = gpu_run(w.keys, g_out, w.open_desc, w.suite_hint, open_=True)
+    o_back = g_out
+    o_st, o_pn = orc.batch_open(w.keys, o_back, w.open_desc, w.suite_hint, threads=16)
+    assert (o_st == 0).all() and (g_st == o_st).all()
+    assert (g_pn == o_pn).all() and (g_pn == w.pns).all()
+    assert np.array_equal(g_back, o_back)
+
+
 # ---------------------------------------------------------------------------------------------
 # batches big enough that every wave of the persistent AES-GCM kernels (one 8-wave workgroup per
 # CU) walks several tiles, with the next tile's descriptors prefetched (flat batches) or read
