@@ -7,8 +7,8 @@
 //     rotation. The one-block-per-lane kernels (HP pre-pass, key derivation) keep a small table
 //     (T0 only, 8 replicas, 8 KiB) because they run too few rounds per workgroup to pay for more;
 //   * GHASH multiplies by H^8 in the single-key tile kernels go through an LDS table of
-//     (v x^(4p)) * H^8 for every nibble position p and value v (8 KiB): 32 conflict-free
-//     ds_read_b128 and XORs per multiply, no reduction;
+//     (u x^(8q)) * H^8 for every byte position q and value u (64 KiB): 16 ds_read_b128 and XORs
+//     per multiply, no reduction (r03; a nibble table of 8 KiB took 32 of each);
 //   * GHASH multiplies in the bit-reflected polynomial basis with 32x32 carry-less products built
 //     from integer v_mad_u64_u32 on bit-holed operands (4-bit spacing, <= 8 terms per output
 //     position, so no carry reaches the next kept bit), Karatsuba 128 -> 64 -> 32 (9 products per
@@ -179,11 +179,8 @@ __device__ __forceinline__ void gf_mul(uint32_t (&a)[4], const GfOp& b) {
 }
 
 // ---- tables of the packet tile kernels (mq_aes.hip): one static LDS block per workgroup --------
-//  [0, 8 KiB)       GHASH table (single-key kernels): entry (p, v) at byte 256 p + 16 v holds
-//                   (v x^(4p)) * H^8 as 4 reflected words, p = nibble position 0..31 of the
-//                   operand (nibble p = bits 4p..4p+3 of the reflected value), v = its value.
-//                   a * H^8 = XOR over p of entry (p, nibble p of a). The 16 entries of one
-//                   position cover the 64 banks once, so any lane mix reads conflict-free.
+//  [0, 8 KiB)       single-key kernels: the half tables of H^1 and H^2 for the tags' final
+//                   multiply (g_aes_fin holds H^3 .. H^7); multi-key kernels: unused
 //  [8 KiB, 72 KiB)  wide T-table: row x (256 B) = 32 replicas of T0[x], then 32 replicas of
 //                   T2[x] = ror(T0[x], 16). Lane l reads replica l & 31, so the 32 lanes of each
 //                   ds_read_b32 lane group hit 32 distinct banks. The byte address of
@@ -196,9 +193,26 @@ __shared__ __attribute__((aligned(16))) uint32_t g_aes_lds[(kGhBytes + kTwBytes)
 // multi-key tile kernels: per wave, the GHASH half table (gh_mul_half) of its tile's key
 constexpr uint32_t kGhHalfBytes = 4096, kAesMultiWaves = 12;
 __shared__ __attribute__((aligned(16))) uint32_t g_aes_wtab[kAesMultiWaves * kGhHalfBytes / 4];
-// single-key tile kernels: half tables of H^1 .. H^8 for the tag's final multiply (lane j of a
-// packet multiplies by H^e, e = 1..8 blocks after its last one: table e - 1)
-__shared__ __attribute__((aligned(16))) uint32_t g_aes_fin[8 * kGhHalfBytes / 4];
+// single-key tile kernels: half tables of H^3 .. H^7 for the tag's final multiply (lane j of a
+// packet multiplies by H^e, e = 1..8 blocks after its last one: H^1, H^2 in g_aes_lds's first
+// 8 KiB, fin_table; a lane with e = 8 multiplies its last block by H^8 in the Horner loop instead)
+constexpr uint32_t kFinTables = 5;
+__shared__ __attribute__((aligned(16))) uint32_t g_aes_fin[kFinTables * kGhHalfBytes / 4];
+// single-key tile kernels: the byte-position GHASH table of H^8 (gh_mul_tab8). Entry (q, u) at
+// byte 4096 q + 16 u holds (u x^(8q)) * H^8 as 4 reflected words, q = byte position 0..15 of the
+// operand (byte q = bits 8q..8q+7 of the reflected value: byte q & 3 of word q >> 2), u = its
+// value; a * H^8 = XOR over q of entry (q, byte q of a). 16 reads of 16 B instead of the nibble
+// table's 32 (and half the XORs); 64 KiB fit beside the T-table once the round keys of a
+// single-key workgroup take one 352-B slot (g_aes_keys1) instead of the multi-key kernels' 33 KiB.
+// (Placed at LDS address 0 — 64-KiB alignment — the table's row bases fold into the read offsets,
+// but the T-table then sits above 64 KiB and every T-table lookup needs an add: C +5.8 %, r03ab.)
+constexpr uint32_t kGh8Bytes = 65536;
+__shared__ __attribute__((aligned(16))) uint32_t g_aes_gh8[kGh8Bytes / 4];
+
+// final-multiply half table of H^(e1 + 1), e1 = 0..6
+__device__ __forceinline__ const uint8_t* fin_table(uint32_t e1) {
+  return e1 < 2 ? (const uint8_t*)g_aes_lds + kGhHalfBytes * e1 : (const uint8_t*)g_aes_fin + kGhHalfBytes * (e1 - 2);
+}
 
 __device__ __forceinline__ uint32_t xtime8(uint32_t s) { return ((s << 1) ^ ((s & 0x80) ? 0x11bu : 0u)) & 0xffu; }
 
@@ -376,25 +390,25 @@ __device__ __forceinline__ void gf_mul_xi(const uint32_t (&h)[4], uint32_t i, ui
   gf_fold(p[0], p[1], p[2], p[3], p[4], p[5], p[6], p[7], a);
 }
 
-// GHASH table for multiplier h (reflected words), built by the whole workgroup: basis entries
-// (p, 1 << b) = x^(4p+b) h first, then every other entry as the XOR of its bits' basis entries.
-// Ends with a workgroup barrier.
-__device__ __forceinline__ void build_gh(const uint32_t (&h)[4], int tid, int nthreads) {
-  uint4* gh = (uint4*)g_aes_lds;
+// byte-position GHASH table for multiplier h (reflected words), built by the whole workgroup:
+// basis entries (q, 1 << b) = x^(8q+b) h first, then every other entry as the XOR of its bits'
+// basis entries. Ends with a workgroup barrier.
+__device__ __forceinline__ void build_gh8(const uint32_t (&h)[4], int tid, int nthreads) {
+  uint4* gh = (uint4*)g_aes_gh8;
   for (int i = tid; i < 128; i += nthreads) {
     uint32_t a[4];
     gf_mul_xi(h, (uint32_t)i, a);
-    gh[(i >> 2) * 16 + (1 << (i & 3))] = make_uint4(a[0], a[1], a[2], a[3]);
+    gh[(i >> 3) * 256 + (1 << (i & 7))] = make_uint4(a[0], a[1], a[2], a[3]);
   }
   __syncthreads();
-  for (int e = tid; e < 512; e += nthreads) {
-    const int p = e >> 4, v = e & 15;
-    if (v != 0 && (v & (v - 1)) == 0) continue;  // basis entry
+  for (int e = tid; e < 4096; e += nthreads) {
+    const int q = e >> 8, u = e & 255;
+    if (u != 0 && (u & (u - 1)) == 0) continue;  // basis entry
     uint4 acc = make_uint4(0, 0, 0, 0);
 #pragma unroll
-    for (int b = 0; b < 4; ++b)
-      if ((v >> b) & 1) {
-        const uint4 x = gh[p * 16 + (1 << b)];
+    for (int b = 0; b < 8; ++b)
+      if ((u >> b) & 1) {
+        const uint4 x = gh[q * 256 + (1 << b)];
         acc.x ^= x.x; acc.y ^= x.y; acc.z ^= x.z; acc.w ^= x.w;
       }
     gh[e] = acc;
@@ -430,21 +444,29 @@ __device__ __forceinline__ void gh_fold(uint32_t (&r)[4], const uint4 (&e)[4]) {
   r[0] = xor3(r[0], e[2].x, e[3].x); r[1] = xor3(r[1], e[2].y, e[3].y);
   r[2] = xor3(r[2], e[2].z, e[3].z); r[3] = xor3(r[3], e[2].w, e[3].w);
 }
-__device__ __forceinline__ const uint8_t* gh_row_full(int g) {  // table row of group g's first nibble
-  return (const uint8_t*)g_aes_lds + 256u * (8 * (g >> 1) + 4 * (g & 1));
+// a = a * H^8 through the byte-position table: word w's four bytes, scaled by the 16-B entry size,
+// read rows 4w .. 4w + 3. Words go in groups of 4 reads with at most two groups in flight (the
+// empty asm ties group w's addresses to the accumulator after group w - 2), as in gh_mul_half.
+__device__ __forceinline__ void gh_group8(const uint32_t (&a)[4], int w, uint4 (&e)[4], const uint32_t* dep) {
+  const uint32_t x = a[w];
+  uint32_t ad[4] = {(x << 4) & 0xff0u, (x >> 4) & 0xff0u, (x >> 12) & 0xff0u, (x >> 20) & 0xff0u};
+  if (dep)
+    asm volatile("" : "+v"(ad[0]), "+v"(ad[1]), "+v"(ad[2]), "+v"(ad[3]) : "v"(dep[0]), "v"(dep[1]), "v"(dep[2]), "v"(dep[3]));
+  const uint8_t* t = (const uint8_t*)g_aes_gh8 + 16384u * (uint32_t)w;
+  e[0] = *(const uint4*)(t + ad[0]);
+  e[1] = *(const uint4*)(t + 4096 + ad[1]);
+  e[2] = *(const uint4*)(t + 8192 + ad[2]);
+  e[3] = *(const uint4*)(t + 12288 + ad[3]);
 }
-__device__ __forceinline__ void gh_mul_tab(uint32_t (&a)[4]) {
+__device__ __forceinline__ void gh_mul_tab8(uint32_t (&a)[4]) {
   uint32_t r[4] = {0, 0, 0, 0};
   uint4 e0[4], e1[4];
-  gh_group(a, 0, e0, nullptr, gh_row_full(0));
-  gh_group(a, 1, e1, nullptr, gh_row_full(1));
-#pragma unroll
-  for (int g = 2; g < 8; g += 2) {
-    gh_fold(r, e0);
-    gh_group(a, g, e0, r, gh_row_full(g));
-    gh_fold(r, e1);
-    gh_group(a, g + 1, e1, r, gh_row_full(g + 1));
-  }
+  gh_group8(a, 0, e0, nullptr);
+  gh_group8(a, 1, e1, nullptr);
+  gh_fold(r, e0);
+  gh_group8(a, 2, e0, r);
+  gh_fold(r, e1);
+  gh_group8(a, 3, e1, r);
   gh_fold(r, e0);
   gh_fold(r, e1);
   a[0] = r[0]; a[1] = r[1]; a[2] = r[2]; a[3] = r[3];

@@ -8,11 +8,12 @@
 //   * AES-128 rounds use the wide T-table (T0 and T2, 32 replicas each, 64 KiB per workgroup,
 //     mq_aes.h): one v_perm_b32 per lookup address, conflict-free ds_read_b32, one rotation per
 //     round column; round keys in SGPRs (single-key kernels) or VGPRs;
-//   * GHASH: every Horner step's multiply by H^8 is 32 reads of an LDS table of H^8: one full
-//     table per workgroup in the single-key kernels (mq_aes.h gh_mul_tab), and in the multi-key
-//     kernels a half table per wave, built for the tile's key whenever all its packets share one
-//     (gh_mul_half; the mixed-batch partition lays AES packets out key by key so they do);
-//     otherwise, and for the final multiply by H^e, the bit-holed integer product (gf_mul).
+//   * GHASH: every Horner step's multiply by H^8 reads an LDS table of H^8: the workgroup's
+//     byte-position table in the single-key kernels (16 reads, mq_aes.h gh_mul_tab8), and in the
+//     multi-key kernels a nibble half table per wave, built for the tile's key whenever all its
+//     packets share one (32 reads, gh_mul_half; the mixed-batch partition lays AES packets out key
+//     by key so they do); otherwise, and for the multi-key final multiply by H^e, the bit-holed
+//     integer product (gf_mul).
 //
 // STREAMING tiles (r02): a wave = 8 packets x 8 lanes (mq_tile.h), slot b of a packet on lane
 // b % 8 in iteration b / 8. Slot b >= 1 is CTR block b (counter b + 1) over payload bytes
@@ -133,7 +134,7 @@ struct AesStream {
     return;
 #endif
     uint32_t t[4] = {acc[0], acc[1], acc[2], acc[3]};
-    if (GH == kGhWorkgroup) gh_mul_tab(t);
+    if (GH == kGhWorkgroup) gh_mul_tab8(t);
     else if (GH == kGhWave) gh_mul_half(t, (const uint8_t*)g_aes_wtab + kGhHalfBytes * wave_id());
     else gf_mul(t, m8);
 #pragma unroll
@@ -149,7 +150,11 @@ struct AesStream {
     acc[0] ^= e1; acc[1] ^= row->H[0][1];
 #else
     if (GH == kGhWorkgroup) {  // single key: the workgroup's table of H^(e1 + 1), per lane
-      gh_mul_half(acc, (const uint8_t*)g_aes_fin + kGhHalfBytes * e1);
+      // e1 = 7 (H^8): the lane multiplied its last block in the Horner loop (fin_in_loop)
+      uint32_t t[4] = {acc[0], acc[1], acc[2], acc[3]};
+      gh_mul_half(t, fin_table(min(e1, 6u)));
+#pragma unroll
+      for (int w = 0; w < 4; ++w) acc[w] = e1 == 7 ? acc[w] : t[w];
     } else {
       uint32_t hp[4];
 #pragma unroll
@@ -160,6 +165,12 @@ struct AesStream {
 #endif
 #pragma unroll
     for (int w = 0; w < 4; ++w) tag[w] = bswap32(brev(oct_xor(acc[w]))) ^ oct_bcast0(ej0[w]);
+  }
+
+  // single-key kernels: the lane whose final multiplier would be H^8 (e1 = 7) takes it in its last
+  // Horner step instead, through the H^8 table (finish skips it): no final-multiply table of H^8
+  static __device__ __forceinline__ bool fin_in_loop(const AesPkt& k, int j) {
+    return GH == kGhWorkgroup && ((k.nblk + 8u - (uint32_t)j) & 7u) == 7u;
   }
 
   static __device__ __forceinline__ GfOp prep_m8(const KeyRow* row) {
@@ -221,6 +232,7 @@ struct AesStream {
     bool have_mask = false;
     uint4 cur = data(j + kLanesPerPkt * it_lo);
     const int it_lean = lean_end(k.act, k.P);
+    const bool fin8 = fin_in_loop(k, j);
 #pragma nounroll
     for (int it = it_lo; it < it_hi; ++it) {
       const int b = j + kLanesPerPkt * it;
@@ -288,7 +300,7 @@ struct AesStream {
 #pragma unroll
         for (int q = 0; q < 4; ++q) smp[q] = __builtin_amdgcn_alignbyte(src[q + 1], src[q], o);
       }
-      gh_step(acc, m8, has, b + kLanesPerPkt > (int)k.nblk, x);
+      gh_step(acc, m8, has, b + kLanesPerPkt > (int)k.nblk && !fin8, x);
       cur = nxt;
     }
     uint32_t tag[4];
@@ -370,6 +382,7 @@ struct AesStream {
     uint32_t acc[4] = {0, 0, 0, 0}, ej0[4] = {0, 0, 0, 0};
     uint4 cur = data(j + kLanesPerPkt * it_lo);
     const int it_lean = lean_end(k.act, k.P);
+    const bool fin8 = fin_in_loop(k, j);
 #pragma nounroll
     for (int it = it_lo; it < it_hi; ++it) {
       const int b = j + kLanesPerPkt * it;
@@ -413,7 +426,7 @@ struct AesStream {
 #pragma unroll
         for (int q = 0; q < 4; ++q) ej0[q] = ks[q];
       }
-      gh_step(acc, m8, has, b + kLanesPerPkt > (int)k.nblk, x);
+      gh_step(acc, m8, has, b + kLanesPerPkt > (int)k.nblk && !fin8, x);
       cur = nxt;
     }
     uint32_t tag[4];
@@ -469,21 +482,22 @@ constexpr uint32_t kAesChunk = MQ_AES_CHUNK;
 // tile uses its wave's first slot); single-key kernels, row 0's in slot 0 (copied once per
 // workgroup)
 __shared__ __attribute__((aligned(16))) uint32_t g_aes_keys[kAesMultiWaves * kPktsPerTile * kRkSlotBytes / 4];
+__shared__ __attribute__((aligned(16))) uint32_t g_aes_keys1[kRkSlotBytes / 4];
 
 // the key-dependent tables of a single-key workgroup (row kt[0]); ends with a barrier
 __device__ __forceinline__ void aes_key_tables(const KeyRow* __restrict__ kt) {
-    if (threadIdx.x < kRkSlotBytes / 4) g_aes_keys[threadIdx.x] = kt[0].aes_rk[threadIdx.x];  // aes_rk || hp_rk
+    if (threadIdx.x < kRkSlotBytes / 4) g_aes_keys1[threadIdx.x] = kt[0].aes_rk[threadIdx.x];  // aes_rk || hp_rk
     const uint32_t w = wave_id();
-    if (w < 8) {  // waves 0..7: the half table of H^(w + 1) for the tags' final multiplies
+    if (w < 7) {  // waves 0..6: the half table of H^(w + 1) for the tags' final multiplies
       uint32_t hw[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) hw[q] = brev(kt[0].H[w][q]);
-      build_gh_half((uint8_t*)g_aes_fin + kGhHalfBytes * w, hw, (int)(threadIdx.x & (kWave - 1)));
+      build_gh_half(const_cast<uint8_t*>(fin_table(w)), hw, (int)(threadIdx.x & (kWave - 1)));
     }
     uint32_t h8[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) h8[q] = brev(kt[0].H[7][q]);
-    build_gh(h8, threadIdx.x, blockDim.x);  // ends with a barrier
+    build_gh8(h8, threadIdx.x, blockDim.x);  // ends with a barrier
 }
 
 template <bool SINGLE>
@@ -526,8 +540,8 @@ __device__ __forceinline__ void aes_stream_tiles(const KeyRow* __restrict__ kt, 
     if (SINGLE) {
       AesRk rk;
       load_rk(kt[0].aes_rk, rk);  // wave-uniform: SGPRs
-      if (cached) aes_run<SINGLE, OPEN, kGhWorkgroup, true>(arena, c, row, j, RkRegs{rk}, g_aes_keys);
-      else aes_run<SINGLE, OPEN, kGhWorkgroup, false>(arena, c, row, j, RkRegs{rk}, g_aes_keys);
+      if (cached) aes_run<SINGLE, OPEN, kGhWorkgroup, true>(arena, c, row, j, RkRegs{rk}, g_aes_keys1);
+      else aes_run<SINGLE, OPEN, kGhWorkgroup, false>(arena, c, row, j, RkRegs{rk}, g_aes_keys1);
     } else {
       // a tile whose active packets share one row: round keys in SGPRs, that row's H^8 half table
       // (and key schedules for the HP block) in the wave's LDS, rebuilt only when the row changes
