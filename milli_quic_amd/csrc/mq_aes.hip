@@ -23,7 +23,8 @@
 // 16 B of packet straight from HBM into VGPRs (one iteration ahead), XORs the keystream, stores,
 // and absorbs the ciphertext into its Horner accumulator (multiplier H^8) in the same iteration;
 // a final multiply by H^e (e = blocks after the lane's last one, 1..8) and an octet XOR give the
-// tag. No LDS packet image: the workgroup's LDS is the 72 KiB of tables, so 16 waves per CU
+// tag. No LDS packet image: the workgroup's LDS is its tables (72 KiB in r02; 156 KiB with the r03
+// byte-position GHASH table), so 16 waves per CU
 // (4 per SIMD) fit where the staged design (10-KiB images, r01) ran 8 — measured 1.41 vs 2.23 ms
 // for a config-C seal (tools/ubench/ubench6.hip). Open decrypts in the same single pass,
 // storing plaintext speculatively; a packet whose tag fails is restored by XORing the same
@@ -647,7 +648,8 @@ MQ_AES_KERNELS(mq_aes_seal1_kernel, mq_aes_open1_kernel, true)
 // many packets each (config C with 1024 keys: 128 tiles per key), every key's segment runs at
 // single-key speed — one persistent workgroup per CU walks segments (the hot key's classes at the
 // list's front, then row r's segment, hot[] and rowseg[] from the partition), rebuilding only the
-// key-dependent tables (round keys, the GHASH table of H^8, the half tables of H^1..H^8: a few us)
+// key-dependent tables (round keys, the byte-position GHASH table of H^8, the half tables of
+// H^1..H^7: a few us)
 // between them, its 16 waves striding the segment's tiles. The 12-wave multi-key kernel pays for
 // key changes per tile instead (per-lane key set-up, the bit-holed final multiply: 1024-key C 21 %
 // slower than one key on the same packets, profiles/r03p_scatter_probe.json).
