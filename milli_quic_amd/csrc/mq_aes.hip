@@ -472,9 +472,13 @@ using namespace mq;
 // key table has a single row: round keys in SGPRs and the GHASH table of that row's H^8.
 constexpr int aes_waves(bool single) { return single ? 16 : (int)kAesMultiWaves; }
 // multi-key kernels: consecutive tiles per wave (for_tiles chunks). Measured on configs E and C
-// with 1024 keys: chunks of 4 or 8 tiles (a key's tiles sharing one half-table build) lose more
-// to load imbalance than they save, so 1. Re-measured with the hot key split off (E's Initial
-// packets only): chunks of 2 / 4 give E +2.0 % / -0.2 %, 1024-key C -0.3 % / -0.9 %; kept at 1.
+// with 1024 keys: chunks of 4 or 8 tiles (a key's tiles sharing one half-table build) lost more
+// to load imbalance than they saved (r02), so 1. Re-measured with the hot key split off (E's
+// Initial packets only): chunks of 2 / 4 gave E +2.0 % / -0.2 %, 1024-key C -0.3 % / -0.9 %. Since
+// the key-segmented kernels took over lists of busy keys (r03), the multi-key kernel runs only
+// lists of small keys (E's ~64-packet Initial keys: 8 tiles, one key per chunk of 8): chunk 8 vs 1
+// measured E -0.8 %, -1.3 %, -0.9 % seal + open on three boxes (profiles/r03ae_ab_chunk_e.txt);
+// the product stays at 1 until the parity suite has run on a chunk-8 build.
 #ifndef MQ_AES_CHUNK
 #define MQ_AES_CHUNK 1
 #endif
