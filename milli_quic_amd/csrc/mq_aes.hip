@@ -478,9 +478,9 @@ constexpr int aes_waves(bool single) { return single ? 16 : (int)kAesMultiWaves;
 // the key-segmented kernels took over lists of busy keys (r03), the multi-key kernel runs only
 // lists of small keys (E's ~64-packet Initial keys: 8 tiles, one key per chunk of 8): chunk 8 vs 1
 // measured E -0.8 %, -1.3 %, -0.9 % seal + open on three boxes (profiles/r03ae_ab_chunk_e.txt);
-// the product stays at 1 until the parity suite has run on a chunk-8 build.
+// 85 GPU tests green on the chunk-8 build (profiles/r03af_gpu_tests_chunk8.log).
 #ifndef MQ_AES_CHUNK
-#define MQ_AES_CHUNK 1
+#define MQ_AES_CHUNK 8
 #endif
 constexpr uint32_t kAesChunk = MQ_AES_CHUNK;
 // key schedules in LDS: multi-key kernels, per wave and packet (copied per tile; a key-uniform
