@@ -43,6 +43,9 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)  # ~0.2-0.3 s timed: long enough for SMI samplers
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--warmup-seconds", type=float, default=0.25,
+                    help="after the W warm-up steps, keep running untimed steps until this much time has passed "
+                         "(the GPU's clocks ramp over ~20 ms of load after an idle of a few ms: tools/clock_probe.py)")
     ap.add_argument("--config", default="b", choices=["b", "c", "e"])
     ap.add_argument("--packets", type=int, default=1 << 20, help="packets per GPU")
     ap.add_argument("--keys", type=int, default=1, help="configs b/c: key rows, key_id = g mod K (SURVEY §8d)")
@@ -105,73 +108,57 @@ def rank_keys(cfg, n_keys, dist, device):
 
 
 def build_shard(cfg, n, rank, world, keys):
-    """This rank's shard. Configs b/c: global indices [rank n, (rank+1) n) of one global batch.
-    Config e (mixed, generated per rank): an independent batch per rank (seeded by rank)."""
-    from milli_quic_amd import _lib, workload
+    """This rank's shard of ONE global batch of world x n packets. Configs b/c: global indices
+    [rank n, (rank+1) n). Config e (mixed lengths): the range at byte quantiles of the global
+    batch's packet lengths (shard.shard_range_bytes), so every rank gets about 1/world
+    of the wire bytes. Returns (workload, first global index of the shard)."""
+    from milli_quic_amd import _lib, shard, workload
     if cfg == "e":
-        seed = workload.SEED ^ (rank * 0x9E3779B97F4A7C15 & 0xFFFFFFFFFFFFFFFF)
-        return workload.config_e(n, seed=seed)
+        plan = workload.mixed_plan(n * world)
+        lo, hi = shard.shard_range_bytes(plan.L, rank, world)
+        return workload.config_e(n * world, lo=lo, hi=hi), lo
     suite = _lib.MQ_SUITE_CHACHA20 if cfg == "b" else _lib.MQ_SUITE_AES128GCM
-    return workload.uniform(n, suite, start=rank * n, keys=keys)
+    return workload.uniform(n, suite, start=rank * n, keys=keys), rank * n
 
 
-def sample_for_rank(cfg, n, rank, world):
-    """(global sample indices, local positions of those in this rank's shard)."""
+def sample_for_rank(n_global, first, n_local):
+    """(global sample indices, local positions of those in this rank's shard [first, first + n_local))."""
     from milli_quic_amd import shard
-    if cfg == "e":
-        g = shard.sample_indices(n)
-        return g, g
-    g = shard.sample_indices(n * world)
-    mine = g[(g >= rank * n) & (g < (rank + 1) * n)]
-    return g, mine - rank * n
+    g = shard.sample_indices(n_global)
+    mine = g[(g >= first) & (g < first + n_local)]
+    return g, mine - first
 
 
-def parity_check(cfg, w, g_sample, keys, fails, csum, s_csum, pn_ok, dist=None, device=None):
-    """Whole-job parity after the timed region (the checker, CPU oracle). Configs b/c hold ONE global
-    batch: the ranks all-reduce the checksum of the tags at the fixed global sample and rank 0's
-    oracle seals exactly those packets. Config e: every rank holds its own seeded batch, so every
-    rank checks its own sample against the oracle and the ranks all-reduce the verdicts. Returns
-    the parity record (identical on every rank)."""
+def parity_check(cfg, n_global, g_sample, keys, fails, csum, s_csum, pn_ok, dist=None, device=None):
+    """Whole-job parity after the timed region (the checker, CPU oracle). Every config holds ONE
+    global batch: the ranks all-reduce the checksum of the tags at the fixed global sample and
+    rank 0's oracle seals exactly those packets. Returns the parity record (identical on every
+    rank)."""
     from milli_quic_amd import shard
     world = dist.get_world_size() if dist is not None and dist.is_initialized() else 1
     rank = dist.get_rank() if world > 1 else 0
-    own_bad, o_fail, o_csum = 0, 0, None
-    if cfg == "e":  # this rank's own batch
-        o_fail, o_csum = oracle_sample_checksum(cfg, w, g_sample, keys)
-        own_bad = int(o_fail != 0 or o_csum != s_csum)
-    fails_all, csum_all, s_csum_all, pn_bad, bad_ranks = shard.reduce_sums(
-        [fails, csum, s_csum, 0 if pn_ok else 1, own_bad], dist, device)
-    if cfg != "e":
-        o_fail, o_csum = oracle_sample_checksum(cfg, w, g_sample, keys) if rank == 0 else (0, None)
-        bad0 = int(rank == 0 and not (o_fail == 0 and o_csum == s_csum_all))
-        match = shard.reduce_sums([bad0], dist, device)[0] == 0  # rank 0's verdict on every rank
-        scope = f"global batch of {world * w.n}"
-    else:
-        match = bad_ranks == 0
-        scope = f"each rank's own batch, checked by that rank ({world} ranks)"
-    rec = {"failures": fails_all, "pn_mismatch_ranks": pn_bad, "tag_checksum": csum_all,
-           "sample_packets": int(len(g_sample)) * (world if cfg == "e" else 1),
-           "sample_tag_checksum": s_csum_all, "oracle_sample_tag_checksum": o_csum, "sample_scope": scope,
-           "ranks_mismatching_oracle": bad_ranks if cfg == "e" else None,
-           "match": bool(match and fails_all == 0 and pn_bad == 0)}
-    if cfg == "e":
-        rec["oracle_sample_tag_checksum"] = None  # per rank; see ranks_mismatching_oracle
-    return rec
+    fails_all, csum_all, s_csum_all, pn_bad = shard.reduce_sums(
+        [fails, csum, s_csum, 0 if pn_ok else 1], dist, device)
+    o_fail, o_csum = oracle_sample_checksum(cfg, n_global, g_sample, keys) if rank == 0 else (0, None)
+    bad0 = int(rank == 0 and not (o_fail == 0 and o_csum == s_csum_all))
+    match = shard.reduce_sums([bad0], dist, device)[0] == 0  # rank 0's verdict on every rank
+    return {"failures": fails_all, "pn_mismatch_ranks": pn_bad, "tag_checksum": csum_all,
+            "sample_packets": int(len(g_sample)), "sample_tag_checksum": s_csum_all,
+            "oracle_sample_tag_checksum": o_csum, "sample_scope": f"global batch of {n_global}",
+            "match": bool(match and fails_all == 0 and pn_bad == 0)}
 
 
-def oracle_sample_checksum(cfg, w, g, keys):
+def oracle_sample_checksum(cfg, n_global, g, keys):
     """CPU oracle (the checker) on the sampled global indices: the tag checksum the GPU run must
-    reproduce. Config e: rank 0's own batch."""
+    reproduce."""
     from milli_quic_amd import _lib, shard, workload
     from oracle import oracle
     oracle.load()
     if cfg == "e":
-        sd = w.seal_desc[g].copy()
-        arena = w.arena.copy()
-        st = oracle.batch_seal(w.keys, arena, sd, w.suite_hint, threads=min(16, os.cpu_count() or 1))
-        return int((st != 0).sum()), shard.tag_checksum(arena, sd)
-    suite = _lib.MQ_SUITE_CHACHA20 if cfg == "b" else _lib.MQ_SUITE_AES128GCM
-    sw = workload.uniform_at(g, suite, keys=keys)
+        sw = workload.config_e_at(g, n_global)
+    else:
+        suite = _lib.MQ_SUITE_CHACHA20 if cfg == "b" else _lib.MQ_SUITE_AES128GCM
+        sw = workload.uniform_at(g, suite, keys=keys)
     st = oracle.batch_seal(sw.keys, sw.arena, sw.seal_desc, sw.suite_hint, threads=min(16, os.cpu_count() or 1))
     return int((st != 0).sum()), shard.tag_checksum(sw.arena, sw.seal_desc)
 
@@ -409,7 +396,7 @@ def main():
         raise SystemExit(f"libmq_aead: no usable gfx950 device ({_lib.status_str(rc)})")
 
     keys = rank_keys(args.config, args.keys, dd, dev)
-    w = build_shard(args.config, args.packets, rank, world, keys)
+    w, first = build_shard(args.config, args.packets, rank, world, keys)
     kt = KeyTable(w.keys)
     arena = torch.from_numpy(w.arena).to(dev)
     sd = torch.from_numpy(w.seal_desc.view(np.uint8)).to(dev)
@@ -430,12 +417,21 @@ def main():
         if ev is not None:
             ev[3 * i + 2].record(stream)
 
+    # Events exist before the warm-up: creating them between the warm-up and the timed steps left
+    # the GPU idle for milliseconds, after which its clocks ramp up again over ~20 ms — the first
+    # timed steps ran up to 40 % slower (profiles/r04b_clock_probe.txt)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3 * args.steps)]
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    # correctness gate before timing: the roundtrip must succeed for every packet
-    fails = int((st != 0).sum())
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3 * args.steps)]
+    extra, tw = 0, time.perf_counter()
+    while time.perf_counter() - tw < args.warmup_seconds:  # untimed, the same work: clock ramp
+        for _ in range(4):
+            step()
+        torch.cuda.synchronize()
+        extra += 4
+    # correctness gate: every packet of the warm-up's round trips succeeded (read after the timed
+    # steps, so no host round trip sits between the warm-up and the timed region)
+    fails_warm = (st != 0).sum()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -446,20 +442,21 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    fails += int((st != 0).sum())
-    seal_ms = float(np.mean([ev[3 * i].elapsed_time(ev[3 * i + 1]) for i in range(args.steps)]))
-    open_ms = float(np.mean([ev[3 * i + 1].elapsed_time(ev[3 * i + 2]) for i in range(args.steps)]))
+    fails = int(fails_warm) + int((st != 0).sum())
+    seal_t = np.array([ev[3 * i].elapsed_time(ev[3 * i + 1]) for i in range(args.steps)])
+    open_t = np.array([ev[3 * i + 1].elapsed_time(ev[3 * i + 2]) for i in range(args.steps)])
+    seal_ms, open_ms = float(seal_t.mean()), float(open_t.mean())
     pn_ok = bool((pn.cpu().numpy().view(np.uint64) == w.pns).all())
 
     # cross-rank parity: after the steps every packet holds its plaintext and the tag the last seal
     # wrote; all-reduce failures and tag checksums (whole shard, and the fixed global sample)
     offs_t = torch.from_numpy(w.seal_desc["offset"].astype(np.int64)).to(dev)
     lens_t = torch.from_numpy(w.seal_desc["len"].astype(np.int64)).to(dev)
-    g_sample, local_sample = sample_for_rank(args.config, args.packets, rank, world)
+    g_sample, local_sample = sample_for_rank(args.packets * world, first, w.n)
     ls = torch.from_numpy(local_sample.astype(np.int64)).to(dev)
     csum = shard.tag_checksum_torch(arena, offs_t, lens_t)
     s_csum = shard.tag_checksum_torch(arena, offs_t[ls], lens_t[ls])
-    parity = parity_check(args.config, w, g_sample, keys, fails, csum, s_csum, pn_ok, dd, dev)
+    parity = parity_check(args.config, args.packets * world, g_sample, keys, fails, csum, s_csum, pn_ok, dd, dev)
     fails_all = parity["failures"]
 
     wire = w.wire_bytes
@@ -480,7 +477,13 @@ def main():
                 "kernel": ("seal composite: " if args.config != "e" else "seal batch: ") + " + ".join(kerns),
                 "seal_ms": round(seal_ms, 4), "open_ms": round(open_ms, 4),
                 "open_frac": round(algo_bytes / (open_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                "algorithmic_bytes_per_launch": int(algo_bytes)}
+                "algorithmic_bytes_per_launch": int(algo_bytes),
+                # per-step HIP-event times of the timed steps
+                "per_step_ms": {k: {"min": round(float(t.min()), 4), "median": round(float(np.median(t)), 4),
+                                    "max": round(float(t.max()), 4),
+                                    "first5": [round(float(x), 4) for x in t[:5]],
+                                    "last5": [round(float(x), 4) for x in t[-5:]]}
+                                for k, t in (("seal", seal_t), ("open", open_t))}}
         cpu = ossl = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(w, args.cpu_sample, args.cpu_seconds)
@@ -492,12 +495,16 @@ def main():
         if world > 1 and args.config == "b":
             workload_name = (f"configs[3]: {world}x{args.packets // (1 << 20) or args.packets}M x 1200B "
                              f"ChaCha20-Poly1305 batch sharded across {world} GPUs")
+        elif world > 1:
+            workload_name += f" — one global batch of {world}x{args.packets} packets, " + \
+                ("split at byte quantiles" if args.config == "e" else "contiguous shards") + f" over {world} GPUs"
         out = {
             "metric": "GiB/s device-resident AEAD seal+open, 1M×1200B QUIC packets, 1/2/4/8 GPU",
             # a run whose results differ from the oracle has no throughput (exit status 1 below)
             "value": round(value, 2) if parity["match"] else None,
             "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "warmup": args.warmup, "warmup_extra": {"seconds": args.warmup_seconds, "steps": extra},
+            "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
             "config": {"workload": workload_name, "packets_per_gpu": w.n, "key_rows": len(w.keys),
                        "wire_bytes_per_gpu": wire, "parallelism": f"dp{world} (independent packet shards)",

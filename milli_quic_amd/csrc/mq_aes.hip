@@ -471,18 +471,14 @@ using namespace mq;
 // pointers, the bit-holed GHASH operand) and run 12 waves in 168. The "1" variants run when the
 // key table has a single row: round keys in SGPRs and the GHASH table of that row's H^8.
 constexpr int aes_waves(bool single) { return single ? 16 : (int)kAesMultiWaves; }
-// multi-key kernels: consecutive tiles per wave (for_tiles chunks). Measured on configs E and C
-// with 1024 keys: chunks of 4 or 8 tiles (a key's tiles sharing one half-table build) lost more
-// to load imbalance than they saved (r02), so 1. Re-measured with the hot key split off (E's
-// Initial packets only): chunks of 2 / 4 gave E +2.0 % / -0.2 %, 1024-key C -0.3 % / -0.9 %. Since
-// the key-segmented kernels took over lists of busy keys (r03), the multi-key kernel runs only
-// lists of small keys (E's ~64-packet Initial keys: 8 tiles, one key per chunk of 8): chunk 8 vs 1
-// measured E -0.8 %, -1.3 %, -0.9 % seal + open on three boxes (profiles/r03ae_ab_chunk_e.txt);
-// 85 GPU tests green on the chunk-8 build (profiles/r03af_gpu_tests_chunk8.log).
-#ifndef MQ_AES_CHUNK
-#define MQ_AES_CHUNK 8
-#endif
-constexpr uint32_t kAesChunk = MQ_AES_CHUNK;
+// Work distribution (r04): every wave runs its first tile by grid position, then claims chunks of
+// the rest dynamically (mq_tile.h for_tiles, TileSched; guided chunk sizes, one head per XCD),
+// when the launch has a schedule slot. That replaced (a) the static stride, under which a workgroup
+// placed late — its CU held by the resident per-packet server or by the hot-key kernel forked
+// beside this one — ended the launch a whole share late, and (b) the multi-key
+// kernels' fixed chunks of 8 tiles (r03: a wave meets a key's consecutive tiles, E -0.8..-1.3 %),
+// which left most workgroups idle on small lists: guided chunks are up to kMaxChunk
+// tiles while much is left and single tiles at the end.
 // key schedules in LDS: multi-key kernels, per wave and packet (copied per tile; a key-uniform
 // tile uses its wave's first slot); single-key kernels, row 0's in slot 0 (copied once per
 // workgroup)
@@ -526,13 +522,11 @@ __device__ __forceinline__ void aes_stream_tiles(const KeyRow* __restrict__ kt, 
                                                  const uint32_t* __restrict__ index,
                                                  const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status,
                                                  uint64_t* __restrict__ pn_out, const uint2* __restrict__ hpm,
-                                                 uint32_t skip, uint32_t first, uint32_t stride) {
+                                                 uint32_t skip, const TileSched& ts) {
   const uint32_t w = wave_id();
   const int lane = (int)(threadIdx.x & (kWave - 1)), j = lane & (kLanesPerPkt - 1);
-  constexpr uint32_t W = aes_waves(SINGLE), C = SINGLE ? 1u : kAesChunk;
   uint32_t wt_kid = 0xFFFFFFFFu;  // multi-key: the row whose half table and key schedules the wave holds
-  (void)W;
-  for_tiles<OPEN, C>(first, stride, desc, n, index, n_dev, hpm,
+  for_tiles<OPEN>(ts, desc, n, index, n_dev, hpm,
                   [&](uint32_t t, const TilePrefetch& pf) __attribute__((always_inline)) {
     PktCtx c;
     const KeyRow* row;
@@ -612,38 +606,55 @@ __device__ __forceinline__ bool aes_hot_split(const uint32_t* __restrict__ hot, 
 
 // workgroup-uniform, before any table is built: whether this workgroup of a persistent grid has
 // a tile (a partition list's device count may be small or zero — an AES batch's leftover list is
-// usually empty, and 256 workgroups building their tables for nothing cost ~35 us)
+// usually empty, and 256 workgroups building their tables for nothing cost ~35 us). Its waves' first
+// tiles are skip + blockIdx.x * W + w; every later tile lies beyond all first tiles, so a
+// workgroup without a first tile has none at all.
 template <bool SINGLE>
 __device__ __forceinline__ bool aes_wg_has_work(uint32_t n, const uint32_t* __restrict__ n_dev, uint32_t skip) {
   const uint32_t count = n_dev ? *n_dev : n;
   const uint32_t tiles = (count + kPktsPerTile - 1) / kPktsPerTile;
-  const uint32_t c = SINGLE ? 1u : kAesChunk;
-  return skip + blockIdx.x * aes_waves(SINGLE) * c < tiles;
+  return skip + blockIdx.x * aes_waves(SINGLE) < tiles;
 }
 
+__device__ __forceinline__ TileSched aes_sched(uint32_t* sched, bool single) {
+  const uint32_t W = (uint32_t)aes_waves(single);
+  return TileSched{sched, blockIdx.x * W + wave_id(), gridDim.x * W, blockIdx.x % kSchedHeads};
+}
+
+// sched: the launch's schedule slot (dynamic tiles), null for the static stride. Every workgroup
+// reaches sched_done once: without work at its only exit, else after a barrier behind its tiles.
 #define MQ_AES_KERNELS(NAME_SEAL, NAME_OPEN, SINGLE)                                                      \
   extern "C" __global__ __launch_bounds__(64 * aes_waves(SINGLE)) void NAME_SEAL(                           \
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
-      const uint32_t* __restrict__ n_dev, const uint32_t* __restrict__ hot, uint8_t* __restrict__ status) { \
+      const uint32_t* __restrict__ n_dev, const uint32_t* __restrict__ hot, uint8_t* __restrict__ status, \
+      uint32_t* __restrict__ sched) {                                                                     \
     uint32_t skip;                                                                                        \
-    if (!aes_hot_split<SINGLE>(hot, kt, n_dev, skip) || !aes_wg_has_work<SINGLE>(n, n_dev, skip)) return;   \
+    if (!aes_hot_split<SINGLE>(hot, kt, n_dev, skip) || !aes_wg_has_work<SINGLE>(n, n_dev, skip)) {       \
+      sched_done(sched);                                                                                  \
+      return;                                                                                             \
+    }                                                                                                     \
     aes_tables<SINGLE>(kt);                                                                               \
     aes_stream_tiles<SINGLE, false>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr,  \
-                                    nullptr, skip, blockIdx.x * aes_waves(SINGLE) + wave_id(),            \
-                                    gridDim.x * aes_waves(SINGLE));                                       \
+                                    nullptr, skip, aes_sched(sched, SINGLE));                             \
+    __syncthreads();                                                                                      \
+    sched_done(sched);                                                                                    \
   }                                                                                                       \
   extern "C" __global__ __launch_bounds__(64 * aes_waves(SINGLE)) void NAME_OPEN(                           \
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
       const uint32_t* __restrict__ n_dev, const uint32_t* __restrict__ hot, uint8_t* __restrict__ status, \
-      uint64_t* __restrict__ pn_out, const uint2* __restrict__ hpm) {                                     \
+      uint64_t* __restrict__ pn_out, const uint2* __restrict__ hpm, uint32_t* __restrict__ sched) {       \
     uint32_t skip;                                                                                        \
-    if (!aes_hot_split<SINGLE>(hot, kt, n_dev, skip) || !aes_wg_has_work<SINGLE>(n, n_dev, skip)) return;   \
+    if (!aes_hot_split<SINGLE>(hot, kt, n_dev, skip) || !aes_wg_has_work<SINGLE>(n, n_dev, skip)) {       \
+      sched_done(sched);                                                                                  \
+      return;                                                                                             \
+    }                                                                                                     \
     aes_tables<SINGLE>(kt);                                                                               \
     aes_stream_tiles<SINGLE, true>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm, \
-                                   skip, blockIdx.x * aes_waves(SINGLE) + wave_id(),                      \
-                                   gridDim.x * aes_waves(SINGLE));                                        \
+                                   skip, aes_sched(sched, SINGLE));                                       \
+    __syncthreads();                                                                                      \
+    sched_done(sched);                                                                                    \
   }
 MQ_AES_KERNELS(mq_aes_seal_kernel, mq_aes_open_kernel, false)
 MQ_AES_KERNELS(mq_aes_seal1_kernel, mq_aes_open1_kernel, true)
@@ -657,16 +668,30 @@ MQ_AES_KERNELS(mq_aes_seal1_kernel, mq_aes_open1_kernel, true)
 // between them, its 16 waves striding the segment's tiles. The 12-wave multi-key kernel pays for
 // key changes per tile instead (per-lane key set-up, the bit-holed final multiply: 1024-key C 21 %
 // slower than one key on the same packets, profiles/r03p_scatter_probe.json).
+// Segments go to workgroups dynamically (r04): thread 0 claims the next one from head 0 of the
+// launch's schedule slot (one claim per segment, 256 pullers), so a workgroup placed late takes none
+// of the others' (static: segments blockIdx.x, + gridDim.x, ...).
 template <bool OPEN>
 __device__ __forceinline__ void aes_seg_tiles(const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena,
                                               uint64_t arena_len, const mq_pkt_desc* __restrict__ desc,
                                               const uint32_t* __restrict__ list, const uint32_t* __restrict__ hot,
                                               const uint32_t* __restrict__ rowseg, uint8_t* __restrict__ status,
-                                              uint64_t* __restrict__ pn_out, const uint2* __restrict__ hpm) {
+                                              uint64_t* __restrict__ pn_out, const uint2* __restrict__ hpm,
+                                              uint32_t* __restrict__ sched) {
   constexpr uint32_t W = aes_waves(true);
+  __shared__ uint32_t s_seg;
   build_tw(threadIdx.x, blockDim.x);  // key-independent: once
   const uint32_t w = wave_id();
-  for (uint32_t sg = blockIdx.x; sg <= n_rows; sg += gridDim.x) {  // segment 0: the hot key; 1 + r: row r
+  uint32_t sg = blockIdx.x;
+  for (;;) {  // segment 0: the hot key; 1 + r: row r
+    __syncthreads();  // every wave is done with the previous segment (its tables, s_seg)
+    if (sched) {
+      if (threadIdx.x == 0)
+        s_seg = __hip_atomic_fetch_add(sched, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      sg = s_seg;
+    }
+    if (sg > n_rows) break;  // workgroup-uniform
     uint32_t row, first, ent;
     if (sg == 0) {
       row = hot[0];
@@ -680,26 +705,27 @@ __device__ __forceinline__ void aes_seg_tiles(const KeyRow* __restrict__ kt, uin
     row = __builtin_amdgcn_readfirstlane(row);
     first = __builtin_amdgcn_readfirstlane(first);
     ent = __builtin_amdgcn_readfirstlane(ent);
+    if (!sched) sg += gridDim.x;
     if (row >= n_rows || ent == 0) continue;  // workgroup-uniform
-    __syncthreads();  // every wave is done with the previous segment's tables
     const KeyRow* ks = kt + row;  // the segment's row as a one-row table (validation uses n_rows)
     aes_key_tables(ks);  // ends with a barrier
     aes_stream_tiles<true, OPEN>(ks, n_rows, arena, arena_len, desc, first + ent, list, nullptr, status, pn_out, hpm,
-                                 first / kPktsPerTile, w, W);
+                                 first / kPktsPerTile, TileSched{nullptr, w, W, 0});
   }
+  sched_done(sched);  // after the loop's last barrier
 }
 extern "C" __global__ __launch_bounds__(64 * aes_waves(true)) void mq_aes_seals_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
     const mq_pkt_desc* __restrict__ desc, const uint32_t* __restrict__ list, const uint32_t* __restrict__ hot,
-    const uint32_t* __restrict__ rowseg, uint8_t* __restrict__ status) {
-  aes_seg_tiles<false>(kt, n_rows, arena, arena_len, desc, list, hot, rowseg, status, nullptr, nullptr);
+    const uint32_t* __restrict__ rowseg, uint8_t* __restrict__ status, uint32_t* __restrict__ sched) {
+  aes_seg_tiles<false>(kt, n_rows, arena, arena_len, desc, list, hot, rowseg, status, nullptr, nullptr, sched);
 }
 extern "C" __global__ __launch_bounds__(64 * aes_waves(true)) void mq_aes_opens_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
     const mq_pkt_desc* __restrict__ desc, const uint32_t* __restrict__ list, const uint32_t* __restrict__ hot,
     const uint32_t* __restrict__ rowseg, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,
-    const uint2* __restrict__ hpm) {
-  aes_seg_tiles<true>(kt, n_rows, arena, arena_len, desc, list, hot, rowseg, status, pn_out, hpm);
+    const uint2* __restrict__ hpm, uint32_t* __restrict__ sched) {
+  aes_seg_tiles<true>(kt, n_rows, arena, arena_len, desc, list, hot, rowseg, status, pn_out, hpm, sched);
 }
 
 extern "C" __global__ __launch_bounds__(256) void mq_aes_hp_kernel(
@@ -773,20 +799,23 @@ static uint32_t aes_grid(uint32_t tiles, uint32_t waves, int cus) {
 // cus: the device's compute units (the persistent grid).
 // rowseg (a keyed partition list, mq_partition_rowseg): the key-segmented kernels run the whole
 // list (hot key included) instead of the hot split + multi-key kernel.
+// sched_s / sched_hs: the schedule slots of streams s / hs (mq_runtime.h SchedSlots), null for the
+// static stride.
 hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena, uint64_t arena_len,
                          const mq_pkt_desc* desc, uint32_t n, const uint32_t* index, const uint32_t* n_dev,
                          const uint32_t* hot, uint8_t* status, uint64_t* pn_out, uint2* hpm, bool own_hp,
-                         hipStream_t s, hipStream_t hs, int cus, const uint32_t* rowseg) {
+                         hipStream_t s, hipStream_t hs, int cus, const uint32_t* rowseg, uint32_t* sched_s,
+                         uint32_t* sched_hs) {
   const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
   if (tiles == 0) return hipSuccess;
   if (rowseg && index && hot && n_rows > 1 && !own_hp) {
     const uint32_t blocks = (uint32_t)(cus > 0 ? cus : 256);
     if (open)
       hipLaunchKernelGGL(mq_aes_opens_kernel, dim3(blocks), dim3(64 * aes_waves(true)), 0, s, kt, n_rows, arena,
-                         arena_len, desc, index, hot, rowseg, status, pn_out, hpm);
+                         arena_len, desc, index, hot, rowseg, status, pn_out, hpm, sched_s);
     else
       hipLaunchKernelGGL(mq_aes_seals_kernel, dim3(blocks), dim3(64 * aes_waves(true)), 0, s, kt, n_rows, arena,
-                         arena_len, desc, index, hot, rowseg, status);
+                         arena_len, desc, index, hot, rowseg, status, sched_s);
     return hipGetLastError();
   }
   const uint32_t waves = aes_waves(n_rows == 1), blocks = aes_grid(tiles, waves, cus);
@@ -802,18 +831,20 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
   if (!hot) hs = s;
   // the launch's own HP passes run on s: a forked hot kernel would race them
   if (own_hp && hs != s) return hipErrorInvalidValue;
+  // two kernels at once on one stream's slot would share its heads
+  if (hot && hs == s) sched_hs = nullptr;
   if (open) {
     if (hot)
       hipLaunchKernelGGL(mq_aes_open1_kernel, dim3(hot_blocks), dim3(64 * aes_waves(true)), 0, hs, kt, n_rows,
-                         arena, arena_len, desc, n, index, n_dev, hot, status, pn_out, hpm);
+                         arena, arena_len, desc, n, index, n_dev, hot, status, pn_out, hpm, sched_hs);
     hipLaunchKernelGGL(n_rows == 1 ? mq_aes_open1_kernel : mq_aes_open_kernel, dim3(blocks), dim3(64 * waves),
-                       0, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, hot, status, pn_out, hpm);
+                       0, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, hot, status, pn_out, hpm, sched_s);
   } else {
     if (hot)
       hipLaunchKernelGGL(mq_aes_seal1_kernel, dim3(hot_blocks), dim3(64 * aes_waves(true)), 0, hs, kt, n_rows,
-                         arena, arena_len, desc, n, index, n_dev, hot, status);
+                         arena, arena_len, desc, n, index, n_dev, hot, status, sched_hs);
     hipLaunchKernelGGL(n_rows == 1 ? mq_aes_seal1_kernel : mq_aes_seal_kernel, dim3(blocks), dim3(64 * waves),
-                       0, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, hot, status);
+                       0, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, hot, status, sched_s);
   }
   return hipGetLastError();
 }

@@ -22,6 +22,12 @@ namespace mq {
 
 constexpr int kWave = 64;
 constexpr int kPktsPerTile = 8;
+// dynamic tile schedule slot of a persistent launch (mq_tile.h TileSched), uint32 words: head h at
+// word kSchedHeadWords * h (128 B apart), the finished-workgroup count at kSchedDoneWord
+constexpr uint32_t kSchedHeads = 8;
+constexpr uint32_t kSchedHeadWords = 32;
+constexpr uint32_t kSchedDoneWord = kSchedHeads * kSchedHeadWords;
+constexpr uint32_t kSchedSlotBytes = 4 * (kSchedDoneWord + kSchedHeadWords);  // 1152 B
 constexpr int kLanesPerPkt = kWave / kPktsPerTile;  // 8: one octet of lanes per packet
 constexpr uint32_t kLdsBytes = 10240;                // LDS per tile (wave) -> 16 waves/CU
 constexpr uint32_t kCuLdsBytes = 160 * 1024;         // LDS per CU (gfx950)

@@ -32,7 +32,8 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
                          uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
                          const uint32_t* index, const uint32_t* n_dev, const uint32_t* hot,
                          uint8_t* status, uint64_t* pn_out, uint2* hpm, bool own_hp, hipStream_t s,
-                         hipStream_t hot_stream, int cus, const uint32_t* rowseg = nullptr);
+                         hipStream_t hot_stream, int cus, const uint32_t* rowseg, uint32_t* sched_s,
+                         uint32_t* sched_hs);
 const uint32_t* mq_partition_rowseg(uint32_t n, uint32_t n_rows, const uint32_t* counts);
 hipError_t mq_launch_mixed_open_hp(const KeyRow* kt, uint32_t n_rows, const uint8_t* arena, uint64_t arena_len,
                                    const mq_pkt_desc* desc, uint32_t n, uint2* hpm, hipStream_t s);
@@ -105,6 +106,13 @@ struct HipBackend {
   static void event_destroy(Event e) { (void)hipEventDestroy(e); }
   static bool record(Event e, Stream s) { return hipEventRecord(e, s) == hipSuccess; }
   static bool wait(Stream s, Event e) { return hipStreamWaitEvent(s, e, 0) == hipSuccess; }
+  static void* alloc_zeroed(size_t bytes) {
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return nullptr;  // leaked
+    return p;
+  }
+  static void stream_sync(Stream s) { (void)hipStreamSynchronize(s); }
 };
 typedef mq::DeviceRegistry<HipBackend> Devices;
 typedef Devices::Guard DeviceGuard;
@@ -117,6 +125,23 @@ Devices& devices() {
 mq::SideStreams<HipBackend>& side_streams() {
   static auto* s = new mq::SideStreams<HipBackend>(64);
   return *s;
+}
+
+// Dynamic tile schedule slots of the persistent AES kernels, per (device, stream): mq_runtime.h,
+// mq_tile.h TileSched. MQ_SCHED=0 (diagnostic) selects the static stride.
+mq::SchedSlots<HipBackend>& sched_slots() {
+  static auto* s = new mq::SchedSlots<HipBackend>(1024, mq::kSchedSlotBytes);
+  return *s;
+}
+uint32_t* sched_slot(int dev, hipStream_t s) {
+  static const bool on = [] {
+#ifdef MQ_SCHED_STATIC  // diagnostic builds (tools/build_variant.sh)
+    return false;
+#endif
+    const char* e = std::getenv("MQ_SCHED");
+    return !(e && e[0] == '0');
+  }();
+  return on ? (uint32_t*)sched_slots().get(dev, s) : nullptr;
 }
 
 // The device a new object (key table, AEAD / HP context) is created on: the thread's selection,
@@ -436,7 +461,7 @@ int run_one(Scratch& sc, const KeyRow& row, const uint8_t* aad, uint32_t aad_len
   hipError_t e = row.suite == MQ_SUITE_CHACHA20
                      ? mq_launch_chacha(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, st, pn, nullptr, false, sc.stream)
                      : mq_launch_aes(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, nullptr, st, pn, nullptr, false,
-                                     sc.stream, sc.stream, devices().cus(sc.device));
+                                     sc.stream, sc.stream, devices().cus(sc.device), nullptr, nullptr, nullptr);
   if (e != hipSuccess) return MQ_ERR_HIP;
   // status and the transformed packet in one read-back (the status sits before the packet)
   if ((rc = sc.finish(Scratch::kStatus, Scratch::kHdr - Scratch::kStatus + pkt_len)) != MQ_OK) return rc;
@@ -515,7 +540,10 @@ int mq_device_current(void) { return devices().current(); }
 
 int mq_keytable_device(const mq_keytable* kt) { return kt ? kt->device : -1; }
 
-void mq_stream_release(void* stream) { side_streams().release((hipStream_t)stream); }
+void mq_stream_release(void* stream) {
+  side_streams().release((hipStream_t)stream);
+  sched_slots().release((hipStream_t)stream);
+}
 
 const char* mq_status_str(int status) {
   switch (status) {
@@ -828,7 +856,7 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
                          s);
   } else if (suite_hint == MQ_SUITE_AES128GCM && (kt->rows == 1 || !ws || n > (1u << 30))) {
     e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, n, nullptr, nullptr, nullptr, status, pn_out,
-                      hpm, true, s, s, cus);
+                      hpm, true, s, s, cus, nullptr, sched_slot(kt->device, s), nullptr);
   } else if (suite_hint == MQ_SUITE_MIXED || suite_hint == MQ_SUITE_AES128GCM) {
     // the two index lists (2 x mq_partition_list_cap(n) entries, holes included) are addressed
     // with 32-bit positions: up to 2^30 packets per mixed batch. An AES batch over several key
@@ -868,11 +896,12 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
                                  : mq_partition_rowseg(n, kt->rows, counts);
     auto fork = fork_enabled() && !rowseg ? side_streams().fork(kt->device, s, 1) : mq::SideStreams<HipBackend>::Fork();
     hipStream_t s_hot = fork ? fork.side(0) : s, s_list1 = s;
+    uint32_t* sched_s = sched_slot(kt->device, s);
     e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list, counts, counts + 2, status, pn_out,
-                      hpm, false, s, s_hot, cus, rowseg);
+                      hpm, false, s, s_hot, cus, rowseg, sched_s, s_hot != s ? sched_slot(kt->device, s_hot) : nullptr);
     if (e == hipSuccess && aes_only)
       e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list + cap, counts + 1, nullptr, status,
-                        pn_out, hpm, false, s_list1, s_list1, cus);
+                        pn_out, hpm, false, s_list1, s_list1, cus, nullptr, sched_slot(kt->device, s_list1), nullptr);
     else if (e == hipSuccess)
       e = mq_launch_chacha(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list + cap, counts + 1, status,
                            pn_out, hpm, false, s_list1);

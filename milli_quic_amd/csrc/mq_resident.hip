@@ -515,15 +515,23 @@ extern "C" __global__ __launch_bounds__(kResThreads) void mq_resident_kernel(Res
   }
   for (;;) {
     if (w0u) {  // wave 0 polls; waves 1..3 wait at the barrier below
-      // Request done + 1 is complete when every slot it uses carries that number (the host writes
-      // slot 0 last, so a complete header usually comes in the first poll that sees slot 0).
-      const uint32_t exp = done + 1;
+      // A new request is one whose slot 0 carries another number than the last one served (`done`),
+      // and it is complete when every slot it uses carries that number (the host writes slot 0
+      // last, so a complete header usually comes in the first poll that sees slot 0). Any number
+      // other than `done` is served, not just done + 1: a request the host gave up on (its 10-s
+      // limit) is then simply superseded by the next one (r03 waited for done + 1 and never served
+      // another request after such a timeout).
+      uint32_t exp = done;
       uint32_t leave = 0;
       uint64_t hv = 0;
-      // 0: nothing new, 1: request done + 1 (slot 0), 2: stop, 3: idle
+      // 0: nothing new, 1: a new request (slot 0), 2: stop, 3: idle
       auto test = [&](uint64_t v) -> uint32_t {
         if (__builtin_amdgcn_readlane((int)(uint32_t)v, kHwStop)) return 2;
-        if ((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 0) == exp) return 1;
+        const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 0);
+        if (s0 != done) {
+          exp = s0;
+          return 1;
+        }
         return 0;
       };
       for (;;) {
@@ -547,7 +555,7 @@ extern "C" __global__ __launch_bounds__(kResThreads) void mq_resident_kernel(Res
         // idle: claim the exit, then look once more; a request posted meanwhile is served first
         if (lane == 0) st_sys_sc(&ctl->state, kResExiting);
         wave_sync();
-        if (uni(ld_sys_sc((const uint32_t*)&area->hdr[0] + 1)) != exp) { leave = 1; break; }
+        if (uni(ld_sys_sc((const uint32_t*)&area->hdr[0] + 1)) == done) { leave = 1; break; }
         if (lane == 0) st_sys_sc(&ctl->state, kResRunning);
         t_last = now;
       }
@@ -683,6 +691,13 @@ Resident* resident(int dev) {
 
 uint32_t load_acq(const uint32_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
 
+// How long a call waits for the resident kernel: 10 s, or MQ_RESIDENT_TIMEOUT_US (read per call;
+// tests force the timeout path with it)
+std::chrono::microseconds resident_timeout() {
+  const char* e = std::getenv("MQ_RESIDENT_TIMEOUT_US");
+  return std::chrono::microseconds(e ? std::strtoull(e, nullptr, 10) : 10000000ull);
+}
+
 }  // namespace
 
 // One call through the resident kernel of device `dev` (the caller holds a device guard on it).
@@ -759,7 +774,16 @@ int mq_resident_call(int dev, const ResReq& q, uint64_t uid, const uint8_t* aad,
       r->launched = true;
       relaunched = true;
     }
-    if ((spins & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) return MQ_ERR_HIP;
+    if ((spins & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > resident_timeout()) {
+      // Give up on this request, but leave no kernel behind that could still serve it (it would
+      // write the mailbox while the next call fills it): ask the kernel to leave and
+      // wait for its stream. A kernel not yet placed (every CU busy) starts, sees the stop slot and
+      // leaves. If it served the request meanwhile, the call succeeds after all.
+      __atomic_store_n(&a->hdr[kHwStop], (uint64_t)1, __ATOMIC_SEQ_CST);
+      if (r->launched && hipStreamSynchronize(r->stream) != hipSuccess) return MQ_ERR_HIP;
+      if (load_acq(&a->ctl.done) == seq) break;
+      return MQ_ERR_HIP;  // the next call relaunches (state: exited) and supersedes this request
+    }
   }
   const auto t1 = std::chrono::steady_clock::now();
   *status = (int)__atomic_load_n(&a->ctl.status, __ATOMIC_ACQUIRE);

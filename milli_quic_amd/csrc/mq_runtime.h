@@ -237,4 +237,92 @@ class SideStreams {
   size_t cap_;
 };
 
+// Device words of the persistent tile kernels' dynamic schedule (mq_tile.h TileSched), one slot per
+// (device, stream). Kernels on one stream run one after another and each leaves its slot zeroed
+// when its last workgroup ends, so a slot is never used by two kernels at once; kernels that run
+// concurrently (a forked side stream) are on other streams and so have other slots. The slots of a
+// device are one zeroed allocation made on first use (the caller holds a guard on the device) and
+// never freed (a kernel may still be running when the library is unloaded). A stream beyond the
+// capacity gets no slot: its kernels take the static schedule. release(stream) waits for the
+// stream's work (its kernels may still use the slot), then recycles its slots.
+//
+// Backend additions: void* alloc_zeroed(size_t bytes)  device memory on the current device (null
+// on failure); void stream_sync(Stream)  waits for the stream's work.
+template <class B>
+class SchedSlots {
+ public:
+  typedef typename B::Stream Stream;
+
+  SchedSlots(uint32_t slots, size_t slot_bytes) : slots_(slots), bytes_(slot_bytes) {}
+
+  // the slot of (dev, s), assigned on first use; null when none is left or allocation failed
+  void* get(int dev, Stream s) {
+    if (dev < 0) return nullptr;
+    std::lock_guard<std::mutex> lk(mu_);
+    if ((size_t)dev >= dev_.size()) dev_.resize((size_t)dev + 1);
+    PerDev& d = dev_[(size_t)dev];
+    for (const auto& e : d.map)
+      if (e.first == s) return d.base + bytes_ * e.second;
+    if (!d.base) {
+      if (d.failed) return nullptr;
+      d.base = (uint8_t*)B::alloc_zeroed(bytes_ * slots_);
+      if (!d.base) {
+        d.failed = true;
+        return nullptr;
+      }
+    }
+    uint32_t idx;
+    if (!d.free.empty()) {
+      idx = d.free.back();
+      d.free.pop_back();
+    } else if (d.used < slots_) {
+      idx = d.used++;
+    } else {
+      return nullptr;
+    }
+    d.map.emplace_back(s, idx);
+    return d.base + bytes_ * idx;
+  }
+
+  // Recycles the slots of stream s (every device) once its work has finished.
+  void release(Stream s) {
+    bool had = false;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      for (auto& d : dev_)
+        for (const auto& e : d.map) had = had || e.first == s;
+    }
+    if (!had) return;
+    B::stream_sync(s);  // outside the lock: its kernels may still count on the slot
+    std::lock_guard<std::mutex> lk(mu_);
+    for (auto& d : dev_)
+      for (auto it = d.map.begin(); it != d.map.end();) {
+        if (it->first == s) {
+          d.free.push_back(it->second);
+          it = d.map.erase(it);
+        } else {
+          ++it;
+        }
+      }
+  }
+
+  size_t assigned(int dev) {
+    std::lock_guard<std::mutex> lk(mu_);
+    return (dev >= 0 && (size_t)dev < dev_.size()) ? dev_[(size_t)dev].map.size() : 0;
+  }
+
+ private:
+  struct PerDev {
+    uint8_t* base = nullptr;
+    bool failed = false;
+    uint32_t used = 0;
+    std::vector<std::pair<Stream, uint32_t>> map;
+    std::vector<uint32_t> free;
+  };
+  std::mutex mu_;
+  std::vector<PerDev> dev_;
+  uint32_t slots_;
+  size_t bytes_;
+};
+
 }  // namespace mq

@@ -473,29 +473,148 @@ __device__ __forceinline__ void run_tile(uint8_t* smem, uint32_t tile_id, const 
   tile_status<OPEN>(c, j, status, pn_out);
 }
 
-// Persistent tile loop: this wave runs its tiles calling body(tile, prefetch), each tile's
-// descriptor words (and HP masks) loaded while the previous tile is processed, so a tile starts
-// without waiting on a descriptor fetch; with an index list the list entries are read one tile
-// further ahead still (list entry, then descriptor: two dependent loads off the critical path).
-// Tiles are taken in chunks of C consecutive ones — chunks first, first + stride, ... — so that
-// a multi-key wave meets a key's consecutive tiles (the partition lays them out together) in a
-// row. Tiles below `base` are not this launch's (chunks count from it). A device-side count
-// without an index list runs unprefetched.
-template <bool OPEN, uint32_t C = 1, class F>
-__device__ __forceinline__ void for_tiles(uint32_t first, uint32_t stride, const mq_pkt_desc* __restrict__ desc,
-                                          uint32_t n, const uint32_t* __restrict__ index,
-                                          const uint32_t* __restrict__ n_dev, const uint2* __restrict__ hpm,
-                                          F&& body, uint32_t base = 0) {
-  const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
-  if (n_dev && !index) {
-    for (uint32_t t = base + first; t < tiles; t += stride) body(t, TilePrefetch{false, 0u, 0u, 0u});
-    return;
+// Work distribution of the persistent tile kernels (r04). Wave g of a grid of
+// `waves` waves runs tile base + g first. After that:
+//   static  (ctr null): tiles base + g + waves, base + g + 2 waves, ...;
+//   dynamic (ctr = the launch's schedule slot, mq_runtime.h SchedSlots): chunks of the remaining
+//     tiles claimed with a returning device-scope atomicAdd on a head word. The remaining range is
+//     split into kSchedHeads parts with one head each (one per XCD: ≈88 claims/µs saturate one
+//     word, MI355X_MICROARCH.md 'dequeue'); a wave claims from its XCD's head — chunks of
+//     remaining / (2 x the waves per head), 1..kMaxChunk tiles (guided self-scheduling) — then,
+//     once that part is gone, single tiles from the other heads in turn. The next chunk is claimed
+//     when the current one starts, so a claim's latency hides behind at least one tile.
+// Why: the static stride gives every workgroup a fixed share, so a workgroup that is placed late —
+// its CU held by another kernel, e.g. the resident per-packet server (mq_resident.hip) or the
+// hot-key kernel forked beside this one — ends the launch a whole share late. Dynamically, the
+// others take what it has not started.
+// Slot layout (uint32 words): head h at word kSchedHeadWords * h, the finished-workgroup count at
+// word kSchedDoneWord. The last workgroup to finish zeroes the slot (sched_done) for the next
+// kernel on the same stream.
+// (kSchedHeads, kSchedHeadWords, kSchedDoneWord, kSchedSlotBytes: mq_device.h, shared with the host)
+#ifndef MQ_SCHED_MAX_CHUNK
+#define MQ_SCHED_MAX_CHUNK 16
+#endif
+constexpr uint32_t kMaxChunk = MQ_SCHED_MAX_CHUNK;
+
+struct TileSched {
+  uint32_t* ctr;   // null: static
+  uint32_t g;      // this wave's index in the grid (blockIdx.x * W + wave)
+  uint32_t waves;  // waves in the grid
+  uint32_t xcd;    // this workgroup's head (blockIdx.x % kSchedHeads: workgroups go to the XCDs round robin)
+};
+
+__device__ __forceinline__ uint32_t sched_claim(uint32_t* head, uint32_t c) {
+  uint32_t h = 0;
+  if ((threadIdx.x & (kWave - 1)) == 0) h = __hip_atomic_fetch_add(head, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return (uint32_t)__builtin_amdgcn_readlane((int)h, 0);
+}
+
+// End of a workgroup's part in a dynamically scheduled launch (every workgroup of the grid exactly
+// once, workgroup-uniform, after all its waves are done with the schedule — the callers put it
+// after a barrier or, for a workgroup without work, at its only exit). The last one zeroes the
+// slot: every claim of every wave has returned by then (its value was used), so no claim is lost.
+__device__ __forceinline__ void sched_done(uint32_t* ctr) {
+  if (!ctr || threadIdx.x != 0) return;
+  const uint32_t old = __hip_atomic_fetch_add(ctr + kSchedDoneWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (old + 1 == gridDim.x) {
+#pragma unroll
+    for (uint32_t h = 0; h < kSchedHeads; ++h)
+      __hip_atomic_store(ctr + kSchedHeadWords * h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(ctr + kSchedDoneWord, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+}
+
+// Persistent tile loop: this wave runs its tiles (TileSched) calling body(tile, prefetch), each
+// tile's descriptor words (and HP masks) loaded while the previous tile is processed, so a tile
+// starts without waiting on a descriptor fetch; with an index list the list entries are read one
+// tile further ahead still (list entry, then descriptor: two dependent loads off the critical
+// path). Tiles below `base` are not this launch's. With a device-side count (n_dev) the tiles end
+// at that count.
+template <bool OPEN, class F>
+__device__ __forceinline__ void for_tiles(const TileSched& ts, const mq_pkt_desc* __restrict__ desc, uint32_t n,
+                                          const uint32_t* __restrict__ index, const uint32_t* __restrict__ n_dev,
+                                          const uint2* __restrict__ hpm, F&& body, uint32_t base = 0) {
+  const uint32_t count = n_dev ? *n_dev : n;
+  const uint32_t tiles = (count + kPktsPerTile - 1) / kPktsPerTile;
   const uint32_t lane = threadIdx.x & (kWave - 1), p = lane / kLanesPerPkt, j = lane % kLanesPerPkt;
-  auto next = [&](uint32_t t) { return (t - base + 1) % C != 0 ? t + 1 : t + 1 - C + stride * C; };
+  constexpr uint32_t kNone = 0xFFFFFFFFu;
+  // dynamic schedule (wave-uniform state): the tiles from dyn0 on, split over the heads
+  const uint32_t dyn0 = base + ts.waves;
+  const uint32_t D = tiles > dyn0 ? tiles - dyn0 : 0u;
+  auto head_lo = [&](uint32_t h) { return dyn0 + (uint32_t)(((uint64_t)D * h) / kSchedHeads); };
+  const uint32_t per_head = ts.waves / kSchedHeads > 1u ? ts.waves / kSchedHeads : 1u;
+  uint32_t state = 0;       // 0: own head, 1: the other heads, 2: none left
+  uint32_t seen = 0;        // own head: tiles claimed as of this wave's last claim
+  uint32_t cend = 0;        // end of the chunk being walked
+  // the claim of the next chunk, issued when the current one starts and resolved when it ends: the
+  // atomic's result stays in a VGPR meanwhile (lane 0), so no wave waits on it (or on the stores
+  // before it: vmcnt counts both) in steady state
+  uint32_t qh = 0, qc = 0;
+  bool pending = false;
+  const uint32_t own_lo = head_lo(ts.xcd), own_size = head_lo(ts.xcd + 1) - own_lo;
+  auto issue = [&]() {
+    if (state != 0) return;  // the other heads are claimed at resolve time
+    const uint32_t rem = own_size > seen ? own_size - seen : 0u;
+    uint32_t c = rem / (2 * per_head);
+    qc = c < 1u ? 1u : (c > kMaxChunk ? kMaxChunk : c);
+    qh = 0;
+    if (lane == 0 && own_size)
+      qh = __hip_atomic_fetch_add(ts.ctr + kSchedHeadWords * ts.xcd, qc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    pending = true;
+  };
+  // the next chunk [s, e): the pending own-head claim, else a single tile from another head
+  auto resolve = [&](uint32_t& cs, uint32_t& ce) -> bool {
+    if (state == 0) {
+      const uint32_t got = own_size ? (uint32_t)__builtin_amdgcn_readlane((int)qh, 0) : 0u;
+      const bool ok = pending && got < own_size;
+      pending = false;
+      if (ok) {
+        cs = own_lo + got;
+        ce = own_lo + (got + qc < own_size ? got + qc : own_size);
+        seen = got + qc;
+        return true;
+      }
+      state = 1;
+    }
+    // the other heads, single tiles: one round trip reads all heads (a returning add of 0 on lanes
+    // 0..7: atomics are coherent across the XCDs' L2s, plain loads are not), then a claim from the
+    // first one after this XCD's with tiles left; a lost race rescans (someone else progressed)
+#pragma nounroll
+    for (uint32_t tries = 0; state == 1 && tries < 64; ++tries) {
+      uint32_t v = 0xFFFFFFFFu, sz = 0;
+      if (lane < kSchedHeads) {
+        v = __hip_atomic_fetch_add(ts.ctr + kSchedHeadWords * lane, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sz = head_lo(lane + 1) - head_lo(lane);
+      }
+      const uint32_t open = (uint32_t)__ballot(lane < kSchedHeads && v < sz) & 0xFFu;
+      if (!open) break;
+      const uint32_t x = (ts.xcd + 1) % kSchedHeads;
+      const uint32_t rot = ((open >> x) | (open << (kSchedHeads - x))) & 0xFFu;
+      const uint32_t h = (x + (uint32_t)__builtin_ctz(rot)) % kSchedHeads;
+      const uint32_t lo = head_lo(h), size = head_lo(h + 1) - lo;
+      const uint32_t got = sched_claim(ts.ctr + kSchedHeadWords * h, 1u);
+      if (got < size) {
+        cs = lo + got;
+        ce = cs + 1;
+        return true;
+      }
+    }
+    state = 2;
+    return false;
+  };
+  auto next = [&](uint32_t t) -> uint32_t {
+    if (t >= tiles) return kNone;
+    if (!ts.ctr) return t + ts.waves;
+    if (t + 1 < cend) return t + 1;
+    uint32_t cs, ce;
+    if (!resolve(cs, ce)) return kNone;
+    cend = ce;
+    issue();  // the chunk after this one
+    return cs;
+  };
   auto idx_of = [&](uint32_t t) -> uint32_t {  // packet p's descriptor index (list: a load)
     const uint32_t e = t * kPktsPerTile + p;
-    if (t >= tiles || e >= n) return kListHole;
+    if (t >= tiles || e >= count) return kListHole;
     return index ? index[e] : e;
   };
   auto fetch = [&](uint32_t ix, uint32_t& dw, uint32_t& hm) {
@@ -503,7 +622,12 @@ __device__ __forceinline__ void for_tiles(uint32_t first, uint32_t stride, const
     dw = ok ? reinterpret_cast<const uint32_t*>(desc)[(size_t)ix * 8 + j] : 0u;
     hm = (OPEN && hpm && ok && j < 2) ? reinterpret_cast<const uint32_t*>(hpm)[(size_t)ix * 2 + j] : 0u;
   };
-  uint32_t t = base + first * C, t1 = next(t);
+  uint32_t t = base + ts.g;
+  if (ts.ctr && t < tiles) {
+    cend = t + 1;
+    issue();  // resolved right away by next(t): one wait per wave, at its start
+  }
+  uint32_t t1 = next(t);
   uint32_t ix0 = idx_of(t), ix1 = idx_of(t1), dw, hm;
   fetch(ix0, dw, hm);
   while (t < tiles) {

@@ -151,10 +151,40 @@ def config_c(n=1 << 20, **kw):
     return uniform(n, _lib.MQ_SUITE_AES128GCM, **kw)
 
 
-def config_e(n=1 << 20, seed=SEED, n_conns=4096, lmin=64, lmax=1350):
-    """Mixed batch (config E)."""
+LONG_HDR = 1 + 4 + 1 + 8 + 1 + 8 + 1 + 2  # Initial header without the PN: 26 bytes
+SHORT_HDR = 1 + 8
+
+
+@dataclass
+class MixedPlan:
+    """Per-packet layout of a global config-E batch (no payload bytes): any range or sample of it
+    can be built on its own (sharded runs, sampled parity checks)."""
+    kind: np.ndarray    # 0 Initial AES, 1 1-RTT ChaCha, 2 1-RTT AES
+    pn_len: np.ndarray
+    L: np.ndarray
+    conn: np.ndarray
+    pns: np.ndarray
+    offs: np.ndarray    # byte offset of each packet in the global arena (packed back to back)
+    dcids: np.ndarray
+    keys: list
+    seed: int
+
+    @property
+    def n(self):
+        return len(self.L)
+
+
+_PLAN_CACHE = {}
+
+
+def mixed_plan(n=1 << 20, seed=SEED, n_conns=4096, lmin=64, lmax=1350):
+    """The layout of config E's n-packet batch (random draws in a fixed order, so that the plan of
+    n packets is the same whatever range of it is built later)."""
+    ck = (n, seed, n_conns, lmin, lmax)
+    if ck in _PLAN_CACHE:
+        return _PLAN_CACHE[ck]
     rng = np.random.default_rng(seed & 0xFFFFFFFF)
-    kind = rng.choice(3, size=n, p=[0.25, 0.375, 0.375])  # 0 Initial AES, 1 1-RTT ChaCha, 2 1-RTT AES
+    kind = rng.choice(3, size=n, p=[0.25, 0.375, 0.375])
     pn_len = rng.integers(1, 5, size=n).astype(np.uint8)
     L = rng.integers(lmin, lmax + 1, size=n).astype(np.int64)
     # key rows: [0] 1-RTT ChaCha (A.5), [1] 1-RTT AES (A.1 server), [2..] Initial per connection
@@ -164,47 +194,86 @@ def config_e(n=1 << 20, seed=SEED, n_conns=4096, lmin=64, lmax=1350):
         client, _server = derive_initial_secrets(dcids[c].tobytes())
         keys.append(key_material(_lib.MQ_SUITE_AES128GCM, client))
     conn = rng.integers(0, n_conns, size=n)
-    short_hdr = 1 + 8
-    long_hdr = 1 + 4 + 1 + 8 + 1 + 8 + 1 + 2  # no PN: 26 bytes
-    pn_off = np.where(kind == 0, long_hdr, short_hdr).astype(np.int64)
+    pn_off = np.where(kind == 0, LONG_HDR, SHORT_HDR).astype(np.int64)
     L = np.maximum(L, pn_off + pn_len + 16 + 4).astype(np.int64)  # sample fits: pn_off + 20 <= L
     L = np.maximum(L, pn_off + 20)
     offs = np.zeros(n, dtype=np.int64)
     offs[1:] = np.cumsum(L[:-1])
-    total = int(offs[-1] + L[-1])
-    arena = splitmix_bytes(total, seed)
     pns = (np.uint64(1 << 20) + rng.integers(0, 1 << 30, size=n).astype(np.uint64))
+    plan = MixedPlan(kind, pn_len, L, conn, pns, offs, dcids, keys, seed)
+    _PLAN_CACHE.clear()  # one plan at a time (an 8 x 2^20 plan holds ~0.5 GB)
+    _PLAN_CACHE[ck] = plan
+    return plan
+
+
+def _mixed_build(plan, sel, arena, pos):
+    """Headers and descriptors of the plan's packets `sel` (indices), placed at arena offsets `pos`
+    (their payload bytes already in the arena)."""
+    kind, pn_len, L, pns = plan.kind[sel], plan.pn_len[sel], plan.L[sel], plan.pns[sel]
+    conn = plan.conn[sel]
+    pn_off = np.where(kind == 0, LONG_HDR, SHORT_HDR).astype(np.int64)
     key_id = np.where(kind == 0, 2 + conn, np.where(kind == 1, 0, 1)).astype(np.uint32)
     flags = np.where(kind == 0, _lib.MQ_PKT_LONG_HEADER, 0).astype(np.uint8)
-    # headers
     s = np.nonzero(kind != 0)[0]
-    o = offs[s]
+    o = pos[s]
     arena[o] = (0x40 | (pn_len[s] - 1)).astype(np.uint8)
     for j in range(8):
         arena[o + 1 + j] = DCID8[j]
     li = np.nonzero(kind == 0)[0]
-    o = offs[li]
+    o = pos[li]
     arena[o] = (0xC0 | (pn_len[li] - 1)).astype(np.uint8)
     arena[o + 1] = 0; arena[o + 2] = 0; arena[o + 3] = 0; arena[o + 4] = 1
     arena[o + 5] = 8
     for j in range(8):
-        arena[o + 6 + j] = dcids[conn[li], j]
+        arena[o + 6 + j] = plan.dcids[conn[li], j]
     arena[o + 14] = 8
     for j in range(8):
         arena[o + 15 + j] = (j * 17 + 3) & 0xFF
     arena[o + 23] = 0  # token length
-    length = (L[li] - long_hdr).astype(np.int64)  # PN + payload + tag
+    length = (L[li] - LONG_HDR).astype(np.int64)  # PN + payload + tag
     arena[o + 24] = (0x40 | (length >> 8)).astype(np.uint8)
     arena[o + 25] = (length & 0xFF).astype(np.uint8)
     for j in range(4):
-        sel = pn_len > j
-        idx = np.nonzero(sel)[0]
+        idx = np.nonzero(pn_len > j)[0]
         shift = (8 * (pn_len[idx].astype(np.int64) - 1 - j)).astype(np.uint64)
-        arena[offs[idx] + pn_off[idx] + j] = ((pns[idx] >> shift) & np.uint64(0xFF)).astype(np.uint8)
+        arena[pos[idx] + pn_off[idx] + j] = ((pns[idx] >> shift) & np.uint64(0xFF)).astype(np.uint8)
     # decode_pn must recover pn from pn_len bytes: largest_pn = pn - 1
-    seal = make_descs(offs.astype(np.uint64), L.astype(np.uint32), key_id, pns, pn_off.astype(np.uint16), pn_len,
-                      flags)
-    opn = make_descs(offs.astype(np.uint64), L.astype(np.uint32), key_id, pns - np.uint64(1),
-                     pn_off.astype(np.uint16), 0, flags)
-    assert encode_varint(1000) == b"\x43\xe8"
-    return Workload(f"mixed-{n}", arena, seal, opn, keys, _lib.MQ_SUITE_MIXED, pns)
+    seal = make_descs(pos.astype(np.uint64), L.astype(np.uint32), key_id, pns, pn_off.astype(np.uint16), pn_len, flags)
+    opn = make_descs(pos.astype(np.uint64), L.astype(np.uint32), key_id, pns - np.uint64(1), pn_off.astype(np.uint16),
+                     0, flags)
+    return seal, opn
+
+
+def config_e(n=1 << 20, seed=SEED, n_conns=4096, lmin=64, lmax=1350, lo=0, hi=None):
+    """Mixed batch (config E): packets [lo, hi) of the n-packet global batch (default: all of it).
+    The range's arena is the global arena's bytes from the 16-B chunk holding packet lo's first
+    byte (so a shard is exactly its slice of the global batch), descriptors rebased."""
+    plan = mixed_plan(n, seed, n_conns, lmin, lmax)
+    hi = n if hi is None else hi
+    sel = np.arange(lo, hi)
+    if len(sel) == 0:
+        from .batch import DESC_DTYPE
+        empty = np.zeros(0, dtype=DESC_DTYPE)
+        return Workload(f"mixed-{n}[{lo}:{hi}]", np.zeros(16, np.uint8), empty, empty.copy(), plan.keys,
+                        _lib.MQ_SUITE_MIXED, np.zeros(0, np.uint64))
+    base = int(plan.offs[lo]) & ~15
+    end = int(plan.offs[hi - 1] + plan.L[hi - 1])
+    arena = splitmix_bytes(end - base, seed, start=base)
+    seal, opn = _mixed_build(plan, sel, arena, plan.offs[sel] - base)
+    name = f"mixed-{n}" if (lo, hi) == (0, n) else f"mixed-{n}[{lo}:{hi}]"
+    return Workload(name, arena, seal, opn, plan.keys, _lib.MQ_SUITE_MIXED, plan.pns[sel])
+
+
+def config_e_at(indices, n=1 << 20, seed=SEED, n_conns=4096, lmin=64, lmax=1350):
+    """The packets of the given global indices of config E's n-packet batch, each with its own
+    bytes of the global arena, packed back to back (the oracle seals exactly these)."""
+    plan = mixed_plan(n, seed, n_conns, lmin, lmax)
+    g = np.asarray(indices, dtype=np.int64)
+    Ls = plan.L[g]
+    pos = np.zeros(len(g), dtype=np.int64)
+    pos[1:] = np.cumsum(Ls[:-1])
+    arena = np.empty(int(Ls.sum()), dtype=np.uint8)
+    for k, gi in enumerate(g):
+        arena[pos[k]:pos[k] + Ls[k]] = splitmix_bytes(int(Ls[k]), seed, start=int(plan.offs[gi]))
+    seal, opn = _mixed_build(plan, g, arena, pos)
+    return Workload(f"mixed-sample-{len(g)}", arena, seal, opn, plan.keys, _lib.MQ_SUITE_MIXED, plan.pns[g])

@@ -24,7 +24,7 @@
 struct FakeObj {
   int dev;
   std::atomic<bool> dead{false};
-  std::atomic<int> records{0}, waits{0};
+  std::atomic<int> records{0}, waits{0}, syncs{0};
   explicit FakeObj(int d) : dev(d) {}
 };
 
@@ -82,8 +82,22 @@ struct Fake {
     ++s->waits;
     return true;
   }
+  static void* alloc_zeroed(size_t bytes) {  // leaked on purpose, as the library's slots are
+    ++allocs;
+    void* p = std::calloc(1, bytes);
+    allocated.push_back(p);
+    return p;
+  }
+  static void stream_sync(Stream s) {
+    CHECK(!s->dead);
+    ++s->syncs;
+  }
+  static std::atomic<int> allocs;
+  static std::vector<void*> allocated;
 };
 std::atomic<int> Fake::live_streams{0}, Fake::live_events{0}, Fake::set_calls{0}, Fake::usable_calls{0};
+std::atomic<int> Fake::allocs{0};
+std::vector<void*> Fake::allocated;
 
 typedef mq::DeviceRegistry<Fake> Devices;
 
@@ -230,11 +244,62 @@ static void test_concurrent_forks() {
   for (auto* c : callers) delete c;
 }
 
+// dynamic-schedule slots: one per (device, stream), stable, distinct, bounded; release waits for
+// the stream's work before recycling its slot
+static void test_sched_slots() {
+  mq::SchedSlots<Fake> sl(3, 1024);
+  FakeObj s[5] = {FakeObj(1), FakeObj(1), FakeObj(1), FakeObj(1), FakeObj(3)};
+  uint8_t* a = (uint8_t*)sl.get(1, &s[0]);
+  uint8_t* b = (uint8_t*)sl.get(1, &s[1]);
+  uint8_t* c = (uint8_t*)sl.get(1, &s[2]);
+  CHECK(a && b && c && a != b && b != c && a != c);
+  CHECK(Fake::allocs == 1);  // one allocation per device
+  for (uint8_t* p : {a, b, c}) {
+    const long d = p - a;
+    CHECK(d % 1024 == 0 && d >= -2048 && d <= 2048);
+    for (int k = 0; k < 1024; ++k) CHECK(p[k] == 0);  // zeroed
+  }
+  CHECK(sl.get(1, &s[0]) == a && sl.get(1, &s[2]) == c);  // stable per stream
+  CHECK(sl.get(1, &s[3]) == nullptr);                     // capacity: static schedule
+  CHECK(sl.get(3, &s[4]) != nullptr && Fake::allocs == 2);  // another device, its own slots
+  CHECK(sl.get(-1, &s[0]) == nullptr);
+  CHECK(sl.assigned(1) == 3 && sl.assigned(3) == 1);
+  sl.release(&s[1]);
+  CHECK(s[1].syncs == 1 && s[0].syncs == 0);  // waited for before recycling
+  CHECK(sl.assigned(1) == 2);
+  CHECK(sl.get(1, &s[3]) == b);  // the recycled slot
+  sl.release(&s[1]);
+  CHECK(s[1].syncs == 1);  // nothing held: no wait
+  // concurrent gets of the same streams agree
+  mq::SchedSlots<Fake> many(64, 64);
+  std::vector<FakeObj*> st;
+  for (int k = 0; k < 16; ++k) st.push_back(new FakeObj(0));
+  std::vector<void*> seen[4];
+  std::vector<std::thread> th;
+  for (int t = 0; t < 4; ++t)
+    th.emplace_back([&, t] {
+      for (int k = 0; k < 16; ++k) seen[t].push_back(many.get(0, st[(k + 5 * t) % 16]));
+    });
+  for (auto& x : th) x.join();
+  std::set<void*> uniq;
+  for (int k = 0; k < 16; ++k) {
+    void* p = many.get(0, st[k]);
+    CHECK(p);
+    uniq.insert(p);
+    for (int t = 0; t < 4; ++t) CHECK(seen[t][(k - 5 * t + 80) % 16] == p);
+  }
+  CHECK(uniq.size() == 16);
+  for (auto* x : st) delete x;
+  for (void* p : Fake::allocated) std::free(p);
+  Fake::allocated.clear();
+}
+
 int main() {
   test_per_thread_selection();
   test_guard();
   test_side_streams();
   test_concurrent_forks();
+  test_sched_slots();
   std::printf("runtime ok\n");
   return 0;
 }

@@ -42,27 +42,41 @@ def test_launch_two_ranks_sharded_global_batch(tmp_path, orc, keys):
 
 @pytest.mark.parametrize("corrupt", [None, 1])
 def test_launch_two_ranks_config_e(tmp_path, orc, corrupt):
-    # config E ranks hold independent seeded batches; each rank checks its own sample
-    # against the oracle, so a correct 2-rank run matches and a wrong result on rank 1 does not
+    # config E over N ranks is ONE global mixed batch of N x n packets split at
+    # byte quantiles of the packet lengths; rank 0's oracle checks the global sample
+    # the ranks all-reduce, so a correct 2-rank run matches and a wrong result on rank 1 does not
     out = tmp_path / "r0.json"
     os.environ["MQ_TEST_OUT"] = str(out)
     if corrupt is None:
         os.environ.pop("MQ_TEST_CORRUPT_RANK", None)
     else:
         os.environ["MQ_TEST_CORRUPT_RANK"] = str(corrupt)
+    n = 700
     try:
-        rc = bench.launch_ranks(2, ["--gpus", "2", "--packets", "700", "--config", "e"],
+        rc = bench.launch_ranks(2, ["--gpus", "2", "--packets", str(n), "--config", "e"],
                                 script=os.path.join(HERE, "dist_bench_worker.py"))
     finally:
         os.environ.pop("MQ_TEST_CORRUPT_RANK", None)
     assert rc == 0
     r = json.loads(out.read_text())
-    assert r["world"] == 2 and r["fails"] == 0
+    assert r["world"] == 2 and r["fails"] == 0 and r["oracle_fail"] == 0
     p = r["parity"]
-    assert p["ranks_mismatching_oracle"] == (0 if corrupt is None else 1)
     assert p["match"] == (corrupt is None)
+    assert (p["sample_tag_checksum"] == r["oracle_sample_csum"]) == (corrupt is None)
     # every rank reaches the same verdict
     assert {(tmp_path / f"r0.json.match{k}").read_text() for k in (0, 1)} == {"1" if corrupt is None else "0"}
+    # the shards tile the global batch at its byte median, and hold exactly its packets
+    sh = [json.loads((tmp_path / f"r0.json.shard{k}").read_text()) for k in (0, 1)]
+    w = workload.config_e(2 * n)
+    assert sh[0]["first"] == 0 and sh[1]["first"] == sh[0]["n"] and sh[0]["n"] + sh[1]["n"] == 2 * n
+    L = w.seal_desc["len"].astype(np.int64)
+    assert sh[0]["wire"] == int(L[:sh[0]["n"]].sum()) and sh[1]["wire"] == int(L[sh[0]["n"]:].sum())
+    assert abs(sh[0]["wire"] - sh[1]["wire"]) <= 2 * int(L.max())  # byte-balanced, not count-balanced
+    assert shard.shard_range_bytes(L, 1, 2) == (sh[1]["first"], 2 * n)
+    st = orc.batch_seal(w.keys, w.arena, w.seal_desc, w.suite_hint, threads=4)
+    assert (st == 0).all()
+    if corrupt is None:
+        assert sh[0]["csum"] + sh[1]["csum"] == shard.tag_checksum(w.arena, w.seal_desc)
 
 
 def test_sample_indices_and_shard_positions():
@@ -70,7 +84,7 @@ def test_sample_indices_and_shard_positions():
         g = shard.sample_indices(n * world)
         got = []
         for rank in range(world):
-            gs, local = bench.sample_for_rank("b", n, rank, world)
+            gs, local = bench.sample_for_rank(n * world, rank * n, n)
             assert (gs == g).all() and ((local >= 0) & (local < n)).all()
             got.append(local + rank * n)
         assert (np.concatenate(got) == g).all()

@@ -106,3 +106,29 @@ def test_two_rank_gloo_shards_match_single_process(tmp_path, balance):
         elapsed, wire, fails = z["tot"]
         assert elapsed == 1.5 and fails == 0  # max over ranks (0.5, 1.5); summed failures
     assert int(wire) == total_wire == int(w.seal_desc["len"].astype(np.int64).sum())
+
+
+def test_config_e_ranges_are_slices_of_the_global_batch():
+    """workload.config_e(n, lo=, hi=) and config_e_at(): a shard or a sample of the mixed batch is
+    built on its own and equals its part of the whole (bench.py's sharded config E)."""
+    from milli_quic_amd import workload
+    n = 3000
+    whole = workload.config_e(n, seed=11)
+    L = whole.seal_desc["len"].astype(np.int64)
+    parts = [shard.shard_range_bytes(L, r, 3) for r in range(3)]
+    assert parts[0][0] == 0 and parts[-1][1] == n
+    for (lo, hi) in parts:
+        r = workload.config_e(n, seed=11, lo=lo, hi=hi)
+        base = int(whole.seal_desc["offset"][lo]) & ~15
+        assert r.n == hi - lo and (r.pns == whole.pns[lo:hi]).all()
+        for f in ("len", "key_id", "pn", "pn_offset", "pn_len", "flags"):
+            assert (r.seal_desc[f] == whole.seal_desc[f][lo:hi]).all()
+        assert (r.seal_desc["offset"].astype(np.int64) == whole.seal_desc["offset"][lo:hi].astype(np.int64) - base).all()
+        assert r.arena.tobytes() == whole.arena[base:base + len(r.arena)].tobytes()
+    g = np.array([0, 1, 977, n - 1])
+    s = workload.config_e_at(g, n, seed=11)
+    for k, i in enumerate(g):
+        o, ln = int(whole.seal_desc["offset"][i]), int(L[i])
+        so = int(s.seal_desc["offset"][k])
+        assert s.arena[so:so + ln].tobytes() == whole.arena[o:o + ln].tobytes()
+        assert s.seal_desc["key_id"][k] == whole.seal_desc["key_id"][i]

@@ -39,7 +39,8 @@ def to_dev(a):
 @pytest.mark.parametrize("rank,keys", [(0, 1), (7, 1), (7, 1024)])
 def test_config_d_shard_vs_oracle(orc, rank, keys):
     k = bench.rank_keys("b", keys, None, DEV)
-    w = bench.build_shard("b", N, rank, WORLD, k)
+    w, first = bench.build_shard("b", N, rank, WORLD, k)
+    assert first == rank * N
     assert int(w.pns[0]) == workload.PN0 + rank * N and int(w.pns[-1]) == workload.PN0 + (rank + 1) * N - 1
     kt = KeyTable(w.keys)
     a, sd, od = to_dev(w.arena), to_dev(w.seal_desc), to_dev(w.open_desc)
@@ -49,7 +50,7 @@ def test_config_d_shard_vs_oracle(orc, rank, keys):
     batch.seal(kt, a, sd, st, w.suite_hint, ws)
     torch.cuda.synchronize()
     assert int((st != 0).sum()) == 0
-    g, local = bench.sample_for_rank("b", N, rank, WORLD)
+    g, local = bench.sample_for_rank(N * WORLD, first, N)
     assert len(g) == 4096 and len(local) == 4096 // WORLD
     mine = g[(g >= rank * N) & (g < (rank + 1) * N)]
     sw = workload.uniform_at(mine, w.suite_hint, keys=w.keys)

@@ -127,3 +127,150 @@ def test_resident_threads(orc):
     for x in th:
         x.join()
     assert not errors, errors[:5]
+
+
+def _batch_c(n, stream):
+    """A config-C batch on the device (single-key AES-128-GCM: the persistent single-key kernels,
+    one 16-wave workgroup per CU) and its seal / open closures on `stream`."""
+    from milli_quic_amd import batch, workload
+    from milli_quic_amd.batch import KeyTable
+    w = workload.config_c(n)
+    dev = torch.device("cuda", 0)
+    kt = KeyTable(w.keys)
+    arena = torch.from_numpy(w.arena.copy()).to(dev)
+    sd = torch.from_numpy(w.seal_desc.view(np.uint8).copy()).to(dev)
+    od = torch.from_numpy(w.open_desc.view(np.uint8).copy()).to(dev)
+    st = torch.zeros(w.n, dtype=torch.uint8, device=dev)
+    pn = torch.zeros(w.n, dtype=torch.int64, device=dev)
+    ws = torch.empty(max(batch.workspace_bytes(w.n), 256), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+
+    def seal():
+        batch.seal(kt, arena, sd, st, w.suite_hint, ws, stream.cuda_stream)
+
+    def open_():
+        batch.open_(kt, arena, od, st, pn, w.suite_hint, ws, stream.cuda_stream)
+    return w, arena, st, seal, open_
+
+
+@pytest.mark.timeout(90)
+def test_resident_timeout_then_recovers(orc):
+    # ADVICE r03: a call that times out must not leave the server unable to serve (r03 waited for
+    # done + 1 forever) nor a kernel that writes the mailbox during the next call. The timeout is
+    # forced: the server has idled out, a long AES batch holds every CU (persistent grid, one
+    # 160-KiB workgroup per CU), so the relaunched server cannot be placed within 100 us. The
+    # batch runs on its own stream and only that stream is synchronised (a device-wide sync would
+    # also wait for the resident kernel).
+    s = torch.cuda.Stream()
+    w, arena, st, seal, open_ = _batch_c(1 << 20, s)
+    key = bytes(range(32))
+    aead = crypto.ChaCha20Provider().aead(key)
+    outcomes = []
+    try:
+        for k in range(3):
+            s.synchronize()
+            time.sleep(0.05)  # the server leaves after 2 ms without a call
+            for _ in range(6):
+                seal()
+                open_()
+            os.environ["MQ_RESIDENT_TIMEOUT_US"] = "100"
+            nonce, pt = bytes([k + 1]) * 12, bytes(range(256)) * 3
+            buf = bytearray(pt) + bytearray(16)
+            try:
+                aead.seal_in_place(nonce, b"hdr", buf, len(pt))
+                outcomes.append("served")
+                assert bytes(buf) == orc.aead_seal(2, key, nonce, b"hdr", pt)[1]
+            except crypto.DeviceError:
+                outcomes.append("timeout")
+            finally:
+                os.environ.pop("MQ_RESIDENT_TIMEOUT_US", None)
+            print("resident timeout test: call", k, outcomes[-1], flush=True)
+            # the next calls are served, byte-exact (both while the batch may still run and after)
+            for q in range(4):
+                nonce, pt = bytes([k + 1, q]) * 6, bytes((q * 31 + i) & 0xFF for i in range(1000))
+                buf = bytearray(pt) + bytearray(16)
+                aead.seal_in_place(nonce, b"hdr2", buf, len(pt))
+                assert bytes(buf) == orc.aead_seal(2, key, nonce, b"hdr2", pt)[1], (k, q)
+                assert aead.open_in_place(nonce, b"hdr2", buf, len(buf)) == len(pt)
+                assert bytes(buf[:len(pt)]) == pt
+            s.synchronize()
+    finally:
+        os.environ.pop("MQ_RESIDENT_TIMEOUT_US", None)
+    assert (st.cpu().numpy() == 0).all()
+    assert arena.cpu().numpy().tobytes() == w.arena.tobytes()  # seal + open rounds: plaintext back
+    print("timeout outcomes", outcomes)
+    assert "timeout" in outcomes  # the path under test ran at least once
+
+
+@pytest.mark.timeout(120)
+def test_batch_beside_resident_server(orc):
+    # VERDICT r03 #2: per-packet calls (the resident server holds a CU) while a config-C batch runs.
+    # The persistent AES grid has one workgroup per CU; under r03's static tile stride the workgroup
+    # that found its CU taken started a whole kernel late (~2x). With the dynamic schedule the batch
+    # stays within 1.15x of its time without the server, and its bytes equal the oracle's.
+    s = torch.cuda.Stream()
+    w, arena, st, seal, open_ = _batch_c(1 << 20, s)
+
+    def timed(k):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * k)]
+        for i in range(k):
+            ev[2 * i].record(s)
+            seal()
+            open_()
+            ev[2 * i + 1].record(s)
+        s.synchronize()
+        return float(np.median([ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(k)]))
+
+    for _ in range(3):
+        seal()
+        open_()
+    s.synchronize()
+    time.sleep(0.05)  # no server
+    alone = timed(8)
+    stop, calls, errors = threading.Event(), [0], []
+    key = bytes(range(16))
+    aead = crypto.Aes128GcmProvider().aead(key)
+
+    def per_packet():
+        try:
+            k = 0
+            while not stop.is_set():
+                nonce, pt = k.to_bytes(12, "big"), bytes((k + i) & 0xFF for i in range(1171))
+                buf = bytearray(pt) + bytearray(16)
+                aead.seal_in_place(nonce, b"h" * 13, buf, len(pt))
+                if k % 50 == 0 and bytes(buf) != orc.aead_seal(1, key, nonce, b"h" * 13, pt)[1]:
+                    errors.append(k)
+                calls[0] += 1
+                k += 1
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = threading.Thread(target=per_packet)
+    th.start()
+    try:
+        while calls[0] < 20 and th.is_alive():
+            time.sleep(0.001)
+        beside = timed(8)
+        seal()  # the sealed bytes under the server, checked below
+        s.synchronize()
+        sealed = arena.cpu().numpy().copy()
+        open_()
+        s.synchronize()
+    finally:
+        stop.set()
+        th.join()
+    assert not errors, errors[:3]
+    assert (st.cpu().numpy() == 0).all()
+    assert arena.cpu().numpy().tobytes() == w.arena.tobytes()
+    # every 256th packet of the sealed arena against the oracle
+    idx = np.arange(0, w.n, 256)
+    ref = w.arena.copy()
+    sd = w.seal_desc[idx].copy()
+    assert (orc.batch_seal(w.keys, ref, sd, w.suite_hint) == 0).all()
+    for i in idx:
+        o, L = int(w.seal_desc["offset"][i]), int(w.seal_desc["len"][i])
+        assert sealed[o:o + L].tobytes() == ref[o:o + L].tobytes(), i
+    print(f"config C seal+open: alone {alone:.3f} ms, beside the server {beside:.3f} ms "
+          f"({beside / alone:.3f}x, {calls[0]} per-packet calls)")
+    assert calls[0] > 20
+    assert beside <= 1.15 * alone, (alone, beside)

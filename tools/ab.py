@@ -19,6 +19,7 @@ def main():
                 print(lib, "FAILED", out.stderr[-400:])
                 continue
             s, o = map(float, line[0].split()[1:])
+            print(f"  {lib} seal {s:.4f} open {o:.4f}", flush=True)
             res[lib][0].append(s)
             res[lib][1].append(o)
     for lib, (s, o) in res.items():
