@@ -417,27 +417,35 @@ def main():
         if ev is not None:
             ev[3 * i + 2].record(stream)
 
-    # Events exist before the warm-up: creating them between the warm-up and the timed steps left
-    # the GPU idle for milliseconds, after which its clocks ramp up again over ~20 ms — the first
-    # timed steps ran up to 40 % slower (profiles/r04b_clock_probe.txt)
+    # Nothing that can idle the GPU for milliseconds may sit between the warm-up and the timed steps
+    # (after an idle of a few ms the first ~5 steps run up to 40 % slower while the clocks ramp,
+    # tools/clock_probe.py): the events are created and recorded once before the warm-up (r03 created
+    # them in between), and host_enqueue_ms_first5 in the output shows the timed loop's own pace.
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3 * args.steps)]
+    for e in ev:
+        e.record(stream)
     for _ in range(args.warmup):
         step()
+    # correctness gate: every packet of the warm-up's round trips succeeded (read after the timed
+    # steps). Computed here, before the time-based warm-up: the first launch of a torch kernel in
+    # the process loads its code object, milliseconds in which the GPU idles — after such a gap the
+    # first ~5 steps run up to 40 % slower while the clocks ramp (tools/clock_probe.py,
+    # profiles/r04b_clock_probe.txt), which is what slowed the driver's 20-step runs
+    fails_warm = (st != 0).sum()
     extra, tw = 0, time.perf_counter()
     while time.perf_counter() - tw < args.warmup_seconds:  # untimed, the same work: clock ramp
         for _ in range(4):
             step()
         torch.cuda.synchronize()
         extra += 4
-    # correctness gate: every packet of the warm-up's round trips succeeded (read after the timed
-    # steps, so no host round trip sits between the warm-up and the timed region)
-    fails_warm = (st != 0).sum()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    host_t = []
     for i in range(args.steps):
         step(ev, i)
+        host_t.append(time.perf_counter())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -483,7 +491,9 @@ def main():
                                     "max": round(float(t.max()), 4),
                                     "first5": [round(float(x), 4) for x in t[:5]],
                                     "last5": [round(float(x), 4) for x in t[-5:]]}
-                                for k, t in (("seal", seal_t), ("open", open_t))}}
+                                for k, t in (("seal", seal_t), ("open", open_t))},
+                # host time to enqueue each of the first timed steps (ms): a slow enqueue idles the GPU
+                "host_enqueue_ms_first5": [round((b - a) * 1e3, 3) for a, b in zip([t0] + host_t[:4], host_t[:5])]}
         cpu = ossl = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(w, args.cpu_sample, args.cpu_seconds)

@@ -501,9 +501,11 @@ using namespace mq;
 // tiles, as the AES kernels use, measured 10 % slower here: identical waves stay in phase, so
 // their staging waits line up.) The "1" variants are launched when the key table has a single
 // row (every valid packet on row 0): key material then lives in SGPRs.
+// tb: the workgroup's block of W tiles (blockIdx.x, or the persistent kernels' current block)
 template <bool OPEN, bool SINGLE>
-__device__ __forceinline__ void chacha_tile(const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena,
-                                            uint64_t arena_len, const mq_pkt_desc* __restrict__ desc, uint32_t n,
+__device__ __forceinline__ void chacha_tile(uint32_t tb, const KeyRow* __restrict__ kt, uint32_t n_rows,
+                                            uint8_t* __restrict__ arena, uint64_t arena_len,
+                                            const mq_pkt_desc* __restrict__ desc, uint32_t n,
                                             const uint32_t* __restrict__ index, const uint32_t* __restrict__ n_dev,
                                             uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,
                                             const uint2* __restrict__ hpm) {
@@ -512,7 +514,7 @@ __device__ __forceinline__ void chacha_tile(const KeyRow* __restrict__ kt, uint3
   const uint32_t w = threadIdx.x >> 6;
   uint8_t* wsm = smem + w * kLdsBytes;
   const int lane = threadIdx.x & (kWave - 1), p = lane / kLanesPerPkt, j = lane % kLanesPerPkt;
-  const uint32_t tile_id = blockIdx.x * W + w;
+  const uint32_t tile_id = tb * W + w;
   PktCtx c;
   const KeyRow* row;
   CcPool pool{false, smem, w * kLdsBytes, (uint32_t*)(wsm + kDataBudget + 32u * (uint32_t)p), kt};
@@ -520,7 +522,7 @@ __device__ __forceinline__ void chacha_tile(const KeyRow* __restrict__ kt, uint3
                                                  TilePrefetch{false, 0u, 0u}, c, row)) {
     // past the batch (list capacities exceed the count): a whole workgroup leaves at once, a
     // wave of a live workgroup only joins its barriers and pool
-    if (blockIdx.x * W * kPktsPerTile >= (n_dev ? *n_dev : n)) return;  // workgroup-uniform
+    if (tb * W * kPktsPerTile >= (n_dev ? *n_dev : n)) return;  // workgroup-uniform
     if (j == 0) pool.rec[0] = 0;
     __syncthreads();
     cc_pool_run<SINGLE>(pool);
@@ -564,17 +566,71 @@ __device__ __forceinline__ void chacha_tile(const KeyRow* __restrict__ kt, uint3
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
       const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status) {                                 \
-    chacha_tile<false, SINGLE>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr, nullptr); \
+    chacha_tile<false, SINGLE>(blockIdx.x, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr, \
+                               nullptr);                                                                  \
   }                                                                                                       \
   extern "C" __global__ __launch_bounds__(64 * kCcWaves) __attribute__((amdgpu_waves_per_eu(4))) void NAME_OPEN( \
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
       const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,    \
       const uint2* __restrict__ hpm) {                                                                    \
-    chacha_tile<true, SINGLE>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm); \
+    chacha_tile<true, SINGLE>(blockIdx.x, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm); \
   }
 MQ_CHACHA_KERNELS(mq_chacha_seal_kernel, mq_chacha_open_kernel, false)
 MQ_CHACHA_KERNELS(mq_chacha_seal1_kernel, mq_chacha_open1_kernel, true)
+
+// Partition lists (index != null) run on PERSISTENT workgroups (r04): the list's length is a
+// device count, so a grid covering the list capacity (1.6 x the batch in tiles of W) was mostly
+// workgroups that read the count and left — config E's ChaCha list has ~15k blocks of work in a
+// 52k-block grid, and an empty receive pass spent 350 us dispatching its 32k blocks
+// (profiles/r04g_kernel_stats_recv.csv). Here cus x 4 workgroups (16 waves per CU, as the
+// one-shot grid) take blocks of W tiles: block blockIdx.x first, then blocks claimed from the
+// stream's schedule slot (head 0, one returning atomic per block; the claim for the block after
+// next is issued when a block starts and read when it ends, so nobody waits on it), or, without a
+// slot, by stride. (Flat batches keep the one-shot grid: a persistent grid measured 10 % slower on
+// config B, r02 — identical waves stay in phase and their staging waits line up.)
+template <bool OPEN, bool SINGLE>
+__device__ __forceinline__ void chacha_list(const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena,
+                                            uint64_t arena_len, const mq_pkt_desc* __restrict__ desc, uint32_t n,
+                                            const uint32_t* __restrict__ index, const uint32_t* __restrict__ n_dev,
+                                            uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,
+                                            const uint2* __restrict__ hpm, uint32_t* __restrict__ sched) {
+  constexpr uint32_t W = kCcWaves;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  // the next block goes to every wave through word 7 of wave 0's first pool record, free between
+  // tiles (the pool writes it only after the next tile's first barrier); the four 40-KiB
+  // workgroups of a CU leave no LDS byte for a variable of its own
+  uint32_t* next_slot = (uint32_t*)(smem + kDataBudget) + 7;
+  uint32_t tb = blockIdx.x, pend = 0;
+  if (threadIdx.x == 0 && sched) pend = __hip_atomic_fetch_add(sched, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (;;) {
+    const uint32_t count = n_dev ? *n_dev : n;
+    if (tb * W * kPktsPerTile >= count) break;  // workgroup-uniform
+    chacha_tile<OPEN, SINGLE>(tb, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm);
+    __syncthreads();  // every wave is done with the tile and its scratch
+    if (threadIdx.x == 0) *next_slot = sched ? gridDim.x + pend : tb + gridDim.x;
+    __syncthreads();
+    tb = *next_slot;
+    // the claim after this one: its result is used one block later (issued after the barrier, so
+    // no barrier waits for it until the next tile's first one)
+    if (threadIdx.x == 0 && sched) pend = __hip_atomic_fetch_add(sched, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  sched_done(sched);
+}
+extern "C" __global__ __launch_bounds__(64 * kCcWaves) __attribute__((amdgpu_waves_per_eu(4))) void mq_chacha_seal_list_kernel(
+    const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
+    const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,
+    const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint32_t* __restrict__ sched) {
+  chacha_list<false, false>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr, nullptr, sched);
+}
+extern "C" __global__ __launch_bounds__(64 * kCcWaves) __attribute__((amdgpu_waves_per_eu(4))) void mq_chacha_open_list_kernel(
+    const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
+    const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,
+    const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,
+    const uint2* __restrict__ hpm, uint32_t* __restrict__ sched) {
+  chacha_list<true, false>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm, sched);
+}
 
 extern "C" __global__ __launch_bounds__(256) void mq_chacha_hp_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, const uint32_t* __restrict__ key_ids,
@@ -628,10 +684,12 @@ __global__ __launch_bounds__(256) void mq_chacha_open_hp_kernel(
 }
 
 // ---- host-side launchers (called from mq_host.cpp) -------------------------------------------
+// index != null (a partition list, length on the device): the persistent list kernels, cus x 4
+// workgroups, sched = the stream's schedule slot (null: static stride)
 hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena,
                             uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
                             const uint32_t* index, const uint32_t* n_dev, uint8_t* status,
-                            uint64_t* pn_out, uint2* hpm, bool own_hp, hipStream_t s) {
+                            uint64_t* pn_out, uint2* hpm, bool own_hp, hipStream_t s, int cus, uint32_t* sched) {
   const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
   if (tiles == 0) return hipSuccess;
   if (open && hpm && own_hp) {  // !own_hp: mq_launch_mixed_hp covers both suites' lists
@@ -640,15 +698,26 @@ hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
+  const uint32_t blocks = (tiles + kCcWaves - 1) / kCcWaves;
+  if (index) {
+    const uint32_t per = (uint32_t)(cus > 0 ? cus : 256) * 4u, grid = blocks < per ? blocks : per;
+    if (open)
+      hipLaunchKernelGGL(mq_chacha_open_list_kernel, dim3(grid), dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kt,
+                         n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm, sched);
+    else
+      hipLaunchKernelGGL(mq_chacha_seal_list_kernel, dim3(grid), dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kt,
+                         n_rows, arena, arena_len, desc, n, index, n_dev, status, sched);
+    return hipGetLastError();
+  }
   if (open)
-    hipLaunchKernelGGL(n_rows == 1 ? mq_chacha_open1_kernel : mq_chacha_open_kernel,
-                       dim3((tiles + kCcWaves - 1) / kCcWaves), dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kt,
-                       n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm);
+    hipLaunchKernelGGL(n_rows == 1 ? mq_chacha_open1_kernel : mq_chacha_open_kernel, dim3(blocks),
+                       dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kt, n_rows, arena, arena_len, desc, n, index,
+                       n_dev, status, pn_out, hpm);
   if (open) return hipGetLastError();
   // seal: header protection runs inside the tile kernel (the pool's HP blocks, cc_pool_run)
-  hipLaunchKernelGGL(n_rows == 1 ? mq_chacha_seal1_kernel : mq_chacha_seal_kernel,
-                     dim3((tiles + kCcWaves - 1) / kCcWaves), dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kt,
-                     n_rows, arena, arena_len, desc, n, index, n_dev, status);
+  hipLaunchKernelGGL(n_rows == 1 ? mq_chacha_seal1_kernel : mq_chacha_seal_kernel, dim3(blocks),
+                     dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kt, n_rows, arena, arena_len, desc, n, index,
+                     n_dev, status);
   return hipGetLastError();
 }
 

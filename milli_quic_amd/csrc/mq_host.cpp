@@ -25,7 +25,7 @@ using mq::KeyRow;
 hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena,
                             uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
                             const uint32_t* index, const uint32_t* n_dev, uint8_t* status,
-                            uint64_t* pn_out, uint2* hpm, bool own_hp, hipStream_t s);
+                            uint64_t* pn_out, uint2* hpm, bool own_hp, hipStream_t s, int cus, uint32_t* sched);
 hipError_t mq_launch_chacha_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t* key_ids,
                                const uint8_t* samples, uint8_t* masks, uint32_t n, hipStream_t s);
 hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena,
@@ -40,7 +40,7 @@ hipError_t mq_launch_mixed_open_hp(const KeyRow* kt, uint32_t n_rows, const uint
 hipError_t mq_launch_aes_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t* key_ids,
                             const uint8_t* samples, uint8_t* masks, uint32_t n, hipStream_t s);
 hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_desc* desc, uint32_t n,
-                               uint32_t* list, uint32_t* hist, uint32_t* counts, hipStream_t s);
+                               uint32_t* list, uint32_t* hist, uint32_t* counts, hipStream_t s, bool skip_unkeyed);
 size_t mq_partition_workspace(uint32_t n);
 void mq_partition_layout(uint32_t n, size_t* hist_off, size_t* counts_off);
 uint32_t mq_partition_list_cap(uint32_t n);
@@ -459,7 +459,8 @@ int run_one(Scratch& sc, const KeyRow& row, const uint8_t* aad, uint32_t aad_len
   // the arena is the whole scratch buffer; the packet sits at offset kHdr. NO_HP: no header
   // protection pass to launch (own_hp false)
   hipError_t e = row.suite == MQ_SUITE_CHACHA20
-                     ? mq_launch_chacha(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, st, pn, nullptr, false, sc.stream)
+                     ? mq_launch_chacha(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, st, pn, nullptr, false, sc.stream,
+                                        0, nullptr)
                      : mq_launch_aes(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, nullptr, st, pn, nullptr, false,
                                      sc.stream, sc.stream, devices().cus(sc.device), nullptr, nullptr, nullptr);
   if (e != hipSuccess) return MQ_ERR_HIP;
@@ -837,9 +838,11 @@ void mq_keytable_free(mq_keytable* kt) {
 static size_t ws_align(size_t b) { return (b + 255) & ~(size_t)255; }
 size_t mq_batch_workspace_size(uint32_t n) { return ws_align(8 * (size_t)n) + mq_partition_workspace(n); }
 
+// recv_pass (mq_batch_recv's AEAD passes): descriptors without a valid key row are skipped —
+// no status is written for them; the receive composite reads only what it attempted
 static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t arena_len,
                  const mq_pkt_desc* desc, uint32_t n, uint8_t* status, uint64_t* pn_out,
-                 uint32_t suite_hint, void* workspace, void* stream) {
+                 uint32_t suite_hint, void* workspace, void* stream, bool recv_pass = false) {
   if (!kt || (n && (!arena || !desc || !status))) return MQ_ERR_INVALID_ARG;
   if (((uintptr_t)arena & 15) != 0) return MQ_ERR_INVALID_ARG;  // 16-B staging chunks
   DeviceGuard g(kt->device);  // the table's device; `stream` must belong to it
@@ -853,7 +856,7 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
   uint2* hpm = (open && ws) ? (uint2*)ws : nullptr;
   if (suite_hint == MQ_SUITE_CHACHA20) {
     e = mq_launch_chacha(open, kt->dev, kt->rows, arena, arena_len, desc, n, nullptr, nullptr, status, pn_out, hpm, true,
-                         s);
+                         s, cus, nullptr);
   } else if (suite_hint == MQ_SUITE_AES128GCM && (kt->rows == 1 || !ws || n > (1u << 30))) {
     e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, n, nullptr, nullptr, nullptr, status, pn_out,
                       hpm, true, s, s, cus, nullptr, sched_slot(kt->device, s), nullptr);
@@ -873,7 +876,7 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
     uint32_t* counts = (uint32_t*)(pw + counts_off);
     // list mode: the grids cover the list capacity; the kernels read the real lengths from counts
     const uint32_t cap = mq_partition_list_cap(n);
-    e = mq_launch_partition(kt->dev, kt->rows, desc, n, list, hist, counts, s);
+    e = mq_launch_partition(kt->dev, kt->rows, desc, n, list, hist, counts, s, recv_pass);
     // open: one header-protection pre-pass over the whole batch in descriptor order, both suites,
     // before the tiles (seal needs none: the tiles mask their own packets). r03f ran it on a side
     // stream beside the partition: no gain (E open 1.279 -> 1.280 ms), its blocks delayed the
@@ -904,7 +907,7 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
                         pn_out, hpm, false, s_list1, s_list1, cus, nullptr, sched_slot(kt->device, s_list1), nullptr);
     else if (e == hipSuccess)
       e = mq_launch_chacha(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list + cap, counts + 1, status,
-                           pn_out, hpm, false, s_list1);
+                           pn_out, hpm, false, s_list1, cus, sched_slot(kt->device, s_list1));
     // join even after a failed launch, so no side stream runs ahead of s
     if (!fork.join() && e == hipSuccess) e = hipErrorUnknown;
   } else {
@@ -1040,10 +1043,10 @@ int mq_batch_recv(const mq_keytable* kt, mq_conn_recv* conns, uint32_t n_conns, 
   // anything still unresolved. Fixed rounds keep the call asynchronous (no host read-back).
   constexpr int kRounds = 2;
   for (int round = 0; round < kRounds; ++round) {
-    int r = batch(true, kt, arena, arena_len, p.d1, max_pkts, p.st1, nullptr, MQ_SUITE_MIXED, p.open_ws, stream);
+    int r = batch(true, kt, arena, arena_len, p.d1, max_pkts, p.st1, nullptr, MQ_SUITE_MIXED, p.open_ws, stream, true);
     if (r != MQ_OK) return r;
     if (mq_recv_retry(n_dgrams, max_pkts, n_conns, workspace, open_ws, s) != hipSuccess) return MQ_ERR_HIP;
-    r = batch(true, kt, arena, arena_len, p.d2, max_pkts, p.st2, nullptr, MQ_SUITE_MIXED, p.open_ws, stream);
+    r = batch(true, kt, arena, arena_len, p.d2, max_pkts, p.st2, nullptr, MQ_SUITE_MIXED, p.open_ws, stream, true);
     if (r != MQ_OK) return r;
     if (mq_recv_outcomes(n_dgrams, max_pkts, n_conns, workspace, open_ws, s) != hipSuccess) return MQ_ERR_HIP;
     if (mq_recv_walk(kt->dev, kt->rows, conns, n_conns, n_dgrams, max_pkts, pkts, workspace, open_ws,
@@ -1054,7 +1057,7 @@ int mq_batch_recv(const mq_keytable* kt, mq_conn_recv* conns, uint32_t n_conns, 
   // reference's (MQ_ERR_CRYPTO) holds plaintext; the final walk left its opening key row and PN in
   // d1 (every other entry has no key row and is skipped), and sealing it again under them restores
   // its bytes as received. Statuses land in the st1 scratch.
-  return batch(false, kt, arena, arena_len, p.d1, max_pkts, p.st1, nullptr, MQ_SUITE_MIXED, p.open_ws, stream);
+  return batch(false, kt, arena, arena_len, p.d1, max_pkts, p.st1, nullptr, MQ_SUITE_MIXED, p.open_ws, stream, true);
 }
 
 // ---- TLS 1.3 records (tcp_tls/record.rs:88-143, connection.rs:546-600) -----------------------

@@ -45,6 +45,8 @@ constexpr uint32_t kClasses = kGroups * kLenClasses;
 constexpr uint32_t kBudgetChunks = kDataBudget / 16;
 constexpr uint32_t kNoKey = 0xFFFFFFFFu;
 constexpr uint32_t kKeyClasses = 16;  // keyed layout: per row, min(len / 128, 15), longest first
+// skip_unkeyed (the receive composite's AEAD passes, mq_host.cpp): descriptors without a valid key
+// row are in no list (their statuses are never written; mq_recv.hip reads only attempted ones).
 
 // What the partition reads of a descriptor: key row, length, and whether the row is AES-128-GCM.
 // A thread's kPartItems descriptors are fetched together (fields first, then the rows' suites),
@@ -168,7 +170,7 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_init_kernel(
 extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_count_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_pkt_desc* __restrict__ desc, uint32_t n,
     uint32_t nblocks, const uint2* __restrict__ votes, uint32_t nv, uint32_t* __restrict__ hot_p,
-    uint32_t* __restrict__ hist, uint32_t* __restrict__ bins) {
+    uint32_t* __restrict__ hist, uint32_t* __restrict__ bins, uint32_t skip_unkeyed) {
   __shared__ uint32_t s_cnt[kClasses];
   PartItem it[kPartItems];
   part_fetch(kt, n_rows, desc, n, it);
@@ -181,7 +183,7 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_count_kernel(
 #pragma unroll
   for (int k = 0; k < kPartItems; ++k) {
     const uint32_t i = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
-    const bool in = i < n;
+    const bool in = i < n && !(skip_unkeyed && it[k].key >= n_rows);
     const uint32_t c = in ? part_class(hot, it[k]) : 0u;
     kd[k] = bins && in && c / kLenClasses == 1;
     kb[k] = kd[k] ? key_bin(it[k]) : 0u;
@@ -357,7 +359,8 @@ __device__ void key_scan(uint32_t* __restrict__ bins, uint32_t n_rows, uint32_t*
 extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_scatter_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_pkt_desc* __restrict__ desc, uint32_t n,
     uint32_t nblocks, const uint32_t* __restrict__ hot_p, const uint32_t* __restrict__ hist,
-    const uint32_t* __restrict__ seg, uint32_t* __restrict__ list, uint32_t* __restrict__ bins) {
+    const uint32_t* __restrict__ seg, uint32_t* __restrict__ list, uint32_t* __restrict__ bins,
+    uint32_t skip_unkeyed) {
   __shared__ uint32_t s_rank[kClasses];
   PartItem it[kPartItems];
   part_fetch(kt, n_rows, desc, n, it);
@@ -368,10 +371,11 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_scatter_kerne
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   // keyed bins: the thread's items of one bin claim their positions with one atomic (as counted)
   uint32_t kb[kPartItems], kpos[kPartItems];
-  bool kd[kPartItems];
+  bool kd[kPartItems], skp[kPartItems];
 #pragma unroll
   for (int k = 0; k < kPartItems; ++k) {
     const uint32_t i = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
+    skp[k] = skip_unkeyed && it[k].key >= n_rows;  // in no list (never AES: not keyed either)
     const uint32_t c = i < n ? part_class(hot, it[k]) : 0u;
     kd[k] = bins && i < n && c / kLenClasses == 1;
     kb[k] = kd[k] ? key_bin(it[k]) : 0u;
@@ -400,7 +404,7 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_scatter_kerne
     const uint32_t i = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
     const uint32_t c = i < n ? part_class(hot, it[k]) : 0u;
     const bool keyed = kd[k];
-    const bool in = i < n && !keyed;
+    const bool in = i < n && !keyed && !skp[k];
     // lanes of this wave with the same class (7 ballots), rank among them = peers below
     uint64_t peers = __ballot(in);
 #pragma unroll
@@ -446,7 +450,7 @@ const uint32_t* mq_partition_rowseg(uint32_t n, uint32_t n_rows, const uint32_t*
 }
 
 hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_desc* desc, uint32_t n,
-                               uint32_t* list, uint32_t* hist, uint32_t* counts, hipStream_t s) {
+                               uint32_t* list, uint32_t* hist, uint32_t* counts, hipStream_t s, bool skip_unkeyed) {
   const uint32_t nblocks = (n + kPartBlock - 1) / kPartBlock;
   if (nblocks == 0) return hipMemsetAsync(counts, 0, 4 * sizeof(uint32_t), s);
   const uint32_t cap = mq_partition_list_cap(n);
@@ -463,11 +467,11 @@ hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_d
   hipLaunchKernelGGL(mq_part_init_kernel, dim3(grid), dim3(kPartThreads), 0, s, kt, n_rows, desc, n, votes,
                      max(nv, used), (uint4*)list, list_q, (uint4*)bins, bins_q);
   hipLaunchKernelGGL(mq_part_count_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, kt, n_rows, desc, n,
-                     nblocks, votes, max(nv, used), hot, hist, bins);
+                     nblocks, votes, max(nv, used), hot, hist, bins, (uint32_t)skip_unkeyed);
   hipLaunchKernelGGL(mq_part_scan_kernel, dim3(1), dim3(64 * kScanWaves), 0, s, hist, nblocks, cap, counts, seg,
                      bins, n_rows, bins ? bins + key_bins(n) : nullptr);
   hipLaunchKernelGGL(mq_part_scatter_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, kt, n_rows, desc, n,
-                     nblocks, hot, hist, seg, list, bins);
+                     nblocks, hot, hist, seg, list, bins, (uint32_t)skip_unkeyed);
   return hipGetLastError();
 }
 

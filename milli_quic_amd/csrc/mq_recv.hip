@@ -303,101 +303,131 @@ extern "C" __global__ __launch_bounds__(256) void mq_recv_unmask_kernel(const ui
 // nothing new is attempted; the last walk (`final`) marks what is still unresolved DEFERRED.
 enum : uint8_t { kNone = 0, kOk1 = 1, kOk0 = 2, kFail = 3 };
 
-extern "C" __global__ __launch_bounds__(64) void mq_recv_walk_kernel(
+// What a walk reads of one packet: its record, its header-protection values, the inputs of its
+// last attempt and that attempt's outcome
+struct WalkEnt {
+  RecvWork w;
+  RecvPlan p, t;
+  uint32_t i;
+  uint8_t o;
+};
+
+// one packet of a connection's run, in arrival order (the sequential reference's decision, the
+// attempt to make, the packet's record)
+__device__ __forceinline__ void walk_one(ConnState& s, const mq_conn_recv& c, uint32_t n_rows, const WalkEnt& e,
+                                         RecvPlan* __restrict__ tried, mq_pkt_desc* __restrict__ d1,
+                                         mq_pkt_desc* __restrict__ d2, mq_recv_pkt* __restrict__ out,
+                                         uint32_t& new_attempts, int final_walk) {
+  const uint32_t i = e.i;
+  const RecvWork w = e.w;
+  RecvPlan p = e.p;
+  decide(s, w, c, n_rows, p);
+  mq_pkt_desc a;
+  a.offset = w.offset; a.len = w.len; a.key_id = kNoRow; a.pn = p.lbefore; a.pn_offset = w.pn_off;
+  a.pn_len = 0; a.flags = w.level != MQ_LEVEL_APPLICATION ? MQ_PKT_LONG_HEADER : 0; a.reserved = 0;
+  mq_pkt_desc b = a;
+  uint8_t st = p.status, gen = p.gen;
+  RecvPlan used = p;
+  if (p.status == kPending) {
+    const uint8_t o = e.o;
+    const RecvPlan t = e.t;
+    const bool same = o != kNone && t.pn == p.pn && t.row == p.row && t.retry == p.retry && t.gen == p.gen;
+    if (o == kOk1 || o == kOk0) {
+      // Opened (its bytes are already plaintext, so it is never attempted again). A packet
+      // authenticates under exactly one (key row, pn), the one that opened it, so the
+      // reference's outcome for its own decision p follows: p.row first, then p.retry
+      // (recv.rs:412-474); for a next-generation open the rotation is p's (gen 2).
+      const uint32_t opened = o == kOk1 ? t.row : t.retry;
+      used = p;
+      if (t.pn == p.pn && opened == p.row) {
+        st = MQ_OK;
+        gen = p.gen;
+      } else if (t.pn == p.pn && opened == p.retry) {
+        st = MQ_OK;
+        gen = 0;
+      } else {
+        // the reference's keys fail on it: Error::Crypto. It opened under the speculation's
+        // inputs, so its bytes hold plaintext; the final walk hands it to the re-seal pass
+        // (mq_host.cpp) with the key row and PN that opened it, which brings back ciphertext,
+        // tag and masked header exactly as received — the reference never touches the
+        // datagram of a failed packet (it opens a 2048-B copy, recv.rs:356-361)
+        st = MQ_ERR_CRYPTO;
+        if (final_walk) {
+          a.key_id = opened;
+          a.pn = t.pn;
+          a.pn_len = t.pn_len;
+        }
+      }
+    } else if (same) {  // failed with exactly the reference's inputs
+      st = MQ_ERR_CRYPTO;
+    } else if (final_walk) {
+      st = MQ_ERR_DEFERRED;
+    } else {  // (re)attempt with the inputs the reference would use; speculate it opens
+      tried[i] = p;
+      a.key_id = p.row;
+      b.key_id = p.retry;
+      ++new_attempts;
+      st = MQ_OK;
+    }
+  }
+  d1[i] = a;
+  d2[i] = b;
+  mq_recv_pkt r;
+  r.offset = w.offset; r.len = w.len; r.dgram = w.dgram; r.level = w.level; r.status = st;
+  r.pn = st == MQ_OK ? used.pn : 0;
+  r.payload_offset = st == MQ_OK ? (uint16_t)(w.pn_off + used.pn_len) : 0;
+  r.key_gen = (w.level == MQ_LEVEL_APPLICATION && st == MQ_OK) ? gen : 0;
+  r.reserved[0] = r.reserved[1] = r.reserved[2] = 0;
+  out[i] = r;
+  if (st == MQ_OK) advance(s, w, used, gen);
+}
+
+// A connection per group of kWalkGroup lanes (r04): the group loads the inputs of its next
+// kWalkGroup packets together (one packet per lane: one round trip for the lot, the next round's
+// indices prefetched), then the group's first lane walks them from LDS. r03 walked one packet per
+// lane-step straight from memory (one round trip per packet, 372 us per walk of 2^20 packets over
+// 4096 connections, three walks per batch: profiles/r04g_kernel_stats_recv.csv).
+constexpr uint32_t kWalkGroup = 16, kWalkThreads = 256, kWalkConns = kWalkThreads / kWalkGroup;
+
+extern "C" __global__ __launch_bounds__(kWalkThreads) void mq_recv_walk_kernel(
     const mq_conn_recv* __restrict__ conn0, mq_conn_recv* __restrict__ conns, uint32_t n_conns,
     const RecvWork* __restrict__ work, const uint32_t* __restrict__ svals, const uint32_t* __restrict__ seg_lo,
     const uint32_t* __restrict__ seg_hi, const RecvPlan* __restrict__ hdr, uint32_t n_rows,
     RecvPlan* __restrict__ tried, const uint8_t* __restrict__ outcome, mq_pkt_desc* __restrict__ d1,
     mq_pkt_desc* __restrict__ d2, mq_recv_pkt* __restrict__ out, uint32_t* __restrict__ attempts, int final_walk) {
-  const uint32_t ci = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ci >= n_conns) return;
-  const mq_conn_recv c = conn0[ci];
-  ConnState s = load_state(c);
+  __shared__ WalkEnt s_e[kWalkThreads];
+  const uint32_t g = threadIdx.x / kWalkGroup, q = threadIdx.x % kWalkGroup;
+  const uint32_t ci = blockIdx.x * kWalkConns + g;
+  const bool live = ci < n_conns;
+  const uint32_t lo = live ? seg_lo[ci] : 0u, hi = live ? seg_hi[ci] : 0u;
+  mq_conn_recv c{};
+  ConnState s{};
+  if (live && q == 0) {
+    c = conn0[ci];
+    s = load_state(c);
+  }
   uint32_t new_attempts = 0;
-  // software-pipelined walk: the inputs of packet k + 1 (and the index of k + 2) are loaded
-  // before packet k is processed, so the lane waits on memory once per packet at most instead of
-  // three dependent times (the loads never alias this iteration's stores: indices are distinct)
-  const uint32_t lo = seg_lo[ci], hi = seg_hi[ci];
-  uint32_t i_n = 0, i_nn = 0;
-  RecvWork w_n{};
-  RecvPlan p_n{}, t_n{};
-  uint8_t o_n = kNone;
-  if (lo < hi) {
-    i_n = svals[lo];
-    w_n = work[i_n]; p_n = hdr[i_n]; o_n = outcome[i_n]; t_n = tried[i_n];
-  }
-  if (lo + 1 < hi) i_nn = svals[lo + 1];
-  for (uint32_t k = lo; k < hi; ++k) {
-    const uint32_t i = i_n;
-    const RecvWork w = w_n;
-    RecvPlan p = p_n;
-    const uint8_t o_cur = o_n;
-    const RecvPlan t_cur = t_n;
-    if (k + 1 < hi) {
-      i_n = i_nn;
-      w_n = work[i_n]; p_n = hdr[i_n]; o_n = outcome[i_n]; t_n = tried[i_n];
+  uint32_t nxt = lo + q < hi ? svals[lo + q] : 0u;
+  WalkEnt* ent = s_e + g * kWalkGroup;
+  for (uint32_t k0 = lo;; k0 += kWalkGroup) {
+    const bool act = k0 < hi;
+    if (!wave_any(act)) break;  // the wave's groups have runs of different lengths
+    const uint32_t m = act ? min(kWalkGroup, hi - k0) : 0u;
+    if (q < m) {
+      const uint32_t i = nxt;
+      ent[q].i = i;
+      ent[q].w = work[i];
+      ent[q].p = hdr[i];
+      ent[q].t = tried[i];
+      ent[q].o = outcome[i];
     }
-    if (k + 2 < hi) i_nn = svals[k + 2];
-    decide(s, w, c, n_rows, p);
-    mq_pkt_desc a;
-    a.offset = w.offset; a.len = w.len; a.key_id = kNoRow; a.pn = p.lbefore; a.pn_offset = w.pn_off;
-    a.pn_len = 0; a.flags = w.level != MQ_LEVEL_APPLICATION ? MQ_PKT_LONG_HEADER : 0; a.reserved = 0;
-    mq_pkt_desc b = a;
-    uint8_t st = p.status, gen = p.gen;
-    RecvPlan used = p;
-    if (p.status == kPending) {
-      const uint8_t o = o_cur;
-      const RecvPlan t = t_cur;
-      const bool same = o != kNone && t.pn == p.pn && t.row == p.row && t.retry == p.retry && t.gen == p.gen;
-      if (o == kOk1 || o == kOk0) {
-        // Opened (its bytes are already plaintext, so it is never attempted again). A packet
-        // authenticates under exactly one (key row, pn), the one that opened it, so the
-        // reference's outcome for its own decision p follows: p.row first, then p.retry
-        // (recv.rs:412-474); for a next-generation open the rotation is p's (gen 2).
-        const uint32_t opened = o == kOk1 ? t.row : t.retry;
-        used = p;
-        if (t.pn == p.pn && opened == p.row) {
-          st = MQ_OK;
-          gen = p.gen;
-        } else if (t.pn == p.pn && opened == p.retry) {
-          st = MQ_OK;
-          gen = 0;
-        } else {
-          // the reference's keys fail on it: Error::Crypto. It opened under the speculation's
-          // inputs, so its bytes hold plaintext; the final walk hands it to the re-seal pass
-          // (mq_host.cpp) with the key row and PN that opened it, which brings back ciphertext,
-          // tag and masked header exactly as received — the reference never touches the
-          // datagram of a failed packet (it opens a 2048-B copy, recv.rs:356-361)
-          st = MQ_ERR_CRYPTO;
-          if (final_walk) {
-            a.key_id = opened;
-            a.pn = t.pn;
-            a.pn_len = t.pn_len;
-          }
-        }
-      } else if (same) {  // failed with exactly the reference's inputs
-        st = MQ_ERR_CRYPTO;
-      } else if (final_walk) {
-        st = MQ_ERR_DEFERRED;
-      } else {  // (re)attempt with the inputs the reference would use; speculate it opens
-        tried[i] = p;
-        a.key_id = p.row;
-        b.key_id = p.retry;
-        ++new_attempts;
-        st = MQ_OK;
-      }
-    }
-    d1[i] = a;
-    d2[i] = b;
-    mq_recv_pkt r;
-    r.offset = w.offset; r.len = w.len; r.dgram = w.dgram; r.level = w.level; r.status = st;
-    r.pn = st == MQ_OK ? used.pn : 0;
-    r.payload_offset = st == MQ_OK ? (uint16_t)(w.pn_off + used.pn_len) : 0;
-    r.key_gen = (w.level == MQ_LEVEL_APPLICATION && st == MQ_OK) ? gen : 0;
-    r.reserved[0] = r.reserved[1] = r.reserved[2] = 0;
-    out[i] = r;
-    if (st == MQ_OK) advance(s, w, used, gen);
+    nxt = k0 + kWalkGroup + q < hi ? svals[k0 + kWalkGroup + q] : 0u;
+    wave_sync();
+    if (q == 0)
+      for (uint32_t k = 0; k < m; ++k) walk_one(s, c, n_rows, ent[k], tried, d1, d2, out, new_attempts, final_walk);
+    wave_sync();  // the entries are read before the next round overwrites them
   }
+  if (!live || q != 0) return;
   if (new_attempts) atomicAdd(attempts, new_attempts);
   mq_conn_recv o = c;
   for (int l = 0; l < 3; ++l) { o.largest_pn[l] = s.largest[l]; o.app_row[l] = s.row[l]; }
@@ -532,8 +562,13 @@ hipError_t mq_recv_front(const KeyRow* kt, uint32_t n_rows, mq_conn_recv* conns,
   hipLaunchKernelGGL(mq_recv_unmask_kernel, dim3((max_pkts + 255) / 256), b256, 0, s, arena, w.work, w.hpm, w.total,
                      max_pkts, w.hdr, w.outcome);
   size_t cb = w.cub_bytes;
-  if ((e = hipcub::DeviceRadixSort::SortPairs(w.cub, cb, w.keys, w.skeys, w.vals, w.svals, (int)max_pkts, 0, 32, s)) !=
-      hipSuccess)
+  // keys are connection indices (< n_conns) and 0xFFFFFFFF past the packet count: the low
+  // ceil(log2(n_conns + 1)) bits order them (the padding's all-ones bits sort last), so the radix
+  // sort makes that many passes' worth of digits instead of 32 bits' 
+  int end_bit = 1;
+  while (end_bit < 32 && (1ull << end_bit) <= (uint64_t)n_conns) ++end_bit;
+  if ((e = hipcub::DeviceRadixSort::SortPairs(w.cub, cb, w.keys, w.skeys, w.vals, w.svals, (int)max_pkts, 0, end_bit,
+                                              s)) != hipSuccess)
     return e;
   if (n_conns) {
     if ((e = hipMemsetAsync(w.seg_lo, 0, 4ull * n_conns, s)) != hipSuccess) return e;
@@ -552,7 +587,8 @@ hipError_t mq_recv_walk(const KeyRow* /*kt*/, uint32_t n_rows, mq_conn_recv* con
   hipError_t e;
   if ((e = hipMemsetAsync(w.attempts, 0, 4, s)) != hipSuccess) return e;
   if (n_conns)
-    hipLaunchKernelGGL(mq_recv_walk_kernel, dim3((n_conns + 63) / 64), dim3(64), 0, s, w.conn0, conns, n_conns, w.work,
+    hipLaunchKernelGGL(mq_recv_walk_kernel, dim3((n_conns + kWalkConns - 1) / kWalkConns), dim3(kWalkThreads), 0, s,
+                       w.conn0, conns, n_conns, w.work,
                        w.svals, w.seg_lo, w.seg_hi, w.hdr, n_rows, w.tried, w.outcome, w.d1, w.d2, out, w.attempts,
                        (int)final_walk);
   return hipGetLastError();

@@ -476,25 +476,33 @@ __device__ __forceinline__ void run_tile(uint8_t* smem, uint32_t tile_id, const 
 // Work distribution of the persistent tile kernels (r04). Wave g of a grid of
 // `waves` waves runs tile base + g first. After that:
 //   static  (ctr null): tiles base + g + waves, base + g + 2 waves, ...;
-//   dynamic (ctr = the launch's schedule slot, mq_runtime.h SchedSlots): chunks of the remaining
-//     tiles claimed with a returning device-scope atomicAdd on a head word. The remaining range is
-//     split into kSchedHeads parts with one head each (one per XCD: ≈88 claims/µs saturate one
-//     word, MI355X_MICROARCH.md 'dequeue'); a wave claims from its XCD's head — chunks of
-//     remaining / (2 x the waves per head), 1..kMaxChunk tiles (guided self-scheduling) — then,
-//     once that part is gone, single tiles from the other heads in turn. The next chunk is claimed
-//     when the current one starts, so a claim's latency hides behind at least one tile.
+//   dynamic (ctr = the launch's schedule slot, mq_runtime.h SchedSlots): the remaining tiles are
+//     cut into blocks of kSchedBlock; block k belongs to head k mod kSchedHeads (one head per XCD:
+//     ≈88 claims/µs saturate one word, MI355X_MICROARCH.md 'dequeue'), so every head's tiles sample
+//     the whole range — a length-sorted list (config E: longest class first) gives every XCD the
+//     same mix, and all heads advance through the arena together. A wave claims entries of its
+//     XCD's head with a returning device-scope atomicAdd — chunks of remaining / (2 x the waves per
+//     head), 1..kMaxChunk entries (guided self-scheduling) — then, once that head is empty, single
+//     entries of the other heads. The next chunk is claimed when the current one starts, so a
+//     claim's latency hides behind at least one tile.
 // Why: the static stride gives every workgroup a fixed share, so a workgroup that is placed late —
 // its CU held by another kernel, e.g. the resident per-packet server (mq_resident.hip) or the
 // hot-key kernel forked beside this one — ends the launch a whole share late. Dynamically, the
-// others take what it has not started.
+// others take what it has not started (tests/test_gpu_resident.py: config C 1.01x beside the
+// server). Measured first with each head owning a contiguous eighth and chunks up to 16: config C
+// +8 %, E +5 % over the static stride; chunks up to 4: C -5 %, E +6 % (profiles/r04g_ab_sched.txt).
 // Slot layout (uint32 words): head h at word kSchedHeadWords * h, the finished-workgroup count at
 // word kSchedDoneWord. The last workgroup to finish zeroes the slot (sched_done) for the next
 // kernel on the same stream.
 // (kSchedHeads, kSchedHeadWords, kSchedDoneWord, kSchedSlotBytes: mq_device.h, shared with the host)
 #ifndef MQ_SCHED_MAX_CHUNK
-#define MQ_SCHED_MAX_CHUNK 16
+#define MQ_SCHED_MAX_CHUNK 4
+#endif
+#ifndef MQ_SCHED_BLOCK
+#define MQ_SCHED_BLOCK 16
 #endif
 constexpr uint32_t kMaxChunk = MQ_SCHED_MAX_CHUNK;
+constexpr uint32_t kSchedBlock = MQ_SCHED_BLOCK;
 
 struct TileSched {
   uint32_t* ctr;   // null: static
@@ -538,20 +546,28 @@ __device__ __forceinline__ void for_tiles(const TileSched& ts, const mq_pkt_desc
   const uint32_t tiles = (count + kPktsPerTile - 1) / kPktsPerTile;
   const uint32_t lane = threadIdx.x & (kWave - 1), p = lane / kLanesPerPkt, j = lane % kLanesPerPkt;
   constexpr uint32_t kNone = 0xFFFFFFFFu;
-  // dynamic schedule (wave-uniform state): the tiles from dyn0 on, split over the heads
+  // dynamic schedule (wave-uniform state): the tiles from dyn0 on, in blocks dealt to the heads
   const uint32_t dyn0 = base + ts.waves;
   const uint32_t D = tiles > dyn0 ? tiles - dyn0 : 0u;
-  auto head_lo = [&](uint32_t h) { return dyn0 + (uint32_t)(((uint64_t)D * h) / kSchedHeads); };
+  const uint32_t nb = (D + kSchedBlock - 1) / kSchedBlock;  // blocks; the last may be partial
+  auto head_size = [&](uint32_t h) -> uint32_t {  // entries (tiles) of head h
+    const uint32_t cnt = nb > h ? (nb - 1 - h) / kSchedHeads + 1 : 0u;
+    const uint32_t part = ((nb - 1) % kSchedHeads == h && D % kSchedBlock) ? kSchedBlock - D % kSchedBlock : 0u;
+    return cnt * kSchedBlock - (cnt ? part : 0u);
+  };
+  auto tile_of = [&](uint32_t h, uint32_t e) -> uint32_t {  // entry e of head h
+    return dyn0 + ((e / kSchedBlock) * kSchedHeads + h) * kSchedBlock + e % kSchedBlock;
+  };
   const uint32_t per_head = ts.waves / kSchedHeads > 1u ? ts.waves / kSchedHeads : 1u;
   uint32_t state = 0;       // 0: own head, 1: the other heads, 2: none left
-  uint32_t seen = 0;        // own head: tiles claimed as of this wave's last claim
-  uint32_t cend = 0;        // end of the chunk being walked
+  uint32_t seen = 0;        // own head: entries claimed as of this wave's last claim
+  uint32_t ch = 0, ce = 0, cend = 0;  // the chunk being walked: head, entry, end entry
   // the claim of the next chunk, issued when the current one starts and resolved when it ends: the
   // atomic's result stays in a VGPR meanwhile (lane 0), so no wave waits on it (or on the stores
   // before it: vmcnt counts both) in steady state
   uint32_t qh = 0, qc = 0;
   bool pending = false;
-  const uint32_t own_lo = head_lo(ts.xcd), own_size = head_lo(ts.xcd + 1) - own_lo;
+  const uint32_t own_size = head_size(ts.xcd);
   auto issue = [&]() {
     if (state != 0) return;  // the other heads are claimed at resolve time
     const uint32_t rem = own_size > seen ? own_size - seen : 0u;
@@ -562,40 +578,41 @@ __device__ __forceinline__ void for_tiles(const TileSched& ts, const mq_pkt_desc
       qh = __hip_atomic_fetch_add(ts.ctr + kSchedHeadWords * ts.xcd, qc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     pending = true;
   };
-  // the next chunk [s, e): the pending own-head claim, else a single tile from another head
-  auto resolve = [&](uint32_t& cs, uint32_t& ce) -> bool {
+  // the next chunk: the pending own-head claim, else a single entry of another head
+  auto resolve = [&]() -> bool {
     if (state == 0) {
       const uint32_t got = own_size ? (uint32_t)__builtin_amdgcn_readlane((int)qh, 0) : 0u;
       const bool ok = pending && got < own_size;
       pending = false;
       if (ok) {
-        cs = own_lo + got;
-        ce = own_lo + (got + qc < own_size ? got + qc : own_size);
+        ch = ts.xcd;
+        ce = got;
+        cend = got + qc < own_size ? got + qc : own_size;
         seen = got + qc;
         return true;
       }
       state = 1;
     }
-    // the other heads, single tiles: one round trip reads all heads (a returning add of 0 on lanes
-    // 0..7: atomics are coherent across the XCDs' L2s, plain loads are not), then a claim from the
-    // first one after this XCD's with tiles left; a lost race rescans (someone else progressed)
+    // the other heads, single entries: one round trip reads all heads (a returning add of 0 on
+    // lanes 0..7: atomics are coherent across the XCDs' L2s, plain loads are not), then a claim from
+    // the first one after this XCD's with entries left; a lost race rescans (someone progressed)
 #pragma nounroll
     for (uint32_t tries = 0; state == 1 && tries < 64; ++tries) {
       uint32_t v = 0xFFFFFFFFu, sz = 0;
       if (lane < kSchedHeads) {
         v = __hip_atomic_fetch_add(ts.ctr + kSchedHeadWords * lane, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sz = head_lo(lane + 1) - head_lo(lane);
+        sz = head_size(lane);
       }
       const uint32_t open = (uint32_t)__ballot(lane < kSchedHeads && v < sz) & 0xFFu;
       if (!open) break;
       const uint32_t x = (ts.xcd + 1) % kSchedHeads;
       const uint32_t rot = ((open >> x) | (open << (kSchedHeads - x))) & 0xFFu;
       const uint32_t h = (x + (uint32_t)__builtin_ctz(rot)) % kSchedHeads;
-      const uint32_t lo = head_lo(h), size = head_lo(h + 1) - lo;
       const uint32_t got = sched_claim(ts.ctr + kSchedHeadWords * h, 1u);
-      if (got < size) {
-        cs = lo + got;
-        ce = cs + 1;
+      if (got < head_size(h)) {
+        ch = h;
+        ce = got;
+        cend = got + 1;
         return true;
       }
     }
@@ -605,12 +622,10 @@ __device__ __forceinline__ void for_tiles(const TileSched& ts, const mq_pkt_desc
   auto next = [&](uint32_t t) -> uint32_t {
     if (t >= tiles) return kNone;
     if (!ts.ctr) return t + ts.waves;
-    if (t + 1 < cend) return t + 1;
-    uint32_t cs, ce;
-    if (!resolve(cs, ce)) return kNone;
-    cend = ce;
+    if (ce + 1 < cend) return tile_of(ch, ++ce);
+    if (!resolve()) return kNone;
     issue();  // the chunk after this one
-    return cs;
+    return tile_of(ch, ce);
   };
   auto idx_of = [&](uint32_t t) -> uint32_t {  // packet p's descriptor index (list: a load)
     const uint32_t e = t * kPktsPerTile + p;
@@ -623,10 +638,7 @@ __device__ __forceinline__ void for_tiles(const TileSched& ts, const mq_pkt_desc
     hm = (OPEN && hpm && ok && j < 2) ? reinterpret_cast<const uint32_t*>(hpm)[(size_t)ix * 2 + j] : 0u;
   };
   uint32_t t = base + ts.g;
-  if (ts.ctr && t < tiles) {
-    cend = t + 1;
-    issue();  // resolved right away by next(t): one wait per wave, at its start
-  }
+  if (ts.ctr && t < tiles) issue();  // resolved right away by next(t): one wait per wave, at its start
   uint32_t t1 = next(t);
   uint32_t ix0 = idx_of(t), ix1 = idx_of(t1), dw, hm;
   fetch(ix0, dw, hm);

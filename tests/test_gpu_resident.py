@@ -153,6 +153,13 @@ def _batch_c(n, stream):
     return w, arena, st, seal, open_
 
 
+def _plaintext_back(arena, w):
+    """After seal + open every 1200-B packet holds its header and plaintext again (the tag bytes
+    stay). A plain bool: pytest's diff of two 1.26-GB byte strings would run for minutes."""
+    got = arena.cpu().numpy().reshape(w.n, 1200)[:, :1184]
+    return bool(np.array_equal(got, w.arena.reshape(w.n, 1200)[:, :1184]))
+
+
 @pytest.mark.timeout(90)
 def test_resident_timeout_then_recovers(orc):
     # ADVICE r03: a call that times out must not leave the server unable to serve (r03 waited for
@@ -197,7 +204,7 @@ def test_resident_timeout_then_recovers(orc):
     finally:
         os.environ.pop("MQ_RESIDENT_TIMEOUT_US", None)
     assert (st.cpu().numpy() == 0).all()
-    assert arena.cpu().numpy().tobytes() == w.arena.tobytes()  # seal + open rounds: plaintext back
+    assert _plaintext_back(arena, w)  # seal + open rounds: every packet's plaintext back
     print("timeout outcomes", outcomes)
     assert "timeout" in outcomes  # the path under test ran at least once
 
@@ -213,6 +220,9 @@ def test_batch_beside_resident_server(orc):
 
     def timed(k):
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * k)]
+        for _ in range(10):  # untimed: clocks ramp up after an idle gap (tools/clock_probe.py)
+            seal()
+            open_()
         for i in range(k):
             ev[2 * i].record(s)
             seal()
@@ -251,6 +261,8 @@ def test_batch_beside_resident_server(orc):
         while calls[0] < 20 and th.is_alive():
             time.sleep(0.001)
         beside = timed(8)
+        print(f"config C seal+open: alone {alone:.3f} ms, beside the server {beside:.3f} ms "
+              f"({beside / alone:.3f}x, {calls[0]} per-packet calls so far)", flush=True)
         seal()  # the sealed bytes under the server, checked below
         s.synchronize()
         sealed = arena.cpu().numpy().copy()
@@ -261,7 +273,7 @@ def test_batch_beside_resident_server(orc):
         th.join()
     assert not errors, errors[:3]
     assert (st.cpu().numpy() == 0).all()
-    assert arena.cpu().numpy().tobytes() == w.arena.tobytes()
+    assert _plaintext_back(arena, w)
     # every 256th packet of the sealed arena against the oracle
     idx = np.arange(0, w.n, 256)
     ref = w.arena.copy()
@@ -270,7 +282,5 @@ def test_batch_beside_resident_server(orc):
     for i in idx:
         o, L = int(w.seal_desc["offset"][i]), int(w.seal_desc["len"][i])
         assert sealed[o:o + L].tobytes() == ref[o:o + L].tobytes(), i
-    print(f"config C seal+open: alone {alone:.3f} ms, beside the server {beside:.3f} ms "
-          f"({beside / alone:.3f}x, {calls[0]} per-packet calls)")
     assert calls[0] > 20
     assert beside <= 1.15 * alone, (alone, beside)

@@ -50,7 +50,7 @@ def bench_derive(reps, n=1 << 20):
     return {"connections": n, "ms": round(ms, 4), "connections_per_s": round(n / ms * 1e3)}
 
 
-def bench_protect_recv(reps, n=1 << 20, n_conns=4096):
+def bench_protect_recv(reps, n=1 << 20, n_conns=4096, only="both"):
     fl = 1171
     w = workload.uniform(64, _lib.MQ_SUITE_CHACHA20, n_keys=n_conns)
     kt = KeyTable(w.keys)
@@ -68,8 +68,11 @@ def bench_protect_recv(reps, n=1 << 20, n_conns=4096):
     st = torch.zeros(n, dtype=torch.uint8, device=DEV)
     ln = torch.zeros(n, dtype=torch.int32, device=DEV)
     ws = torch.empty(send.workspace_bytes(n), dtype=torch.uint8, device=DEV)
-    ms_p = timed(lambda: send.protect(kt, dc, frames, out, dr, st, ln, _lib.MQ_SUITE_CHACHA20, ws), reps)
+    ms_p = timed(lambda: send.protect(kt, dc, frames, out, dr, st, ln, _lib.MQ_SUITE_CHACHA20, ws),
+                 reps if only != "recv" else 0)
     assert int((st != 0).sum()) == 0
+    if only == "protect":
+        return ({"ms": round(ms_p, 4)}, None)
     sealed = out.clone()
     rc = np.zeros(n_conns, dtype=recv.CONN_DTYPE)
     rc["app_row"][:, 1] = np.arange(n_conns)
