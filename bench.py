@@ -254,10 +254,12 @@ def cpu_openssl(w, sample, min_seconds=3.0):
 # ---- end-to-end (host-resident) ---------------------------------------------------------------
 def end_to_end(torch, batch, kt, w, sd, od, dev, chunks=8, reps=3):
     """Host-resident rate (the path starts and ends in a socket buffer): pinned host arena ->
-    H2D -> seal -> D2H, then H2D -> open -> D2H, pipelined over `chunks` descriptor ranges on
-    two streams so copies overlap kernels. Returns GiB/s of wire bytes per direction, next to the
-    ceiling: the best plain pinned H2D + D2H of the same bytes (no kernel) over 2-4 streams and
-    8-32 chunks, and the pipeline's fraction of it."""
+    H2D -> seal -> D2H, then H2D -> open -> D2H, pipelined over chunks of descriptor ranges on
+    several streams so copies overlap kernels. Returns GiB/s of wire bytes per direction, next to
+    the link's bound: the pipeline moves every wire byte in and out, so it cannot beat the slower
+    of the plain H2D and D2H rates (each the best over the same stream / chunk settings, 5
+    repetitions). r03 bounded it by a plain H2D + D2H pipeline of copies, which the kernel pipeline
+    beat (1.044, VERDICT r03 #7): that was a schedule, not a bound."""
     n = w.n
     host = torch.from_numpy(w.arena).pin_memory()
     back = torch.empty_like(host).pin_memory()
@@ -266,11 +268,12 @@ def end_to_end(torch, batch, kt, w, sd, od, dev, chunks=8, reps=3):
     pn = torch.zeros(n, dtype=torch.int64, device=dev)
     offs = w.seal_desc["offset"].astype(np.int64)
     ends = offs + w.seal_desc["len"].astype(np.int64)
+    configs = ((2, chunks), (3, 16), (4, 32))
 
-    def run(desc, mode, nch, nstreams):
+    def run(desc, mode, nch, nstreams, nrep=reps):
         per = (n + nch - 1) // nch
         wsl = [torch.empty(max(batch.workspace_bytes(per), 256), dtype=torch.uint8, device=dev)
-               for _ in range(nstreams)] if mode != "copy" else None
+               for _ in range(nstreams)] if mode in ("seal", "open") else None
         bounds = [(n * k) // nch for k in range(nch + 1)]
         streams = [torch.cuda.Stream(device=dev) for _ in range(nstreams)]
 
@@ -282,26 +285,31 @@ def end_to_end(torch, batch, kt, w, sd, od, dev, chunks=8, reps=3):
                 a, b = int(offs[lo:hi].min()), int(ends[lo:hi].max())
                 s = streams[k % nstreams]
                 with torch.cuda.stream(s):
-                    arena[a:b].copy_(host[a:b], non_blocking=True)
+                    if mode != "d2h":
+                        arena[a:b].copy_(host[a:b], non_blocking=True)
                     if mode == "open":
                         batch.open_(kt, arena, desc[32 * lo:32 * hi], st[lo:hi], pn[lo:hi], w.suite_hint,
                                     wsl[k % nstreams], s.cuda_stream)
                     elif mode == "seal":
                         batch.seal(kt, arena, desc[32 * lo:32 * hi], st[lo:hi], w.suite_hint, wsl[k % nstreams],
                                    s.cuda_stream)
-                    back[a:b].copy_(arena[a:b], non_blocking=True)
+                    if mode != "h2d":
+                        back[a:b].copy_(arena[a:b], non_blocking=True)
             torch.cuda.synchronize()
 
         one_pass()  # warm
-        t0 = time.perf_counter()
-        for _ in range(reps):
+        best = None
+        for _ in range(nrep):
+            t0 = time.perf_counter()
             one_pass()
-        return (time.perf_counter() - t0) / reps
+            dt = time.perf_counter() - t0
+            best = dt if best is None or dt < best else best
+        return best
 
     res, cfg_used = {}, {}
     for name, desc in (("seal", sd), ("open", od)):
         best_rate = 0.0
-        for nstreams, nch in ((2, chunks), (3, 16), (4, 32)):
+        for nstreams, nch in configs:
             host.copy_(torch.from_numpy(w.arena) if name == "seal" else sealed)
             dt = run(desc, name, nch, nstreams)
             r = w.wire_bytes / dt / 2 ** 30
@@ -310,17 +318,16 @@ def end_to_end(torch, batch, kt, w, sd, od, dev, chunks=8, reps=3):
             if name == "seal":
                 sealed = back.clone()  # the open pass starts from the sealed bytes
         res[name] = round(best_rate, 2)
-    best = None
-    for nstreams in (2, 3, 4):
-        for nch in (8, 16, 32):
-            dt = run(None, "copy", nch, nstreams)
-            r = w.wire_bytes / dt / 2 ** 30
-            if best is None or r > best[0]:
-                best = (r, nstreams, nch)
+    link = {}
+    for mode in ("h2d", "d2h"):
+        link[mode] = max(w.wire_bytes / run(None, mode, nch, nstreams, 5) / 2 ** 30 for nstreams, nch in configs)
+    bound = min(link.values())
     return {"unit": "GiB/s of wire bytes, host-resident (pinned) in and out", "pipeline_config": cfg_used,
             "seal": res["seal"], "open": res["open"],
-            "copy_ceiling": round(best[0], 2), "copy_ceiling_config": {"streams": best[1], "chunks": best[2]},
-            "frac_of_copy_ceiling": {"seal": round(res["seal"] / best[0], 3), "open": round(res["open"] / best[0], 3)}}
+            "h2d_alone": round(link["h2d"], 2), "d2h_alone": round(link["d2h"], 2),
+            "link_bound": round(bound, 2),
+            "link_bound_note": "every wire byte goes in and comes out: no pipeline beats the slower direction alone",
+            "frac_of_link_bound": {"seal": round(res["seal"] / bound, 3), "open": round(res["open"] / bound, 3)}}
 
 
 # ---- roofline bookkeeping ---------------------------------------------------------------------

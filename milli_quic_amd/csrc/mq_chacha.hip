@@ -169,9 +169,9 @@ __device__ __forceinline__ void load_key8(const uint32_t* src, uint32_t (&k)[8])
 }
 
 // ---- keystream pool of a workgroup (kCcWaves waves, one staged tile each) ---------------------
-// A 1200-B packet takes 20 ChaCha20 blocks (one-time key and 19 keystream; the header-protection
-// block runs in a one-packet-per-lane pass: the open pre-pass before, the seal post-pass after),
-// but an octet runs 24 slots in three iterations, so 1/6 of the rounds went idle. Each wave runs
+// A 1200-B packet takes 20 ChaCha20 blocks (one-time key and 19 keystream; open's header-protection
+// block runs in the one-packet-per-lane pre-pass, seal's in this pool, below), but an octet runs 24
+// slots in three iterations, so 1/6 of the rounds went idle. Each wave runs
 // iterations 0 and 1 of its own packets; every later keystream block (slot >= 16) goes to the
 // workgroup's pool, which all its lanes work off together between two barriers (open: once the
 // MACs have read the ciphertext; seal: before the MACs): 4 waves x 8 packets x 4 blocks = 128
@@ -313,10 +313,10 @@ struct ChaChaPolicy {
     hp_mask_words(smp, row, m0, m1);
   }
 
-  // send composite (transmit.rs:625-755), AEAD part: keystream block ctr of the packet runs on
-  // lane ctr % 8 in iteration ctr / 8 (ctr 0 = the Poly1305 key); with the pool, blocks >= 16 run
-  // in the workgroup's pool before the MACs. Header protection follows in
-  // mq_chacha_seal_hp_kernel (the sample is ciphertext, so it needs the sealed packet).
+  // send composite (transmit.rs:625-755): keystream block ctr of the packet runs on lane ctr % 8 in
+  // iteration ctr / 8 (ctr 0 = the Poly1305 key); with the pool, blocks >= 16 and the
+  // header-protection block (its sample is ciphertext of block 1) run in the workgroup's pool
+  // before the MACs, and the mask is applied once the MAC has read the unprotected header.
   template <bool SINGLE, class S, class G>
   static __device__ __forceinline__ void seal(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j,
                                               G& stg, const CcPool& pool) {

@@ -214,6 +214,17 @@ struct ConnState {
   uint8_t phase, flags, updates;
 };
 
+// the running largest PN of a level, without indexing the array by a run-time value (an indexed
+// private array lives in scratch memory: r03's walk waited on a scratch round trip per packet)
+__device__ __forceinline__ uint64_t largest_of(const ConnState& s, uint32_t level) {
+  return level == 0 ? s.largest[0] : level == 1 ? s.largest[1] : s.largest[2];
+}
+__device__ __forceinline__ void raise_largest(ConnState& s, uint32_t level, uint64_t pn) {
+#pragma unroll
+  for (uint32_t l = 0; l < 3; ++l)
+    if (level == l && pn > s.largest[l]) s.largest[l] = pn;
+}
+
 __device__ __forceinline__ ConnState load_state(const mq_conn_recv& c) {
   ConnState s;
   for (int l = 0; l < 3; ++l) { s.largest[l] = c.largest_pn[l]; s.row[l] = c.app_row[l]; }
@@ -249,7 +260,7 @@ __device__ __forceinline__ void decide(const ConnState& s, const RecvWork& w, co
   p.lbefore = 0;
   p.status = w.pre;
   if (w.pre != kPending) return;
-  p.lbefore = s.largest[w.level];
+  p.lbefore = largest_of(s, w.level);
   p.pn = decode_pn(p.trunc, p.pn_len, p.lbefore);
   if (p.pn > (1ull << 62) - 1) { p.status = MQ_ERR_PROTOCOL; return; }  // recv.rs:393-395, 994-997
   if (w.level != MQ_LEVEL_APPLICATION) {
@@ -268,7 +279,7 @@ __device__ __forceinline__ void decide(const ConnState& s, const RecvWork& w, co
 }
 
 __device__ __forceinline__ void advance(ConnState& s, const RecvWork& w, const RecvPlan& p, uint8_t gen) {
-  if (p.pn > s.largest[w.level]) s.largest[w.level] = p.pn;  // recv.rs:239-247
+  raise_largest(s, w.level, p.pn);  // recv.rs:239-247
   if (w.level == MQ_LEVEL_APPLICATION && gen == 2) {          // confirm_peer_key_update (keys.rs:532-583)
     s.row[0] = s.row[1];
     s.row[1] = s.row[2];
@@ -283,11 +294,8 @@ extern "C" __global__ __launch_bounds__(256) void mq_recv_unmask_kernel(const ui
                                                                         const RecvWork* __restrict__ work,
                                                                         const uint2* __restrict__ hpm,
                                                                         const uint32_t* __restrict__ total,
-                                                                        uint32_t max_pkts, RecvPlan* __restrict__ hdr,
-                                                                        uint8_t* __restrict__ outcome) {
+                                                                        uint32_t max_pkts, RecvPlan* __restrict__ hdr) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= max_pkts) return;
-  outcome[i] = 0;
   if (i >= min(*total, max_pkts)) return;
   const RecvWork w = work[i];
   RecvPlan p;
@@ -296,7 +304,27 @@ extern "C" __global__ __launch_bounds__(256) void mq_recv_unmask_kernel(const ui
   hdr[i] = p;
 }
 
-// ---- walk: one lane per connection replays its packets in arrival order ---------------------------
+// Records and header values in connection order (r04): everything after the sort — the walks, the
+// AEAD passes' descriptors and statuses, the outcomes — is indexed by the sorted position k, so a
+// walk reads each connection's run contiguously; only the output records keep arrival order.
+extern "C" __global__ __launch_bounds__(256) void mq_recv_gather_kernel(const uint32_t* __restrict__ total,
+                                                                        uint32_t max_pkts,
+                                                                        const uint32_t* __restrict__ svals,
+                                                                        const RecvWork* __restrict__ work,
+                                                                        const RecvPlan* __restrict__ hdr,
+                                                                        RecvWork* __restrict__ work_s,
+                                                                        RecvPlan* __restrict__ hdr_s,
+                                                                        uint8_t* __restrict__ outcome) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= max_pkts) return;
+  outcome[k] = 0;
+  if (k >= min(*total, max_pkts)) return;
+  const uint32_t i = svals[k];
+  work_s[k] = work[i];
+  hdr_s[k] = hdr[i];
+}
+
+// ---- walk: connections replay their packets in arrival order ---------------------------------------
 // With every outcome known so far it decides each packet exactly as the sequential reference does;
 // a packet whose AEAD attempt is missing or was made with other inputs gets a new attempt (d1 / d2)
 // and is SPECULATED to open, so the walk can go on. Repeated after each pair of AEAD passes until
@@ -313,9 +341,10 @@ struct WalkEnt {
 };
 
 // one packet of a connection's run, in arrival order (the sequential reference's decision, the
-// attempt to make, the packet's record)
+// attempt to make, the packet's record): k = its sorted position (attempt, descriptors), e.i = its
+// arrival index (the output record)
 __device__ __forceinline__ void walk_one(ConnState& s, const mq_conn_recv& c, uint32_t n_rows, const WalkEnt& e,
-                                         RecvPlan* __restrict__ tried, mq_pkt_desc* __restrict__ d1,
+                                         uint32_t k, RecvPlan* __restrict__ tried, mq_pkt_desc* __restrict__ d1,
                                          mq_pkt_desc* __restrict__ d2, mq_recv_pkt* __restrict__ out,
                                          uint32_t& new_attempts, int final_walk) {
   const uint32_t i = e.i;
@@ -363,15 +392,15 @@ __device__ __forceinline__ void walk_one(ConnState& s, const mq_conn_recv& c, ui
     } else if (final_walk) {
       st = MQ_ERR_DEFERRED;
     } else {  // (re)attempt with the inputs the reference would use; speculate it opens
-      tried[i] = p;
+      tried[k] = p;
       a.key_id = p.row;
       b.key_id = p.retry;
       ++new_attempts;
       st = MQ_OK;
     }
   }
-  d1[i] = a;
-  d2[i] = b;
+  d1[k] = a;
+  d2[k] = b;
   mq_recv_pkt r;
   r.offset = w.offset; r.len = w.len; r.dgram = w.dgram; r.level = w.level; r.status = st;
   r.pn = st == MQ_OK ? used.pn : 0;
@@ -383,10 +412,11 @@ __device__ __forceinline__ void walk_one(ConnState& s, const mq_conn_recv& c, ui
 }
 
 // A connection per group of kWalkGroup lanes (r04): the group loads the inputs of its next
-// kWalkGroup packets together (one packet per lane: one round trip for the lot, the next round's
-// indices prefetched), then the group's first lane walks them from LDS. r03 walked one packet per
-// lane-step straight from memory (one round trip per packet, 372 us per walk of 2^20 packets over
-// 4096 connections, three walks per batch: profiles/r04g_kernel_stats_recv.csv).
+// kWalkGroup packets together (one packet per lane, a contiguous piece of the run in sorted
+// order), then the group's first lane walks them from LDS. r03 walked one packet per lane-step
+// straight from memory in arrival-order arrays (a scattered round trip per packet, 372 us per walk
+// of 2^20 packets over 4096 connections, three walks per batch: profiles/r04g_kernel_stats_recv.csv;
+// 351 us with the groups but still arrival-order arrays, r04h).
 constexpr uint32_t kWalkGroup = 16, kWalkThreads = 256, kWalkConns = kWalkThreads / kWalkGroup;
 
 extern "C" __global__ __launch_bounds__(kWalkThreads) void mq_recv_walk_kernel(
@@ -407,24 +437,23 @@ extern "C" __global__ __launch_bounds__(kWalkThreads) void mq_recv_walk_kernel(
     s = load_state(c);
   }
   uint32_t new_attempts = 0;
-  uint32_t nxt = lo + q < hi ? svals[lo + q] : 0u;
   WalkEnt* ent = s_e + g * kWalkGroup;
   for (uint32_t k0 = lo;; k0 += kWalkGroup) {
     const bool act = k0 < hi;
     if (!wave_any(act)) break;  // the wave's groups have runs of different lengths
     const uint32_t m = act ? min(kWalkGroup, hi - k0) : 0u;
-    if (q < m) {
-      const uint32_t i = nxt;
-      ent[q].i = i;
-      ent[q].w = work[i];
-      ent[q].p = hdr[i];
-      ent[q].t = tried[i];
-      ent[q].o = outcome[i];
+    if (q < m) {  // work, hdr, tried, outcome: sorted order
+      const uint32_t k = k0 + q;
+      ent[q].i = svals[k];
+      ent[q].w = work[k];
+      ent[q].p = hdr[k];
+      ent[q].t = tried[k];
+      ent[q].o = outcome[k];
     }
-    nxt = k0 + kWalkGroup + q < hi ? svals[k0 + kWalkGroup + q] : 0u;
     wave_sync();
     if (q == 0)
-      for (uint32_t k = 0; k < m; ++k) walk_one(s, c, n_rows, ent[k], tried, d1, d2, out, new_attempts, final_walk);
+      for (uint32_t k = 0; k < m; ++k)
+        walk_one(s, c, n_rows, ent[k], k0 + k, tried, d1, d2, out, new_attempts, final_walk);
     wave_sync();  // the entries are read before the next round overwrites them
   }
   if (!live || q != 0) return;
@@ -463,8 +492,8 @@ size_t al(size_t b) { return (b + 255) & ~(size_t)255; }
 
 struct RecvWs {
   uint32_t *counts, *base, *total, *keys, *vals, *skeys, *svals, *seg_lo, *seg_hi, *attempts;
-  RecvWork* work;
-  RecvPlan *hdr, *tried;
+  RecvWork *work, *work_s;
+  RecvPlan *hdr, *hdr_s, *tried;
   mq_conn_recv* conn0;
   uint2* hpm;
   mq_pkt_desc *d1, *d2;
@@ -500,6 +529,8 @@ RecvWs layout(uint8_t* p, uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_conns
   w.conn0 = (mq_conn_recv*)take(sizeof(mq_conn_recv) * (size_t)n_conns);
   w.work = (RecvWork*)take(sizeof(RecvWork) * (size_t)max_pkts);
   w.hdr = (RecvPlan*)take(sizeof(RecvPlan) * (size_t)max_pkts);
+  w.work_s = (RecvWork*)take(sizeof(RecvWork) * (size_t)max_pkts);
+  w.hdr_s = (RecvPlan*)take(sizeof(RecvPlan) * (size_t)max_pkts);
   w.tried = (RecvPlan*)take(sizeof(RecvPlan) * (size_t)max_pkts);
   w.hpm = (uint2*)take(8ull * max_pkts);
   w.d1 = (mq_pkt_desc*)take(sizeof(mq_pkt_desc) * (size_t)max_pkts);
@@ -560,7 +591,7 @@ hipError_t mq_recv_front(const KeyRow* kt, uint32_t n_rows, mq_conn_recv* conns,
   if ((e = mq_launch_chacha_prepass(kt, n_rows, arena, arena_len, w.d1, max_pkts, w.hpm, s)) != hipSuccess) return e;
   if ((e = mq_launch_aes_prepass(kt, n_rows, arena, arena_len, w.d1, max_pkts, w.hpm, s)) != hipSuccess) return e;
   hipLaunchKernelGGL(mq_recv_unmask_kernel, dim3((max_pkts + 255) / 256), b256, 0, s, arena, w.work, w.hpm, w.total,
-                     max_pkts, w.hdr, w.outcome);
+                     max_pkts, w.hdr);
   size_t cb = w.cub_bytes;
   // keys are connection indices (< n_conns) and 0xFFFFFFFF past the packet count: the low
   // ceil(log2(n_conns + 1)) bits order them (the padding's all-ones bits sort last), so the radix
@@ -576,6 +607,8 @@ hipError_t mq_recv_front(const KeyRow* kt, uint32_t n_rows, mq_conn_recv* conns,
   }
   hipLaunchKernelGGL(mq_recv_seg_kernel, dim3((max_pkts + 255) / 256), b256, 0, s, w.skeys, max_pkts, n_conns, w.seg_lo,
                      w.seg_hi);
+  hipLaunchKernelGGL(mq_recv_gather_kernel, dim3((max_pkts + 255) / 256), b256, 0, s, w.total, max_pkts, w.svals, w.work,
+                     w.hdr, w.work_s, w.hdr_s, w.outcome);
   return mq_recv_walk(kt, n_rows, conns, n_conns, n_dgrams, max_pkts, out, ws_ptr, open_ws_bytes, false, s);
 }
 
@@ -588,9 +621,8 @@ hipError_t mq_recv_walk(const KeyRow* /*kt*/, uint32_t n_rows, mq_conn_recv* con
   if ((e = hipMemsetAsync(w.attempts, 0, 4, s)) != hipSuccess) return e;
   if (n_conns)
     hipLaunchKernelGGL(mq_recv_walk_kernel, dim3((n_conns + kWalkConns - 1) / kWalkConns), dim3(kWalkThreads), 0, s,
-                       w.conn0, conns, n_conns, w.work,
-                       w.svals, w.seg_lo, w.seg_hi, w.hdr, n_rows, w.tried, w.outcome, w.d1, w.d2, out, w.attempts,
-                       (int)final_walk);
+                       w.conn0, conns, n_conns, w.work_s, w.svals, w.seg_lo, w.seg_hi, w.hdr_s, n_rows, w.tried,
+                       w.outcome, w.d1, w.d2, out, w.attempts, (int)final_walk);
   return hipGetLastError();
 }
 
