@@ -114,12 +114,13 @@ class SideStreams {
  public:
   typedef typename B::Stream Stream;
   typedef typename B::Event Event;
+  static constexpr int kSteps = 8;  // caller -> side hand-offs of one fork (chunked pipelines)
 
   struct Entry {
     int dev = -1;
     Stream caller{};
     Stream side[kSides]{};
-    Event fork{}, join[kSides]{};
+    Event fork{}, join[kSides]{}, step[kSteps]{};
     bool ok = false;
     std::mutex mu;  // one fork/launch/join sequence at a time
     ~Entry() {
@@ -129,6 +130,8 @@ class SideStreams {
         if (side[k]) B::stream_destroy(side[k]);
         if (join[k]) B::event_destroy(join[k]);
       }
+      for (int k = 0; k < kSteps; ++k)
+        if (step[k]) B::event_destroy(step[k]);
       if (fork) B::event_destroy(fork);
     }
   };
@@ -144,6 +147,11 @@ class SideStreams {
     }
     explicit operator bool() const { return e_ != nullptr; }
     Stream side(int k) const { return e_->side[k]; }
+    // hand-off k (< kSteps) of a pipeline: side stream `sd`'s later work waits for the caller's
+    // work so far (e.g. chunk k built on the caller's stream, then sealed on the side stream)
+    bool hand_off(int k, int sd) {
+      return k >= 0 && k < kSteps && B::record(e_->step[k], e_->caller) && B::wait(e_->side[sd], e_->step[k]);
+    }
     // returns false if a join could not be enqueued (the caller's stream then does not wait)
     bool join() {
       if (!e_ || joined_) return true;
@@ -221,6 +229,7 @@ class SideStreams {
       e->caller = caller;
       bool ok = B::event_create(&e->fork);
       for (int k = 0; k < kSides && ok; ++k) ok = B::stream_create(&e->side[k]) && B::event_create(&e->join[k]);
+      for (int k = 0; k < kSteps && ok; ++k) ok = B::event_create(&e->step[k]);
       e->ok = ok;
       lru_.push_front(e);
       if (lru_.size() > cap_) {

@@ -174,6 +174,8 @@ static void test_side_streams() {
       CHECK(f.side(0)->dev == 1 && f.side(1)->dev == 1);  // created on the caller's device
       CHECK(f.side(0)->waits == 1 && f.side(1)->waits == 1);
       sides.insert(f.side(0));
+      CHECK(f.hand_off(0, 1) && f.side(1)->waits == 2);  // a pipeline step: side 1 waits on the caller
+      CHECK(!f.hand_off(8, 0) && !f.hand_off(-1, 0));
       CHECK(f.join());
       CHECK(callers[0].waits == 2);  // the caller waits for both side streams
       CHECK(f.join() && callers[0].waits == 2);  // a second join is a no-op
@@ -193,7 +195,7 @@ static void test_side_streams() {
       auto f = ss.fork(1, &callers[k], 2);
       CHECK(f);
     }
-    CHECK(ss.size() == 4 && Fake::live_streams == 8 && Fake::live_events == 12);
+    CHECK(ss.size() == 4 && Fake::live_streams == 8 && Fake::live_events == 4 * (3 + 8));
     ss.release(&callers[5]);
     CHECK(ss.size() == 3 && Fake::live_streams == 6);
     ss.release(&callers[5]);  // nothing left for it

@@ -22,4 +22,18 @@ for a in protect recv; do
   step prof_$a
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$a -o run -- python3 tools/prof_aux.py $a 5 > $O/prof_$a.log 2>&1 || { tail $O/prof_$a.log; exit 1; }
 done
-echo R04J_OK
+
+for a in "c --config c" "e --config e" "ck --config c --keys 1024"; do
+  set -- $a; name=$1; shift
+  step bench_$name
+  timeout -k 10 300 python3 bench.py --no-cpu-baseline "$@" > $O/bench_$name.json 2> $O/bench_$name.err || { tail $O/bench_$name.err; exit 1; }
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print(sys.argv[1], d['value'], r['seal_ms'], r['open_ms'], r['frac'])" $O/bench_$name.json
+done
+step prof_e
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_e -o run -- python3 bench.py --no-cpu-baseline --config e > $O/prof_e.json 2> $O/prof_e.err || { tail $O/prof_e.err; exit 1; }
+echo R04J_DONE
+step prof_d20
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_d20 -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > $O/prof_d20.json 2> $O/prof_d20.err || { tail $O/prof_d20.err; exit 1; }
+python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print('prof_d20', d['value'], r['seal_ms'], r['open_ms'])" $O/prof_d20.json
+grep -E "chacha_(seal|open)1" $O/prof_d20/run_kernel_stats.csv
+echo R04J_ALL_DONE
