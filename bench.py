@@ -439,12 +439,13 @@ def main():
     # first ~5 steps run up to 40 % slower while the clocks ramp (tools/clock_probe.py,
     # profiles/r04b_clock_probe.txt), which is what slowed the driver's 20-step runs
     fails_warm = (st != 0).sum()
+    if world > 1:  # ranks start the time-based warm-up together, so they also end it together
+        dist.barrier()
     extra, tw = 0, time.perf_counter()
     while time.perf_counter() - tw < args.warmup_seconds:  # untimed, the same work: clock ramp
-        for _ in range(4):
-            step()
-        torch.cuda.synchronize()
-        extra += 4
+        step()
+        torch.cuda.synchronize()  # per step: a rank overshoots the deadline by at most one step
+        extra += 1
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

@@ -13,6 +13,7 @@
 //         one-time key) -> Poly1305 over the untouched ciphertext -> tag check -> only then the
 //         keystream XOR (held first block + the rest); failed packets are never stored.
 #include "mq_tile.h"
+#include "mq_build.h"
 
 namespace mq {
 
@@ -610,7 +611,7 @@ __device__ __forceinline__ void chacha_list(const KeyRow* __restrict__ kt, uint3
     __syncthreads();  // every wave is done with the tile and its scratch
     if (threadIdx.x == 0) *next_slot = sched ? gridDim.x + pend : tb + gridDim.x;
     __syncthreads();
-    tb = *next_slot;
+    tb = (uint32_t)__builtin_amdgcn_readfirstlane((int)*next_slot);  // uniform: keeps tile indexing scalar
     // the claim after this one: its result is used one block later (issued after the barrier, so
     // no barrier waits for it until the next tile's first one)
     if (threadIdx.x == 0 && sched) pend = __hip_atomic_fetch_add(sched, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -631,6 +632,129 @@ extern "C" __global__ __launch_bounds__(64 * kCcWaves) __attribute__((amdgpu_wav
     const uint2* __restrict__ hpm, uint32_t* __restrict__ sched) {
   chacha_list<true, false>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm, sched);
 }
+
+// ---- fused send composite (mq_batch_protect with the ChaCha20 suite hint, r04) -----------------
+// build + seal + header protection in one pass: the tile's eight packets are BUILT from their
+// requests straight into the wave's LDS image (layout from mq_build.h, the frames at any alignment
+// with unaligned 16-B loads, header / PN / PADDING / tag-room chunks byte-wise), sealed there by the
+// same ChaChaPolicy::seal as a staged batch, and written to `out` once. The two-kernel composite
+// (mq_build_kernel, then the seal kernel over its descriptors) moved every packet through HBM twice:
+// written by the build, read back and rewritten by the seal — 4.9 GB per 2^20 x 1200 B against the
+// 2.4 GB of frames in and packets out here. Tiles whose images exceed the LDS budget build in HBM
+// (the build kernel's stores) and seal there (direct path). Statuses and lengths as the composite:
+// the build's status when it fails (pkt_len = `needed` or 0), else the seal's.
+#ifndef MQ_PROTECT_BATCH
+#define MQ_PROTECT_BATCH 5
+#endif
+constexpr uint32_t kProtectBatch = MQ_PROTECT_BATCH;  // image chunks per lane whose loads fly together (5:
+                                                      // no spills beside the seal state; 8 or 10 spill)
+
+template <bool SINGLE>
+__device__ __forceinline__ void chacha_protect_tile(uint32_t tb, const KeyRow* __restrict__ kt, uint32_t n_rows,
+                                                    const mq_conn_send* __restrict__ conns, uint32_t n_conns,
+                                                    const uint8_t* __restrict__ frames, uint64_t frames_len,
+                                                    uint8_t* __restrict__ out, uint64_t out_len,
+                                                    const mq_send_req* __restrict__ req, uint32_t n,
+                                                    uint32_t suite_hint, uint8_t* __restrict__ status,
+                                                    uint32_t* __restrict__ pkt_len) {
+  constexpr uint32_t W = kCcWaves;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t w = threadIdx.x >> 6;
+  uint8_t* wsm = smem + w * kLdsBytes;
+  const int lane = threadIdx.x & (kWave - 1), p = lane / kLanesPerPkt, j = lane % kLanesPerPkt;
+  const uint32_t tile_id = tb * W + w;
+  CcPool pool{false, smem, w * kLdsBytes, (uint32_t*)(wsm + kDataBudget + 32u * (uint32_t)p), kt};
+  const uint32_t tile0 = tile_id * kPktsPerTile;
+  if (tile0 >= n) {  // a wave past the batch in a live workgroup joins the barriers and the pool
+    if (j == 0) pool.rec[0] = 0;
+    __syncthreads();
+    cc_pool_run<SINGLE>(pool);
+    __syncthreads();
+    return;
+  }
+  PktCtx c;
+  c.tile = tile_id;
+  c.i = tile0 + (uint32_t)p;
+  c.valid = c.i < n;
+  c.pre_hp = false;
+  c.hm0 = c.hm1 = 0;
+  const BuildLayout b = build_layout(c.i, c.valid, kt, n_rows, conns, n_conns, frames_len, out_len, req, suite_hint);
+  c.d = b.d;
+  c.pn = b.pn;
+  if (!c.valid || b.st != MQ_OK) c.st = c.valid ? b.st : (int)MQ_ERR_INVALID_ARG;
+  else c.st = validate<MQ_SUITE_CHACHA20, false, SINGLE>(c.d, kt, n_rows, out_len);
+  c.act = c.valid && c.st == MQ_OK;
+  const KeyRow* row = SINGLE ? kt : kt + (c.act ? c.d.key_id : 0u);
+  c.otk = (uint32_t*)(wsm + kLdsBytes - 32u * kPktsPerTile + 32u * (uint32_t)p);
+  Placement pl;
+  pl.off = c.act ? c.d.offset : 0;
+  pl.len = c.act ? c.d.len : 0u;
+  const uint64_t nch64 = c.act ? ((pl.off & 15) + (uint64_t)c.d.len + 15) >> 4 : 0u;
+  const uint32_t nch = (uint32_t)(nch64 < 0xFFFFu ? nch64 : 0xFFFFu);
+  const uint32_t incl = oct_incl_scan(nch);
+  const uint32_t total = lane_u32(incl, kWave - 1);
+  const uint8_t* fr = frames + b.frames_offset;
+  if (total * 16u <= kDataBudget) {
+    pl.slot = incl - nch;
+    pool.on = true;
+    // the image: chunk k holds packet bytes [16k - head, 16k - head + 16); lane j builds k = j,
+    // j + 8, ... (kProtectBatch chunks' loads issued before any of their LDS stores)
+    uint8_t* img = wsm + 16u * pl.slot;
+    const int head = (int)pl.head();
+    for (uint32_t k0 = (uint32_t)j; k0 < nch; k0 += kLanesPerPkt * kProtectBatch) {
+      uint4 v[kProtectBatch];
+#pragma unroll
+      for (uint32_t t = 0; t < kProtectBatch; ++t) {
+        const uint32_t k = k0 + kLanesPerPkt * t;
+        const int x0 = 16 * (int)k - head;
+        const bool whole = k < nch && x0 >= (int)b.hp && (uint32_t)x0 + 16u <= b.hp + b.m;
+        v[t] = whole ? ld16(fr + ((uint32_t)x0 - b.hp)) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (uint32_t t = 0; t < kProtectBatch; ++t) {
+        const uint32_t k = k0 + kLanesPerPkt * t;
+        const int x0 = 16 * (int)k - head;
+        const bool whole = x0 >= (int)b.hp && (uint32_t)x0 + 16u <= b.hp + b.m;
+        const bool zero = x0 >= (int)(b.hp + b.m);  // PADDING / tag room (and bytes past the packet)
+        if (k < nch && (whole || zero)) *(uint4*)(img + 16u * k) = v[t];
+      }
+    }
+    // edge chunks, byte-wise, outside the unrolled batch: those holding header / PN bytes, and the
+    // one where the frames end mid-chunk
+    const uint32_t kh = (uint32_t)(head + (int)b.hp + 15) >> 4, fe = (uint32_t)head + b.hp + b.m;
+    for (uint32_t k = (uint32_t)j; k < kh && k < nch; k += kLanesPerPkt)
+      *(uint4*)(img + 16u * k) = build_edge_chunk(b, fr, 16 * (int)k - head, pl.len);
+    if ((fe & 15u) && (fe >> 4) >= kh && (fe >> 4) < nch && ((fe >> 4) & (kLanesPerPkt - 1)) == (uint32_t)j)
+      *(uint4*)(img + 16u * (fe >> 4)) = build_edge_chunk(b, fr, 16 * (int)(fe >> 4) - head, pl.len);
+    LdsSpace sp{wsm};
+    NoStager stg;  // complete(): the wave's image stores are done before any lane reads the image
+    ChaChaPolicy::template seal<SINGLE, LdsSpace>(sp, pl.slot * 16u + pl.head(), c, row, j, stg, pool);
+    wave_sync();
+    stage_out(wsm, out, lane, c.act, pl);
+  } else {
+    if (c.act) build_store<kProtectBatch>(b, j, frames, out);
+    wave_sync();  // the packets are in HBM before the seal reads them
+    GlobalSpace sp{out, out_len};
+    NoStager stg;
+    ChaChaPolicy::template seal<SINGLE, GlobalSpace>(sp, c.act ? c.d.offset : 0, c, row, j, stg, pool);
+  }
+  if (c.valid && j == 0) {
+    status[c.i] = (uint8_t)c.st;
+    pkt_len[c.i] = (b.st != MQ_OK || c.st == MQ_OK) ? b.len_out : 0u;
+  }
+}
+
+#define MQ_CHACHA_PROTECT_KERNEL(NAME, SINGLE)                                                             \
+  extern "C" __global__ __launch_bounds__(64 * kCcWaves) __attribute__((amdgpu_waves_per_eu(4))) void NAME( \
+      const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_conn_send* __restrict__ conns, uint32_t n_conns, \
+      const uint8_t* __restrict__ frames, uint64_t frames_len, uint8_t* __restrict__ out, uint64_t out_len,   \
+      const mq_send_req* __restrict__ req, uint32_t n, uint32_t suite_hint, uint8_t* __restrict__ status,     \
+      uint32_t* __restrict__ pkt_len) {                                                                       \
+    chacha_protect_tile<SINGLE>(blockIdx.x, kt, n_rows, conns, n_conns, frames, frames_len, out, out_len, req, n, \
+                                suite_hint, status, pkt_len);                                                 \
+  }
+MQ_CHACHA_PROTECT_KERNEL(mq_chacha_protect_kernel, false)
+MQ_CHACHA_PROTECT_KERNEL(mq_chacha_protect1_kernel, true)
 
 extern "C" __global__ __launch_bounds__(256) void mq_chacha_hp_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, const uint32_t* __restrict__ key_ids,
@@ -718,6 +842,19 @@ hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_
   hipLaunchKernelGGL(n_rows == 1 ? mq_chacha_seal1_kernel : mq_chacha_seal_kernel, dim3(blocks),
                      dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kt, n_rows, arena, arena_len, desc, n, index,
                      n_dev, status);
+  return hipGetLastError();
+}
+
+hipError_t mq_launch_chacha_protect(const KeyRow* kt, uint32_t n_rows, const mq_conn_send* conns, uint32_t n_conns,
+                                    const uint8_t* frames, uint64_t frames_len, uint8_t* out, uint64_t out_len,
+                                    const mq_send_req* req, uint32_t n, uint32_t suite_hint, uint8_t* status,
+                                    uint32_t* pkt_len, hipStream_t s) {
+  const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
+  if (tiles == 0) return hipSuccess;
+  const uint32_t blocks = (tiles + kCcWaves - 1) / kCcWaves;
+  hipLaunchKernelGGL(n_rows == 1 ? mq_chacha_protect1_kernel : mq_chacha_protect_kernel, dim3(blocks),
+                     dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kt, n_rows, conns, n_conns, frames, frames_len,
+                     out, out_len, req, n, suite_hint, status, pkt_len);
   return hipGetLastError();
 }
 

@@ -50,8 +50,12 @@ hipError_t mq_launch_derive_initial(const mq::MQDeriveConsts& k, const uint8_t* 
 hipError_t mq_launch_build(const KeyRow* kt, uint32_t n_rows, const mq_conn_send* conns, uint32_t n_conns,
                            const uint8_t* frames, uint64_t frames_len, uint8_t* out, uint64_t out_len,
                            const mq_send_req* req, uint32_t n, mq_pkt_desc* desc, uint8_t* bstatus,
-                           uint32_t* pkt_len, hipStream_t s);
+                           uint32_t* pkt_len, uint32_t suite_hint, hipStream_t s);
 hipError_t mq_launch_send_status(const uint8_t* bstatus, uint8_t* status, uint32_t n, hipStream_t s);
+hipError_t mq_launch_chacha_protect(const KeyRow* kt, uint32_t n_rows, const mq_conn_send* conns, uint32_t n_conns,
+                                    const uint8_t* frames, uint64_t frames_len, uint8_t* out, uint64_t out_len,
+                                    const mq_send_req* req, uint32_t n, uint32_t suite_hint, uint8_t* status,
+                                    uint32_t* pkt_len, hipStream_t s);
 size_t mq_recv_workspace(uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_conns, size_t open_ws_bytes);
 hipError_t mq_recv_front(const KeyRow* kt, uint32_t n_rows, mq_conn_recv* conns, uint32_t n_conns, uint8_t* arena,
                          uint64_t arena_len, const mq_dgram* dg, uint32_t n_dgrams, uint32_t max_pkts,
@@ -1005,6 +1009,15 @@ int mq_batch_protect(const mq_keytable* kt, const mq_conn_send* conns, uint32_t 
   if (!g.ok()) return MQ_ERR_NO_DEVICE;
   if (n == 0) return MQ_OK;
   hipStream_t s = (hipStream_t)stream;
+  // ChaCha20 batches (r04): one fused kernel builds each tile's packets into LDS and seals them
+  // there (mq_chacha.hip); MQ_PROTECT_FUSED=0 (diagnostic, read per call so tests compare both)
+  // keeps the two-kernel composite below
+  const char* fe = std::getenv("MQ_PROTECT_FUSED");
+  if (!(fe && fe[0] == '0') && suite_hint == MQ_SUITE_CHACHA20)
+    return mq_launch_chacha_protect(kt->dev, kt->rows, conns, n_conns, frames, frames_len, out, out_len, req, n,
+                                    suite_hint, status, pkt_len, s) == hipSuccess
+               ? MQ_OK
+               : MQ_ERR_HIP;
   uint8_t* ws = (uint8_t*)workspace;
   mq_pkt_desc* desc = (mq_pkt_desc*)ws;
   uint8_t* bstatus = ws + ws_align(sizeof(mq_pkt_desc) * (size_t)n);
@@ -1019,7 +1032,7 @@ int mq_batch_protect(const mq_keytable* kt, const mq_conn_send* conns, uint32_t 
                                                   : mq::SideStreams<HipBackend>::Fork();
   if (!fork) {
     if (mq_launch_build(kt->dev, kt->rows, conns, n_conns, frames, frames_len, out, out_len, req, n, desc, bstatus,
-                        pkt_len, s) != hipSuccess)
+                        pkt_len, suite_hint, s) != hipSuccess)
       return MQ_ERR_HIP;
     const int sr = batch(false, kt, out, out_len, desc, n, status, nullptr, suite_hint, seal_ws, stream);
     if (sr != MQ_OK) return sr;
@@ -1030,7 +1043,7 @@ int mq_batch_protect(const mq_keytable* kt, const mq_conn_send* conns, uint32_t 
   for (uint32_t k = 0; k < kProtectChunks && rc == MQ_OK; ++k) {
     const uint32_t lo = (uint32_t)((uint64_t)n * k / kProtectChunks), hi = (uint32_t)((uint64_t)n * (k + 1) / kProtectChunks);
     if (mq_launch_build(kt->dev, kt->rows, conns, n_conns, frames, frames_len, out, out_len, req + lo, hi - lo,
-                        desc + lo, bstatus + lo, pkt_len + lo, s) != hipSuccess ||
+                        desc + lo, bstatus + lo, pkt_len + lo, suite_hint, s) != hipSuccess ||
         !fork.hand_off((int)k, 0)) {
       rc = MQ_ERR_HIP;
       break;

@@ -61,6 +61,43 @@ def test_protect_vs_oracle(orc, seed):
     assert g_out.tobytes() == o_out.tobytes()
 
 
+def chacha_heavy_batch(n, seed):
+    """random_batch with most requests 1-RTT on the ChaCha20 row (the fused protect kernel's
+    case), the rest Initial / Handshake or 1-RTT on the AES row (suite errors under the hint)."""
+    keys, conns, frames, req, out = random_batch(n, seed)
+    conns["key_row"][2:, 2] = 0
+    rng = np.random.default_rng(seed + 100)
+    req["level"] = np.where(rng.random(n) < 0.85, send.APPLICATION, req["level"])
+    return keys, conns, frames, req, out
+
+
+@pytest.mark.parametrize("hint", [_lib.MQ_SUITE_CHACHA20, _lib.MQ_SUITE_AES128GCM])
+@pytest.mark.parametrize("seed", [2, 9])
+def test_protect_suite_hint_vs_oracle(orc, seed, hint):
+    # a single-suite hint: rows of the other suite fail with MQ_ERR_SUITE before anything is
+    # written (orc_batch_protect); ChaCha20 runs the fused build + seal kernel, unaligned output
+    # slots and packets past the LDS image budget (direct path) included
+    keys, conns, frames, req, out = chacha_heavy_batch(3000, seed)
+    g_out, g_st, g_ln = gpu_protect(keys, conns, frames, out, req, hint)
+    o_out = out.copy()
+    o_st, o_ln = orc.batch_protect(keys, conns, frames, o_out, req, hint)
+    assert (g_st == o_st).all(), np.nonzero(g_st != o_st)
+    assert (g_ln == o_ln).all(), np.nonzero(g_ln != o_ln)
+    assert g_out.tobytes() == o_out.tobytes()
+    assert (o_st == 0).sum() > 1000
+
+
+def test_protect_fused_matches_two_kernel(monkeypatch):
+    # the fused ChaCha20 kernel and the build-then-seal composite (MQ_PROTECT_FUSED=0) agree byte
+    # for byte, statuses and lengths included
+    keys, conns, frames, req, out = chacha_heavy_batch(5000, 4)
+    a = gpu_protect(keys, conns, frames, out, req, _lib.MQ_SUITE_CHACHA20)
+    monkeypatch.setenv("MQ_PROTECT_FUSED", "0")
+    b = gpu_protect(keys, conns, frames, out, req, _lib.MQ_SUITE_CHACHA20)
+    for x, y in zip(a, b):
+        assert x.tobytes() == y.tobytes()
+
+
 def test_full_size_protect_then_open():
     # 2^20 1-RTT packets of 1171-byte frames (config B's payload), ChaCha20; the built packets
     # are exactly config B's wire format and open through mq_batch_open

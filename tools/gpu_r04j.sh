@@ -1,5 +1,5 @@
-# Round-4 call J: receive / send GPU tests, aux components with the product library and with the
-# 4-chunk build batch (MQ_LIB), kernel stats of the receive / protect composites.
+# Round-4 call J: receive / send GPU tests, aux components with the fused ChaCha protect and with
+# two-kernel composite (MQ_PROTECT_FUSED=0), kernel stats of the receive / protect composites.
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/${1:-r04j}
@@ -12,8 +12,8 @@ for r in 1 2; do
   step aux_$r
   timeout -k 10 300 python tools/bench_aux.py > $O/aux_$r.json 2> $O/aux_$r.err || { tail $O/aux_$r.err; exit 1; }
   cat $O/aux_$r.json
-  MQ_LIB=tools/ab_libs/bb4.so timeout -k 10 300 python tools/bench_aux.py > $O/aux_bb4_$r.json 2> $O/aux_bb4_$r.err || { tail $O/aux_bb4_$r.err; exit 1; }
-  cat $O/aux_bb4_$r.json
+  MQ_PROTECT_FUSED=0 timeout -k 10 300 python tools/bench_aux.py > $O/aux_unfused_$r.json 2> $O/aux_unfused_$r.err || { tail $O/aux_unfused_$r.err; exit 1; }
+  cat $O/aux_unfused_$r.json
 done
 step e2e
 timeout -k 10 600 python3 bench.py --no-cpu-baseline --e2e > $O/bench_b_e2e.json 2> $O/bench_b_e2e.err || { tail $O/bench_b_e2e.err; exit 1; }
