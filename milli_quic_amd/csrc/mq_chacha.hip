@@ -15,6 +15,8 @@
 #include "mq_tile.h"
 #include "mq_build.h"
 
+#include <cstdlib>
+
 namespace mq {
 
 // Byte stride between the LDS images of a packet's consecutive keystream blocks: 64. The
@@ -210,11 +212,11 @@ struct CcPool {
 };
 
 template <bool SINGLE>
-__device__ __forceinline__ void cc_pool_run(const CcPool& pool) {
+__device__ __forceinline__ void cc_pool_run(const CcPool& pool, uint32_t tid = threadIdx.x) {
   constexpr uint32_t kQ = kPktsPerTile * kCcWaves;  // packets of the workgroup
   static_assert(kQ <= kWave, "one packet per lane in the pool scan");
-  const int lane = threadIdx.x & (kWave - 1);
-  const uint32_t w = threadIdx.x >> 6;
+  const int lane = tid & (kWave - 1);
+  const uint32_t w = tid >> 6;
   auto rec = [&](uint32_t q) -> uint32_t* {
     return (uint32_t*)(pool.wg + (q >> 3) * kLdsBytes + kDataBudget + 32u * (q & 7));
   };
@@ -503,8 +505,10 @@ using namespace mq;
 // their staging waits line up.) The "1" variants are launched when the key table has a single
 // row (every valid packet on row 0): key material then lives in SGPRs.
 // tb: the workgroup's block of W tiles (blockIdx.x, or the persistent kernels' current block)
+// tid: threadIdx.x (the persistent list kernels pass an opaque copy per tile, so nothing derived
+// from it is hoisted out of their loop and held across every tile — that pressure spilled)
 template <bool OPEN, bool SINGLE>
-__device__ __forceinline__ void chacha_tile(uint32_t tb, const KeyRow* __restrict__ kt, uint32_t n_rows,
+__device__ __forceinline__ void chacha_tile(uint32_t tb, uint32_t tid, const KeyRow* __restrict__ kt, uint32_t n_rows,
                                             uint8_t* __restrict__ arena, uint64_t arena_len,
                                             const mq_pkt_desc* __restrict__ desc, uint32_t n,
                                             const uint32_t* __restrict__ index, const uint32_t* __restrict__ n_dev,
@@ -512,21 +516,21 @@ __device__ __forceinline__ void chacha_tile(uint32_t tb, const KeyRow* __restric
                                             const uint2* __restrict__ hpm) {
   constexpr uint32_t W = kCcWaves;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const uint32_t w = threadIdx.x >> 6;
+  const uint32_t w = tid >> 6;
   uint8_t* wsm = smem + w * kLdsBytes;
-  const int lane = threadIdx.x & (kWave - 1), p = lane / kLanesPerPkt, j = lane % kLanesPerPkt;
+  const int lane = tid & (kWave - 1), p = lane / kLanesPerPkt, j = lane % kLanesPerPkt;
   const uint32_t tile_id = tb * W + w;
   PktCtx c;
   const KeyRow* row;
   CcPool pool{false, smem, w * kLdsBytes, (uint32_t*)(wsm + kDataBudget + 32u * (uint32_t)p), kt};
   if (!tile_ctx<MQ_SUITE_CHACHA20, OPEN, SINGLE>(tile_id, kt, n_rows, arena_len, desc, n, index, n_dev, hpm,
-                                                 TilePrefetch{false, 0u, 0u}, c, row)) {
+                                                 TilePrefetch{false, 0u, 0u}, c, row, tid)) {
     // past the batch (list capacities exceed the count): a whole workgroup leaves at once, a
     // wave of a live workgroup only joins its barriers and pool
     if (tb * W * kPktsPerTile >= (n_dev ? *n_dev : n)) return;  // workgroup-uniform
     if (j == 0) pool.rec[0] = 0;
     __syncthreads();
-    cc_pool_run<SINGLE>(pool);
+    cc_pool_run<SINGLE>(pool, tid);
     __syncthreads();
     return;
   }
@@ -567,7 +571,7 @@ __device__ __forceinline__ void chacha_tile(uint32_t tb, const KeyRow* __restric
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
       const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status) {                                 \
-    chacha_tile<false, SINGLE>(blockIdx.x, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr, \
+    chacha_tile<false, SINGLE>(blockIdx.x, threadIdx.x, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr, \
                                nullptr);                                                                  \
   }                                                                                                       \
   extern "C" __global__ __launch_bounds__(64 * kCcWaves) __attribute__((amdgpu_waves_per_eu(4))) void NAME_OPEN( \
@@ -575,7 +579,7 @@ __device__ __forceinline__ void chacha_tile(uint32_t tb, const KeyRow* __restric
       const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
       const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,    \
       const uint2* __restrict__ hpm) {                                                                    \
-    chacha_tile<true, SINGLE>(blockIdx.x, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm); \
+    chacha_tile<true, SINGLE>(blockIdx.x, threadIdx.x, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm); \
   }
 MQ_CHACHA_KERNELS(mq_chacha_seal_kernel, mq_chacha_open_kernel, false)
 MQ_CHACHA_KERNELS(mq_chacha_seal1_kernel, mq_chacha_open1_kernel, true)
@@ -607,7 +611,11 @@ __device__ __forceinline__ void chacha_list(const KeyRow* __restrict__ kt, uint3
   for (;;) {
     const uint32_t count = n_dev ? *n_dev : n;
     if (tb * W * kPktsPerTile >= count) break;  // workgroup-uniform
-    chacha_tile<OPEN, SINGLE>(tb, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm);
+    uint32_t tid = threadIdx.x;
+    // open: an opaque copy per tile (chacha_tile) — 10 spilled VGPRs to 2; seal spills more with it
+    // (9 to 24), so it keeps the plain index there
+    if (OPEN) asm volatile("" : "+v"(tid));
+    chacha_tile<OPEN, SINGLE>(tb, tid, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm);
     __syncthreads();  // every wave is done with the tile and its scratch
     if (threadIdx.x == 0) *next_slot = sched ? gridDim.x + pend : tb + gridDim.x;
     __syncthreads();
@@ -823,7 +831,11 @@ hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_
     if (e != hipSuccess) return e;
   }
   const uint32_t blocks = (tiles + kCcWaves - 1) / kCcWaves;
-  if (index) {
+  static const bool persistent = [] {  // MQ_CC_LIST=0 (diagnostic): lists on the one-shot grid (r03)
+    const char* e = std::getenv("MQ_CC_LIST");
+    return !(e && e[0] == '0');
+  }();
+  if (index && persistent) {
     const uint32_t per = (uint32_t)(cus > 0 ? cus : 256) * 4u, grid = blocks < per ? blocks : per;
     if (open)
       hipLaunchKernelGGL(mq_chacha_open_list_kernel, dim3(grid), dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kt,

@@ -331,93 +331,105 @@ extern "C" __global__ __launch_bounds__(256) void mq_recv_gather_kernel(const ui
 // nothing new is attempted; the last walk (`final`) marks what is still unresolved DEFERRED.
 enum : uint8_t { kNone = 0, kOk1 = 1, kOk0 = 2, kFail = 3 };
 
-// What a walk reads of one packet: its record, its header-protection values, the inputs of its
-// last attempt and that attempt's outcome
-struct WalkEnt {
-  RecvWork w;
-  RecvPlan p, t;
-  uint32_t i;
-  uint8_t o;
+// A connection per wave (r04). The wave loads the inputs of its next 64 packets together (lane q:
+// packet k0 + q of the run, contiguous in sorted order) and decides them IN PARALLEL against the
+// state at the chunk's start: every lane decodes its PN with that largest PN, takes its decision and
+// outcome, then a per-level exclusive prefix max over the lanes gives the largest PN each packet
+// really follows (only opened packets raise it, recv.rs:239-247) and the lanes decide again with
+// it. The chunk is exact when every PN comes out the same (induction over the lanes: same PNs, same
+// statuses, so the same prefix max) and no packet confirms a key update (the only other state
+// change, keys.rs:532-583). Otherwise — a PN window crossing or a rotation in the chunk — the
+// wave's first lane replays the chunk in arrival order from LDS, as the sequential reference does.
+// Then every lane writes its packet's descriptors, attempt and output record. r03 walked one
+// packet per lane-step straight from memory (372 us per walk of 2^20 packets over 4096
+// connections, three walks per batch); r04's first version, a 16-lane group per connection whose
+// first lane replayed every packet, still took 285-310 us (profiles/r04j_kernel_trace_recv.csv):
+// ~600 single-lane instructions per packet.
+struct WalkIn {      // 32 B: the state-dependent decision's inputs
+  uint64_t tpn;      // last attempt: pn, rows, generation (tried[k]); o = its outcome
+  uint32_t trow, tretry;
+  uint32_t trunc;
+  uint8_t pn_len, phase, level, pre;
+  uint8_t o, tgen, pad0, pad1;
+  uint32_t pad2;
 };
+struct WalkOut {     // 32 B: the decision
+  uint64_t pn, lbefore;
+  uint32_t row, retry;
+  uint8_t st, gen, pgen, mode;  // mode: 0 no AEAD, 1 (re)attempt, 2 hand to the re-seal pass
+  uint32_t pad;
+};
+constexpr uint32_t kWalkThreads = 256, kWalkConns = kWalkThreads / kWave;
 
-// one packet of a connection's run, in arrival order (the sequential reference's decision, the
-// attempt to make, the packet's record): k = its sorted position (attempt, descriptors), e.i = its
-// arrival index (the output record)
-__device__ __forceinline__ void walk_one(ConnState& s, const mq_conn_recv& c, uint32_t n_rows, const WalkEnt& e,
-                                         uint32_t k, RecvPlan* __restrict__ tried, mq_pkt_desc* __restrict__ d1,
-                                         mq_pkt_desc* __restrict__ d2, mq_recv_pkt* __restrict__ out,
-                                         uint32_t& new_attempts, int final_walk) {
-  const uint32_t i = e.i;
-  const RecvWork w = e.w;
-  RecvPlan p = e.p;
+// the sequential reference's decision for one packet in state s, and its outcome from what is known
+// (the state is advanced by the caller: raise_largest / advance when st == MQ_OK)
+__device__ __forceinline__ WalkOut walk_eval(const ConnState& s, const mq_conn_recv& c, uint32_t n_rows,
+                                             const WalkIn& in, int final_walk) {
+  RecvWork w;
+  w.level = in.level;
+  w.pre = in.pre;
+  RecvPlan p;
+  p.trunc = in.trunc;
+  p.pn_len = in.pn_len;
+  p.phase = in.phase;
   decide(s, w, c, n_rows, p);
-  mq_pkt_desc a;
-  a.offset = w.offset; a.len = w.len; a.key_id = kNoRow; a.pn = p.lbefore; a.pn_offset = w.pn_off;
-  a.pn_len = 0; a.flags = w.level != MQ_LEVEL_APPLICATION ? MQ_PKT_LONG_HEADER : 0; a.reserved = 0;
-  mq_pkt_desc b = a;
-  uint8_t st = p.status, gen = p.gen;
-  RecvPlan used = p;
+  WalkOut r;
+  r.pn = p.pn; r.lbefore = p.lbefore; r.row = p.row; r.retry = p.retry; r.pgen = p.gen; r.pad = 0;
+  uint8_t st = p.status, gen = p.gen, mode = 0;
   if (p.status == kPending) {
-    const uint8_t o = e.o;
-    const RecvPlan t = e.t;
-    const bool same = o != kNone && t.pn == p.pn && t.row == p.row && t.retry == p.retry && t.gen == p.gen;
-    if (o == kOk1 || o == kOk0) {
+    const bool same = in.o != kNone && in.tpn == p.pn && in.trow == p.row && in.tretry == p.retry && in.tgen == p.gen;
+    if (in.o == kOk1 || in.o == kOk0) {
       // Opened (its bytes are already plaintext, so it is never attempted again). A packet
-      // authenticates under exactly one (key row, pn), the one that opened it, so the
-      // reference's outcome for its own decision p follows: p.row first, then p.retry
-      // (recv.rs:412-474); for a next-generation open the rotation is p's (gen 2).
-      const uint32_t opened = o == kOk1 ? t.row : t.retry;
-      used = p;
-      if (t.pn == p.pn && opened == p.row) {
+      // authenticates under exactly one (key row, pn), the one that opened it, so the reference's
+      // outcome for its own decision p follows: p.row first, then p.retry (recv.rs:412-474); for
+      // a next-generation open the rotation is p's (gen 2).
+      const uint32_t opened = in.o == kOk1 ? in.trow : in.tretry;
+      if (in.tpn == p.pn && opened == p.row) {
         st = MQ_OK;
-        gen = p.gen;
-      } else if (t.pn == p.pn && opened == p.retry) {
+      } else if (in.tpn == p.pn && opened == p.retry) {
         st = MQ_OK;
         gen = 0;
       } else {
         // the reference's keys fail on it: Error::Crypto. It opened under the speculation's
         // inputs, so its bytes hold plaintext; the final walk hands it to the re-seal pass
-        // (mq_host.cpp) with the key row and PN that opened it, which brings back ciphertext,
-        // tag and masked header exactly as received — the reference never touches the
-        // datagram of a failed packet (it opens a 2048-B copy, recv.rs:356-361)
+        // (mq_host.cpp) with the key row and PN that opened it, which brings back ciphertext, tag
+        // and masked header exactly as received — the reference never touches the datagram of a
+        // failed packet (it opens a 2048-B copy, recv.rs:356-361)
         st = MQ_ERR_CRYPTO;
-        if (final_walk) {
-          a.key_id = opened;
-          a.pn = t.pn;
-          a.pn_len = t.pn_len;
-        }
+        if (final_walk) mode = 2;
       }
     } else if (same) {  // failed with exactly the reference's inputs
       st = MQ_ERR_CRYPTO;
     } else if (final_walk) {
       st = MQ_ERR_DEFERRED;
     } else {  // (re)attempt with the inputs the reference would use; speculate it opens
-      tried[k] = p;
-      a.key_id = p.row;
-      b.key_id = p.retry;
-      ++new_attempts;
+      mode = 1;
       st = MQ_OK;
     }
   }
-  d1[k] = a;
-  d2[k] = b;
-  mq_recv_pkt r;
-  r.offset = w.offset; r.len = w.len; r.dgram = w.dgram; r.level = w.level; r.status = st;
-  r.pn = st == MQ_OK ? used.pn : 0;
-  r.payload_offset = st == MQ_OK ? (uint16_t)(w.pn_off + used.pn_len) : 0;
-  r.key_gen = (w.level == MQ_LEVEL_APPLICATION && st == MQ_OK) ? gen : 0;
-  r.reserved[0] = r.reserved[1] = r.reserved[2] = 0;
-  out[i] = r;
-  if (st == MQ_OK) advance(s, w, used, gen);
+  r.st = st;
+  r.gen = gen;
+  r.mode = mode;
+  return r;
 }
 
-// A connection per group of kWalkGroup lanes (r04): the group loads the inputs of its next
-// kWalkGroup packets together (one packet per lane, a contiguous piece of the run in sorted
-// order), then the group's first lane walks them from LDS. r03 walked one packet per lane-step
-// straight from memory in arrival-order arrays (a scattered round trip per packet, 372 us per walk
-// of 2^20 packets over 4096 connections, three walks per batch: profiles/r04g_kernel_stats_recv.csv;
-// 351 us with the groups but still arrival-order arrays, r04h).
-constexpr uint32_t kWalkGroup = 16, kWalkThreads = 256, kWalkConns = kWalkThreads / kWalkGroup;
+__device__ __forceinline__ uint64_t shfl_up_u64(uint64_t x, int d) {
+  const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)x, d, kWave), hi = (uint32_t)__shfl_up((int)(uint32_t)(x >> 32), d, kWave);
+  return (uint64_t)hi << 32 | lo;
+}
+// exclusive prefix max over the wave's lanes (lane 0: 0) and the wave's total max
+__device__ __forceinline__ uint64_t excl_max_u64(uint64_t v, uint32_t lane, uint64_t& total) {
+  uint64_t x = v;
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const uint64_t y = shfl_up_u64(x, d);
+    if (lane >= (uint32_t)d) x = x > y ? x : y;
+  }
+  total = (uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), kWave - 1) << 32 |
+          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, kWave - 1);
+  const uint64_t e = shfl_up_u64(x, 1);
+  return lane == 0 ? 0ull : e;
+}
 
 extern "C" __global__ __launch_bounds__(kWalkThreads) void mq_recv_walk_kernel(
     const mq_conn_recv* __restrict__ conn0, mq_conn_recv* __restrict__ conns, uint32_t n_conns,
@@ -425,45 +437,130 @@ extern "C" __global__ __launch_bounds__(kWalkThreads) void mq_recv_walk_kernel(
     const uint32_t* __restrict__ seg_hi, const RecvPlan* __restrict__ hdr, uint32_t n_rows,
     RecvPlan* __restrict__ tried, const uint8_t* __restrict__ outcome, mq_pkt_desc* __restrict__ d1,
     mq_pkt_desc* __restrict__ d2, mq_recv_pkt* __restrict__ out, uint32_t* __restrict__ attempts, int final_walk) {
-  __shared__ WalkEnt s_e[kWalkThreads];
-  const uint32_t g = threadIdx.x / kWalkGroup, q = threadIdx.x % kWalkGroup;
-  const uint32_t ci = blockIdx.x * kWalkConns + g;
-  const bool live = ci < n_conns;
-  const uint32_t lo = live ? seg_lo[ci] : 0u, hi = live ? seg_hi[ci] : 0u;
-  mq_conn_recv c{};
-  ConnState s{};
-  if (live && q == 0) {
-    c = conn0[ci];
-    s = load_state(c);
-  }
+  __shared__ WalkIn s_in[kWalkThreads];
+  __shared__ WalkOut s_out[kWalkThreads];
+  const uint32_t wv = threadIdx.x / kWave, q = threadIdx.x % kWave;
+  const uint32_t ci = blockIdx.x * kWalkConns + wv;
+  if (ci >= n_conns) return;  // wave-uniform; the kernel has no workgroup barrier
+  const uint32_t lo = seg_lo[ci], hi = seg_hi[ci];
+  const mq_conn_recv c = conn0[ci];  // every lane: the state is kept wave-uniform
+  ConnState s = load_state(c);
   uint32_t new_attempts = 0;
-  WalkEnt* ent = s_e + g * kWalkGroup;
-  for (uint32_t k0 = lo;; k0 += kWalkGroup) {
-    const bool act = k0 < hi;
-    if (!wave_any(act)) break;  // the wave's groups have runs of different lengths
-    const uint32_t m = act ? min(kWalkGroup, hi - k0) : 0u;
-    if (q < m) {  // work, hdr, tried, outcome: sorted order
-      const uint32_t k = k0 + q;
-      ent[q].i = svals[k];
-      ent[q].w = work[k];
-      ent[q].p = hdr[k];
-      ent[q].t = tried[k];
-      ent[q].o = outcome[k];
+  WalkIn* sin = s_in + wv * kWave;
+  WalkOut* sout = s_out + wv * kWave;
+  for (uint32_t k0 = lo; k0 < hi; k0 += kWave) {  // wave-uniform
+    const uint32_t m = min((uint32_t)kWave, hi - k0), k = k0 + q;
+    const bool mine = q < m;
+    RecvWork w{};
+    RecvPlan p{}, t{};
+    uint8_t o = kNone;
+    uint32_t i = 0;
+    WalkIn in{};
+    if (mine) {  // work, hdr, tried, outcome: sorted order
+      i = svals[k];
+      w = work[k];
+      p = hdr[k];
+      t = tried[k];
+      o = outcome[k];
+      in.tpn = t.pn; in.trow = t.row; in.tretry = t.retry; in.trunc = p.trunc;
+      in.pn_len = p.pn_len; in.phase = p.phase; in.level = w.level; in.pre = w.pre;
+      in.o = o; in.tgen = t.gen;
     }
-    wave_sync();
-    if (q == 0)
-      for (uint32_t k = 0; k < m; ++k)
-        walk_one(s, c, n_rows, ent[k], k0 + k, tried, d1, d2, out, new_attempts, final_walk);
-    wave_sync();  // the entries are read before the next round overwrites them
+    // parallel decision against the chunk-start state, then against each packet's true largest PN
+    WalkOut r = walk_eval(s, c, n_rows, in, final_walk);
+    bool ok = mine && r.st == MQ_OK;
+    const bool rot = ok && w.level == MQ_LEVEL_APPLICATION && r.gen == 2;
+    bool exact = false;
+    if (!wave_any(rot)) {
+      uint64_t tot[3], mx = 0;
+#pragma unroll
+      for (uint32_t l = 0; l < 3; ++l) {
+        const uint64_t e = excl_max_u64(ok && w.level == l ? r.pn : 0ull, q, tot[l]);
+        if (w.level == l) mx = e;
+      }
+      ConnState sx = s;
+#pragma unroll
+      for (uint32_t l = 0; l < 3; ++l)
+        if (w.level == l && mx > sx.largest[l]) sx.largest[l] = mx;
+      const WalkOut r2 = walk_eval(sx, c, n_rows, in, final_walk);
+      exact = !wave_any(mine && (r2.pn != r.pn || r2.st != r.st));
+      if (exact) {
+        r = r2;
+#pragma unroll
+        for (uint32_t l = 0; l < 3; ++l)
+          if (tot[l] > s.largest[l]) s.largest[l] = tot[l];
+      }
+    }
+    if (!exact) {  // the sequential replay of the chunk by lane 0, from LDS
+      if (mine) sin[q] = in;
+      wave_sync();
+      if (q == 0) {
+        for (uint32_t x = 0; x < m; ++x) {
+          const WalkIn e = sin[x];
+          const WalkOut rx = walk_eval(s, c, n_rows, e, final_walk);
+          sout[x] = rx;
+          if (rx.st == MQ_OK) {
+            RecvWork wx;
+            wx.level = e.level;
+            RecvPlan px;
+            px.pn = rx.pn;
+            advance(s, wx, px, rx.gen);
+          }
+        }
+      }
+      wave_sync();
+      if (mine) r = sout[q];
+      // lane 0's state to every lane
+#pragma unroll
+      for (uint32_t l = 0; l < 3; ++l) {
+        s.largest[l] = (uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(s.largest[l] >> 32)) << 32 |
+                       (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)s.largest[l]);
+        s.row[l] = (uint32_t)__builtin_amdgcn_readfirstlane((int)s.row[l]);
+      }
+      s.phase = (uint8_t)__builtin_amdgcn_readfirstlane((int)s.phase);
+      s.flags = (uint8_t)__builtin_amdgcn_readfirstlane((int)s.flags);
+      s.updates = (uint8_t)__builtin_amdgcn_readfirstlane((int)s.updates);
+      wave_sync();  // the entries are read before the next round overwrites them
+    }
+    bool att = false;
+    if (mine) {
+      mq_pkt_desc a;
+      a.offset = w.offset; a.len = w.len; a.key_id = kNoRow; a.pn = r.lbefore; a.pn_offset = w.pn_off;
+      a.pn_len = 0; a.flags = w.level != MQ_LEVEL_APPLICATION ? MQ_PKT_LONG_HEADER : 0; a.reserved = 0;
+      mq_pkt_desc b = a;
+      if (r.mode == 1) {
+        RecvPlan tp;
+        tp.pn = r.pn; tp.lbefore = r.lbefore; tp.row = r.row; tp.retry = r.retry; tp.trunc = p.trunc;
+        tp.status = kPending; tp.gen = r.pgen; tp.phase = p.phase; tp.pn_len = p.pn_len;
+        tried[k] = tp;
+        a.key_id = r.row;
+        b.key_id = r.retry;
+      } else if (r.mode == 2) {
+        a.key_id = o == kOk1 ? t.row : t.retry;
+        a.pn = t.pn;
+        a.pn_len = t.pn_len;
+      }
+      d1[k] = a;
+      d2[k] = b;
+      mq_recv_pkt rec;
+      rec.offset = w.offset; rec.len = w.len; rec.dgram = w.dgram; rec.level = w.level; rec.status = r.st;
+      rec.pn = r.st == MQ_OK ? r.pn : 0;
+      rec.payload_offset = r.st == MQ_OK ? (uint16_t)(w.pn_off + p.pn_len) : 0;
+      rec.key_gen = (w.level == MQ_LEVEL_APPLICATION && r.st == MQ_OK) ? r.gen : 0;
+      rec.reserved[0] = rec.reserved[1] = rec.reserved[2] = 0;
+      out[i] = rec;
+      att = r.mode == 1;
+    }
+    new_attempts += (uint32_t)__popcll(__ballot(att));
   }
-  if (!live || q != 0) return;
+  if (q != 0) return;
   if (new_attempts) atomicAdd(attempts, new_attempts);
-  mq_conn_recv o = c;
-  for (int l = 0; l < 3; ++l) { o.largest_pn[l] = s.largest[l]; o.app_row[l] = s.row[l]; }
-  o.key_phase = s.phase;
-  o.flags = s.flags;
-  o.key_updates = s.updates;
-  conns[ci] = o;
+  mq_conn_recv u = c;
+  for (int l = 0; l < 3; ++l) { u.largest_pn[l] = s.largest[l]; u.app_row[l] = s.row[l]; }
+  u.key_phase = s.phase;
+  u.flags = s.flags;
+  u.key_updates = s.updates;
+  conns[ci] = u;
 }
 
 // retry pass descriptors: only 1-RTT packets whose current keys failed (recv.rs:441-474)

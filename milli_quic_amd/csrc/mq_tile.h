@@ -362,8 +362,8 @@ __device__ __forceinline__ bool tile_ctx(uint32_t tile_id, const KeyRow* __restr
                                          uint64_t arena_len, const mq_pkt_desc* __restrict__ desc, uint32_t n,
                                          const uint32_t* __restrict__ index, const uint32_t* __restrict__ n_dev,
                                          const uint2* __restrict__ hpm, const TilePrefetch& pf, PktCtx& c,
-                                         const KeyRow*& row) {
-  const int lane = threadIdx.x & (kWave - 1), p = lane / kLanesPerPkt;
+                                         const KeyRow*& row, uint32_t tid = threadIdx.x) {
+  const int lane = tid & (kWave - 1), p = lane / kLanesPerPkt;
   const uint32_t count = n_dev ? *n_dev : n;
   const uint32_t tile0 = tile_id * kPktsPerTile;
   if (tile0 >= count) return false;  // wave-uniform

@@ -84,7 +84,7 @@ def test_protect_suite_hint_vs_oracle(orc, seed, hint):
     assert (g_st == o_st).all(), np.nonzero(g_st != o_st)
     assert (g_ln == o_ln).all(), np.nonzero(g_ln != o_ln)
     assert g_out.tobytes() == o_out.tobytes()
-    assert (o_st == 0).sum() > 1000
+    assert (o_st == 0).sum() > (1000 if hint == _lib.MQ_SUITE_CHACHA20 else 100)
 
 
 def test_protect_fused_matches_two_kernel(monkeypatch):
