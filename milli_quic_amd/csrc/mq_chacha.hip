@@ -594,6 +594,7 @@ MQ_CHACHA_KERNELS(mq_chacha_seal1_kernel, mq_chacha_open1_kernel, true)
 // next is issued when a block starts and read when it ends, so nobody waits on it), or, without a
 // slot, by stride. (Flat batches keep the one-shot grid: a persistent grid measured 10 % slower on
 // config B, r02 — identical waves stay in phase and their staging waits line up.)
+// SINGLE: the list's packets share one key row (kt points at it)
 template <bool OPEN, bool SINGLE>
 __device__ __forceinline__ void chacha_list(const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena,
                                             uint64_t arena_len, const mq_pkt_desc* __restrict__ desc, uint32_t n,
@@ -615,7 +616,11 @@ __device__ __forceinline__ void chacha_list(const KeyRow* __restrict__ kt, uint3
     // open: an opaque copy per tile (chacha_tile) — 10 spilled VGPRs to 2; seal spills more with it
     // (9 to 24), so it keeps the plain index there
     if (OPEN) asm volatile("" : "+v"(tid));
-    chacha_tile<OPEN, SINGLE>(tb, tid, kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm);
+    // single-key seal: the key table pointer opaque per tile too, so its key words are loaded per
+    // tile rather than held in SGPRs across the loop (spilled 29 VGPRs)
+    const KeyRow* ktt = kt;
+    if (SINGLE && !OPEN) asm volatile("" : "+s"(ktt));
+    chacha_tile<OPEN, SINGLE>(tb, tid, ktt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm);
     __syncthreads();  // every wave is done with the tile and its scratch
     if (threadIdx.x == 0) *next_slot = sched ? gridDim.x + pend : tb + gridDim.x;
     __syncthreads();
@@ -627,19 +632,25 @@ __device__ __forceinline__ void chacha_list(const KeyRow* __restrict__ kt, uint3
   __syncthreads();
   sched_done(sched);
 }
-extern "C" __global__ __launch_bounds__(64 * kCcWaves) __attribute__((amdgpu_waves_per_eu(4))) void mq_chacha_seal_list_kernel(
-    const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
-    const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,
-    const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint32_t* __restrict__ sched) {
-  chacha_list<false, false>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr, nullptr, sched);
-}
-extern "C" __global__ __launch_bounds__(64 * kCcWaves) __attribute__((amdgpu_waves_per_eu(4))) void mq_chacha_open_list_kernel(
-    const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
-    const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,
-    const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,
-    const uint2* __restrict__ hpm, uint32_t* __restrict__ sched) {
-  chacha_list<true, false>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm, sched);
-}
+// The "1" list kernels: every packet of the list is on one key row (the key table has a single
+// non-AES row, mq_host.cpp), kt points at it, so key material is wave-uniform, in SGPRs, as in the
+// flat single-key kernels.
+#define MQ_CHACHA_LIST_KERNELS(NAME_SEAL, NAME_OPEN, SINGLE)                                                \
+  extern "C" __global__ __launch_bounds__(64 * kCcWaves) __attribute__((amdgpu_waves_per_eu(4))) void NAME_SEAL( \
+      const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,     \
+      const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,                \
+      const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint32_t* __restrict__ sched) {    \
+    chacha_list<false, SINGLE>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr, nullptr, sched); \
+  }                                                                                                        \
+  extern "C" __global__ __launch_bounds__(64 * kCcWaves) __attribute__((amdgpu_waves_per_eu(4))) void NAME_OPEN( \
+      const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,     \
+      const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,                \
+      const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,     \
+      const uint2* __restrict__ hpm, uint32_t* __restrict__ sched) {                                       \
+    chacha_list<true, SINGLE>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm, sched); \
+  }
+MQ_CHACHA_LIST_KERNELS(mq_chacha_seal_list_kernel, mq_chacha_open_list_kernel, false)
+MQ_CHACHA_LIST_KERNELS(mq_chacha_seal_list1_kernel, mq_chacha_open_list1_kernel, true)
 
 // ---- fused send composite (mq_batch_protect with the ChaCha20 suite hint, r04) -----------------
 // build + seal + header protection in one pass: the tile's eight packets are BUILT from their
@@ -821,7 +832,8 @@ __global__ __launch_bounds__(256) void mq_chacha_open_hp_kernel(
 hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena,
                             uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
                             const uint32_t* index, const uint32_t* n_dev, uint8_t* status,
-                            uint64_t* pn_out, uint2* hpm, bool own_hp, hipStream_t s, int cus, uint32_t* sched) {
+                            uint64_t* pn_out, uint2* hpm, bool own_hp, hipStream_t s, int cus, uint32_t* sched,
+                            int64_t single_row) {
   const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
   if (tiles == 0) return hipSuccess;
   if (open && hpm && own_hp) {  // !own_hp: mq_launch_mixed_hp covers both suites' lists
@@ -837,12 +849,17 @@ hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_
   }();
   if (index && persistent) {
     const uint32_t per = (uint32_t)(cus > 0 ? cus : 256) * 4u, grid = blocks < per ? blocks : per;
+    // single_row >= 0: every packet of the list is on that row (the single-key list kernels)
+    const bool one = single_row >= 0 && (uint64_t)single_row < n_rows;
+    const KeyRow* kl = one ? kt + single_row : kt;
     if (open)
-      hipLaunchKernelGGL(mq_chacha_open_list_kernel, dim3(grid), dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kt,
-                         n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm, sched);
+      hipLaunchKernelGGL(one ? mq_chacha_open_list1_kernel : mq_chacha_open_list_kernel, dim3(grid),
+                         dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kl, n_rows, arena, arena_len, desc, n, index,
+                         n_dev, status, pn_out, hpm, sched);
     else
-      hipLaunchKernelGGL(mq_chacha_seal_list_kernel, dim3(grid), dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kt,
-                         n_rows, arena, arena_len, desc, n, index, n_dev, status, sched);
+      hipLaunchKernelGGL(one ? mq_chacha_seal_list1_kernel : mq_chacha_seal_list_kernel, dim3(grid),
+                         dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kl, n_rows, arena, arena_len, desc, n, index,
+                         n_dev, status, sched);
     return hipGetLastError();
   }
   if (open)

@@ -63,6 +63,7 @@ struct MQRecvPass {
   mq_pkt_desc *d1, *d2;
   uint8_t *st1, *st2;
   void* open_ws;
+  const uint32_t *live1, *live2;  // keyed descriptors of d1 (the last walk) / d2 (the retry kernel)
 };
 
 // ------------------------------------------------------------------------------------------

@@ -25,7 +25,8 @@ using mq::KeyRow;
 hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena,
                             uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
                             const uint32_t* index, const uint32_t* n_dev, uint8_t* status,
-                            uint64_t* pn_out, uint2* hpm, bool own_hp, hipStream_t s, int cus, uint32_t* sched);
+                            uint64_t* pn_out, uint2* hpm, bool own_hp, hipStream_t s, int cus, uint32_t* sched,
+                            int64_t single_row);
 hipError_t mq_launch_chacha_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t* key_ids,
                                const uint8_t* samples, uint8_t* masks, uint32_t n, hipStream_t s);
 hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena,
@@ -40,7 +41,8 @@ hipError_t mq_launch_mixed_open_hp(const KeyRow* kt, uint32_t n_rows, const uint
 hipError_t mq_launch_aes_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t* key_ids,
                             const uint8_t* samples, uint8_t* masks, uint32_t n, hipStream_t s);
 hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_desc* desc, uint32_t n,
-                               uint32_t* list, uint32_t* hist, uint32_t* counts, hipStream_t s, bool skip_unkeyed);
+                               uint32_t* list, uint32_t* hist, uint32_t* counts, hipStream_t s, bool skip_unkeyed,
+                               const uint32_t* live);
 size_t mq_partition_workspace(uint32_t n);
 void mq_partition_layout(uint32_t n, size_t* hist_off, size_t* counts_off);
 uint32_t mq_partition_list_cap(uint32_t n);
@@ -464,7 +466,7 @@ int run_one(Scratch& sc, const KeyRow& row, const uint8_t* aad, uint32_t aad_len
   // protection pass to launch (own_hp false)
   hipError_t e = row.suite == MQ_SUITE_CHACHA20
                      ? mq_launch_chacha(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, st, pn, nullptr, false, sc.stream,
-                                        0, nullptr)
+                                        0, nullptr, -1)
                      : mq_launch_aes(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, nullptr, st, pn, nullptr, false,
                                      sc.stream, sc.stream, devices().cus(sc.device), nullptr, nullptr, nullptr);
   if (e != hipSuccess) return MQ_ERR_HIP;
@@ -533,7 +535,33 @@ struct mq_keytable {
   KeyRow* dev = nullptr;
   uint32_t rows = 0;
   int device = -1;  // where the rows live; every batch call on this table runs there
+  // host view of the rows' suites (as last written by mq_keytable_update; a device-side write —
+  // mq_batch_derive_initial — only turns rows into AES-128-GCM ones, so the count of non-AES rows
+  // is never underestimated): a table with ONE non-AES row puts every packet of a mixed batch's
+  // second list on that row, and the ChaCha20 list kernels take the single-key path
+  std::vector<uint8_t> suite;
+  uint32_t non_aes = 0;
+  int64_t single_row() const {
+    if (non_aes != 1) return -1;
+    for (uint32_t r = 0; r < rows; ++r)
+      if (suite[r] != MQ_SUITE_AES128GCM) return r;
+    return -1;
+  }
 };
+
+// the host view of rows [first, first + n) after a write (suite_of(i): row first + i's new suite)
+template <class F>
+static void kt_mirror(mq_keytable* kt, uint32_t first, uint32_t n, F suite_of) {
+  if (kt->suite.size() != kt->rows) {
+    kt->suite.assign(kt->rows, 0);
+    kt->non_aes = kt->rows;
+  }
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint8_t o = kt->suite[first + i], v = suite_of(i);
+    kt->non_aes += (v != MQ_SUITE_AES128GCM) - (o != MQ_SUITE_AES128GCM);
+    kt->suite[first + i] = v;
+  }
+}
 
 extern "C" {
 
@@ -824,6 +852,7 @@ int mq_keytable_update(mq_keytable* kt, uint32_t first_row, const mq_key_materia
   if (!g.ok()) return MQ_ERR_NO_DEVICE;
   if (hipMemcpy(kt->dev + first_row, host.data(), sizeof(KeyRow) * n_rows, hipMemcpyHostToDevice) != hipSuccess)
     return MQ_ERR_HIP;
+  kt_mirror(kt, first_row, n_rows, [&](uint32_t i) { return (uint8_t)host[i].suite; });
   return MQ_OK;
 }
 
@@ -843,10 +872,14 @@ static size_t ws_align(size_t b) { return (b + 255) & ~(size_t)255; }
 size_t mq_batch_workspace_size(uint32_t n) { return ws_align(8 * (size_t)n) + mq_partition_workspace(n); }
 
 // recv_pass (mq_batch_recv's AEAD passes): descriptors without a valid key row are skipped —
-// no status is written for them; the receive composite reads only what it attempted
+// no status is written for them; the receive composite reads only what it attempted. live (receive
+// passes): device word with the pass's number of keyed descriptors, 0 = the partition publishes
+// empty lists at once (mq_partition.hip). hpm_ready: the open pre-pass values are already in the
+// workspace (the receive walk writes them), so no header-protection pre-pass runs.
 static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t arena_len,
                  const mq_pkt_desc* desc, uint32_t n, uint8_t* status, uint64_t* pn_out,
-                 uint32_t suite_hint, void* workspace, void* stream, bool recv_pass = false) {
+                 uint32_t suite_hint, void* workspace, void* stream, bool recv_pass = false,
+                 const uint32_t* live = nullptr, bool hpm_ready = false) {
   if (!kt || (n && (!arena || !desc || !status))) return MQ_ERR_INVALID_ARG;
   if (((uintptr_t)arena & 15) != 0) return MQ_ERR_INVALID_ARG;  // 16-B staging chunks
   DeviceGuard g(kt->device);  // the table's device; `stream` must belong to it
@@ -860,7 +893,7 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
   uint2* hpm = (open && ws) ? (uint2*)ws : nullptr;
   if (suite_hint == MQ_SUITE_CHACHA20) {
     e = mq_launch_chacha(open, kt->dev, kt->rows, arena, arena_len, desc, n, nullptr, nullptr, status, pn_out, hpm, true,
-                         s, cus, nullptr);
+                         s, cus, nullptr, -1);
   } else if (suite_hint == MQ_SUITE_AES128GCM && (kt->rows == 1 || !ws || n > (1u << 30))) {
     e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, n, nullptr, nullptr, nullptr, status, pn_out,
                       hpm, true, s, s, cus, nullptr, sched_slot(kt->device, s), nullptr);
@@ -880,12 +913,13 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
     uint32_t* counts = (uint32_t*)(pw + counts_off);
     // list mode: the grids cover the list capacity; the kernels read the real lengths from counts
     const uint32_t cap = mq_partition_list_cap(n);
-    e = mq_launch_partition(kt->dev, kt->rows, desc, n, list, hist, counts, s, recv_pass);
+    e = mq_launch_partition(kt->dev, kt->rows, desc, n, list, hist, counts, s, recv_pass, live);
     // open: one header-protection pre-pass over the whole batch in descriptor order, both suites,
     // before the tiles (seal needs none: the tiles mask their own packets). r03f ran it on a side
     // stream beside the partition: no gain (E open 1.279 -> 1.280 ms), its blocks delayed the
     // partition's single-workgroup scan (27 -> 85 us)
-    if (e == hipSuccess && open && hpm) e = mq_launch_mixed_open_hp(kt->dev, kt->rows, arena, arena_len, desc, n, hpm, s);
+    if (e == hipSuccess && open && hpm && !hpm_ready)
+      e = mq_launch_mixed_open_hp(kt->dev, kt->rows, arena, arena_len, desc, n, hpm, s);
     if (e != hipSuccess) return MQ_ERR_HIP;
     // The hot AES key's segment (counts + 2: its row and segment length, list 0's front;
     // single-key kernel) runs on a side stream beside the other AES keys' tiles on s: each CU moves
@@ -911,7 +945,7 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
                         pn_out, hpm, false, s_list1, s_list1, cus, nullptr, sched_slot(kt->device, s_list1), nullptr);
     else if (e == hipSuccess)
       e = mq_launch_chacha(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list + cap, counts + 1, status,
-                           pn_out, hpm, false, s_list1, cus, sched_slot(kt->device, s_list1));
+                           pn_out, hpm, false, s_list1, cus, sched_slot(kt->device, s_list1), kt->single_row());
     // join even after a failed launch, so no side stream runs ahead of s
     if (!fork.join() && e == hipSuccess) e = hipErrorUnknown;
   } else {
@@ -987,6 +1021,9 @@ int mq_batch_derive_initial(mq_keytable* kt, uint32_t first_row, const uint8_t* 
   if ((uint64_t)first_row + 2ull * n > kt->rows) return MQ_ERR_INVALID_ARG;
   DeviceGuard g(kt->device);
   if (!g.ok()) return MQ_ERR_NO_DEVICE;
+  // the derived rows are AES-128-GCM, or suite 0 for an over-long DCID — unknown here, so the host
+  // view counts them as non-AES (the single-key list path only ever needs a table it is sure of)
+  kt_mirror(kt, first_row, 2 * n, [](uint32_t) { return (uint8_t)0; });
   return mq_launch_derive_initial(derive_consts(), dcids, dcid_lens, n, kt->dev + first_row, km_out, status,
                                   (hipStream_t)stream) == hipSuccess
              ? MQ_OK
@@ -1080,12 +1117,16 @@ int mq_batch_recv(const mq_keytable* kt, mq_conn_recv* conns, uint32_t n_conns, 
   // walk -> AEAD passes -> walk ...: the first walk speculates that every packet opens, later walks
   // re-attempt what the real outcomes changed (rare: after a failed packet); the last walk defers
   // anything still unresolved. Fixed rounds keep the call asynchronous (no host read-back).
+  // Passes with nothing keyed (live word 0: in a batch where every packet opens, everything after
+  // the first pass) cost a few empty launches; the walks write the open pre-pass values.
   constexpr int kRounds = 2;
   for (int round = 0; round < kRounds; ++round) {
-    int r = batch(true, kt, arena, arena_len, p.d1, max_pkts, p.st1, nullptr, MQ_SUITE_MIXED, p.open_ws, stream, true);
+    int r = batch(true, kt, arena, arena_len, p.d1, max_pkts, p.st1, nullptr, MQ_SUITE_MIXED, p.open_ws, stream, true,
+                  p.live1, true);
     if (r != MQ_OK) return r;
     if (mq_recv_retry(n_dgrams, max_pkts, n_conns, workspace, open_ws, s) != hipSuccess) return MQ_ERR_HIP;
-    r = batch(true, kt, arena, arena_len, p.d2, max_pkts, p.st2, nullptr, MQ_SUITE_MIXED, p.open_ws, stream, true);
+    r = batch(true, kt, arena, arena_len, p.d2, max_pkts, p.st2, nullptr, MQ_SUITE_MIXED, p.open_ws, stream, true,
+              p.live2, true);
     if (r != MQ_OK) return r;
     if (mq_recv_outcomes(n_dgrams, max_pkts, n_conns, workspace, open_ws, s) != hipSuccess) return MQ_ERR_HIP;
     if (mq_recv_walk(kt->dev, kt->rows, conns, n_conns, n_dgrams, max_pkts, pkts, workspace, open_ws,
@@ -1096,7 +1137,8 @@ int mq_batch_recv(const mq_keytable* kt, mq_conn_recv* conns, uint32_t n_conns, 
   // reference's (MQ_ERR_CRYPTO) holds plaintext; the final walk left its opening key row and PN in
   // d1 (every other entry has no key row and is skipped), and sealing it again under them restores
   // its bytes as received. Statuses land in the st1 scratch.
-  return batch(false, kt, arena, arena_len, p.d1, max_pkts, p.st1, nullptr, MQ_SUITE_MIXED, p.open_ws, stream, true);
+  return batch(false, kt, arena, arena_len, p.d1, max_pkts, p.st1, nullptr, MQ_SUITE_MIXED, p.open_ws, stream, true,
+               p.live1);
 }
 
 // ---- TLS 1.3 records (tcp_tls/record.rs:88-143, connection.rs:546-600) -----------------------

@@ -47,6 +47,11 @@ constexpr uint32_t kNoKey = 0xFFFFFFFFu;
 constexpr uint32_t kKeyClasses = 16;  // keyed layout: per row, min(len / 128, 15), longest first
 // skip_unkeyed (the receive composite's AEAD passes, mq_host.cpp): descriptors without a valid key
 // row are in no list (their statuses are never written; mq_recv.hip reads only attempted ones).
+// live (receive passes, may be null): a device word counting the pass's keyed descriptors; when it
+// is 0 every kernel returns at once and the scan publishes empty lists, so a pass with nothing to
+// open costs a few launches instead of four passes over the batch's descriptors (r04: ~110 us per
+// empty pass, four such passes per receive batch, profiles/r04k2_kernel_trace_recv.csv).
+__device__ __forceinline__ bool pass_empty(const uint32_t* live) { return live && *live == 0; }
 
 // What the partition reads of a descriptor: key row, length, and whether the row is AES-128-GCM.
 // A thread's kPartItems descriptors are fetched together (fields first, then the rows' suites),
@@ -154,7 +159,8 @@ __device__ __forceinline__ uint32_t fold_votes(const uint2* __restrict__ votes, 
 extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_init_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_pkt_desc* __restrict__ desc, uint32_t n,
     uint2* __restrict__ votes, uint32_t nv, uint4* __restrict__ list, uint32_t list_q, uint4* __restrict__ bins,
-    uint32_t bins_q) {
+    uint32_t bins_q, const uint32_t* __restrict__ live) {
+  if (pass_empty(live)) return;
   if (blockIdx.x < nv) {  // block-uniform
     const uint2 v = vote_slice(kt, n_rows, desc, n, blockIdx.x);
     if (threadIdx.x == 0) votes[blockIdx.x] = v;
@@ -170,7 +176,9 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_init_kernel(
 extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_count_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_pkt_desc* __restrict__ desc, uint32_t n,
     uint32_t nblocks, const uint2* __restrict__ votes, uint32_t nv, uint32_t* __restrict__ hot_p,
-    uint32_t* __restrict__ hist, uint32_t* __restrict__ bins, uint32_t skip_unkeyed) {
+    uint32_t* __restrict__ hist, uint32_t* __restrict__ bins, uint32_t skip_unkeyed,
+    const uint32_t* __restrict__ live) {
+  if (pass_empty(live)) return;
   __shared__ uint32_t s_cnt[kClasses];
   PartItem it[kPartItems];
   part_fetch(kt, n_rows, desc, n, it);
@@ -227,7 +235,14 @@ extern "C" __global__ __launch_bounds__(64 * kScanWaves) void mq_part_scan_kerne
                                                                                  uint32_t* __restrict__ seg,
                                                                                  uint32_t* __restrict__ bins,
                                                                                  uint32_t n_rows,
-                                                                                 uint32_t* __restrict__ rowseg) {
+                                                                                 uint32_t* __restrict__ rowseg,
+                                                                                 const uint32_t* __restrict__ live) {
+  if (pass_empty(live)) {  // empty lists: no hot key, no row segments
+    if (threadIdx.x == 0) { counts[0] = 0; counts[1] = 0; counts[2] = kNoKey; counts[3] = 0; }
+    if (rowseg)
+      for (uint32_t r = threadIdx.x; r < n_rows; r += blockDim.x) *(uint2*)(rowseg + 2 * (size_t)r) = make_uint2(0, 0);
+    return;
+  }
   __shared__ uint32_t s_list0;
   __shared__ uint32_t s_tot[kClasses];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -360,7 +375,8 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_scatter_kerne
     const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_pkt_desc* __restrict__ desc, uint32_t n,
     uint32_t nblocks, const uint32_t* __restrict__ hot_p, const uint32_t* __restrict__ hist,
     const uint32_t* __restrict__ seg, uint32_t* __restrict__ list, uint32_t* __restrict__ bins,
-    uint32_t skip_unkeyed) {
+    uint32_t skip_unkeyed, const uint32_t* __restrict__ live) {
+  if (pass_empty(live)) return;
   __shared__ uint32_t s_rank[kClasses];
   PartItem it[kPartItems];
   part_fetch(kt, n_rows, desc, n, it);
@@ -450,7 +466,8 @@ const uint32_t* mq_partition_rowseg(uint32_t n, uint32_t n_rows, const uint32_t*
 }
 
 hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_desc* desc, uint32_t n,
-                               uint32_t* list, uint32_t* hist, uint32_t* counts, hipStream_t s, bool skip_unkeyed) {
+                               uint32_t* list, uint32_t* hist, uint32_t* counts, hipStream_t s, bool skip_unkeyed,
+                               const uint32_t* live) {
   const uint32_t nblocks = (n + kPartBlock - 1) / kPartBlock;
   if (nblocks == 0) return hipMemsetAsync(counts, 0, 4 * sizeof(uint32_t), s);
   const uint32_t cap = mq_partition_list_cap(n);
@@ -465,13 +482,13 @@ hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_d
   const uint32_t S = min(n, kVoteSample), used = (S + kVoteSlice - 1) / kVoteSlice;  // slices with samples
   const uint32_t grid = max(init_blocks, used);
   hipLaunchKernelGGL(mq_part_init_kernel, dim3(grid), dim3(kPartThreads), 0, s, kt, n_rows, desc, n, votes,
-                     max(nv, used), (uint4*)list, list_q, (uint4*)bins, bins_q);
+                     max(nv, used), (uint4*)list, list_q, (uint4*)bins, bins_q, live);
   hipLaunchKernelGGL(mq_part_count_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, kt, n_rows, desc, n,
-                     nblocks, votes, max(nv, used), hot, hist, bins, (uint32_t)skip_unkeyed);
+                     nblocks, votes, max(nv, used), hot, hist, bins, (uint32_t)skip_unkeyed, live);
   hipLaunchKernelGGL(mq_part_scan_kernel, dim3(1), dim3(64 * kScanWaves), 0, s, hist, nblocks, cap, counts, seg,
-                     bins, n_rows, bins ? bins + key_bins(n) : nullptr);
+                     bins, n_rows, bins ? bins + key_bins(n) : nullptr, live);
   hipLaunchKernelGGL(mq_part_scatter_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, kt, n_rows, desc, n,
-                     nblocks, hot, hist, seg, list, bins, (uint32_t)skip_unkeyed);
+                     nblocks, hot, hist, seg, list, bins, (uint32_t)skip_unkeyed, live);
   return hipGetLastError();
 }
 

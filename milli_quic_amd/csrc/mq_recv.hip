@@ -247,6 +247,7 @@ __device__ __forceinline__ void unmask(const RecvWork& w, const uint8_t* arena, 
   p.trunc = trunc;
   p.pn_len = (uint8_t)pn_len;
   p.phase = (b0 >> 2) & 1;
+  p.row = b0;  // header entries carry the unmasked first byte here (the open pre-pass value)
 }
 
 // what the sequential reference decides for one packet in state s: decoded PN and key choice
@@ -289,29 +290,17 @@ __device__ __forceinline__ void advance(ConnState& s, const RecvWork& w, const R
   }
 }
 
-// header-protection removal of every packet from the arena as received (state independent)
-extern "C" __global__ __launch_bounds__(256) void mq_recv_unmask_kernel(const uint8_t* __restrict__ arena,
-                                                                        const RecvWork* __restrict__ work,
-                                                                        const uint2* __restrict__ hpm,
-                                                                        const uint32_t* __restrict__ total,
-                                                                        uint32_t max_pkts, RecvPlan* __restrict__ hdr) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= min(*total, max_pkts)) return;
-  const RecvWork w = work[i];
-  RecvPlan p;
-  p.trunc = 0; p.pn_len = 0; p.phase = 0;
-  if (w.pre == kPending) unmask(w, arena, hpm[i], p);
-  hdr[i] = p;
-}
-
-// Records and header values in connection order (r04): everything after the sort — the walks, the
-// AEAD passes' descriptors and statuses, the outcomes — is indexed by the sorted position k, so a
-// walk reads each connection's run contiguously; only the output records keep arrival order.
+// Records in connection order (r04): everything after the sort — the walks, the AEAD passes'
+// descriptors and statuses, the outcomes — is indexed by the sorted position k, so a walk reads each
+// connection's run contiguously; only the output records keep arrival order. The header-protection
+// removal (state independent) happens here too, straight into connection order (r04: it was a
+// pass of its own in arrival order, 64 us per 2^20 packets, profiles/r04k2_kernel_trace_recv.csv).
 extern "C" __global__ __launch_bounds__(256) void mq_recv_gather_kernel(const uint32_t* __restrict__ total,
                                                                         uint32_t max_pkts,
                                                                         const uint32_t* __restrict__ svals,
                                                                         const RecvWork* __restrict__ work,
-                                                                        const RecvPlan* __restrict__ hdr,
+                                                                        const uint8_t* __restrict__ arena,
+                                                                        const uint2* __restrict__ hpm,
                                                                         RecvWork* __restrict__ work_s,
                                                                         RecvPlan* __restrict__ hdr_s,
                                                                         uint8_t* __restrict__ outcome) {
@@ -320,8 +309,11 @@ extern "C" __global__ __launch_bounds__(256) void mq_recv_gather_kernel(const ui
   outcome[k] = 0;
   if (k >= min(*total, max_pkts)) return;
   const uint32_t i = svals[k];
-  work_s[k] = work[i];
-  hdr_s[k] = hdr[i];
+  const RecvWork w = work[i];
+  RecvPlan p{};
+  if (w.pre == kPending) unmask(w, arena, hpm[i], p);
+  work_s[k] = w;
+  hdr_s[k] = p;
 }
 
 // ---- walk: connections replay their packets in arrival order ---------------------------------------
@@ -436,7 +428,8 @@ extern "C" __global__ __launch_bounds__(kWalkThreads) void mq_recv_walk_kernel(
     const RecvWork* __restrict__ work, const uint32_t* __restrict__ svals, const uint32_t* __restrict__ seg_lo,
     const uint32_t* __restrict__ seg_hi, const RecvPlan* __restrict__ hdr, uint32_t n_rows,
     RecvPlan* __restrict__ tried, const uint8_t* __restrict__ outcome, mq_pkt_desc* __restrict__ d1,
-    mq_pkt_desc* __restrict__ d2, mq_recv_pkt* __restrict__ out, uint32_t* __restrict__ attempts, int final_walk) {
+    mq_pkt_desc* __restrict__ d2, mq_recv_pkt* __restrict__ out, uint32_t* __restrict__ attempts, int final_walk,
+    uint2* __restrict__ hpm) {
   __shared__ WalkIn s_in[kWalkThreads];
   __shared__ WalkOut s_out[kWalkThreads];
   const uint32_t wv = threadIdx.x / kWave, q = threadIdx.x % kWave;
@@ -448,9 +441,37 @@ extern "C" __global__ __launch_bounds__(kWalkThreads) void mq_recv_walk_kernel(
   uint32_t new_attempts = 0;
   WalkIn* sin = s_in + wv * kWave;
   WalkOut* sout = s_out + wv * kWave;
+  // Settled prefix (walks after the first): while every packet so far OPENED with the keys the
+  // speculation chose (outcome kOk1, no key update), the reference's decisions are exactly the
+  // speculation's — same state, same inputs — so the previous walk's records stand; the walk only
+  // clears the chunk's descriptors (nothing to attempt) and raises the largest PNs. The first chunk
+  // that is not settled switches the connection to the full path for the rest of its run.
+  bool settled = true;
   for (uint32_t k0 = lo; k0 < hi; k0 += kWave) {  // wave-uniform
     const uint32_t m = min((uint32_t)kWave, hi - k0), k = k0 + q;
     const bool mine = q < m;
+    if (settled) {
+      uint8_t so = kOk1;
+      RecvPlan st{};
+      if (mine) {
+        so = outcome[k];
+        st = tried[k];
+      }
+      if (!wave_any(mine && (so != kOk1 || st.gen == 2))) {
+        if (mine) {
+          d1[k].key_id = kNoRow;
+          d2[k].key_id = kNoRow;
+        }
+#pragma unroll
+        for (uint32_t l = 0; l < 3; ++l) {
+          uint64_t tot;
+          (void)excl_max_u64(mine && st.status == l ? st.pn : 0ull, q, tot);
+          if (tot > s.largest[l]) s.largest[l] = tot;
+        }
+        continue;
+      }
+      settled = false;
+    }
     RecvWork w{};
     RecvPlan p{}, t{};
     uint8_t o = kNone;
@@ -531,10 +552,14 @@ extern "C" __global__ __launch_bounds__(kWalkThreads) void mq_recv_walk_kernel(
       if (r.mode == 1) {
         RecvPlan tp;
         tp.pn = r.pn; tp.lbefore = r.lbefore; tp.row = r.row; tp.retry = r.retry; tp.trunc = p.trunc;
-        tp.status = kPending; tp.gen = r.pgen; tp.phase = p.phase; tp.pn_len = p.pn_len;
+        // tried entries: status = the packet's level (the settled prefix's largest PNs)
+        tp.status = w.level; tp.gen = r.pgen; tp.phase = p.phase; tp.pn_len = p.pn_len;
         tried[k] = tp;
         a.key_id = r.row;
         b.key_id = r.retry;
+        // the open pre-pass value of both passes (prepass_decode: truncated PN, unmasked first
+        // byte), from the front's unmask — so the passes run no header-protection pre-pass
+        hpm[k] = make_uint2(p.trunc, 0x100u | (p.row & 0xffu));
       } else if (r.mode == 2) {
         a.key_id = o == kOk1 ? t.row : t.retry;
         a.pn = t.pn;
@@ -549,7 +574,7 @@ extern "C" __global__ __launch_bounds__(kWalkThreads) void mq_recv_walk_kernel(
       rec.key_gen = (w.level == MQ_LEVEL_APPLICATION && r.st == MQ_OK) ? r.gen : 0;
       rec.reserved[0] = rec.reserved[1] = rec.reserved[2] = 0;
       out[i] = rec;
-      att = r.mode == 1;
+      att = r.mode != 0;  // keyed d1 entry: an attempt, or a re-seal (final walk)
     }
     new_attempts += (uint32_t)__popcll(__ballot(att));
   }
@@ -563,12 +588,20 @@ extern "C" __global__ __launch_bounds__(kWalkThreads) void mq_recv_walk_kernel(
   conns[ci] = u;
 }
 
-// retry pass descriptors: only 1-RTT packets whose current keys failed (recv.rs:441-474)
+// retry pass descriptors: only 1-RTT packets whose current keys failed (recv.rs:441-474); live[1]
+// counts them (live[0]: the walk's keyed primary descriptors — none, none to retry either)
 extern "C" __global__ __launch_bounds__(256) void mq_recv_retry_kernel(const uint8_t* __restrict__ st1,
-                                                                       mq_pkt_desc* __restrict__ d2, uint32_t max_pkts) {
+                                                                       mq_pkt_desc* __restrict__ d2, uint32_t max_pkts,
+                                                                       uint32_t* __restrict__ live) {
+  if (live[0] == 0) return;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= max_pkts) return;
-  if (!(d2[i].key_id != kNoRow && st1[i] == MQ_ERR_CRYPTO)) d2[i].key_id = kNoRow;
+  bool keep = false;
+  if (i < max_pkts) {
+    keep = d2[i].key_id != kNoRow && st1[i] == MQ_ERR_CRYPTO;
+    if (!keep && d2[i].key_id != kNoRow) d2[i].key_id = kNoRow;
+  }
+  const uint32_t c = (uint32_t)__popcll(__ballot(keep));
+  if (c && (threadIdx.x & (kWave - 1)) == 0) atomicAdd(live + 1, c);
 }
 
 // outcomes of this round's attempts
@@ -577,7 +610,9 @@ extern "C" __global__ __launch_bounds__(256) void mq_recv_outcome_kernel(const m
                                                                          const uint8_t* __restrict__ st1,
                                                                          const uint8_t* __restrict__ st2,
                                                                          uint8_t* __restrict__ outcome,
-                                                                         uint32_t max_pkts) {
+                                                                         uint32_t max_pkts,
+                                                                         const uint32_t* __restrict__ live) {
+  if (live[0] == 0) return;  // nothing attempted this round
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= max_pkts || d1[i].key_id == kNoRow) return;
   outcome[i] = st1[i] == MQ_OK ? kOk1 : (d2[i].key_id != kNoRow && st2[i] == MQ_OK) ? kOk0 : kFail;
@@ -590,7 +625,7 @@ size_t al(size_t b) { return (b + 255) & ~(size_t)255; }
 struct RecvWs {
   uint32_t *counts, *base, *total, *keys, *vals, *skeys, *svals, *seg_lo, *seg_hi, *attempts;
   RecvWork *work, *work_s;
-  RecvPlan *hdr, *hdr_s, *tried;
+  RecvPlan *hdr_s, *tried;
   mq_conn_recv* conn0;
   uint2* hpm;
   mq_pkt_desc *d1, *d2;
@@ -625,7 +660,6 @@ RecvWs layout(uint8_t* p, uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_conns
   w.seg_hi = (uint32_t*)take(4ull * n_conns);
   w.conn0 = (mq_conn_recv*)take(sizeof(mq_conn_recv) * (size_t)n_conns);
   w.work = (RecvWork*)take(sizeof(RecvWork) * (size_t)max_pkts);
-  w.hdr = (RecvPlan*)take(sizeof(RecvPlan) * (size_t)max_pkts);
   w.work_s = (RecvWork*)take(sizeof(RecvWork) * (size_t)max_pkts);
   w.hdr_s = (RecvPlan*)take(sizeof(RecvPlan) * (size_t)max_pkts);
   w.tried = (RecvPlan*)take(sizeof(RecvPlan) * (size_t)max_pkts);
@@ -663,6 +697,7 @@ hipError_t mq_recv_front(const KeyRow* kt, uint32_t n_rows, mq_conn_recv* conns,
                          hipStream_t s) {
   RecvWs w = layout((uint8_t*)ws_ptr, n_dgrams, max_pkts, n_conns, open_ws_bytes);
   pass->d1 = w.d1; pass->d2 = w.d2; pass->st1 = w.st1; pass->st2 = w.st2; pass->open_ws = w.open_ws;
+  pass->live1 = w.attempts; pass->live2 = w.attempts + 1;
   const dim3 b256(256);
   hipError_t e = hipSuccess;
   if (n_dgrams) {
@@ -687,8 +722,6 @@ hipError_t mq_recv_front(const KeyRow* kt, uint32_t n_rows, mq_conn_recv* conns,
                      n_rows, w.keys, w.vals, w.d1);
   if ((e = mq_launch_chacha_prepass(kt, n_rows, arena, arena_len, w.d1, max_pkts, w.hpm, s)) != hipSuccess) return e;
   if ((e = mq_launch_aes_prepass(kt, n_rows, arena, arena_len, w.d1, max_pkts, w.hpm, s)) != hipSuccess) return e;
-  hipLaunchKernelGGL(mq_recv_unmask_kernel, dim3((max_pkts + 255) / 256), b256, 0, s, arena, w.work, w.hpm, w.total,
-                     max_pkts, w.hdr);
   size_t cb = w.cub_bytes;
   // keys are connection indices (< n_conns) and 0xFFFFFFFF past the packet count: the low
   // ceil(log2(n_conns + 1)) bits order them (the padding's all-ones bits sort last), so the radix
@@ -705,7 +738,7 @@ hipError_t mq_recv_front(const KeyRow* kt, uint32_t n_rows, mq_conn_recv* conns,
   hipLaunchKernelGGL(mq_recv_seg_kernel, dim3((max_pkts + 255) / 256), b256, 0, s, w.skeys, max_pkts, n_conns, w.seg_lo,
                      w.seg_hi);
   hipLaunchKernelGGL(mq_recv_gather_kernel, dim3((max_pkts + 255) / 256), b256, 0, s, w.total, max_pkts, w.svals, w.work,
-                     w.hdr, w.work_s, w.hdr_s, w.outcome);
+                     arena, w.hpm, w.work_s, w.hdr_s, w.outcome);
   return mq_recv_walk(kt, n_rows, conns, n_conns, n_dgrams, max_pkts, out, ws_ptr, open_ws_bytes, false, s);
 }
 
@@ -719,7 +752,7 @@ hipError_t mq_recv_walk(const KeyRow* /*kt*/, uint32_t n_rows, mq_conn_recv* con
   if (n_conns)
     hipLaunchKernelGGL(mq_recv_walk_kernel, dim3((n_conns + kWalkConns - 1) / kWalkConns), dim3(kWalkThreads), 0, s,
                        w.conn0, conns, n_conns, w.work_s, w.svals, w.seg_lo, w.seg_hi, w.hdr_s, n_rows, w.tried,
-                       w.outcome, w.d1, w.d2, out, w.attempts, (int)final_walk);
+                       w.outcome, w.d1, w.d2, out, w.attempts, (int)final_walk, (uint2*)w.open_ws);
   return hipGetLastError();
 }
 
@@ -727,8 +760,11 @@ hipError_t mq_recv_walk(const KeyRow* /*kt*/, uint32_t n_rows, mq_conn_recv* con
 hipError_t mq_recv_retry(uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_conns, void* ws_ptr, size_t open_ws_bytes,
                          hipStream_t s) {
   RecvWs w = layout((uint8_t*)ws_ptr, n_dgrams, max_pkts, n_conns, open_ws_bytes);
+  hipError_t e;
+  if ((e = hipMemsetAsync(w.attempts + 1, 0, 4, s)) != hipSuccess) return e;
   if (max_pkts)
-    hipLaunchKernelGGL(mq_recv_retry_kernel, dim3((max_pkts + 255) / 256), dim3(256), 0, s, w.st1, w.d2, max_pkts);
+    hipLaunchKernelGGL(mq_recv_retry_kernel, dim3((max_pkts + 255) / 256), dim3(256), 0, s, w.st1, w.d2, max_pkts,
+                       w.attempts);
   return hipGetLastError();
 }
 
@@ -737,6 +773,6 @@ hipError_t mq_recv_outcomes(uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_con
   RecvWs w = layout((uint8_t*)ws_ptr, n_dgrams, max_pkts, n_conns, open_ws_bytes);
   if (max_pkts)
     hipLaunchKernelGGL(mq_recv_outcome_kernel, dim3((max_pkts + 255) / 256), dim3(256), 0, s, w.d1, w.d2, w.st1, w.st2,
-                       w.outcome, max_pkts);
+                       w.outcome, max_pkts, (const uint32_t*)w.attempts);
   return hipGetLastError();
 }

@@ -1,5 +1,5 @@
 # Round-4 call J: receive / send GPU tests, aux components with the fused ChaCha protect and with
-# two-kernel composite (MQ_PROTECT_FUSED=0), kernel stats of the receive / protect composites.
+# two-kernel composite (MQ_PROTECT_FUSED=0; and ChaCha lists on the one-shot grid, MQ_CC_LIST=0), kernel stats of the receive / protect composites.
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/${1:-r04j}
@@ -12,7 +12,7 @@ for r in 1 2; do
   step aux_$r
   timeout -k 10 300 python tools/bench_aux.py > $O/aux_$r.json 2> $O/aux_$r.err || { tail $O/aux_$r.err; exit 1; }
   cat $O/aux_$r.json
-  MQ_PROTECT_FUSED=0 timeout -k 10 300 python tools/bench_aux.py > $O/aux_unfused_$r.json 2> $O/aux_unfused_$r.err || { tail $O/aux_unfused_$r.err; exit 1; }
+  MQ_PROTECT_FUSED=0 MQ_CC_LIST=0 timeout -k 10 300 python tools/bench_aux.py > $O/aux_unfused_$r.json 2> $O/aux_unfused_$r.err || { tail $O/aux_unfused_$r.err; exit 1; }
   cat $O/aux_unfused_$r.json
 done
 step e2e
@@ -29,6 +29,9 @@ for a in "c --config c" "e --config e" "ck --config c --keys 1024"; do
   timeout -k 10 300 python3 bench.py --no-cpu-baseline "$@" > $O/bench_$name.json 2> $O/bench_$name.err || { tail $O/bench_$name.err; exit 1; }
   python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print(sys.argv[1], d['value'], r['seal_ms'], r['open_ms'], r['frac'])" $O/bench_$name.json
 done
+step bench_e_oneshot
+MQ_CC_LIST=0 timeout -k 10 300 python3 bench.py --no-cpu-baseline --config e > $O/bench_e_oneshot.json 2> $O/bench_e_oneshot.err || { tail $O/bench_e_oneshot.err; exit 1; }
+python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print(sys.argv[1], d['value'], r['seal_ms'], r['open_ms'], r['frac'])" $O/bench_e_oneshot.json
 step prof_e
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_e -o run -- python3 bench.py --no-cpu-baseline --config e > $O/prof_e.json 2> $O/prof_e.err || { tail $O/prof_e.err; exit 1; }
 echo R04J_DONE
