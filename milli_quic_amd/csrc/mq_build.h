@@ -187,21 +187,81 @@ __device__ __forceinline__ void build_store(const BuildLayout& b, int j, const u
   }
 }
 
-// The built packet's bytes [16 k, 16 k + 16) for a chunk k holding any byte outside the frames
-// (header / PN, the frames' edges, PADDING, tag room), byte-wise; bytes past the packet are zero.
-// x0 = packet byte at the chunk's first byte (negative: bytes before the packet).
-__device__ __forceinline__ uint4 build_edge_chunk(const BuildLayout& b, const uint8_t* __restrict__ fr, int x0,
-                                                  uint32_t len) {
-  uint64_t lo = 0, hi = 0;  // no private array indexed at run time (it would live in scratch)
-  for (int y = 0; y < 16; ++y) {
-    const int x = x0 + y;
-    if (x < 0 || (uint32_t)x >= len) continue;
-    const uint32_t ux = (uint32_t)x;
-    const uint64_t v = ux < b.hp ? b.header(ux) : ux < b.hp + b.m ? fr[ux - b.hp] : (uint8_t)0;
-    if (y < 8) lo |= v << (8 * y);
-    else hi |= v << (8 * (y - 8));
+
+// Header bytes 8j .. 8j + 7 of a packet for octet lane j, from two 8-byte windows of its connection
+// row (mq_conn_send: dcid_len @0, scid_len @1, key_phase @2, dcid @4, scid @24) — the DCID bytes
+// and the SCID bytes those header positions would hold — so a lane waits on two loads rather than
+// one dependent load per byte, and no byte is picked from a run-time-indexed private array (which
+// the compiler would keep in scratch).
+__device__ __forceinline__ uint64_t conn_window(const mq_conn_send* cp, int off) {  // row bytes [off, off + 8)
+  const int c = min(max(off, 0), (int)sizeof(mq_conn_send) - 8);
+  const uint8_t* p = reinterpret_cast<const uint8_t*>(cp) + c;
+  uint64_t v = (uint64_t)*(const u32_u*)p | (uint64_t)*(const u32_u*)(p + 4) << 32;
+  if (off > c) v = off - c >= 8 ? 0ull : v >> (8 * (off - c));
+  if (off < c) v = c - off >= 8 ? 0ull : v << (8 * (c - off));
+  return v;
+}
+
+struct HeaderLane {
+  uint64_t wd, ws;      // row bytes under this lane's DCID / SCID positions
+  uint32_t dl, sl, kp;  // CID lengths, key phase
+  __device__ __forceinline__ void load(const mq_conn_send* cp, uint32_t level, int j) {
+    const uint32_t w0 = *(const u32_u*)cp;
+    dl = w0 & 0xffu; sl = (w0 >> 8) & 0xffu; kp = (w0 >> 16) & 0xffu;
+    // 1-RTT: dcid[x - 1] = row byte x + 3; long: dcid[x - 6] = row byte x - 2, scid[x - 7 - dl] =
+    // row byte x + 17 - dl
+    wd = conn_window(cp, 8 * j + (level == MQ_LEVEL_APPLICATION ? 3 : -2));
+    ws = conn_window(cp, 8 * j + 17 - (int)dl);
   }
-  return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+  // header byte x = 8j + u (x < hdr_len); header_byte's layout
+  __device__ __forceinline__ uint8_t byte(uint32_t level, uint32_t pn_len, uint64_t payload_length, uint32_t x,
+                                          uint32_t u) const {
+    const uint8_t d = (uint8_t)(wd >> (8 * u)), sc = (uint8_t)(ws >> (8 * u));
+    if (level == MQ_LEVEL_APPLICATION) return x == 0 ? (uint8_t)(0x40 | ((kp & 1) << 2) | (pn_len - 1)) : d;
+    const bool initial = level == MQ_LEVEL_INITIAL;
+    if (x == 0) return (uint8_t)((initial ? 0xC0 : 0xE0) | ((pn_len - 1) & 3));
+    if (x < 5) return x == 4 ? 1 : 0;  // QUIC_VERSION_1
+    if (x == 5) return (uint8_t)dl;
+    if (x < 6 + dl) return d;
+    if (x == 6 + dl) return (uint8_t)sl;
+    if (x < 7 + dl + sl) return sc;
+    uint32_t p = 7 + dl + sl;
+    if (initial) {
+      if (x == p) return 0;  // token length (the reference sends no token, transmit.rs:519)
+      ++p;
+    }
+    const uint32_t n = varint_len(payload_length), k = x - p;  // varint.rs:72-110
+    uint8_t v = (uint8_t)(payload_length >> (8 * (n - 1 - k)));
+    if (k == 0) v |= n == 1 ? 0 : n == 2 ? 0x40 : n == 4 ? 0x80 : 0xc0;
+    return v;
+  }
+};
+
+// The frames part of an image chunk whose first byte is packet byte x0 (header positions and
+// bytes past the frames zero): one 16-B load when the chunk's frames window lies inside the frames
+// buffer (fo: the packet's frames offset, flen: the buffer's length), byte-wise at its ends.
+__device__ __forceinline__ uint4 edge_frames(const BuildLayout& b, const uint8_t* __restrict__ fr, int x0,
+                                             uint64_t fo, uint64_t flen) {
+  const int64_t src = (int64_t)x0 - (int64_t)b.hp;  // frames offset of the chunk's first byte
+  uint32_t w[4];
+  if (src + (int64_t)fo >= 0 && (uint64_t)((int64_t)fo + src) + 16 <= flen) {
+    u4w(ld16(fr + src), w);
+  } else {
+    uint64_t lo = 0, hi = 0;
+    for (int y = 0; y < 16; ++y) {
+      const int64_t f = src + y;
+      if (f < 0 || f >= (int64_t)b.m) continue;
+      const uint64_t v = fr[f];
+      if (y < 8) lo |= v << (8 * y);
+      else hi |= v << (8 * (y - 8));
+    }
+    w[0] = (uint32_t)lo; w[1] = (uint32_t)(lo >> 32); w[2] = (uint32_t)hi; w[3] = (uint32_t)(hi >> 32);
+  }
+  // keep packet bytes [hp, hp + m) of the chunk
+  const int lo = min(max((int)b.hp - x0, 0), 16), hi = min(max((int)(b.hp + b.m) - x0, 0), 16);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) w[q] &= byte_mask(hi, q) & ~byte_mask(lo, q);
+  return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 }  // namespace mq

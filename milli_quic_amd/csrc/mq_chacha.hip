@@ -727,7 +727,11 @@ __device__ __forceinline__ void chacha_protect_tile(uint32_t tb, const KeyRow* _
         const uint32_t k = k0 + kLanesPerPkt * t;
         const int x0 = 16 * (int)k - head;
         const bool whole = k < nch && x0 >= (int)b.hp && (uint32_t)x0 + 16u <= b.hp + b.m;
+#if MQ_PROF_SKIP & 512  // phase-cost diagnostic: no frames loads
+        v[t] = make_uint4(x0, 0, 0, 0);
+#else
         v[t] = whole ? ld16(fr + ((uint32_t)x0 - b.hp)) : make_uint4(0, 0, 0, 0);
+#endif
       }
 #pragma unroll
       for (uint32_t t = 0; t < kProtectBatch; ++t) {
@@ -741,10 +745,28 @@ __device__ __forceinline__ void chacha_protect_tile(uint32_t tb, const KeyRow* _
     // edge chunks, byte-wise, outside the unrolled batch: those holding header / PN bytes, and the
     // one where the frames end mid-chunk
     const uint32_t kh = (uint32_t)(head + (int)b.hp + 15) >> 4, fe = (uint32_t)head + b.hp + b.m;
+#if !(MQ_PROF_SKIP & 256)  // phase-cost diagnostic: no edge chunks
+    // their frames bytes first (one guarded 16-B load each, zeros elsewhere), then the header and PN
+    // bytes on top, eight per lane from the connection row's words: r04's first version built
+    // each edge chunk byte by byte on one lane, a dependent load per byte (0.12 of its 1.40 ms,
+    // profiles/r04n_protect_phases.txt)
     for (uint32_t k = (uint32_t)j; k < kh && k < nch; k += kLanesPerPkt)
-      *(uint4*)(img + 16u * k) = build_edge_chunk(b, fr, 16 * (int)k - head, pl.len);
+      *(uint4*)(img + 16u * k) = edge_frames(b, fr, 16 * (int)k - head, b.frames_offset, frames_len);
     if ((fe & 15u) && (fe >> 4) >= kh && (fe >> 4) < nch && ((fe >> 4) & (kLanesPerPkt - 1)) == (uint32_t)j)
-      *(uint4*)(img + 16u * (fe >> 4)) = build_edge_chunk(b, fr, 16 * (int)(fe >> 4) - head, pl.len);
+      *(uint4*)(img + 16u * (fe >> 4)) = edge_frames(b, fr, 16 * (int)(fe >> 4) - head, b.frames_offset, frames_len);
+    if (c.act && 8u * (uint32_t)j < b.hp) {
+      HeaderLane hl;
+      hl.load(b.cp, b.level, j);
+      uint8_t* hd = img + head;
+#pragma unroll
+      for (uint32_t u = 0; u < 8; ++u) {
+        const uint32_t x = 8u * (uint32_t)j + u;
+        if (x < b.hp)
+          hd[x] = x < b.hdr ? hl.byte(b.level, b.pn_len, b.payload_length, x, u)
+                            : (uint8_t)(b.pn >> (8 * (b.pn_len - 1 - (x - b.hdr))));
+      }
+    }
+#endif
     LdsSpace sp{wsm};
     NoStager stg;  // complete(): the wave's image stores are done before any lane reads the image
     ChaChaPolicy::template seal<SINGLE, LdsSpace>(sp, pl.slot * 16u + pl.head(), c, row, j, stg, pool);

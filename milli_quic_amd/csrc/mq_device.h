@@ -211,6 +211,7 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap
 // unaligned access enabled). A store writes exactly its 16 bytes, so lanes storing adjacent
 // ranges of a packet (or of neighbouring packets) never need a read-modify-write.
 typedef uint4 __attribute__((aligned(1))) uint4_u;
+typedef uint32_t __attribute__((aligned(1))) u32_u;  // unaligned dword access
 __device__ __forceinline__ uint4 ld16(const uint8_t* p) { return *(const uint4_u*)p; }
 __device__ __forceinline__ void st16(uint8_t* p, const uint32_t (&w)[4]) {
   *(uint4_u*)p = make_uint4(w[0], w[1], w[2], w[3]);

@@ -239,7 +239,6 @@ __device__ __forceinline__ bool prepass_pick(uint32_t t, uint32_t suite, const K
 // Pre-pass header read: the received first byte and the 20 bytes at pn_offset (PN bytes, then the
 // sample) as 5 little-endian words, with one 16-B and one 4-B unaligned load — prepass_pick has
 // checked that the packet, and so these bytes, lie inside the arena
-typedef uint32_t __attribute__((aligned(1))) u32_u;
 __device__ __forceinline__ void prepass_header(const uint8_t* __restrict__ arena, const mq_pkt_desc& d, uint8_t& b0,
                                                uint32_t (&w)[5]) {
   const uint8_t* p = arena + d.offset + d.pn_offset;
