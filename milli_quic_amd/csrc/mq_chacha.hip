@@ -855,7 +855,7 @@ hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_
                             uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
                             const uint32_t* index, const uint32_t* n_dev, uint8_t* status,
                             uint64_t* pn_out, uint2* hpm, bool own_hp, hipStream_t s, int cus, uint32_t* sched,
-                            int64_t single_row) {
+                            int64_t single_row, bool persistent) {
   const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
   if (tiles == 0) return hipSuccess;
   if (open && hpm && own_hp) {  // !own_hp: mq_launch_mixed_hp covers both suites' lists
@@ -865,15 +865,20 @@ hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_
     if (e != hipSuccess) return e;
   }
   const uint32_t blocks = (tiles + kCcWaves - 1) / kCcWaves;
-  static const bool persistent = [] {  // MQ_CC_LIST=0 (diagnostic): lists on the one-shot grid (r03)
+  // Lists run on the persistent grid when asked for (the receive composite's passes: an empty
+  // list then costs 1024 workgroups, not a grid over the list capacity), else on the one-shot grid,
+  // which measured 1.1 % faster on config E (r04q: 557.9 vs 551.6 GiB/s, three alternating runs).
+  // MQ_CC_LIST=0 / 1 (diagnostic) forces either.
+  static const int forced = [] {
     const char* e = std::getenv("MQ_CC_LIST");
-    return !(e && e[0] == '0');
+    return e ? (e[0] == '0' ? 0 : 1) : -1;
   }();
+  if (forced >= 0) persistent = forced == 1;
+  // single_row >= 0: every packet of the list is on that row (the single-key kernels)
+  const bool one = index && single_row >= 0 && (uint64_t)single_row < n_rows;
+  const KeyRow* kl = one ? kt + single_row : kt;
   if (index && persistent) {
     const uint32_t per = (uint32_t)(cus > 0 ? cus : 256) * 4u, grid = blocks < per ? blocks : per;
-    // single_row >= 0: every packet of the list is on that row (the single-key list kernels)
-    const bool one = single_row >= 0 && (uint64_t)single_row < n_rows;
-    const KeyRow* kl = one ? kt + single_row : kt;
     if (open)
       hipLaunchKernelGGL(one ? mq_chacha_open_list1_kernel : mq_chacha_open_list_kernel, dim3(grid),
                          dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kl, n_rows, arena, arena_len, desc, n, index,
@@ -885,13 +890,13 @@ hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_
     return hipGetLastError();
   }
   if (open)
-    hipLaunchKernelGGL(n_rows == 1 ? mq_chacha_open1_kernel : mq_chacha_open_kernel, dim3(blocks),
-                       dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kt, n_rows, arena, arena_len, desc, n, index,
+    hipLaunchKernelGGL(n_rows == 1 || one ? mq_chacha_open1_kernel : mq_chacha_open_kernel, dim3(blocks),
+                       dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kl, n_rows, arena, arena_len, desc, n, index,
                        n_dev, status, pn_out, hpm);
   if (open) return hipGetLastError();
   // seal: header protection runs inside the tile kernel (the pool's HP blocks, cc_pool_run)
-  hipLaunchKernelGGL(n_rows == 1 ? mq_chacha_seal1_kernel : mq_chacha_seal_kernel, dim3(blocks),
-                     dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kt, n_rows, arena, arena_len, desc, n, index,
+  hipLaunchKernelGGL(n_rows == 1 || one ? mq_chacha_seal1_kernel : mq_chacha_seal_kernel, dim3(blocks),
+                     dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kl, n_rows, arena, arena_len, desc, n, index,
                      n_dev, status);
   return hipGetLastError();
 }

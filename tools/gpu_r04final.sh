@@ -2,8 +2,9 @@
 # bench configs (written into profiles/ first, so the bench lines' roofline.traffic reads them);
 # bench lines B (with CPU baselines), B end-to-end, C, C/1024 keys, E, B/1024 keys; rocprofv3
 # kernel stats of B, C, C/1024 keys, E; PMC instruction / LDS passes of B and C; the 2-rank
-# launcher rehearsal (gloo); per-packet latency; aux components; smoke. Every GPU step is
-# time-limited; the script stops at the first failure.
+# launcher rehearsal (gloo); kernel stats of the driver's own bench command and of the receive /
+# protect composites; per-packet latency; aux components; smoke. Every GPU step is time-limited;
+# the script stops at the first failure.
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/${1:-r04final}
@@ -54,6 +55,12 @@ for c in b c; do
     timeout -k 10 240 rocprofv3 --pmc "$@" --output-format csv -d $O/pmc_$c/$name -o run -- python3 tools/prof_driver.py $c 1048576 2 > $O/pmc_${c}_$name.log 2>&1 || { echo "pmc $c $name failed"; exit 1; }
   done
   python tools/pmc_summary.py $O/pmc_$c --tiles 131072 > $O/pmc_$c.txt || exit 1
+done
+step prof_driver_cmd
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_d20 -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > $O/prof_d20.json 2> $O/prof_d20.err || { tail $O/prof_d20.err; exit 1; }
+for a in protect recv; do
+  step prof_$a
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$a -o run -- python3 tools/prof_aux.py $a 5 > $O/prof_$a.log 2>&1 || { tail $O/prof_$a.log; exit 1; }
 done
 step gloo_2rank
 MQ_BENCH_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --no-cpu-baseline > $O/bench_b_2rank_gloo.json 2> $O/bench_b_2rank_gloo.err || { tail $O/bench_b_2rank_gloo.err; exit 1; }
