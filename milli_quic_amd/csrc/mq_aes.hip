@@ -24,9 +24,9 @@
 // and absorbs the ciphertext into its Horner accumulator (multiplier H^8) in the same iteration;
 // a final multiply by H^e (e = blocks after the lane's last one, 1..8) and an octet XOR give the
 // tag. No LDS packet image: the workgroup's LDS is its tables (72 KiB in r02; 156 KiB with the r03
-// byte-position GHASH table), so 16 waves per CU
-// (4 per SIMD) fit where the staged design (10-KiB images, r01) ran 8 — measured 1.41 vs 2.23 ms
-// for a config-C seal (tools/ubench/ubench6.hip). Open decrypts in the same single pass,
+// byte-position GHASH table), so 12-16 waves per CU
+// (3-4 per SIMD; 12 since r04, see aes_waves) fit where the staged design (10-KiB images, r01) ran
+// 8 — measured 1.41 vs 2.23 ms for a config-C seal (tools/ubench/ubench6.hip). Open decrypts in the same single pass,
 // storing plaintext speculatively; a packet whose tag fails is restored by XORing the same
 // keystream again, so every failed packet ends byte-identical to its input (recv.rs:416-421).
 #include "mq_aes.h"
@@ -35,6 +35,28 @@
 #include <cstdlib>
 
 namespace mq {
+
+// Packet data streams of the AES kernels. MQ_AES_NT (diagnostic build): non-temporal loads / stores,
+// so the streamed packet bytes do not displace the kernel's spill slots from the L2.
+#if MQ_AES_NT
+typedef unsigned int aes_v4u __attribute__((ext_vector_type(4)));
+typedef aes_v4u __attribute__((aligned(1))) aes_v4u_u;
+__device__ __forceinline__ uint4 ald16(const uint8_t* p) {
+  const aes_v4u v = __builtin_nontemporal_load((const aes_v4u_u*)p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void ast16(uint8_t* p, const uint32_t (&w)[4]) {
+  aes_v4u v = {w[0], w[1], w[2], w[3]};
+  __builtin_nontemporal_store(v, (aes_v4u_u*)p);
+}
+#else
+__device__ __forceinline__ uint4 ald16(const uint8_t* p) { return ld16(p); }
+__device__ __forceinline__ void ast16(uint8_t* p, const uint32_t (&w)[4]) { st16(p, w); }
+#endif
+__device__ __forceinline__ void ast_block(uint8_t* p, const uint32_t (&w)[4], uint32_t rem) {
+  if (rem >= 16) ast16(p, w);
+  else st_bytes(p, w, rem);
+}
 
 // DirectionalKeys::nonce (src/crypto/mod.rs:66-74), as big-endian AES input words
 __device__ __forceinline__ void nonce_be(const KeyRow* row, uint64_t pn, uint32_t (&nb)[3]) {
@@ -223,9 +245,9 @@ struct AesStream {
       h[0] = 23; h[1] = 3; h[2] = 3; h[3] = (uint8_t)(rlen >> 8); h[4] = (uint8_t)rlen;
     }
     auto data = [&](int b) -> uint4 {
-      if (k.act && b >= 1 && (uint32_t)b < k.nblk) return ld16(arena + k.pay + 16ull * (uint32_t)(b - 1));
+      if (k.act && b >= 1 && (uint32_t)b < k.nblk) return ald16(arena + k.pay + 16ull * (uint32_t)(b - 1));
       if (k.act && !k.rec && b <= 0 && b >= 1 - (int)k.A)
-        return ld16(arena + k.pkt + 16ull * (uint32_t)((int)k.A + b - 1));
+        return ald16(arena + k.pkt + 16ull * (uint32_t)((int)k.A + b - 1));
       return make_uint4(0, 0, 0, 0);
     };
     uint32_t acc[4] = {0, 0, 0, 0}, ej0[4] = {0, 0, 0, 0}, smp[4] = {0, 0, 0, 0};
@@ -243,7 +265,7 @@ struct AesStream {
         uint32_t ks[4], ct[4], x[4];
         ctr<CACHED>(key, L, k, cc, ub, ks);
         ct[0] = cur.x ^ ks[0]; ct[1] = cur.y ^ ks[1]; ct[2] = cur.z ^ ks[2]; ct[3] = cur.w ^ ks[3];
-        if (k.act) st16(arena + k.pay + 16ull * (ub - 1), ct);
+        if (k.act) ast16(arena + k.pay + 16ull * (ub - 1), ct);
 #pragma unroll
         for (int q = 0; q < 4; ++q) x[q] = refl(ct[q]);
         gh_step(acc, m8, true, false, x);
@@ -276,7 +298,7 @@ struct AesStream {
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) ct[q] = pt[q] ^ ks[q];
-        st_block(arena + k.pay + off, ct, rem);
+        ast_block(arena + k.pay + off, ct, rem);
         gh_block(ct, rem, x);
         has = true;
       } else if (k.act && b <= 0 && b >= 1 - (int)k.A) {  // AAD block A + b - 1
@@ -376,8 +398,8 @@ struct AesStream {
     if (CACHED) cc = ctr_cache(key, L, k.nb);
     const GfOp m8 = prep_m8(row);
     auto data = [&](int b) -> uint4 {
-      if (k.act && b >= 1 && (uint32_t)b < k.nblk) return ld16(arena + k.pay + 16ull * (uint32_t)(b - 1));
-      if (k.act && b <= 0 && b >= 1 - (int)k.A) return ld16(arena + k.pkt + 16ull * (uint32_t)((int)k.A + b - 1));
+      if (k.act && b >= 1 && (uint32_t)b < k.nblk) return ald16(arena + k.pay + 16ull * (uint32_t)(b - 1));
+      if (k.act && b <= 0 && b >= 1 - (int)k.A) return ald16(arena + k.pkt + 16ull * (uint32_t)((int)k.A + b - 1));
       return make_uint4(0, 0, 0, 0);
     };
     uint32_t acc[4] = {0, 0, 0, 0}, ej0[4] = {0, 0, 0, 0};
@@ -394,7 +416,7 @@ struct AesStream {
         ctr<CACHED>(key, L, k, cc, ub, ks);
         x[0] = refl(cur.x); x[1] = refl(cur.y); x[2] = refl(cur.z); x[3] = refl(cur.w);
         pt[0] = cur.x ^ ks[0]; pt[1] = cur.y ^ ks[1]; pt[2] = cur.z ^ ks[2]; pt[3] = cur.w ^ ks[3];
-        if (k.act) st16(arena + k.pay + 16ull * (ub - 1), pt);
+        if (k.act) ast16(arena + k.pay + 16ull * (ub - 1), pt);
         gh_step(acc, m8, true, false, x);
         cur = nxt;
         continue;
@@ -411,7 +433,7 @@ struct AesStream {
         has = true;
 #pragma unroll
         for (int q = 0; q < 4; ++q) pt[q] = m[q] ^ ks[q];
-        st_block(arena + k.pay + off, pt, rem);
+        ast_block(arena + k.pay + off, pt, rem);
       } else if (k.act && b <= 0 && b >= 1 - (int)k.A) {  // AAD block: the unprotected header
         uint32_t m[4];
         u4w(cur, m);
@@ -466,11 +488,18 @@ struct AesStream {
 using namespace mq;
 
 // Tile kernels: persistent workgroups of aes_waves(SINGLE) waves share the LDS tables (built once
-// per workgroup); wave w walks tiles blockIdx.x * W + w + k * gridDim.x * W. Single-key kernels
-// fit 128 VGPRs (16 waves per CU); the multi-key ones hold more state per packet (LDS key
-// pointers, the bit-holed GHASH operand) and run 12 waves in 168. The "1" variants run when the
-// key table has a single row: round keys in SGPRs and the GHASH table of that row's H^8.
-constexpr int aes_waves(bool single) { return single ? 16 : (int)kAesMultiWaves; }
+// per workgroup); wave w walks tiles blockIdx.x * W + w + k * gridDim.x * W. Every AES kernel runs
+// 12 waves per CU in 168 VGPRs (r04; the multi-key ones always did: more state per packet — LDS key
+// pointers, the bit-holed GHASH operand). The single-key kernels ran 16 waves in 128 VGPRs until
+// r04 and spilled ~36 VGPRs per lane inside the tile loop: 116 B of scratch per lane, 3.8 MB per
+// XCD, which the streamed packets kept evicting from the L2 — C's seal moved 3.92 GB per launch
+// (1.56x algorithmic, writes 1.49x); at 12 waves it moves 2.83 GB (1.12x, writes 1.10x) in the same
+// time (profiles/r04r_ab_aes_waves.txt). The "1" variants run when the key table has a single row:
+// round keys in SGPRs and the GHASH table of that row's H^8.
+#ifndef MQ_AES_SINGLE_WAVES
+#define MQ_AES_SINGLE_WAVES 12
+#endif
+constexpr int aes_waves(bool single) { return single ? MQ_AES_SINGLE_WAVES : (int)kAesMultiWaves; }
 // Work distribution (r04): every wave runs its first tile by grid position, then claims chunks of
 // the rest dynamically (mq_tile.h for_tiles, TileSched; guided chunk sizes, one head per XCD),
 // when the launch has a schedule slot. That replaced (a) the static stride, under which a workgroup
@@ -665,7 +694,7 @@ MQ_AES_KERNELS(mq_aes_seal1_kernel, mq_aes_open1_kernel, true)
 // list's front, then row r's segment, hot[] and rowseg[] from the partition), rebuilding only the
 // key-dependent tables (round keys, the byte-position GHASH table of H^8, the half tables of
 // H^1..H^7: a few us)
-// between them, its 16 waves striding the segment's tiles. The 12-wave multi-key kernel pays for
+// between them, its waves striding the segment's tiles. The multi-key kernel pays for
 // key changes per tile instead (per-lane key set-up, the bit-holed final multiply: 1024-key C 21 %
 // slower than one key on the same packets, profiles/r03p_scatter_probe.json).
 // Segments go to workgroups dynamically (r04): thread 0 claims the next one from head 0 of the
