@@ -500,6 +500,11 @@ using namespace mq;
 #define MQ_AES_SINGLE_WAVES 12
 #endif
 constexpr int aes_waves(bool single) { return single ? MQ_AES_SINGLE_WAVES : (int)kAesMultiWaves; }
+// the key-segmented single-key kernels (mq_aes_seals / opens_kernel)
+#ifndef MQ_AES_SEG_WAVES
+#define MQ_AES_SEG_WAVES MQ_AES_SINGLE_WAVES
+#endif
+constexpr int aes_seg_waves() { return MQ_AES_SEG_WAVES; }
 // Work distribution (r04): every wave runs its first tile by grid position, then claims chunks of
 // the rest dynamically (mq_tile.h for_tiles, TileSched; guided chunk sizes, one head per XCD),
 // when the launch has a schedule slot. That replaced (a) the static stride, under which a workgroup
@@ -707,7 +712,7 @@ __device__ __forceinline__ void aes_seg_tiles(const KeyRow* __restrict__ kt, uin
                                               const uint32_t* __restrict__ rowseg, uint8_t* __restrict__ status,
                                               uint64_t* __restrict__ pn_out, const uint2* __restrict__ hpm,
                                               uint32_t* __restrict__ sched) {
-  constexpr uint32_t W = aes_waves(true);
+  constexpr uint32_t W = aes_seg_waves();
   __shared__ uint32_t s_seg;
   build_tw(threadIdx.x, blockDim.x);  // key-independent: once
   const uint32_t w = wave_id();
@@ -743,13 +748,13 @@ __device__ __forceinline__ void aes_seg_tiles(const KeyRow* __restrict__ kt, uin
   }
   sched_done(sched);  // after the loop's last barrier
 }
-extern "C" __global__ __launch_bounds__(64 * aes_waves(true)) void mq_aes_seals_kernel(
+extern "C" __global__ __launch_bounds__(64 * aes_seg_waves()) void mq_aes_seals_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
     const mq_pkt_desc* __restrict__ desc, const uint32_t* __restrict__ list, const uint32_t* __restrict__ hot,
     const uint32_t* __restrict__ rowseg, uint8_t* __restrict__ status, uint32_t* __restrict__ sched) {
   aes_seg_tiles<false>(kt, n_rows, arena, arena_len, desc, list, hot, rowseg, status, nullptr, nullptr, sched);
 }
-extern "C" __global__ __launch_bounds__(64 * aes_waves(true)) void mq_aes_opens_kernel(
+extern "C" __global__ __launch_bounds__(64 * aes_seg_waves()) void mq_aes_opens_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
     const mq_pkt_desc* __restrict__ desc, const uint32_t* __restrict__ list, const uint32_t* __restrict__ hot,
     const uint32_t* __restrict__ rowseg, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,
@@ -840,10 +845,10 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
   if (rowseg && index && hot && n_rows > 1 && !own_hp) {
     const uint32_t blocks = (uint32_t)(cus > 0 ? cus : 256);
     if (open)
-      hipLaunchKernelGGL(mq_aes_opens_kernel, dim3(blocks), dim3(64 * aes_waves(true)), 0, s, kt, n_rows, arena,
+      hipLaunchKernelGGL(mq_aes_opens_kernel, dim3(blocks), dim3(64 * aes_seg_waves()), 0, s, kt, n_rows, arena,
                          arena_len, desc, index, hot, rowseg, status, pn_out, hpm, sched_s);
     else
-      hipLaunchKernelGGL(mq_aes_seals_kernel, dim3(blocks), dim3(64 * aes_waves(true)), 0, s, kt, n_rows, arena,
+      hipLaunchKernelGGL(mq_aes_seals_kernel, dim3(blocks), dim3(64 * aes_seg_waves()), 0, s, kt, n_rows, arena,
                          arena_len, desc, index, hot, rowseg, status, sched_s);
     return hipGetLastError();
   }
