@@ -314,10 +314,15 @@ int mq_batch_open(const mq_keytable* kt, uint8_t* arena, uint64_t arena_len,
  * 0x40 | key_phase << 2 | pn_len - 1), encode_pn, PADDING (Initial to 1200 with pad_to_min,
  * else pn_len + payload + tag >= 20), seal with AAD = header || PN, header protection — writing
  * the protected packet at out + req.out_offset. pkt_len[i] = packet length (MQ_OK), or the
- * reference's `needed` for MQ_ERR_BUFFER_TOO_SMALL. Packets that fail leave `out` untouched.
- * MQ_ERR_INVALID_ARG per packet for a bad conn / level / key row / range. `frames`, `out`,
- * `conns`, `req`, `status`, `pkt_len` and `workspace` (mq_batch_protect_workspace_size(n)
- * bytes) are device memory; frames and out must not overlap. */
+ * reference's `needed` for MQ_ERR_BUFFER_TOO_SMALL, else 0. Packets that fail leave `out`
+ * untouched. Per packet, in this order: MQ_ERR_INVALID_ARG for a bad conn / level / key row /
+ * range; MQ_ERR_SUITE for a row of another suite than suite_hint (MQ_SUITE_MIXED: any) or an
+ * Initial row that is not AES-128-GCM; MQ_ERR_INVALID_ARG for a CID over 20 bytes; then the
+ * buffer checks; a row of neither suite fails the seal (MQ_ERR_SUITE). With MQ_SUITE_CHACHA20
+ * the whole batch is one kernel that builds each packet in LDS and seals it there (the
+ * workspace is then unused). `frames`, `out`, `conns`, `req`, `status`, `pkt_len` and
+ * `workspace` (mq_batch_protect_workspace_size(n) bytes) are device memory; frames and out must
+ * not overlap. */
 size_t mq_batch_protect_workspace_size(uint32_t n);
 int mq_batch_protect(const mq_keytable* kt, const mq_conn_send* conns, uint32_t n_conns,
                      const uint8_t* frames, uint64_t frames_len, uint8_t* out, uint64_t out_len,
