@@ -191,7 +191,10 @@ constexpr uint32_t kGhBytes = 8192, kTwBytes = 65536;
 constexpr uint32_t kRkSlotBytes = 2 * 176;  // aes_rk || hp_rk
 __shared__ __attribute__((aligned(16))) uint32_t g_aes_lds[(kGhBytes + kTwBytes) / 4];
 // multi-key tile kernels: per wave, the GHASH half table (gh_mul_half) of its tile's key
-constexpr uint32_t kGhHalfBytes = 4096, kAesMultiWaves = 12;
+#ifndef MQ_AES_MULTI_WAVES
+#define MQ_AES_MULTI_WAVES 12
+#endif
+constexpr uint32_t kGhHalfBytes = 4096, kAesMultiWaves = MQ_AES_MULTI_WAVES;
 __shared__ __attribute__((aligned(16))) uint32_t g_aes_wtab[kAesMultiWaves * kGhHalfBytes / 4];
 // single-key tile kernels: half tables of H^3 .. H^7 for the tag's final multiply (lane j of a
 // packet multiplies by H^e, e = 1..8 blocks after its last one: H^1, H^2 in g_aes_lds's first
