@@ -5,6 +5,9 @@ export TMPDIR=/tmp
 O=gpurun_out/${1:-r04t}
 mkdir -p $O
 L=milli_quic_amd/libmq_aead.so
+echo "== recv tests $(date +%T)"
+timeout -k 10 300 python -u -m pytest tests/test_gpu_recv.py -m gpu -x -q --timeout 150 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
 echo "== ab_e $(date +%T)"
 timeout -k 10 600 python tools/ab.py e 1048576 $L tools/ab_libs/m8.so > $O/ab_e.txt 2>&1 || { cat $O/ab_e.txt; exit 1; }
 grep sum $O/ab_e.txt
