@@ -239,11 +239,14 @@ __device__ __forceinline__ ConnState load_state(const mq_conn_recv& c) {
 __device__ __forceinline__ void unmask(const RecvWork& w, const uint8_t* arena, uint2 m, RecvPlan& p) {
   const bool lng = w.level != MQ_LEVEL_APPLICATION;
   const uint8_t* pk = arena + w.offset;
-  const uint8_t b0 = pk[0] ^ ((uint8_t)m.x & (lng ? 0x0f : 0x1f));
+  // the first byte and the four bytes at pn_offset in one round of loads (a pending packet has
+  // pn_offset + 20 <= len, so all four lie inside it)
+  const uint8_t raw0 = pk[0];
+  const uint32_t pnw = *(const u32_u*)(pk + w.pn_off) ^ ((m.x >> 8) | (m.y << 24));
+  const uint8_t b0 = raw0 ^ ((uint8_t)m.x & (lng ? 0x0f : 0x1f));
   const uint32_t pn_len = (b0 & 3u) + 1;
-  const uint32_t mk = (m.x >> 8) | (m.y << 24);
   uint32_t trunc = 0;
-  for (uint32_t b = 0; b < pn_len; ++b) trunc = (trunc << 8) | (uint8_t)(pk[w.pn_off + b] ^ (uint8_t)(mk >> (8 * b)));
+  for (uint32_t b = 0; b < pn_len; ++b) trunc = (trunc << 8) | ((pnw >> (8 * b)) & 0xffu);
   p.trunc = trunc;
   p.pn_len = (uint8_t)pn_len;
   p.phase = (b0 >> 2) & 1;
