@@ -57,6 +57,14 @@ __device__ __forceinline__ void ast_block(uint8_t* p, const uint32_t (&w)[4], ui
   if (rem >= 16) ast16(p, w);
   else st_bytes(p, w, rem);
 }
+// bytes [lo, hi) of a 16-B block at p
+__device__ __forceinline__ void st_range(uint8_t* p, const uint32_t (&w)[4], uint32_t lo, uint32_t hi) {
+  if (lo == 0 && hi >= 16) {
+    st16(p, w);
+    return;
+  }
+  for (uint32_t b = lo; b < hi; ++b) p[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+}
 
 // DirectionalKeys::nonce (src/crypto/mod.rs:66-74), as big-endian AES input words
 __device__ __forceinline__ void nonce_be(const KeyRow* row, uint64_t pn, uint32_t (&nb)[3]) {
@@ -256,6 +264,23 @@ struct AesStream {
     uint4 cur = data(j + kLanesPerPkt * it_lo);
     const int it_lean = lean_end(k.act, k.P);
     const bool fin8 = fin_in_loop(k, j);
+#if MQ_AES_DEFER
+    // First-line deferral (r04, build option, off in the product): the payload bytes in the rest of
+    // the packet's first 128-B line (after the header; at most blocks 1-7, iteration 0) are stored
+    // at the end, with the tag and the header-protection bytes, so that line — shared with the
+    // previous packet's tail, which is written last — goes to HBM once instead of as an early and a
+    // late partial write. Measured (profiles/r04v_ab_aes_defer.txt): C seal writes 1.38 -> 1.31 GB
+    // (1.10 -> 1.045 x algorithmic) but the seal 3-5 % slower (C, C/1024 keys: one more spilled
+    // VGPR in the tile loop and the split block's byte stores), so the product keeps the writes.
+    // Single-key kernels only: the multi-key ones have no registers to spare (15 -> 41 spills).
+    const uint32_t line_rest = 128u - (uint32_t)(k.pkt & 127u);
+    const uint32_t dl = (GH != kGhWorkgroup || !k.act || k.rec || line_rest <= k.aad_len)
+                            ? 0u
+                            : min(min(line_rest - k.aad_len, 112u), k.P);
+#else
+    const uint32_t dl = 0;
+#endif
+    uint32_t dct[4] = {0, 0, 0, 0}, dn = 0, doff = 0;  // this lane's deferred bytes (one block at most)
 #pragma nounroll
     for (int it = it_lo; it < it_hi; ++it) {
       const int b = j + kLanesPerPkt * it;
@@ -298,7 +323,15 @@ struct AesStream {
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) ct[q] = pt[q] ^ ks[q];
-        ast_block(arena + k.pay + off, ct, rem);
+        if (off < dl) {  // its first bytes are in the packet's first line: kept for the end
+#pragma unroll
+          for (int q = 0; q < 4; ++q) dct[q] = ct[q];
+          doff = off;
+          dn = min(rem, dl - off);
+          if (dn < rem) st_range(arena + k.pay + off, ct, dn, rem);
+        } else {
+          ast_block(arena + k.pay + off, ct, rem);
+        }
         gh_block(ct, rem, x);
         has = true;
       } else if (k.act && b <= 0 && b >= 1 - (int)k.A) {  // AAD block A + b - 1
@@ -329,6 +362,7 @@ struct AesStream {
     uint32_t tag[4];
     finish(acc, row, j, k, ej0, tag);
     if (k.act && j == 0) st16(arena + k.pay + k.P, tag);
+    if (dn) st_range(arena + k.pay + doff, dct, 0, dn);  // the first line's deferred bytes
     // packets of fewer than 7 CTR blocks (no free slot for the HP block; a sample that may reach
     // into the tag): one more AES block for the wave once ciphertext and tag are stored — length-
     // sorted batches put such packets in a few tiles of their own
