@@ -56,7 +56,7 @@ __device__ __forceinline__ bool pass_empty(const uint32_t* live) { return live &
 // What the partition reads of a descriptor: key row, length, and whether the row is AES-128-GCM.
 // A thread's kPartItems descriptors are fetched together (fields first, then the rows' suites),
 // so it waits on memory twice rather than twice per descriptor.
-struct PartItem { uint32_t key, len; bool aes; };
+struct PartItem { uint32_t key, len, nch; bool aes; };  // nch: 16-B chunks of its LDS image
 __device__ __forceinline__ void part_fetch(const KeyRow* __restrict__ kt, uint32_t n_rows,
                                            const mq_pkt_desc* __restrict__ desc, uint32_t n,
                                            PartItem (&it)[kPartItems]) {
@@ -66,6 +66,7 @@ __device__ __forceinline__ void part_fetch(const KeyRow* __restrict__ kt, uint32
     const uint32_t i = base + k * kPartThreads;
     it[k].key = i < n ? desc[i].key_id : 0xFFFFFFFFu;
     it[k].len = i < n ? desc[i].len : 0u;
+    it[k].nch = i < n ? (((uint32_t)desc[i].offset & 15u) + it[k].len + 15u) >> 4 : 0u;
   }
 #pragma unroll
   for (int k = 0; k < kPartItems; ++k) it[k].aes = it[k].key < n_rows && kt[it[k].key].suite == MQ_SUITE_AES128GCM;
@@ -108,11 +109,16 @@ __device__ __forceinline__ uint2 block_vote(uint2 v) {  // kPartThreads threads:
 // alignment (4b + 5 chunks), so the class's tiles stay on the staged path; classes that would
 // need fewer than kMinPpt per tile (and the open-ended last one) keep 8 and take the direct path.
 constexpr uint32_t kMinPpt = 5;
-__device__ __forceinline__ uint32_t class_ppt(uint32_t c) {
+// cmax (r04): the largest image of the class's packets in this batch, in chunks (the count
+// kernel's atomicMax; 0 = no packet), so aligned packets are not priced at the worst alignment —
+// 1200-B packets at 16-B offsets take 75 chunks, 8 to a tile, where the class bound (77) gave 7
+// and a receive batch of 1200-B packets ran 8/7 as many tiles.
+__device__ __forceinline__ uint32_t class_ppt(uint32_t c, uint32_t cmax) {
   if (c < 2 * kLenClasses) return kPktsPerTile;  // groups 0 and 1: AES
   const uint32_t b = kLenClasses - 1 - (c % kLenClasses);
   if (b == kLenClasses - 1) return kPktsPerTile;
-  const uint32_t x = kBudgetChunks / (4 * b + 5);
+  const uint32_t worst = 4 * b + 5, need = cmax && cmax < worst ? cmax : worst;
+  const uint32_t x = kBudgetChunks / need;
   return x >= kPktsPerTile ? kPktsPerTile : (x >= kMinPpt ? x : kPktsPerTile);
 }
 }  // namespace
@@ -159,8 +165,9 @@ __device__ __forceinline__ uint32_t fold_votes(const uint2* __restrict__ votes, 
 extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_init_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_pkt_desc* __restrict__ desc, uint32_t n,
     uint2* __restrict__ votes, uint32_t nv, uint4* __restrict__ list, uint32_t list_q, uint4* __restrict__ bins,
-    uint32_t bins_q, const uint32_t* __restrict__ live) {
+    uint32_t bins_q, const uint32_t* __restrict__ live, uint32_t* __restrict__ cmax) {
   if (pass_empty(live)) return;
+  if (blockIdx.x == 0 && threadIdx.x < kLenClasses) cmax[threadIdx.x] = 0;
   if (blockIdx.x < nv) {  // block-uniform
     const uint2 v = vote_slice(kt, n_rows, desc, n, blockIdx.x);
     if (threadIdx.x == 0) votes[blockIdx.x] = v;
@@ -177,12 +184,14 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_count_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_pkt_desc* __restrict__ desc, uint32_t n,
     uint32_t nblocks, const uint2* __restrict__ votes, uint32_t nv, uint32_t* __restrict__ hot_p,
     uint32_t* __restrict__ hist, uint32_t* __restrict__ bins, uint32_t skip_unkeyed,
-    const uint32_t* __restrict__ live) {
+    const uint32_t* __restrict__ live, uint32_t* __restrict__ cmax) {
   if (pass_empty(live)) return;
   __shared__ uint32_t s_cnt[kClasses];
+  __shared__ uint32_t s_max[kLenClasses];  // list 1's classes: the largest image, in chunks
   PartItem it[kPartItems];
   part_fetch(kt, n_rows, desc, n, it);
   if (threadIdx.x < kClasses) s_cnt[threadIdx.x] = 0;
+  if (threadIdx.x < kLenClasses) s_max[threadIdx.x] = 0;
   const uint32_t hot = fold_votes(votes, nv);  // the same in every wave of every block
   if (blockIdx.x == 0 && threadIdx.x == 0) *hot_p = hot;  // for the scatter
   __syncthreads();
@@ -196,6 +205,7 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_count_kernel(
     kd[k] = bins && in && c / kLenClasses == 1;
     kb[k] = kd[k] ? key_bin(it[k]) : 0u;
     if (in && !kd[k]) atomicAdd(&s_cnt[c], 1u);
+    if (in && c >= 2 * kLenClasses) atomicMax(&s_max[c - 2 * kLenClasses], it[k].nch);
   }
   // keyed bins: one global atomic per distinct bin of the thread's items (a thread's items are
   // kPartThreads descriptors apart: with keys assigned round-robin over 1024 rows, as in config C
@@ -214,6 +224,7 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_count_kernel(
   }
   __syncthreads();
   if (threadIdx.x < kClasses) hist[(size_t)threadIdx.x * nblocks + blockIdx.x] = s_cnt[threadIdx.x];
+  if (threadIdx.x < kLenClasses && s_max[threadIdx.x]) atomicMax(&cmax[threadIdx.x], s_max[threadIdx.x]);
 }
 
 // Single workgroup: per class, the exclusive scan of its per-block counts (in place: the rank of
@@ -236,7 +247,8 @@ extern "C" __global__ __launch_bounds__(64 * kScanWaves) void mq_part_scan_kerne
                                                                                  uint32_t* __restrict__ bins,
                                                                                  uint32_t n_rows,
                                                                                  uint32_t* __restrict__ rowseg,
-                                                                                 const uint32_t* __restrict__ live) {
+                                                                                 const uint32_t* __restrict__ live,
+                                                                                 const uint32_t* __restrict__ cmax) {
   if (pass_empty(live)) {  // empty lists: no hot key, no row segments
     if (threadIdx.x == 0) { counts[0] = 0; counts[1] = 0; counts[2] = kNoKey; counts[3] = 0; }
     if (rowseg)
@@ -284,7 +296,7 @@ extern "C" __global__ __launch_bounds__(64 * kScanWaves) void mq_part_scan_kerne
   if (wave < 2) {  // wave s lays out list s: lane = class (list 0: classes 0..63, list 1: 64..95)
     const uint32_t s = (uint32_t)wave, c = (s == 0 ? 0u : 2 * kLenClasses) + (uint32_t)lane;
     const bool in = c < (s == 0 ? 2 * kLenClasses : kClasses);
-    const uint32_t ppt = in ? class_ppt(c) : 1u;
+    const uint32_t ppt = in ? class_ppt(c, c >= 2 * kLenClasses ? cmax[c - 2 * kLenClasses] : 0u) : 1u;
     const uint32_t ent = in ? kPktsPerTile * ((s_tot[c] + ppt - 1) / ppt) : 0u;
     const uint32_t incl = wave_incl_scan(ent), e = lane_u32(incl, kWave - 1);
     if (in) seg[c] = s * cap + incl - ent;
@@ -375,9 +387,11 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_scatter_kerne
     const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_pkt_desc* __restrict__ desc, uint32_t n,
     uint32_t nblocks, const uint32_t* __restrict__ hot_p, const uint32_t* __restrict__ hist,
     const uint32_t* __restrict__ seg, uint32_t* __restrict__ list, uint32_t* __restrict__ bins,
-    uint32_t skip_unkeyed, const uint32_t* __restrict__ live) {
+    uint32_t skip_unkeyed, const uint32_t* __restrict__ live, const uint32_t* __restrict__ cmax) {
   if (pass_empty(live)) return;
   __shared__ uint32_t s_rank[kClasses];
+  __shared__ uint32_t s_cmax[kLenClasses];
+  if (threadIdx.x < kLenClasses) s_cmax[threadIdx.x] = cmax[threadIdx.x];
   PartItem it[kPartItems];
   part_fetch(kt, n_rows, desc, n, it);
   const uint32_t hot = *hot_p;
@@ -435,7 +449,7 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_scatter_kerne
     const int leader = in ? __ffsll((unsigned long long)peers) - 1 : lane;
     base = (uint32_t)__shfl((int)base, leader, kWave);
     if (in) {
-      const uint32_t r = base + rank, ppt = class_ppt(c);
+      const uint32_t r = base + rank, ppt = class_ppt(c, c >= 2 * kLenClasses ? s_cmax[c - 2 * kLenClasses] : 0u);
       list[seg[c] + kPktsPerTile * (r / ppt) + r % ppt] = i;
     }
   }
@@ -450,8 +464,9 @@ static bool keyed_layout(uint32_t n, uint32_t n_rows) {
          (uint64_t)n + kPktsPerTile * kLenClasses + (uint64_t)(kPktsPerTile - 1) * n_rows <= mq_partition_list_cap(n);
 }
 
-// meta: counts[0..1] | hot row | hot segment entries | seg[kClasses] | slice votes (kVoteSlices pairs)
-constexpr uint32_t kMetaWords = 4 + kClasses + 2 * kVoteSlices;
+// meta: counts[0..1] | hot row | hot segment entries | seg[kClasses] | slice votes (kVoteSlices pairs) |
+// cmax[kLenClasses] (list 1's largest image per class, chunks)
+constexpr uint32_t kMetaWords = 4 + kClasses + 2 * kVoteSlices + kLenClasses;  // + list 1's class maxima
 
 // list (2 x cap entries) | class histograms (kClasses per block) |
 // meta (2 totals, hot row, hot segment entries, kClasses segment starts) | keyed bins, 256-B aligned pieces
@@ -474,6 +489,7 @@ hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_d
   uint32_t* hot = counts + 2;  // meta (kMetaWords): counts[0..1] | hot row | hot entries | seg | votes
   uint32_t* seg = counts + 4;
   uint2* votes = (uint2*)(counts + 4 + kClasses);
+  uint32_t* cmax = counts + 4 + kClasses + 2 * kVoteSlices;
   uint32_t* bins = keyed_layout(n, n_rows) ? (uint32_t*)((uint8_t*)counts + part_align(sizeof(uint32_t) * kMetaWords))
                                            : nullptr;
   const uint32_t list_q = cap / 2, bins_q = bins ? kKeyClasses / 4 * n_rows : 0u;  // 16-B words
@@ -482,13 +498,13 @@ hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_d
   const uint32_t S = min(n, kVoteSample), used = (S + kVoteSlice - 1) / kVoteSlice;  // slices with samples
   const uint32_t grid = max(init_blocks, used);
   hipLaunchKernelGGL(mq_part_init_kernel, dim3(grid), dim3(kPartThreads), 0, s, kt, n_rows, desc, n, votes,
-                     max(nv, used), (uint4*)list, list_q, (uint4*)bins, bins_q, live);
+                     max(nv, used), (uint4*)list, list_q, (uint4*)bins, bins_q, live, cmax);
   hipLaunchKernelGGL(mq_part_count_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, kt, n_rows, desc, n,
-                     nblocks, votes, max(nv, used), hot, hist, bins, (uint32_t)skip_unkeyed, live);
+                     nblocks, votes, max(nv, used), hot, hist, bins, (uint32_t)skip_unkeyed, live, cmax);
   hipLaunchKernelGGL(mq_part_scan_kernel, dim3(1), dim3(64 * kScanWaves), 0, s, hist, nblocks, cap, counts, seg,
-                     bins, n_rows, bins ? bins + key_bins(n) : nullptr, live);
+                     bins, n_rows, bins ? bins + key_bins(n) : nullptr, live, cmax);
   hipLaunchKernelGGL(mq_part_scatter_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, kt, n_rows, desc, n,
-                     nblocks, hot, hist, seg, list, bins, (uint32_t)skip_unkeyed, live);
+                     nblocks, hot, hist, seg, list, bins, (uint32_t)skip_unkeyed, live, cmax);
   return hipGetLastError();
 }
 
