@@ -621,12 +621,86 @@ extern "C" __global__ __launch_bounds__(256) void mq_recv_outcome_kernel(const m
   outcome[i] = st1[i] == MQ_OK ? kOk1 : (d2[i].key_id != kNoRow && st2[i] == MQ_OK) ? kOk0 : kFail;
 }
 
+// ---- stable sort of the records by connection (r04) ----------------------------------------------
+// LSD radix sort, 8-bit digits, as many passes as the connection indices need (4096 connections and
+// the padding key: 13 bits, two passes). Per pass: block digit histograms (count), their exclusive
+// scan in digit-major order (hipcub), and a stable scatter — a block's 4096 items in four rounds of
+// 1024 in index order; inside a round, a wave ranks its lanes among equal digits with eight ballots
+// and the waves take their places by a per-digit prefix over the workgroup. r03/r04 used hipcub's
+// SortPairs, which rocprim runs as a block sort plus 18 merge passes for 2^20 pairs at this key
+// width: 158 us (profiles/r04w kernel trace); this is two passes of three kernels.
+constexpr uint32_t kSortThreads = 1024, kSortItems = 4, kSortBlock = kSortThreads * kSortItems, kSortDigits = 256;
+constexpr uint32_t kSortWaves = kSortThreads / kWave;
+
+extern "C" __global__ __launch_bounds__(kSortThreads) void mq_sort_count_kernel(const uint32_t* __restrict__ keys,
+                                                                                uint32_t n, uint32_t shift,
+                                                                                uint32_t nblocks,
+                                                                                uint32_t* __restrict__ hist) {
+  __shared__ uint32_t s_h[kSortDigits];
+  if (threadIdx.x < kSortDigits) s_h[threadIdx.x] = 0;
+  __syncthreads();
+#pragma unroll
+  for (uint32_t k = 0; k < kSortItems; ++k) {
+    const uint32_t i = blockIdx.x * kSortBlock + k * kSortThreads + threadIdx.x;
+    if (i < n) atomicAdd(&s_h[(keys[i] >> shift) & (kSortDigits - 1)], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < kSortDigits) hist[(size_t)threadIdx.x * nblocks + blockIdx.x] = s_h[threadIdx.x];
+}
+
+// vals_in == nullptr: the values are the indices (the first pass)
+extern "C" __global__ __launch_bounds__(kSortThreads) void mq_sort_scatter_kernel(
+    const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, uint32_t n, uint32_t shift,
+    uint32_t nblocks, const uint32_t* __restrict__ hist, uint32_t* __restrict__ keys_out,
+    uint32_t* __restrict__ vals_out) {
+  __shared__ uint32_t s_run[kSortDigits];                // this block's next position per digit
+  __shared__ uint32_t s_wc[kSortWaves][kSortDigits];     // a round's count per (wave, digit)
+  const uint32_t lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  if (threadIdx.x < kSortDigits) s_run[threadIdx.x] = hist[(size_t)threadIdx.x * nblocks + blockIdx.x];
+  for (uint32_t k = 0; k < kSortItems; ++k) {
+    for (uint32_t q = threadIdx.x; q < kSortWaves * kSortDigits; q += kSortThreads) (&s_wc[0][0])[q] = 0;
+    __syncthreads();
+    const uint32_t i = blockIdx.x * kSortBlock + k * kSortThreads + threadIdx.x;
+    const bool in = i < n;
+    const uint32_t key = in ? keys_in[i] : 0u, val = in ? (vals_in ? vals_in[i] : i) : 0u;
+    const uint32_t d = (key >> shift) & (kSortDigits - 1);
+    uint64_t peers = __ballot(in);
+#pragma unroll
+    for (int bit = 0; bit < 8; ++bit) {
+      const uint64_t b = __ballot((d >> bit) & 1u);
+      peers &= ((d >> bit) & 1u) ? b : ~b;
+    }
+    const uint32_t rank = (uint32_t)__popcll(peers & below);
+    if (in && rank == 0) s_wc[w][d] = (uint32_t)__popcll(peers);  // the group's first lane
+    __syncthreads();
+    if (threadIdx.x < kSortDigits) {  // per digit: the waves' exclusive prefix, then the round total
+      uint32_t run = s_run[threadIdx.x];
+#pragma unroll
+      for (uint32_t v = 0; v < kSortWaves; ++v) {
+        const uint32_t c = s_wc[v][threadIdx.x];
+        s_wc[v][threadIdx.x] = run;
+        run += c;
+      }
+      s_run[threadIdx.x] = run;
+    }
+    __syncthreads();
+    if (in) {
+      const uint32_t pos = s_wc[w][d] + rank;
+      keys_out[pos] = key;
+      vals_out[pos] = val;
+    }
+    __syncthreads();  // s_wc is rewritten by the next round
+  }
+}
+
 // ---- launch helpers ------------------------------------------------------------------------------
 namespace {
 size_t al(size_t b) { return (b + 255) & ~(size_t)255; }
 
 struct RecvWs {
   uint32_t *counts, *base, *total, *keys, *vals, *skeys, *svals, *seg_lo, *seg_hi, *attempts;
+  uint32_t *shist, *tkeys, *tvals;  // the sort's digit histograms and ping-pong buffers
   RecvWork *work, *work_s;
   RecvPlan *hdr_s, *tried;
   mq_conn_recv* conn0;
@@ -639,11 +713,13 @@ struct RecvWs {
   size_t bytes;
 };
 
+uint32_t sort_blocks(uint32_t n) { return (n + kSortBlock - 1) / kSortBlock; }
+
 size_t cub_bytes(uint32_t n_dgrams, uint32_t max_pkts) {
   size_t a = 0, b = 0;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, a, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n_dgrams + 1);
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                           (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)max_pkts, 0, 32);
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                         (int)(kSortDigits * sort_blocks(max_pkts)));
   return a > b ? a : b;
 }
 
@@ -659,6 +735,9 @@ RecvWs layout(uint8_t* p, uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_conns
   w.vals = (uint32_t*)take(4ull * max_pkts);
   w.skeys = (uint32_t*)take(4ull * max_pkts);
   w.svals = (uint32_t*)take(4ull * max_pkts);
+  w.shist = (uint32_t*)take(4ull * kSortDigits * sort_blocks(max_pkts));
+  w.tkeys = (uint32_t*)take(4ull * max_pkts);
+  w.tvals = (uint32_t*)take(4ull * max_pkts);
   w.seg_lo = (uint32_t*)take(4ull * n_conns);
   w.seg_hi = (uint32_t*)take(4ull * n_conns);
   w.conn0 = (mq_conn_recv*)take(sizeof(mq_conn_recv) * (size_t)n_conns);
@@ -725,15 +804,29 @@ hipError_t mq_recv_front(const KeyRow* kt, uint32_t n_rows, mq_conn_recv* conns,
                      n_rows, w.keys, w.vals, w.d1);
   if ((e = mq_launch_chacha_prepass(kt, n_rows, arena, arena_len, w.d1, max_pkts, w.hpm, s)) != hipSuccess) return e;
   if ((e = mq_launch_aes_prepass(kt, n_rows, arena, arena_len, w.d1, max_pkts, w.hpm, s)) != hipSuccess) return e;
-  size_t cb = w.cub_bytes;
   // keys are connection indices (< n_conns) and 0xFFFFFFFF past the packet count: the low
   // ceil(log2(n_conns + 1)) bits order them (the padding's all-ones bits sort last), so the radix
   // sort makes that many passes' worth of digits instead of 32 bits' 
   int end_bit = 1;
   while (end_bit < 32 && (1ull << end_bit) <= (uint64_t)n_conns) ++end_bit;
-  if ((e = hipcub::DeviceRadixSort::SortPairs(w.cub, cb, w.keys, w.skeys, w.vals, w.svals, (int)max_pkts, 0, end_bit,
-                                              s)) != hipSuccess)
-    return e;
+  {  // stable LSD passes of 8-bit digits; the last one writes skeys / svals
+    const uint32_t passes = ((uint32_t)end_bit + 7) / 8, nb = sort_blocks(max_pkts);
+    const uint32_t* kin = w.keys;
+    const uint32_t* vin = nullptr;  // first pass: the values are the indices
+    for (uint32_t p = 0; p < passes; ++p) {
+      uint32_t* kout = ((passes - 1 - p) % 2 == 0) ? w.skeys : w.tkeys;
+      uint32_t* vout = ((passes - 1 - p) % 2 == 0) ? w.svals : w.tvals;
+      hipLaunchKernelGGL(mq_sort_count_kernel, dim3(nb), dim3(kSortThreads), 0, s, kin, max_pkts, 8 * p, nb, w.shist);
+      size_t sb = w.cub_bytes;
+      if ((e = hipcub::DeviceScan::ExclusiveSum(w.cub, sb, w.shist, w.shist, (int)(kSortDigits * nb), s)) != hipSuccess)
+        return e;
+      hipLaunchKernelGGL(mq_sort_scatter_kernel, dim3(nb), dim3(kSortThreads), 0, s, kin, vin, max_pkts, 8 * p, nb,
+                         (const uint32_t*)w.shist, kout, vout);
+      kin = kout;
+      vin = vout;
+    }
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
   if (n_conns) {
     if ((e = hipMemsetAsync(w.seg_lo, 0, 4ull * n_conns, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(w.seg_hi, 0, 4ull * n_conns, s)) != hipSuccess) return e;
