@@ -158,3 +158,29 @@ def test_fuzz_batches_vs_oracle(orc, seed):
         ok = o_st == 0
         quic = (opn["flags"] & _lib.MQ_PKT_NO_HP) == 0
         assert (g_pn[ok & quic] == o_pn[ok & quic]).all(), hint
+
+
+@pytest.mark.parametrize("first_row", ["chacha", "empty"])
+def test_fuzz_single_non_aes_row(orc, first_row):
+    # r04: a key table whose only non-AES row is row 0 runs the mixed batch's second list on the
+    # single-key ChaCha kernels (key material of that row in SGPRs). Every other row is AES; the
+    # batch's out-of-range key ids land in the same list and must still fail alone, and an empty
+    # (suite 0) row 0 must fail its packets with MQ_ERR_SUITE
+    keys, arena, seal, opn = random_batch(505 if first_row == "chacha" else 606, 3000)
+    rng = np.random.default_rng(7)
+    for r in range(1, len(keys)):
+        keys[r] = make_key_material(_lib.MQ_SUITE_AES128GCM, rng.bytes(16), rng.bytes(12), rng.bytes(16))
+    if first_row == "empty":
+        keys[0] = _lib.KeyMaterial()
+    g_out, g_st, _ = gpu(keys, arena, seal, _lib.MQ_SUITE_MIXED, False)
+    o_out, o_st, _ = oracle(orc, keys, arena, seal, _lib.MQ_SUITE_MIXED, False)
+    assert (g_st == o_st).all(), np.nonzero(g_st != o_st)[0][:10]
+    assert g_out.tobytes() == o_out.tobytes()
+    on0 = seal["key_id"] == 0
+    assert on0.sum() > 300 and (o_st[on0] == 0).any() == (first_row == "chacha")
+    g_back, g_st, g_pn = gpu(keys, o_out, opn, _lib.MQ_SUITE_MIXED, True)
+    o_back, o_st, o_pn = oracle(orc, keys, o_out, opn, _lib.MQ_SUITE_MIXED, True)
+    assert (g_st == o_st).all(), np.nonzero(g_st != o_st)[0][:10]
+    assert g_back.tobytes() == o_back.tobytes()
+    ok = (o_st == 0) & ((opn["flags"] & _lib.MQ_PKT_NO_HP) == 0)
+    assert (g_pn[ok] == o_pn[ok]).all()

@@ -41,14 +41,15 @@ def gpu_recv(keys, conns, arena, dgrams, max_pkts):
 
 @pytest.mark.parametrize("seed,n_conns,n_app,tamper_flip", [(3, 6, 20, False), (11, 64, 60, False),
                                                             (5, 16, 30, True), (13, 4, 300, False),
-                                                            (17, 3, 450, True)])
+                                                            (17, 3, 450, True), (19, 300, 12, False)])
 def test_recv_vs_oracle(orc, seed, n_conns, n_app, tamper_flip):
     # tamper_flip: the first packet after a key-phase flip fails to open, so the
     # walk's speculation (it rotated there) is wrong; the next packet must be reported as the
     # reference's next-generation open (key_gen 2) and rotate the connection. The 300- / 450-packet
     # runs span several of the walk's 64-packet chunks (r04): chunks decided in parallel, chunks
     # replayed sequentially (PN-window crossings, the key update, tampered packets), and the later
-    # walks' settled prefixes ending at a failed packet
+    # walks' settled prefixes ending at a failed packet. 300 connections: the record sort takes two
+    # 8-bit digit passes (r04's own stable radix sort)
     keys, conns, scripts = build_traffic(orc, seed=seed, n_conns=n_conns, n_app=n_app, tamper_flip=tamper_flip)
     arena, dgrams = assemble(orc, keys, conns, scripts, seed=seed)
     oc, oa = conns.copy(), arena.copy()
