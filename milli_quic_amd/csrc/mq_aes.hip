@@ -736,64 +736,100 @@ MQ_AES_KERNELS(mq_aes_seal1_kernel, mq_aes_open1_kernel, true)
 // between them, its waves striding the segment's tiles. The multi-key kernel pays for
 // key changes per tile instead (per-lane key set-up, the bit-holed final multiply: 1024-key C 21 %
 // slower than one key on the same packets, profiles/r03p_scatter_probe.json).
-// Segments go to workgroups dynamically (r04): thread 0 claims the next one from head 0 of the
-// launch's schedule slot (one claim per segment, 256 pullers), so a workgroup placed late takes none
-// of the others' (static: segments blockIdx.x, + gridDim.x, ...).
+// Work goes to workgroups in SLICES of the list (r04): list 0 is the hot key's segment followed by
+// the rows' segments, back to back in whole tiles, and slice u is its tiles [uP, uP + P), P =
+// list tiles / (4 x workgroups) clamped to [16, 128] (config C with 1024 keys: 128, one row's
+// segment per slice). A workgroup claims slices from head 0 of the launch's schedule slot (or by
+// stride without one) and runs the part of each segment inside its slice, rebuilding the tables
+// only when the row changes. Until r04 the unit was a whole segment: with two keys of 2^19 packets
+// each, each segment ran on ONE workgroup, 6.3 GiB/s (gpurun_out/r04za).
+constexpr uint32_t kSegMinSlice = 16, kSegMaxSlice = 128;  // tiles
+
+// the row whose segment holds list entry e >= rowseg[0] (the first row's start): the last row r
+// with rowseg[2r] <= e (a row without packets starts where the next one does, so the last of
+// equal starts is the one with packets). 64-ary search, every wave computing the same answer.
+__device__ __forceinline__ uint32_t seg_row_of(const uint32_t* __restrict__ rowseg, uint32_t n_rows, uint32_t e) {
+  const int lane = (int)(threadIdx.x & (kWave - 1));
+  uint32_t lo = 0, span = n_rows;  // the answer lies in [lo, lo + span)
+  while (span > 1) {               // uniform
+    const uint32_t step = (span + kWave - 1) / kWave, idx = lo + (uint32_t)lane * step;
+    const bool ok = idx < lo + span && rowseg[2 * (size_t)idx] <= e;  // a prefix of the lanes (lane 0 holds)
+    const uint64_t m = __ballot(ok);
+    const uint32_t k = 63u - (uint32_t)__builtin_clzll(m | 1ull);
+    const uint32_t nlo = lo + k * step;
+    span = min(step, lo + span - nlo);
+    lo = nlo;
+  }
+  return lo;
+}
+
 template <bool OPEN>
 __device__ __forceinline__ void aes_seg_tiles(const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena,
                                               uint64_t arena_len, const mq_pkt_desc* __restrict__ desc,
-                                              const uint32_t* __restrict__ list, const uint32_t* __restrict__ hot,
-                                              const uint32_t* __restrict__ rowseg, uint8_t* __restrict__ status,
-                                              uint64_t* __restrict__ pn_out, const uint2* __restrict__ hpm,
-                                              uint32_t* __restrict__ sched) {
+                                              const uint32_t* __restrict__ list, const uint32_t* __restrict__ n_dev,
+                                              const uint32_t* __restrict__ hot, const uint32_t* __restrict__ rowseg,
+                                              uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,
+                                              const uint2* __restrict__ hpm, uint32_t* __restrict__ sched) {
   constexpr uint32_t W = aes_seg_waves();
   __shared__ uint32_t s_seg;
   build_tw(threadIdx.x, blockDim.x);  // key-independent: once
   const uint32_t w = wave_id();
-  uint32_t sg = blockIdx.x;
-  for (;;) {  // segment 0: the hot key; 1 + r: row r
-    __syncthreads();  // every wave is done with the previous segment (its tables, s_seg)
+  const uint32_t entries = __builtin_amdgcn_readfirstlane(*n_dev), tiles = entries / kPktsPerTile;
+  const uint32_t hot_row = __builtin_amdgcn_readfirstlane(hot[0]), hot_e = __builtin_amdgcn_readfirstlane(hot[1]);
+  const uint32_t P = min(max((tiles + 4 * gridDim.x - 1) / (4 * gridDim.x), kSegMinSlice), kSegMaxSlice);
+  uint32_t sg = blockIdx.x, built = 0xFFFFFFFFu;  // built: the row whose tables are in LDS
+  for (;;) {
+    __syncthreads();  // every wave is done with the previous slice (its tiles, s_seg)
     if (sched) {
       if (threadIdx.x == 0)
         s_seg = __hip_atomic_fetch_add(sched, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __syncthreads();
       sg = s_seg;
     }
-    if (sg > n_rows) break;  // workgroup-uniform
-    uint32_t row, first, ent;
-    if (sg == 0) {
-      row = hot[0];
-      first = 0;
-      ent = hot[1];
-    } else {
-      row = sg - 1;
-      first = rowseg[2 * row];
-      ent = rowseg[2 * row + 1];
-    }
-    row = __builtin_amdgcn_readfirstlane(row);
-    first = __builtin_amdgcn_readfirstlane(first);
-    ent = __builtin_amdgcn_readfirstlane(ent);
+    if ((uint64_t)sg * P >= tiles) break;  // workgroup-uniform
+    const uint32_t e1 = kPktsPerTile * min(sg * P + P, tiles);
+    uint32_t e = kPktsPerTile * sg * P;
     if (!sched) sg += gridDim.x;
-    if (row >= n_rows || ent == 0) continue;  // workgroup-uniform
-    const KeyRow* ks = kt + row;  // the segment's row as a one-row table (validation uses n_rows)
-    aes_key_tables(ks);  // ends with a barrier
-    aes_stream_tiles<true, OPEN>(ks, n_rows, arena, arena_len, desc, first + ent, list, nullptr, status, pn_out, hpm,
-                                 first / kPktsPerTile, TileSched{nullptr, w, W, 0});
+    while (e < e1) {  // the segments overlapping the slice, workgroup-uniform
+      uint32_t row, end;
+      if (e < hot_e) {
+        row = hot_row;
+        end = hot_e;
+      } else {
+        const uint32_t r = __builtin_amdgcn_readfirstlane(seg_row_of(rowseg, n_rows, e));
+        row = r;
+        end = __builtin_amdgcn_readfirstlane(rowseg[2 * (size_t)r] + rowseg[2 * (size_t)r + 1]);
+      }
+      end = min(end, e1);
+      if (end <= e) break;  // no segment holds e (a broken layout: leave the slice)
+      if (row < n_rows) {
+        const KeyRow* ks = kt + row;  // the segment's row as a one-row table (validation uses n_rows)
+        if (row != built) {
+          __syncthreads();  // the previous segment's tiles are done with the tables
+          aes_key_tables(ks);  // ends with a barrier
+          built = row;
+        }
+        aes_stream_tiles<true, OPEN>(ks, n_rows, arena, arena_len, desc, end, list, nullptr, status, pn_out, hpm,
+                                     e / kPktsPerTile, TileSched{nullptr, w, W, 0});
+      }
+      e = end;
+    }
   }
   sched_done(sched);  // after the loop's last barrier
 }
 extern "C" __global__ __launch_bounds__(64 * aes_seg_waves()) void mq_aes_seals_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
-    const mq_pkt_desc* __restrict__ desc, const uint32_t* __restrict__ list, const uint32_t* __restrict__ hot,
-    const uint32_t* __restrict__ rowseg, uint8_t* __restrict__ status, uint32_t* __restrict__ sched) {
-  aes_seg_tiles<false>(kt, n_rows, arena, arena_len, desc, list, hot, rowseg, status, nullptr, nullptr, sched);
+    const mq_pkt_desc* __restrict__ desc, const uint32_t* __restrict__ list, const uint32_t* __restrict__ n_dev,
+    const uint32_t* __restrict__ hot, const uint32_t* __restrict__ rowseg, uint8_t* __restrict__ status,
+    uint32_t* __restrict__ sched) {
+  aes_seg_tiles<false>(kt, n_rows, arena, arena_len, desc, list, n_dev, hot, rowseg, status, nullptr, nullptr, sched);
 }
 extern "C" __global__ __launch_bounds__(64 * aes_seg_waves()) void mq_aes_opens_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
-    const mq_pkt_desc* __restrict__ desc, const uint32_t* __restrict__ list, const uint32_t* __restrict__ hot,
-    const uint32_t* __restrict__ rowseg, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,
-    const uint2* __restrict__ hpm, uint32_t* __restrict__ sched) {
-  aes_seg_tiles<true>(kt, n_rows, arena, arena_len, desc, list, hot, rowseg, status, pn_out, hpm, sched);
+    const mq_pkt_desc* __restrict__ desc, const uint32_t* __restrict__ list, const uint32_t* __restrict__ n_dev,
+    const uint32_t* __restrict__ hot, const uint32_t* __restrict__ rowseg, uint8_t* __restrict__ status,
+    uint64_t* __restrict__ pn_out, const uint2* __restrict__ hpm, uint32_t* __restrict__ sched) {
+  aes_seg_tiles<true>(kt, n_rows, arena, arena_len, desc, list, n_dev, hot, rowseg, status, pn_out, hpm, sched);
 }
 
 extern "C" __global__ __launch_bounds__(256) void mq_aes_hp_kernel(
@@ -880,10 +916,10 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
     const uint32_t blocks = (uint32_t)(cus > 0 ? cus : 256);
     if (open)
       hipLaunchKernelGGL(mq_aes_opens_kernel, dim3(blocks), dim3(64 * aes_seg_waves()), 0, s, kt, n_rows, arena,
-                         arena_len, desc, index, hot, rowseg, status, pn_out, hpm, sched_s);
+                         arena_len, desc, index, n_dev, hot, rowseg, status, pn_out, hpm, sched_s);
     else
       hipLaunchKernelGGL(mq_aes_seals_kernel, dim3(blocks), dim3(64 * aes_seg_waves()), 0, s, kt, n_rows, arena,
-                         arena_len, desc, index, hot, rowseg, status, sched_s);
+                         arena_len, desc, index, n_dev, hot, rowseg, status, sched_s);
     return hipGetLastError();
   }
   const uint32_t waves = aes_waves(n_rows == 1), blocks = aes_grid(tiles, waves, cus);

@@ -933,7 +933,8 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
     // key-segmented single-key kernels run list 0 whole, no fork (mq_aes.hip aes_seg_tiles)
     constexpr uint32_t kSegPackets = 512;
     const char* seg_env = std::getenv("MQ_AES_SEG");  // diagnostic: 0 = never
-    const uint32_t* rowseg = (seg_env && seg_env[0] == '0') || (uint64_t)n < (uint64_t)kSegPackets * kt->rows
+    const bool seg_force = seg_env && seg_env[0] == '1';  // diagnostic: 1 = whenever keyed
+    const uint32_t* rowseg = (seg_env && seg_env[0] == '0') || (!seg_force && (uint64_t)n < (uint64_t)kSegPackets * kt->rows)
                                  ? nullptr
                                  : mq_partition_rowseg(n, kt->rows, counts);
     auto fork = fork_enabled() && !rowseg ? side_streams().fork(kt->device, s, 1) : mq::SideStreams<HipBackend>::Fork();

@@ -83,6 +83,16 @@ __device__ __forceinline__ uint32_t part_class(uint32_t hot, const PartItem& x) 
 __device__ __forceinline__ uint32_t key_bin(const PartItem& x) {
   return x.key * kKeyClasses + (kKeyClasses - 1 - min(x.len >> 7, kKeyClasses - 1));
 }
+// Tables of at most kBinSlots bins (<= 128 rows) count in LDS per block, then one global atomic per
+// bin of the block: a batch over 2 or 3 AES keys otherwise put every packet of a row on ONE global
+// counter, 131k-350k atomics on one address per kernel (config C over 2 keys: 248 GiB/s,
+// gpurun_out/r04zb; 741 with the LDS counts, r04zc). Larger tables keep the per-thread combining
+// below (an LDS hash of bins measured C with 1024 keys 2.8 % and E 1.1 % slower, r04zc).
+constexpr uint32_t kBinSlots = 2048;
+__device__ __forceinline__ bool bins_in_lds(const uint32_t* bins, uint32_t n_rows) {
+  return bins && n_rows * kKeyClasses <= kBinSlots;
+}
+
 // Boyer-Moore majority pairs (candidate, count); combining any partition of the input in any
 // order keeps the majority element if there is one
 __device__ __forceinline__ uint2 vote_join(uint2 a, uint2 b) {
@@ -188,10 +198,14 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_count_kernel(
   if (pass_empty(live)) return;
   __shared__ uint32_t s_cnt[kClasses];
   __shared__ uint32_t s_max[kLenClasses];  // list 1's classes: the largest image, in chunks
+  __shared__ uint32_t s_bcnt[kBinSlots];
+  const bool lds_bins = bins_in_lds(bins, n_rows);  // kernel-uniform
   PartItem it[kPartItems];
   part_fetch(kt, n_rows, desc, n, it);
   if (threadIdx.x < kClasses) s_cnt[threadIdx.x] = 0;
   if (threadIdx.x < kLenClasses) s_max[threadIdx.x] = 0;
+  if (lds_bins)
+    for (uint32_t q = threadIdx.x; q < n_rows * kKeyClasses; q += blockDim.x) s_bcnt[q] = 0;
   const uint32_t hot = fold_votes(votes, nv);  // the same in every wave of every block
   if (blockIdx.x == 0 && threadIdx.x == 0) *hot_p = hot;  // for the scatter
   __syncthreads();
@@ -220,9 +234,12 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_count_kernel(
       if (j < k && same) first = false;
       if (j > k && same) ++cnt;
     }
-    if (first) atomicAdd(&bins[kb[k]], cnt);
+    if (first) atomicAdd(lds_bins ? &s_bcnt[kb[k]] : &bins[kb[k]], cnt);
   }
   __syncthreads();
+  if (lds_bins)
+    for (uint32_t q = threadIdx.x; q < n_rows * kKeyClasses; q += blockDim.x)
+      if (s_bcnt[q]) atomicAdd(&bins[q], s_bcnt[q]);
   if (threadIdx.x < kClasses) hist[(size_t)threadIdx.x * nblocks + blockIdx.x] = s_cnt[threadIdx.x];
   if (threadIdx.x < kLenClasses && s_max[threadIdx.x]) atomicMax(&cmax[threadIdx.x], s_max[threadIdx.x]);
 }
@@ -391,7 +408,11 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_scatter_kerne
   if (pass_empty(live)) return;
   __shared__ uint32_t s_rank[kClasses];
   __shared__ uint32_t s_cmax[kLenClasses];
+  __shared__ uint32_t s_bcnt[kBinSlots];
+  const bool lds_bins = bins_in_lds(bins, n_rows);  // kernel-uniform
   if (threadIdx.x < kLenClasses) s_cmax[threadIdx.x] = cmax[threadIdx.x];
+  if (lds_bins)
+    for (uint32_t q = threadIdx.x; q < n_rows * kKeyClasses; q += blockDim.x) s_bcnt[q] = 0;
   PartItem it[kPartItems];
   part_fetch(kt, n_rows, desc, n, it);
   const uint32_t hot = *hot_p;
@@ -421,13 +442,22 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_scatter_kerne
       if (j > k && same) ++cnt;
     }
     uint32_t base = 0;
-    if (kd[k] && lead == k) base = atomicAdd(&bins[kb[k]], cnt);
+    if (kd[k] && lead == k) base = atomicAdd(lds_bins ? &s_bcnt[kb[k]] : &bins[kb[k]], cnt);
     // a follower takes the leader's position (its base: the leader comes first in k order) + rank
 #pragma unroll
     for (int j = 0; j < kPartItems; ++j)
       if (j == lead && j < k) base = kpos[j];
-    kpos[k] = kd[k] ? base + rank : 0u;
-    if (kd[k]) list[kpos[k]] = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;  // any order in a bin
+    kpos[k] = kd[k] ? base + rank : 0u;  // lds_bins: the rank inside the block's count of the bin
+    if (kd[k] && !lds_bins) list[kpos[k]] = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;  // any order in a bin
+  }
+  if (lds_bins) {  // kernel-uniform: the block's base in each bin, one global atomic per bin
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < n_rows * kKeyClasses; q += blockDim.x)
+      if (s_bcnt[q]) s_bcnt[q] = atomicAdd(&bins[q], s_bcnt[q]);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPartItems; ++k)
+      if (kd[k]) list[s_bcnt[kb[k]] + kpos[k]] = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
   }
 #pragma unroll
   for (int k = 0; k < kPartItems; ++k) {

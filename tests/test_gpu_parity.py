@@ -218,7 +218,8 @@ def oracle_run(orc, keys, arena, desc, hint, open_=False):
 @pytest.mark.parametrize("n,n_keys,majority,hint", [
     (4000, 97, False, _lib.MQ_SUITE_MIXED), (4000, 5, False, _lib.MQ_SUITE_MIXED), (4000, 2, True, _lib.MQ_SUITE_MIXED),
     (4000, 97, False, _lib.MQ_SUITE_AES128GCM), (20000, 1024, False, _lib.MQ_SUITE_AES128GCM),
-    (4000, 1024, False, _lib.MQ_SUITE_AES128GCM), (40000, 64, False, _lib.MQ_SUITE_AES128GCM)])
+    (4000, 1024, False, _lib.MQ_SUITE_AES128GCM), (40000, 64, False, _lib.MQ_SUITE_AES128GCM),
+    (60000, 2, False, _lib.MQ_SUITE_AES128GCM), (30000, 3, True, _lib.MQ_SUITE_MIXED)])
 def test_mixed_hint_aes_keys_vs_oracle(orc, n, n_keys, majority, hint):
     # An all-AES batch over several key rows, through the partition (MQ_SUITE_MIXED, or the AES
     # hint with a workspace): the majority vote's key goes first by length class; without a
@@ -228,7 +229,9 @@ def test_mixed_hint_aes_keys_vs_oracle(orc, n, n_keys, majority, hint):
     # the list capacity — 4000 packets over 1024 rows do not, so they share length classes
     # (mixed-key tiles: the bit-holed product). With >= 512 packets per row on average (5 or 2
     # keys over 4000 packets, 64 keys over 40000) the key-segmented single-key kernels run the
-    # whole list, one key segment at a time. Results equal the oracle either way.
+    # whole list in slices of the list (r04: 2 keys of 30000 packets each, or 3 keys with 3/4 of
+    # the packets on key 0, are many slices per key, and slice edges fall inside segments).
+    # Results equal the oracle either way.
     w = workload.uniform(n, _lib.MQ_SUITE_AES128GCM, L=700, n_keys=n_keys)
     seal, opn = w.seal_desc.copy(), w.open_desc.copy()
     if majority:
