@@ -352,6 +352,31 @@ def test_direct_path_and_disorder(orc, suite):
             assert g_back.reshape(w.n, 1500)[:, :1484].tobytes() == keep
 
 
+@pytest.mark.parametrize("L,n_keys", [(1232, 1), (1350, 2), (1452, 1), (1500, 3), (1583, 1), (1600, 2), (2048, 1)])
+def test_chacha_long_packets_rounds(orc, L, n_keys):
+    # r04: a flat ChaCha20 tile whose eight images exceed the 10-KiB LDS image (packets over
+    # ~1216 B) is staged in two rounds, octets 0-3 then 4-7, every wave of its workgroup joining
+    # the second round's barriers, instead of running in HBM (tiles whose halves do not fit, over
+    # ~2416 B, stay direct: the fuzz batches). Without a workspace (open: header protection inside
+    # the tile) as well. Against the oracle; a short tail tile and packets at every 16-B alignment.
+    suite = _lib.MQ_SUITE_CHACHA20
+    w = workload.uniform(1203, suite, L=L, n_keys=n_keys)
+    o_out, o_st, _ = oracle_run(orc, w.keys, w.arena, w.seal_desc, suite)
+    assert (o_st == 0).all()
+    o_back, o_st2, o_pn = oracle_run(orc, w.keys, o_out, w.open_desc, suite, open_=True)
+    for use_ws in (True, False):
+        g_out, g_st, _ = gpu_run(w.keys, w.arena, w.seal_desc, suite, use_ws=use_ws)
+        assert (g_st == o_st).all() and g_out.tobytes() == o_out.tobytes(), (L, use_ws)
+        g_back, g_st, g_pn = gpu_run(w.keys, o_out, w.open_desc, suite, open_=True, use_ws=use_ws)
+        assert (g_st == o_st2).all() and g_back.tobytes() == o_back.tobytes(), (L, use_ws)
+        assert (g_pn == o_pn).all() and (g_pn == w.pns).all()
+    # then a batch of 1200-B packets (one round) on the same stream
+    s = workload.uniform(64, suite, L=1200)
+    g_out, g_st, _ = gpu_run(s.keys, s.arena, s.seal_desc, suite)
+    o_out, o_st, _ = oracle_run(orc, s.keys, s.arena, s.seal_desc, suite)
+    assert (g_st == o_st).all() and g_out.tobytes() == o_out.tobytes()
+
+
 @pytest.mark.parametrize("L", [21, 36, 63, 64, 65, 100, 1350])
 def test_small_and_odd_sizes(orc, L):
     for suite in (1, 2):
