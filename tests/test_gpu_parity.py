@@ -353,12 +353,12 @@ def test_direct_path_and_disorder(orc, suite):
 
 
 @pytest.mark.parametrize("L,n_keys", [(1232, 1), (1350, 2), (1452, 1), (1500, 3), (1583, 1), (1600, 2), (2048, 1)])
-def test_chacha_long_packets_rounds(orc, L, n_keys):
-    # r04: a flat ChaCha20 tile whose eight images exceed the 10-KiB LDS image (packets over
-    # ~1216 B) is staged in two rounds, octets 0-3 then 4-7, every wave of its workgroup joining
-    # the second round's barriers, instead of running in HBM (tiles whose halves do not fit, over
-    # ~2416 B, stay direct: the fuzz batches). Without a workspace (open: header protection inside
-    # the tile) as well. Against the oracle; a short tail tile and packets at every 16-B alignment.
+def test_chacha_long_packets(orc, L, n_keys):
+    # a flat ChaCha20 tile whose eight images exceed the 10-KiB LDS image (packets over ~1216 B)
+    # runs the direct path (in HBM; the staged-rounds variants measured in r04 cost config B
+    # 1.5-3.8 %, profiles/r04zh_long_packets_rejected.txt). Without a workspace (open: header
+    # protection inside the tile) as well. Against the oracle; a short tail tile and packets at
+    # every 16-B alignment.
     suite = _lib.MQ_SUITE_CHACHA20
     w = workload.uniform(1203, suite, L=L, n_keys=n_keys)
     o_out, o_st, _ = oracle_run(orc, w.keys, w.arena, w.seal_desc, suite)
