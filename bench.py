@@ -252,14 +252,15 @@ def cpu_openssl(w, sample, min_seconds=3.0):
 
 
 # ---- end-to-end (host-resident) ---------------------------------------------------------------
-def end_to_end(torch, batch, kt, w, sd, od, dev, chunks=8, reps=3):
+def end_to_end(torch, batch, kt, w, sd, od, dev, reps=3):
     """Host-resident rate (the path starts and ends in a socket buffer): pinned host arena ->
-    H2D -> seal -> D2H, then H2D -> open -> D2H, pipelined over chunks of descriptor ranges on
-    several streams so copies overlap kernels. Returns GiB/s of wire bytes per direction, next to
-    the link's bound: the pipeline moves every wire byte in and out, so it cannot beat the slower
-    of the plain H2D and D2H rates (each the best over the same stream / chunk settings, 5
-    repetitions). r03 bounded it by a plain H2D + D2H pipeline of copies, which the kernel pipeline
-    beat (1.044, VERDICT r03 #7): that was a schedule, not a bound."""
+    H2D -> seal -> D2H, then H2D -> open -> D2H, pipelined over chunks of descriptor ranges. Since
+    r05 the two copy directions run on copy streams of their own and the kernels on a third,
+    joined by events, so chunk k's D2H runs beside chunk k + 1's H2D and chunk k's kernel (r02-r04
+    ran each chunk's H2D, kernel and D2H on one stream: the directions barely overlapped, 0.60 of
+    the one-way bound). The ceiling is measured the same way with no kernel: the
+    duplex copy rate (every chunk H2D on one stream while the previous chunk goes D2H on the
+    other), next to each direction alone. Returns GiB/s of wire bytes."""
     n = w.n
     host = torch.from_numpy(w.arena).pin_memory()
     back = torch.empty_like(host).pin_memory()
@@ -268,32 +269,42 @@ def end_to_end(torch, batch, kt, w, sd, od, dev, chunks=8, reps=3):
     pn = torch.zeros(n, dtype=torch.int64, device=dev)
     offs = w.seal_desc["offset"].astype(np.int64)
     ends = offs + w.seal_desc["len"].astype(np.int64)
-    configs = ((2, chunks), (3, 16), (4, 32))
+    configs = (16, 32, 64)  # chunks per pass
+    s_in, s_k, s_out = (torch.cuda.Stream(device=dev) for _ in range(3))
+    ws = torch.empty(max(batch.workspace_bytes(n), 256), dtype=torch.uint8, device=dev)
 
-    def run(desc, mode, nch, nstreams, nrep=reps):
-        per = (n + nch - 1) // nch
-        wsl = [torch.empty(max(batch.workspace_bytes(per), 256), dtype=torch.uint8, device=dev)
-               for _ in range(nstreams)] if mode in ("seal", "open") else None
+    def run(desc, mode, nch, nrep=reps):
+        """mode: seal / open (copy in, kernel, copy out), duplex (both copies, no kernel), h2d, d2h"""
         bounds = [(n * k) // nch for k in range(nch + 1)]
-        streams = [torch.cuda.Stream(device=dev) for _ in range(nstreams)]
+        spans = [(int(offs[bounds[k]:bounds[k + 1]].min()), int(ends[bounds[k]:bounds[k + 1]].max()))
+                 for k in range(nch) if bounds[k + 1] > bounds[k]]
+        idx = [(bounds[k], bounds[k + 1]) for k in range(nch) if bounds[k + 1] > bounds[k]]
 
         def one_pass():
-            for k in range(nch):
-                lo, hi = bounds[k], bounds[k + 1]
-                if hi == lo:
-                    continue
-                a, b = int(offs[lo:hi].min()), int(ends[lo:hi].max())
-                s = streams[k % nstreams]
-                with torch.cuda.stream(s):
-                    if mode != "d2h":
+            prev_out = torch.cuda.Event()
+            prev_out.record(s_out)
+            for (a, b), (lo, hi) in zip(spans, idx):
+                e_in, e_k = torch.cuda.Event(), torch.cuda.Event()
+                if mode != "d2h":
+                    with torch.cuda.stream(s_in):
                         arena[a:b].copy_(host[a:b], non_blocking=True)
-                    if mode == "open":
-                        batch.open_(kt, arena, desc[32 * lo:32 * hi], st[lo:hi], pn[lo:hi], w.suite_hint,
-                                    wsl[k % nstreams], s.cuda_stream)
-                    elif mode == "seal":
-                        batch.seal(kt, arena, desc[32 * lo:32 * hi], st[lo:hi], w.suite_hint, wsl[k % nstreams],
-                                   s.cuda_stream)
-                    if mode != "h2d":
+                    e_in.record(s_in)
+                else:
+                    e_in.record(s_in)
+                if mode in ("seal", "open"):
+                    s_k.wait_event(e_in)
+                    with torch.cuda.stream(s_k):
+                        if mode == "open":
+                            batch.open_(kt, arena, desc[32 * lo:32 * hi], st[lo:hi], pn[lo:hi], w.suite_hint, ws,
+                                        s_k.cuda_stream)
+                        else:
+                            batch.seal(kt, arena, desc[32 * lo:32 * hi], st[lo:hi], w.suite_hint, ws, s_k.cuda_stream)
+                    e_k.record(s_k)
+                else:
+                    e_k = e_in
+                if mode != "h2d":
+                    s_out.wait_event(e_k)  # duplex: chunk k goes out while chunk k + 1 comes in
+                    with torch.cuda.stream(s_out):
                         back[a:b].copy_(arena[a:b], non_blocking=True)
             torch.cuda.synchronize()
 
@@ -309,25 +320,29 @@ def end_to_end(torch, batch, kt, w, sd, od, dev, chunks=8, reps=3):
     res, cfg_used = {}, {}
     for name, desc in (("seal", sd), ("open", od)):
         best_rate = 0.0
-        for nstreams, nch in configs:
+        for nch in configs:
             host.copy_(torch.from_numpy(w.arena) if name == "seal" else sealed)
-            dt = run(desc, name, nch, nstreams)
+            dt = run(desc, name, nch)
             r = w.wire_bytes / dt / 2 ** 30
             if r > best_rate:
-                best_rate, cfg_used[name] = r, {"streams": nstreams, "chunks": nch}
+                best_rate, cfg_used[name] = r, {"streams": "h2d + kernel + d2h", "chunks": nch}
             if name == "seal":
                 sealed = back.clone()  # the open pass starts from the sealed bytes
         res[name] = round(best_rate, 2)
-    link = {}
-    for mode in ("h2d", "d2h"):
-        link[mode] = max(w.wire_bytes / run(None, mode, nch, nstreams, 5) / 2 ** 30 for nstreams, nch in configs)
-    bound = min(link.values())
+    link, link_cfg = {}, {}
+    for mode in ("duplex", "h2d", "d2h"):
+        rates = {nch: w.wire_bytes / run(None, mode, nch, 5) / 2 ** 30 for nch in configs}
+        link_cfg[mode] = max(rates, key=rates.get)
+        link[mode] = rates[link_cfg[mode]]
+    ceiling = link["duplex"]
     return {"unit": "GiB/s of wire bytes, host-resident (pinned) in and out", "pipeline_config": cfg_used,
             "seal": res["seal"], "open": res["open"],
+            "duplex_copy_ceiling": round(ceiling, 2), "duplex_chunks": link_cfg["duplex"],
             "h2d_alone": round(link["h2d"], 2), "d2h_alone": round(link["d2h"], 2),
-            "link_bound": round(bound, 2),
-            "link_bound_note": "every wire byte goes in and comes out: no pipeline beats the slower direction alone",
-            "frac_of_link_bound": {"seal": round(res["seal"] / bound, 3), "open": round(res["open"] / bound, 3)}}
+            "ceiling_note": "every wire byte goes in and comes out; the ceiling is the same chunked "
+                            "pipeline with no kernel (H2D of chunk k+1 beside D2H of chunk k)",
+            "frac_of_ceiling": {"seal": round(res["seal"] / ceiling, 3), "open": round(res["open"] / ceiling, 3)},
+            "device_resident_note": "never `value`: the device-resident rate is the metric"}
 
 
 # ---- roofline bookkeeping ---------------------------------------------------------------------

@@ -493,6 +493,469 @@ struct ChaChaPolicy {
   }
 };
 
+// ---- narrow tiles: G lanes per packet, 64 / G packets per wave (r05) ---------------------------
+// The octet tile gives every packet 8 lanes whatever its length. A 64-B packet needs 2 ChaCha20
+// blocks (one-time key, one keystream block) and 5 MAC blocks, so 3/4 of its octet's keystream
+// slots idle and the per-packet work (powers of r, the final multiply, the octet reduction, the
+// header-protection block, descriptor and placement) is paid per 8 packets: flat 64-B batches ran
+// at 122 GiB/s against 1034 at 1200 B. A narrow tile packs Q = 64 / G packets into
+// the wave with G in {1, 2, 4} (G = 8: the octet layout without the keystream pool): keystream
+// block c of a packet on group lane c % G in iteration c / G, the header-protection block as the
+// packet's next slot when it falls in a later iteration than keystream block 1 (whose ciphertext
+// is its sample), the MAC a G-way interleaved Horner (multiplier r^G, final r^(G-j), group sum).
+// No LDS scratch: the one-time key travels by DPP from group lane 0, the mask stays in the
+// registers of the lane that made it, so the whole 10 KiB minus a 64-B read slack holds images.
+// Staging maps image chunk c (lane-linear LDS destination, as LDS-DMA requires) to its packet by a
+// binary search over the tile's slots; write-back runs per packet, chunk j, j + G, ... on group
+// lane j. Used by flat ChaCha20 batches of short packets (mq_launch_chacha picks the narrow kernel
+// by the arena's bytes per packet) and by the short length classes of a mixed batch's ChaCha20 list
+// (mq_partition.hip regions).
+constexpr uint32_t kNarrowSlack = 64;                              // load_raw overreach past an image
+constexpr uint32_t kNarrowChunks = (kLdsBytes - kNarrowSlack) / 16;  // 636
+
+template <int G>
+struct NarrowStager {
+  static constexpr int Q = kWave / G;
+  uint8_t* smem;
+  const uint8_t* arena;
+  uint64_t arena_len;
+  uint32_t total;  // image chunks of the tile
+  uint32_t slot;   // this lane's packet: first chunk (group-uniform)
+  uint64_t base;   // its image start in the arena (16-B aligned)
+  int lane;
+  uint32_t tail_c = 0xFFFFFFFFu;  // a chunk that would read past the arena end: guarded load
+  uint64_t tail_src = 0;
+
+  // the packet of image chunk c < total: the last q with slot_q <= c (an empty packet shares the
+  // next one's slot; the later one of equal slots is the one with chunks)
+  __device__ __forceinline__ uint32_t owner(uint32_t c) const {
+    uint32_t q = 0;
+#pragma unroll
+    for (int step = Q / 2; step >= 1; step >>= 1) {
+      const uint32_t v = (uint32_t)__shfl((int)slot, G * (int)(q + step), kWave);
+      if (v <= c) q += step;
+    }
+    return q;
+  }
+  __device__ __forceinline__ void issue() {
+#if MQ_PROF_SKIP & 8
+    return;
+#endif
+    for (uint32_t k = 0; k < total; k += kWave) {  // wave-uniform
+      const uint32_t c = k + (uint32_t)lane;
+      const uint32_t q = owner(c < total ? c : 0u);
+      const uint32_t sq = (uint32_t)__shfl((int)slot, G * (int)q, kWave);
+      const uint64_t bq = (uint64_t)(uint32_t)__shfl((int)(uint32_t)(base >> 32), G * (int)q, kWave) << 32 |
+                          (uint32_t)__shfl((int)(uint32_t)base, G * (int)q, kWave);
+      const uint64_t src = bq + 16ull * (c - sq);
+      if (c < total) {
+        if (src + 16 <= arena_len)
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(arena + src),
+                                           (__attribute__((address_space(3))) void*)(smem + 16u * k), 16, 0, 0);
+        else {
+          tail_c = c;
+          tail_src = src;
+        }
+      }
+    }
+  }
+  __device__ __forceinline__ void complete() {
+    wave_sync();  // s_waitcnt vmcnt(0) covers the LDS-DMA writes
+    if (tail_c != 0xFFFFFFFFu) *(uint4*)(smem + 16u * tail_c) = load_chunk_guarded(arena, tail_src, arena_len);
+    wave_sync();
+  }
+};
+
+// LDS -> HBM of a narrow tile's packets with write = 1: group lane j stores chunks j, j + G, ... of
+// its packet, whole chunks with 16-B stores, the partial first / last chunk byte-exact (bytes of
+// neighbouring packets are never touched)
+template <int G>
+__device__ __forceinline__ void narrow_stage_out(const uint8_t* smem, uint8_t* arena, int j, bool write,
+                                                 const Placement& pl) {
+#if MQ_PROF_SKIP & 4
+  return;
+#endif
+  const uint32_t nch = write ? pl.nch() : 0u, head = pl.head();
+  const uint32_t tail_end = ((head + pl.len - 1u) & 15u) + 1u;
+  const uint32_t nmax = wave_max_any(nch);
+  uint8_t* dst = arena + pl.base();
+  const uint8_t* src = smem + 16u * pl.slot;
+  for (uint32_t c = (uint32_t)j; c < nmax + (uint32_t)j; c += G) {  // wave-uniform trip count (nmax / G)
+    if (c < nch) {
+      const uint32_t lo = c == 0 ? head : 0u, hi = c + 1 == nch ? tail_end : 16u;
+      const uint4 v = *(const uint4*)(src + 16u * c);
+      if (lo == 0 && hi == 16) {
+        *(uint4*)(dst + 16u * c) = v;
+      } else {
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        for (uint32_t b = lo; b < hi; ++b) dst[16u * c + b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+      }
+    }
+  }
+}
+
+// Poly1305 tag of a narrow tile's packet (poly_tag with G lanes): lane j takes MAC blocks
+// G k + j - z, Horner with r^G, final multiply by r^(G - j), group sum. r, s: the one-time key.
+template <int G, class S>
+__device__ __forceinline__ void poly_tag_g(const S& sp, typename S::off_t pkt, typename S::off_t pay, uint32_t aad_len,
+                                           uint32_t ct_len, const uint32_t (&rk)[4], const uint32_t (&s)[4], int j,
+                                           bool act, uint32_t (&tag)[4]) {
+#if MQ_PROF_SKIP & 2
+  for (int w = 0; w < 4; ++w) tag[w] = s[w] ^ rk[w] ^ aad_len ^ ct_len;
+  return;
+#endif
+  typedef Grp<G> Gp;
+  const P26 r = p26_from_words(rk[0] & 0x0fffffffu, rk[1] & 0x0ffffffcu, rk[2] & 0x0ffffffcu, rk[3] & 0x0ffffffcu, 0);
+  // powers: v = r^(j + 1) on group lane j; rG = r^G, rj = r^(G - j)
+  P26 v = r, rG = r, rj = r;
+  if (G >= 2) {
+    P26 t = r;
+    p26_mul(t, p26_mult(r));  // r^2
+#pragma unroll
+    for (int l = 0; l < 5; ++l) v.l[l] = (j & 1) ? t.l[l] : v.l[l];
+    if (G >= 4) {
+      P26 u = v;
+      p26_mul(u, p26_mult(t));
+#pragma unroll
+      for (int l = 0; l < 5; ++l) v.l[l] = (j & 2) ? u.l[l] : v.l[l];
+    }
+    if (G == 8) {
+      P26 r4, u = v;
+#pragma unroll
+      for (int l = 0; l < 5; ++l) r4.l[l] = oct_lane3(v.l[l]);
+      p26_mul(u, p26_mult(r4));
+#pragma unroll
+      for (int l = 0; l < 5; ++l) v.l[l] = (j & 4) ? u.l[l] : v.l[l];
+    }
+#pragma unroll
+    for (int l = 0; l < 5; ++l) {
+      rG.l[l] = Gp::last(v.l[l]);
+      rj.l[l] = Gp::mirror(v.l[l]);
+    }
+  }
+  const P26m mG = p26_mult(rG), mlast = p26_mult(rj);
+  const uint32_t A = (aad_len + 15) >> 4, T = (ct_len + 15) >> 4, nb = A + T + 1;
+  const uint32_t K = (nb + G - 1) / G;
+  const uint32_t Kmax = wave_max_any(act ? K : 0u);
+  const int z = (int)(G * Kmax) - (int)nb;  // prepended zero blocks: every packet runs Kmax steps
+  P26 acc;
+#pragma unroll
+  for (int l = 0; l < 5; ++l) acc.l[l] = 0;
+  struct Blk { typename S::off_t src; int rem; bool pre, lens; };
+  auto where = [&](int i) {
+    Blk b;
+    const bool aad = i < (int)A;
+    b.pre = i < 0;
+    b.lens = i == (int)(A + T);
+    b.src = aad ? pkt + 16 * (uint32_t)max(i, 0) : pay + 16 * (uint32_t)(i - (int)A);
+    b.rem = aad ? (int)aad_len - 16 * i : (int)ct_len - 16 * (i - (int)A);
+    if (b.pre || b.lens) b.src = pkt;
+    return b;
+  };
+  auto absorb = [&](const Blk& b, uint32_t (&m)[4]) {
+    if (wave_any(act && (b.pre || b.lens || b.rem < 16))) {
+#pragma unroll
+      for (int w = 0; w < 4; ++w) m[w] &= byte_mask(b.pre ? 0 : b.rem, w);
+      if (b.lens) { m[0] = aad_len; m[1] = 0; m[2] = ct_len; m[3] = 0; }
+    }
+    const P26 x = p26_from_words(m[0], m[1], m[2], m[3], b.pre ? 0u : 1u);
+#pragma unroll
+    for (int l = 0; l < 5; ++l) acc.l[l] += x.l[l];
+  };
+  if (Kmax > 0) {
+    int i = j - z;
+    Blk b = where(i);
+    uint32_t m[4];
+    load_words<4>(sp, b.src, m);
+    const uint32_t sel_pay = sel_load((uint32_t)(pay & 3));
+    const int ct_full_end = (int)A + (int)(ct_len >> 4);
+    const int zA = (int)A + z;
+    const uint32_t k_lo = act ? (uint32_t)((zA + G - 1) / G) : 0u;
+    const int hi = ct_full_end + z - 2 * G + 1;  // lean iff G k + 2G - 1 - z < ct_full_end
+    const uint32_t k_hi = !act ? 0xFFFFFFFFu : (hi <= 0 ? 0u : (uint32_t)((hi + G - 1) / G));
+    const uint32_t klo = wave_max_any(k_lo), khi = min(wave_min_any(k_hi), Kmax - 1);
+    for (uint32_t k = 0; k + 1 < Kmax; ++k) {
+      if (k == klo && k < khi) {  // the lean stretch: only the block address advances
+        typename S::off_t a = b.src & ~(typename S::off_t)3;
+        uint32_t sel = sel_pay;
+        pin(sel);
+        for (; k < khi; ++k) {
+          const P26 x = p26_from_words(m[0], m[1], m[2], m[3], 1u);
+#pragma unroll
+          for (int l = 0; l < 5; ++l) acc.l[l] += x.l[l];
+          a += 16 * G;
+          load_words_sel<4>(sp, a, sel, m);
+          p26_mul(acc, mG);
+        }
+        const uint32_t nl = khi - klo;
+        i += (int)(G * nl);
+        b.src += 16 * G * nl;
+        b.rem -= (int)(16 * G * nl);
+        if (k + 1 >= Kmax) break;
+      }
+      absorb(b, m);
+      const bool steady = !act || (i >= (int)A && i + G < ct_full_end);
+      i += G;
+      if (!wave_any(!steady)) {
+        b.src += 16 * G;
+        b.rem -= 16 * G;
+        load_words_sel<4>(sp, b.src & ~(typename S::off_t)3, sel_pay, m);
+      } else {
+        b = where(i);
+        load_words<4>(sp, b.src, m);
+      }
+      p26_mul(acc, mG);
+    }
+    absorb(b, m);
+    p26_mul(acc, mlast);
+  }
+#pragma unroll
+  for (int l = 0; l < 5; ++l) acc.l[l] = Gp::sum(acc.l[l]);
+  p26_finish(acc, s, tag);
+}
+
+template <int G, bool SINGLE>
+struct NarrowPolicy {
+  typedef Grp<G> Gp;
+
+  // the one-time key (block 0, group lane 0's keystream words 0..7) on every lane of the group
+  static __device__ __forceinline__ void otk_bcast(const uint32_t (&otk)[8], uint32_t (&r)[4], uint32_t (&s)[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      r[k] = Gp::bcast0(otk[k]);
+      s[k] = Gp::bcast0(otk[4 + k]);
+    }
+  }
+
+  // send composite (transmit.rs:625-755) on a narrow tile. Slot order: keystream blocks 1 .. nblk-1
+  // first, the one-time key (block 0) in slot nblk - 1 — made last, so its 8 words are not held
+  // through the loop — then the header-protection block in slot nblk.
+  template <class S, class St>
+  static __device__ __forceinline__ void seal(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j,
+                                              St& stg) {
+    const mq_pkt_desc& d = c.d;
+    uint32_t key[8];
+    load_key8(row->key, key);
+    const uint32_t aad_len = c.act ? (uint32_t)d.pn_offset + d.pn_len : 0u;
+    const uint32_t P = c.act ? d.len - aad_len - 16 : 0u;
+    const typename S::off_t pay = pkt + aad_len;
+    uint32_t n0 = row->iv[0], n1 = row->iv[1] ^ bswap32((uint32_t)(c.pn >> 32)), n2 = row->iv[2] ^ bswap32((uint32_t)c.pn);
+    // retire the key loads before the LDS-DMA is issued (else the first wait covers the DMA too);
+    // a single-key tile keeps its key in SGPRs
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (SINGLE) asm volatile("" : "+s"(key[k]));
+      else pin(key[k]);
+    }
+    pin(n0); pin(n1); pin(n2);
+    stg.issue();
+    const uint32_t nblk = 1 + (P + 63) / 64;
+    const bool hp = c.act && !(d.flags & MQ_PKT_NO_HP);
+    // the header-protection block in slot nblk: its sample (payload [4 - pn_len, 20 - pn_len)) is
+    // ciphertext of keystream block 1 (slot 0, iteration 0), so slot nblk must fall in a later
+    // iteration (nblk >= G), and must not reach into the tag (only the MAC produces it)
+    const bool hp_in = hp && P + d.pn_len >= 20u && nblk >= (uint32_t)G;
+    const uint32_t S_ = nblk + (hp_in ? 1u : 0u);
+    const uint32_t Imax = wave_max_any(c.act ? (S_ + G - 1) / G : 0u);
+    uint32_t otk[8] = {0, 0, 0, 0, 0, 0, 0, 0}, m0 = 0, m1 = 0;
+    for (uint32_t it = 0; it < Imax; ++it) {
+      const uint32_t slot = (uint32_t)j + G * it;
+      const bool is_otk = c.act && slot + 1 == nblk;
+      const uint32_t ctr = is_otk ? 0u : slot + 1;  // keystream block of the slot
+      const bool a = c.act && ctr < nblk;            // a keystream block (or the one-time key)
+      const bool is_hp = hp_in && slot == nblk;
+      uint32_t w[17];
+      if (it > 0) ChaChaPolicy::load_block(sp, pay, a && !is_otk ? ctr : 0u, w);
+      uint32_t ks[16];
+      if (wave_any(is_hp)) {  // the HP lanes run the HP key on the sample (ciphertext by now)
+        uint32_t smp[4], kh[8], kk[8];
+        load_words<4>(sp, is_hp ? pay + 4u - d.pn_len : pay, smp);
+        load_key8(row->hp, kh);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) kk[k] = is_hp ? kh[k] : key[k];
+        chacha20_block(kk, is_hp ? smp[0] : ctr, is_hp ? smp[1] : n0, is_hp ? smp[2] : n1, is_hp ? smp[3] : n2, ks);
+      } else {
+        chacha20_block(key, ctr, n0, n1, n2, ks);
+      }
+      if (it == 0) {
+        stg.complete();
+        const bool rec = c.act && is_record(d);
+        if (wave_any(rec)) {  // TLS record: header (AAD) and inner content type before any use
+          if (rec && j == 0) write_record_header(sp, pkt, d);
+          wave_sync();
+        }
+        ChaChaPolicy::load_block(sp, pay, a && !is_otk ? ctr : 0u, w);
+      }
+      if (is_otk) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) otk[k] = ks[k];
+      } else if (a) {
+        ChaChaPolicy::store_block(sp, pay, ctr, P, ks, w);
+      }
+      if (is_hp) {
+        m0 = ks[0];
+        m1 = ks[1];
+      }
+      wave_sync();
+    }
+    if (Imax == 0) stg.complete();
+    // the one-time key from its group lane (nblk - 1) % G to the whole group
+    uint32_t r[4], s[4], tag[4];
+    const int src = (int)(threadIdx.x & (kWave - 1)) - j + (int)((nblk + G - 1) % G);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      r[k] = G == 1 ? otk[k] : (uint32_t)__shfl((int)otk[k], src, kWave);
+      s[k] = G == 1 ? otk[4 + k] : (uint32_t)__shfl((int)otk[4 + k], src, kWave);
+    }
+    poly_tag_g<G>(sp, pkt, pay, aad_len, P, r, s, j, c.act, tag);
+    if (c.act && j == 0) store_words<4>(sp, pay + P, tag);
+    // header protection (transmit.rs:713-738), once the MAC has read the unprotected header
+    const bool late = hp && !hp_in;  // tiny payloads and G > nblk: one more block for the wave
+    if (wave_any(late)) {
+      wave_sync();  // ciphertext and tags are in place
+      uint32_t a0, a1;
+      ChaChaPolicy::hp_mask(sp, pkt + d.pn_offset + 4, row, a0, a1);
+      if (late) {
+        m0 = a0;
+        m1 = a1;
+      }
+    }
+    const int jh = hp_in ? (int)(nblk % G) : 0;  // the group lane holding the mask
+    wave_sync();
+    if (hp && j == jh) apply_hp(sp, pkt, d, m0, m1);
+    wave_sync();
+  }
+
+  // receive composite (recv.rs:340-421 / 953-1025) on a narrow tile: HP removal, decode_pn, verify,
+  // then decrypt
+  template <class S, class St>
+  static __device__ __forceinline__ void open(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j,
+                                              bool direct, St& stg) {
+    const mq_pkt_desc& d = c.d;
+    stg.issue();
+    uint32_t pn_len = d.pn_len, trunc = 0;
+    uint8_t orig_b0 = 0, b0 = 0;
+    uint32_t orig_pn = 0;
+    const bool hp = c.act && !(d.flags & MQ_PKT_NO_HP);
+    if (c.pre_hp) {
+      if (hp) b0 = header_from_prepass(c, pn_len, trunc);
+    } else {
+      stg.complete();
+      if (wave_any(hp)) {  // every lane of a group computes its packet's mask (one block for the wave)
+        uint32_t m0, m1;
+        ChaChaPolicy::hp_mask(sp, hp ? pkt + d.pn_offset + 4 : pkt, row, m0, m1);
+        if (hp) b0 = header_from_mask(sp, pkt, c, m0, m1, pn_len, trunc);
+      }
+    }
+    uint32_t key[8];
+    load_key8(row->key, key);
+    const uint32_t aad_len = c.act ? (uint32_t)d.pn_offset + pn_len : 0u;
+    const uint32_t P = c.act ? d.len - aad_len - 16 : 0u;
+    const typename S::off_t pay = pkt + aad_len;
+    const uint32_t n0 = row->iv[0], n1 = row->iv[1] ^ bswap32((uint32_t)(c.pn >> 32)),
+                   n2 = row->iv[2] ^ bswap32((uint32_t)c.pn);
+    const uint32_t nblk = 1 + (P + 63) / 64;
+    const uint32_t Imax = wave_max_any(c.act ? (nblk + G - 1) / G : 0u);
+    const uint32_t ctr0 = (uint32_t)j;  // iteration 0 before the MAC (group lane 0: the one-time key)
+    uint32_t ks0[16];
+    chacha20_block(key, ctr0, n0, n1, n2, ks0);
+    if (c.pre_hp) stg.complete();
+    const bool hdr_written = hp && write_unmasked_header(sp, pkt, c, j, b0, pn_len, trunc, orig_b0, orig_pn);
+    wave_sync();
+    uint32_t otk[8], r[4], s[4], tag[4], got[4];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) otk[k] = ks0[k];
+    otk_bcast(otk, r, s);
+    poly_tag_g<G>(sp, pkt, pay, aad_len, P, r, s, j, c.act, tag);
+    load_words<4>(sp, pay + P, got);
+    const uint32_t diff = (tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) | (tag[3] ^ got[3]);
+    if (c.act && diff != 0) {  // Error::Crypto, buffer left as received
+      c.st = MQ_ERR_CRYPTO;
+      c.act = false;
+    }
+    wave_sync();  // every lane's MAC reads precede any plaintext write
+    if (c.act && ctr0 >= 1 && ctr0 < nblk) {
+      uint32_t w[17];
+      ChaChaPolicy::load_block(sp, pay, ctr0, w);
+      ChaChaPolicy::store_block(sp, pay, ctr0, P, ks0, w);
+    }
+    for (uint32_t it = 1; it < Imax; ++it) {
+      const uint32_t ctr = (uint32_t)j + G * it;
+      const bool a = c.act && ctr < nblk;
+      uint32_t w[17];
+      ChaChaPolicy::load_block(sp, pay, a ? ctr : 0u, w);
+      uint32_t ks[16];
+      chacha20_block(key, ctr, n0, n1, n2, ks);
+      if (a) ChaChaPolicy::store_block(sp, pay, ctr, P, ks, w);
+    }
+    wave_sync();
+    if (direct && hdr_written && !c.act) {  // direct path writes HBM in place: undo the unmask
+      sp.st8(pkt, orig_b0);
+      for (uint32_t b = 0; b < pn_len; ++b) sp.st8(pkt + d.pn_offset + b, (uint8_t)(orig_pn >> (8 * b)));
+    }
+  }
+};
+
+// One narrow tile: entries [e0, e0 + Q) of the batch (index != null: of the list `index`, holes
+// skipped; else descriptor indices), count = the entries' end. Every lane of the wave calls it.
+template <int G, bool OPEN, bool SINGLE>
+__device__ __forceinline__ void narrow_tile(uint8_t* wsm, const KeyRow* __restrict__ kt, uint32_t n_rows,
+                                            uint8_t* __restrict__ arena, uint64_t arena_len,
+                                            const mq_pkt_desc* __restrict__ desc, uint32_t e0, uint32_t count,
+                                            const uint32_t* __restrict__ index, uint8_t* __restrict__ status,
+                                            uint64_t* __restrict__ pn_out, const uint2* __restrict__ hpm) {
+  constexpr int Q = kWave / G;
+  const int lane = threadIdx.x & (kWave - 1), p = lane / G, j = lane % G;
+  PktCtx c;
+  const uint32_t e = e0 + (uint32_t)p;
+  c.tile = e0 / Q;
+  c.valid = e < count;
+  c.i = c.valid ? (index ? index[e] : e) : 0u;
+  if (c.i == kListHole) { c.valid = false; c.i = 0; }
+  if (c.valid) {
+    c.d = desc[c.i];
+  } else {
+    c.d.offset = 0; c.d.len = 0; c.d.key_id = 0; c.d.pn = 0; c.d.pn_offset = 0; c.d.pn_len = 0;
+    c.d.flags = 0; c.d.reserved = 0;
+  }
+  c.pre_hp = OPEN && hpm != nullptr;
+  c.hm0 = c.hm1 = 0;
+  if (OPEN && hpm && c.valid) {
+    const uint2 m = hpm[c.i];
+    c.hm0 = m.x;
+    c.hm1 = m.y;
+  }
+  c.st = c.valid ? validate<MQ_SUITE_CHACHA20, OPEN, SINGLE>(c.d, kt, n_rows, arena_len) : (int)MQ_ERR_INVALID_ARG;
+  c.act = c.valid && c.st == MQ_OK;
+  c.pn = c.d.pn;
+  c.otk = nullptr;
+  const KeyRow* row = SINGLE ? kt : kt + (c.act ? c.d.key_id : 0u);
+  Placement pl;
+  pl.off = c.act ? c.d.offset : 0;
+  pl.len = c.act ? c.d.len : 0u;
+  const uint64_t nch64 = c.act ? ((pl.off & 15) + (uint64_t)c.d.len + 15) >> 4 : 0u;
+  const uint32_t nch = (uint32_t)(nch64 < 0xFFFFu ? nch64 : 0xFFFFu);
+  const uint32_t incl = wave_incl_scan(j == 0 ? nch : 0u);  // the groups' inclusive prefix
+  const uint32_t total = lane_u32(incl, kWave - 1);
+  (void)Q;
+  if (total <= kNarrowChunks) {
+    pl.slot = incl - nch;
+    NarrowStager<G> stg{wsm, arena, arena_len, total, pl.slot, pl.base(), lane};
+    LdsSpace sp{wsm};
+    const uint32_t pkt = pl.slot * 16u + pl.head();
+    if (OPEN) NarrowPolicy<G, SINGLE>::template open<LdsSpace>(sp, pkt, c, row, j, false, stg);
+    else NarrowPolicy<G, SINGLE>::template seal<LdsSpace>(sp, pkt, c, row, j, stg);
+    wave_sync();
+    narrow_stage_out<G>(wsm, arena, j, c.act, pl);
+  } else {
+    GlobalSpace sp{arena, arena_len};
+    NoStager stg;
+    if (OPEN) NarrowPolicy<G, SINGLE>::template open<GlobalSpace>(sp, pl.off, c, row, j, true, stg);
+    else NarrowPolicy<G, SINGLE>::template seal<GlobalSpace>(sp, pl.off, c, row, j, stg);
+  }
+  tile_status<OPEN>(c, j, status, pn_out);
+}
+
 }  // namespace mq
 
 using namespace mq;
@@ -629,6 +1092,9 @@ __device__ __forceinline__ void chacha_list(const KeyRow* __restrict__ kt, uint3
     // no barrier waits for it until the next tile's first one)
     if (threadIdx.x == 0 && sched) pend = __hip_atomic_fetch_add(sched, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  // the last claim is never used, but it must have returned before sched_done can zero head 0
+  // (ADVICE r04): consuming its value makes thread 0 wait for it whatever the barrier lowers to
+  if (threadIdx.x == 0) asm volatile("" ::"v"(pend));
   __syncthreads();
   sched_done(sched);
 }
@@ -651,6 +1117,71 @@ __device__ __forceinline__ void chacha_list(const KeyRow* __restrict__ kt, uint3
   }
 MQ_CHACHA_LIST_KERNELS(mq_chacha_seal_list_kernel, mq_chacha_open_list_kernel, false)
 MQ_CHACHA_LIST_KERNELS(mq_chacha_seal_list1_kernel, mq_chacha_open_list1_kernel, true)
+
+// Flat batches of short packets (r05): one wave per 64 consecutive descriptors. The wave sizes
+// its 64 images and takes the narrowest lane group whose rounds fit the LDS image: G = 1 (one
+// round of 64 packets), 2 (two of 32), 4 (four of 16) or 8 (eight of 8, the octet layout without
+// the pool); a round over the budget runs on HBM (direct). No barriers: every wave is independent.
+template <bool OPEN, bool SINGLE>
+__device__ __forceinline__ void chacha_narrow_flat(const KeyRow* __restrict__ kt, uint32_t n_rows,
+                                                   uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                   const mq_pkt_desc* __restrict__ desc, uint32_t n,
+                                                   uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,
+                                                   const uint2* __restrict__ hpm) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t w = wave_id();
+  uint8_t* wsm = smem + w * kLdsBytes;
+  const uint32_t e0 = (blockIdx.x * kCcWaves + w) * (uint32_t)kWave;
+  if (e0 >= n) return;
+  const uint32_t lane = threadIdx.x & (kWave - 1), e = e0 + lane;
+  uint32_t nch = 0;
+  if (e < n) {  // offset and length only; validity is the tile's business (an over-count is harmless)
+    const uint32_t* dw = reinterpret_cast<const uint32_t*>(desc + e);
+    const uint64_t x = ((dw[0] & 15u) + (uint64_t)dw[2] + 15u) >> 4;
+    nch = (uint32_t)(x < 0xFFFFu ? x : 0xFFFFu);
+  }
+  const uint32_t incl = wave_incl_scan(nch);
+  auto fits = [&](uint32_t Q) -> bool {  // every round of Q packets within the budget (uniform)
+    for (uint32_t r = 0; r < (uint32_t)kWave / Q; ++r) {
+      const uint32_t hi = lane_u32(incl, (int)(r * Q + Q - 1)), lo = r ? lane_u32(incl, (int)(r * Q - 1)) : 0u;
+      if (hi - lo > kNarrowChunks) return false;
+    }
+    return true;
+  };
+#ifdef MQ_NARROW_ONLY  // register-pressure diagnostic: one lane group only
+  (void)fits;
+  for (uint32_t r = 0; r < MQ_NARROW_ONLY; ++r)
+    narrow_tile<MQ_NARROW_ONLY, OPEN, SINGLE>(wsm, kt, n_rows, arena, arena_len, desc, e0 + 64 / MQ_NARROW_ONLY * r, n,
+                                              nullptr, status, pn_out, hpm);
+  return;
+#endif
+  if (fits(64)) {
+    narrow_tile<1, OPEN, SINGLE>(wsm, kt, n_rows, arena, arena_len, desc, e0, n, nullptr, status, pn_out, hpm);
+  } else if (fits(32)) {
+    for (uint32_t r = 0; r < 2; ++r)
+      narrow_tile<2, OPEN, SINGLE>(wsm, kt, n_rows, arena, arena_len, desc, e0 + 32 * r, n, nullptr, status, pn_out, hpm);
+  } else if (fits(16)) {
+    for (uint32_t r = 0; r < 4; ++r)
+      narrow_tile<4, OPEN, SINGLE>(wsm, kt, n_rows, arena, arena_len, desc, e0 + 16 * r, n, nullptr, status, pn_out, hpm);
+  } else {
+    for (uint32_t r = 0; r < 8; ++r)
+      narrow_tile<8, OPEN, SINGLE>(wsm, kt, n_rows, arena, arena_len, desc, e0 + 8 * r, n, nullptr, status, pn_out, hpm);
+  }
+}
+#define MQ_CHACHA_NARROW_KERNELS(NAME_SEAL, NAME_OPEN, SINGLE)                                                \
+  extern "C" __global__ __launch_bounds__(64 * kCcWaves) __attribute__((amdgpu_waves_per_eu(4))) void NAME_SEAL( \
+      const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,        \
+      const mq_pkt_desc* __restrict__ desc, uint32_t n, uint8_t* __restrict__ status) {                       \
+    chacha_narrow_flat<false, SINGLE>(kt, n_rows, arena, arena_len, desc, n, status, nullptr, nullptr);       \
+  }                                                                                                           \
+  extern "C" __global__ __launch_bounds__(64 * kCcWaves) __attribute__((amdgpu_waves_per_eu(4))) void NAME_OPEN( \
+      const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,        \
+      const mq_pkt_desc* __restrict__ desc, uint32_t n, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out, \
+      const uint2* __restrict__ hpm) {                                                                        \
+    chacha_narrow_flat<true, SINGLE>(kt, n_rows, arena, arena_len, desc, n, status, pn_out, hpm);             \
+  }
+MQ_CHACHA_NARROW_KERNELS(mq_chacha_seal_narrow_kernel, mq_chacha_open_narrow_kernel, false)
+MQ_CHACHA_NARROW_KERNELS(mq_chacha_seal_narrow1_kernel, mq_chacha_open_narrow1_kernel, true)
 
 // ---- fused send composite (mq_batch_protect with the ChaCha20 suite hint, r04) -----------------
 // build + seal + header protection in one pass: the tile's eight packets are BUILT from their
@@ -888,6 +1419,28 @@ hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_
                          dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kl, n_rows, arena, arena_len, desc, n, index,
                          n_dev, status, sched);
     return hipGetLastError();
+  }
+  // Flat batches of short packets run the narrow kernels (r05): the arena's bytes per packet bound
+  // the average packet length from above, so a batch averaging at most kNarrowAvg bytes per packet
+  // takes them (configs B and E never do). MQ_CC_NARROW=0 / 1 (read per call: tests run both
+  // kernels on the same batch) forces either.
+  if (!index) {
+    constexpr uint64_t kNarrowAvg = 640;
+    bool narrow = arena_len <= kNarrowAvg * (uint64_t)n;
+    const char* ne = std::getenv("MQ_CC_NARROW");
+    if (ne) narrow = ne[0] == '1';
+    if (narrow) {
+      const uint32_t nb = (uint32_t)(((uint64_t)n + kWave * kCcWaves - 1) / (kWave * kCcWaves));
+      if (open)
+        hipLaunchKernelGGL(n_rows == 1 ? mq_chacha_open_narrow1_kernel : mq_chacha_open_narrow_kernel, dim3(nb),
+                           dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kt, n_rows, arena, arena_len, desc, n,
+                           status, pn_out, hpm);
+      else
+        hipLaunchKernelGGL(n_rows == 1 ? mq_chacha_seal_narrow1_kernel : mq_chacha_seal_narrow_kernel, dim3(nb),
+                           dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kt, n_rows, arena, arena_len, desc, n,
+                           status);
+      return hipGetLastError();
+    }
   }
   if (open)
     hipLaunchKernelGGL(n_rows == 1 || one ? mq_chacha_open1_kernel : mq_chacha_open_kernel, dim3(blocks),

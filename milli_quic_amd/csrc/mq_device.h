@@ -328,6 +328,52 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
   return x;
 }
 __device__ __forceinline__ bool wave_any(bool b) { return __builtin_amdgcn_ballot_w64(b) != 0; }
+// maximum / minimum over the wave of ANY per-lane value (quads, then octets, then the octet fold)
+__device__ __forceinline__ uint32_t wave_max_any(uint32_t x) {
+  x = max(x, quad_swap1(x));
+  x = max(x, quad_swap2(x));
+  x = max(x, half_mirror(x));
+  return wave_max_u32(x);
+}
+__device__ __forceinline__ uint32_t wave_min_any(uint32_t x) { return ~wave_max_any(~x); }
+
+// Lane groups of G = 1, 2, 4 or 8 lanes (one packet per group, lane = G p + j; the narrow ChaCha20
+// tiles, mq_chacha.hip): broadcast of group lane 0, of the last lane, the mirror j -> G-1-j, the sum
+// over the group. DPP quad_perm inside a quad (G <= 4), the octet ops above for G = 8.
+template <int G>
+struct Grp {
+  static_assert(G == 1 || G == 2 || G == 4 || G == 8, "lane group of 1, 2, 4 or 8");
+  template <int SEL>
+  static __device__ __forceinline__ uint32_t qp(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, SEL, 0xf, 0xf, false);
+  }
+  static __device__ __forceinline__ uint32_t bcast0(uint32_t x) {
+    if (G == 1) return x;
+    if (G == 2) return qp<0xA0>(x);  // [0,0,2,2]
+    if (G == 4) return qp<0x00>(x);  // [0,0,0,0]
+    return oct_bcast0(x);
+  }
+  static __device__ __forceinline__ uint32_t last(uint32_t x) {
+    if (G == 1) return x;
+    if (G == 2) return qp<0xF5>(x);  // [1,1,3,3]
+    if (G == 4) return qp<0xFF>(x);  // [3,3,3,3]
+    return oct_lane7(x);
+  }
+  static __device__ __forceinline__ uint32_t mirror(uint32_t x) {
+    if (G == 1) return x;
+    if (G == 2) return quad_swap1(x);
+    if (G == 4) return qp<0x1B>(x);  // [3,2,1,0]
+    return half_mirror(x);
+  }
+  static __device__ __forceinline__ uint32_t sum(uint32_t x) {
+    if (G == 1) return x;
+    x += quad_swap1(x);
+    if (G == 2) return x;
+    x += quad_swap2(x);
+    if (G == 4) return x;
+    return x + half_mirror(x);
+  }
+};
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t x) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) {

@@ -128,15 +128,16 @@ Devices& devices() {
   static Devices* d = new Devices();
   return *d;
 }
-mq::SideStreams<HipBackend>& side_streams() {
-  static auto* s = new mq::SideStreams<HipBackend>(64);
-  return *s;
-}
-
 // Dynamic tile schedule slots of the persistent AES kernels, per (device, stream): mq_runtime.h,
 // mq_tile.h TileSched. MQ_SCHED=0 (diagnostic) selects the static stride.
 mq::SchedSlots<HipBackend>& sched_slots() {
   static auto* s = new mq::SchedSlots<HipBackend>(1024, mq::kSchedSlotBytes);
+  return *s;
+}
+// Side streams hand their schedule slots back when their entry goes (evicted or released), so a
+// server that keeps creating and dropping caller streams never runs out of slots.
+mq::SideStreams<HipBackend>& side_streams() {
+  static auto* s = new mq::SideStreams<HipBackend>(64, [](hipStream_t side) { sched_slots().release(side); });
   return *s;
 }
 uint32_t* sched_slot(int dev, hipStream_t s) {
@@ -147,7 +148,15 @@ uint32_t* sched_slot(int dev, hipStream_t s) {
     const char* e = std::getenv("MQ_SCHED");
     return !(e && e[0] == '0');
   }();
-  return on ? (uint32_t*)sched_slots().get(dev, s) : nullptr;
+  if (!on) return nullptr;
+  // A slot assumes that kernels on its handle never overlap. Two handles break that:
+  // hipStreamPerThread is one value naming a different stream on every host thread, and the legacy
+  // handle is shared in the same way; and a stream under capture records kernels into a graph that
+  // may be replayed concurrently or on another stream. Those launches take the static stride.
+  if (s == hipStreamPerThread || s == hipStreamLegacy) return nullptr;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  return (uint32_t*)sched_slots().get(dev, s);
 }
 
 // The device a new object (key table, AEAD / HP context) is created on: the thread's selection,

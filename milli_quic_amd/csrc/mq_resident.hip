@@ -663,6 +663,7 @@ struct Resident {
   uint64_t idle = 0, life = 0;
   int khz = 100000;  // wall-clock rate
   uint32_t host_ns[3] = {0, 0, 0};  // last call: request written, waited for done, result copied
+  std::vector<ResArea*> abandoned;  // mailboxes given up on a wedged kernel (still told to stop at exit)
   std::mutex mu;
 };
 
@@ -670,8 +671,11 @@ std::mutex g_res_mu;
 std::vector<Resident*> g_res;  // per device; never freed (the kernel may outlive static destructors)
 
 void stop_all() {  // atexit: ask every resident kernel to leave (plain stores, no HIP call)
-  for (Resident* r : g_res)
+  for (Resident* r : g_res) {
     if (r && r->host) __atomic_store_n(&r->host->hdr[kHwStop], (uint64_t)1, __ATOMIC_SEQ_CST);
+    if (r)
+      for (ResArea* x : r->abandoned) __atomic_store_n(&x->hdr[kHwStop], (uint64_t)1, __ATOMIC_SEQ_CST);
+  }
 }
 
 Resident* resident(int dev) {
@@ -780,7 +784,28 @@ int mq_resident_call(int dev, const ResReq& q, uint64_t uid, const uint8_t* aad,
       // wait for its stream. A kernel not yet placed (every CU busy) starts, sees the stop slot and
       // leaves. If it served the request meanwhile, the call succeeds after all.
       __atomic_store_n(&a->hdr[kHwStop], (uint64_t)1, __ATOMIC_SEQ_CST);
-      if (r->launched && hipStreamSynchronize(r->stream) != hipSuccess) return MQ_ERR_HIP;
+      // The wait for the kernel to leave is bounded too: a kernel that cannot be
+      // placed or is wedged would otherwise block this call forever. Past a second deadline the
+      // mailbox is abandoned (poisoned): the old area and stream are left to that kernel, and the
+      // next call starts over with a fresh area, stream and kernel.
+      if (r->launched) {
+        const auto t_stop = std::chrono::steady_clock::now();
+        hipError_t q = hipErrorNotReady;
+        while ((q = hipStreamQuery(r->stream)) == hipErrorNotReady &&
+               std::chrono::steady_clock::now() - t_stop < resident_timeout())
+          std::this_thread::yield();
+        if (q == hipErrorNotReady) {
+          r->abandoned.push_back(r->host);  // never freed: the kernel may still write it
+          r->host = nullptr;
+          r->dptr = nullptr;
+          r->stream = nullptr;
+          r->launched = false;
+          r->seq = 0;
+          r->hpow_uid = 0;
+          return MQ_ERR_HIP;
+        }
+        if (q != hipSuccess) return MQ_ERR_HIP;
+      }
       if (load_acq(&a->ctl.done) == seq) break;
       return MQ_ERR_HIP;  // the next call relaunches (state: exited) and supersedes this request
     }

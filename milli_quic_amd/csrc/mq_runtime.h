@@ -116,17 +116,21 @@ class SideStreams {
   typedef typename B::Event Event;
   static constexpr int kSteps = 8;  // caller -> side hand-offs of one fork (chunked pipelines)
 
+  typedef void (*Hook)(Stream);  // called with each side stream before it is destroyed
+
   struct Entry {
     int dev = -1;
     Stream caller{};
     Stream side[kSides]{};
     Event fork{}, join[kSides]{}, step[kSteps]{};
     bool ok = false;
+    Hook on_destroy = nullptr;
     std::mutex mu;  // one fork/launch/join sequence at a time
     ~Entry() {
       // stream_destroy waits for the side stream's work; run it on the entry's device
       typename DeviceRegistry<B>::Guard g(dev);
       for (int k = 0; k < kSides; ++k) {
+        if (side[k] && on_destroy) on_destroy(side[k]);  // e.g. its schedule slot back (mq_host.cpp)
         if (side[k]) B::stream_destroy(side[k]);
         if (join[k]) B::event_destroy(join[k]);
       }
@@ -172,7 +176,7 @@ class SideStreams {
     bool joined_ = false;
   };
 
-  explicit SideStreams(size_t cap = 64) : cap_(cap) {}
+  explicit SideStreams(size_t cap = 64, Hook on_destroy = nullptr) : cap_(cap), hook_(on_destroy) {}
 
   // Fork `used` (<= kSides) side streams off `caller` on device `dev`; an empty Fork (launch on the
   // caller's stream instead) if the streams cannot be created.
@@ -227,6 +231,7 @@ class SideStreams {
       e = std::make_shared<Entry>();
       e->dev = dev;
       e->caller = caller;
+      e->on_destroy = hook_;
       bool ok = B::event_create(&e->fork);
       for (int k = 0; k < kSides && ok; ++k) ok = B::stream_create(&e->side[k]) && B::event_create(&e->join[k]);
       for (int k = 0; k < kSteps && ok; ++k) ok = B::event_create(&e->step[k]);
@@ -244,6 +249,7 @@ class SideStreams {
   std::mutex mu_;
   std::list<std::shared_ptr<Entry>> lru_;
   size_t cap_;
+  Hook hook_;
 };
 
 // Device words of the persistent tile kernels' dynamic schedule (mq_tile.h TileSched), one slot per

@@ -296,12 +296,56 @@ static void test_sched_slots() {
   Fake::allocated.clear();
 }
 
+// side streams give their schedule slots back when their entry is evicted or released (ADVICE
+// r04): a server that churns through more caller streams than there are slots keeps a bounded
+// number of slots assigned, and a released side stream's slot is recycled, not leaked
+static mq::SchedSlots<Fake>* g_churn_slots = nullptr;
+static void churn_hook(FakeObj* side) { g_churn_slots->release(side); }
+
+static void test_side_stream_slot_churn() {
+  mq::SchedSlots<Fake> slots(1024, 64);
+  g_churn_slots = &slots;
+  std::vector<FakeObj*> kept;  // callers that never release their stream
+  {
+    mq::SideStreams<Fake, 2> ss(64, churn_hook);
+    Devices::Guard g(1);
+    for (int k = 0; k < 600; ++k) {  // 1200 side streams: more than the 1024 slots
+      FakeObj* caller = new FakeObj(1);
+      CHECK(slots.get(1, caller) != nullptr);  // the caller stream's own slot
+      {
+        auto f = ss.fork(1, caller, 2);
+        CHECK(f);
+        CHECK(slots.get(1, f.side(0)) != nullptr);  // e.g. the hot-key AES kernel's slot
+        CHECK(slots.get(1, f.side(1)) != nullptr);
+      }
+      if (k % 3 == 0) {  // some callers release their stream explicitly, the rest are evicted
+        slots.release(caller);
+        ss.release(caller);
+        delete caller;
+      } else {
+        kept.push_back(caller);
+      }
+      // at most 64 entries x 2 side streams, plus the callers that never released theirs
+      CHECK(slots.assigned(1) <= 2 * 64 + kept.size());
+    }
+    CHECK(ss.size() == 64 && Fake::live_streams == 128);
+  }
+  // every side stream's slot came back: only the unreleased callers' own slots remain
+  CHECK(slots.assigned(1) == kept.size() && kept.size() == 400);
+  CHECK(Fake::live_streams == 0);
+  for (FakeObj* c : kept) delete c;
+  g_churn_slots = nullptr;
+  for (void* p : Fake::allocated) std::free(p);
+  Fake::allocated.clear();
+}
+
 int main() {
   test_per_thread_selection();
   test_guard();
   test_side_streams();
   test_concurrent_forks();
   test_sched_slots();
+  test_side_stream_slot_churn();
   std::printf("runtime ok\n");
   return 0;
 }

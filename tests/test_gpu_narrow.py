@@ -1,0 +1,192 @@
+"""Narrow ChaCha20-Poly1305 tiles (r05: G lanes per packet, 64 / G packets per wave) against the
+oracle, byte for byte: flat batches of short packets (the narrow kernel, mq_chacha.hip
+chacha_narrow_flat) over random lengths, both header forms, 1..4-byte packet numbers, several key
+rows, packed back to back at every alignment; the same batches forced through the octet kernel
+(MQ_CC_NARROW=0) must give the same bytes, and long packets forced through the narrow kernel
+(MQ_CC_NARROW=1: G = 8 rounds, direct rounds over the LDS budget) as well. Tampered packets, bad
+key ids and a packet ending exactly at an arena end that is not 16-B aligned are included.
+Reference composites: transmit.rs:625-755 (seal + header protection), recv.rs:340-421 /
+953-1025 (header protection removal, decode_pn, open); rustcrypto.rs:111-165, 197-220."""
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from milli_quic_amd import _lib, batch, workload  # noqa: E402
+from milli_quic_amd.batch import KeyTable, make_descs  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+CHACHA = _lib.MQ_SUITE_CHACHA20
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device(mqlib):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    assert mqlib.mq_device_init(0) == 0
+
+
+class _Env:
+    """MQ_CC_NARROW for the calls inside the block (read per call by mq_launch_chacha)."""
+
+    def __init__(self, v):
+        self.v = v
+
+    def __enter__(self):
+        self.old = os.environ.get("MQ_CC_NARROW")
+        if self.v is None:
+            os.environ.pop("MQ_CC_NARROW", None)
+        else:
+            os.environ["MQ_CC_NARROW"] = self.v
+
+    def __exit__(self, *a):
+        if self.old is None:
+            os.environ.pop("MQ_CC_NARROW", None)
+        else:
+            os.environ["MQ_CC_NARROW"] = self.old
+
+
+def to_dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).to(DEV)
+
+
+def gpu_run(keys, arena, desc, open_=False, use_ws=True, hint=CHACHA):
+    kt = KeyTable(keys)
+    n = len(desc)
+    a, d = to_dev(arena), to_dev(desc)
+    st = torch.full((max(n, 1),), 0xEE, dtype=torch.uint8, device=DEV)
+    pn = torch.zeros(max(n, 1), dtype=torch.int64, device=DEV)
+    ws = torch.full((max(batch.workspace_bytes(n), 256),), 0xA5, dtype=torch.uint8, device=DEV) if use_ws else None
+    if open_:
+        batch.open_(kt, a, d, st, pn, hint, ws)
+    else:
+        batch.seal(kt, a, d, st, hint, ws)
+    torch.cuda.synchronize()
+    return a.cpu().numpy(), st.cpu().numpy()[:n], pn.cpu().numpy().view(np.uint64)[:n]
+
+
+def oracle_run(orc, keys, arena, desc, open_=False, hint=CHACHA):
+    a = arena.copy()
+    if open_:
+        st, pn = orc.batch_open(keys, a, desc, hint, threads=8)
+        return a, st, pn
+    return a, orc.batch_seal(keys, a, desc, hint, threads=8), None
+
+
+def short_batch(n, lmin, lmax, n_keys=1, seed=1, long_frac=0.2, lead=0):
+    """n ChaCha20 packets of random lengths in [lmin, lmax] packed back to back after `lead` bytes:
+    short headers (DCID 8) or long ones (26-B Initial layout), pn_len 1..4, key row i mod n_keys.
+    The arena ends exactly at the last packet (its length is usually not a multiple of 16)."""
+    rng = np.random.default_rng(seed)
+    keys = workload.uniform_keys(CHACHA, n_keys)
+    pn_len = rng.integers(1, 5, size=n).astype(np.uint8)
+    long_h = rng.random(n) < long_frac
+    pn_off = np.where(long_h, workload.LONG_HDR, workload.SHORT_HDR).astype(np.int64)
+    L = rng.integers(lmin, lmax + 1, size=n).astype(np.int64)
+    L = np.maximum(L, pn_off + 20)  # the header-protection sample fits
+    offs = lead + np.concatenate([[0], np.cumsum(L[:-1])]).astype(np.int64)
+    arena = workload.splitmix_bytes(int(offs[-1] + L[-1]), seed=seed)
+    pns = (np.uint64(1 << 20) + rng.integers(0, 1 << 30, size=n).astype(np.uint64))
+    for i in range(n):
+        o, pl = int(offs[i]), int(pn_len[i])
+        arena[o] = (0xC0 if long_h[i] else 0x40) | (pl - 1)
+        po = int(pn_off[i])
+        for b in range(pl):
+            arena[o + po + b] = (int(pns[i]) >> (8 * (pl - 1 - b))) & 0xFF
+    kid = (np.arange(n) % n_keys).astype(np.uint32)
+    flags = np.where(long_h, _lib.MQ_PKT_LONG_HEADER, 0).astype(np.uint8)
+    sd = make_descs(offs.astype(np.uint64), L.astype(np.uint32), kid, pns, pn_off.astype(np.uint16), pn_len, flags)
+    od = make_descs(offs.astype(np.uint64), L.astype(np.uint32), kid, pns - np.uint64(1), pn_off.astype(np.uint16), 0,
+                    flags)
+    return keys, arena, sd, od, pns
+
+
+def roundtrip_vs_oracle(orc, keys, arena, sd, od, pns, modes=(None, "0", "1")):
+    o_out, o_st, _ = oracle_run(orc, keys, arena, sd)
+    o_back, o_st2, o_pn = oracle_run(orc, keys, o_out, od, open_=True)
+    assert (o_st == 0).all() and (o_st2 == 0).all()
+    for mode in modes:
+        with _Env(mode):
+            for use_ws in (True, False):
+                g_out, g_st, _ = gpu_run(keys, arena, sd, use_ws=use_ws)
+                assert (g_st == o_st).all(), (mode, use_ws, np.nonzero(g_st != o_st)[0][:8])
+                assert g_out.tobytes() == o_out.tobytes(), (mode, use_ws)
+                g_back, g_st, g_pn = gpu_run(keys, o_out, od, open_=True, use_ws=use_ws)
+                assert (g_st == o_st2).all(), (mode, use_ws)
+                assert g_back.tobytes() == o_back.tobytes(), (mode, use_ws)
+                assert (g_pn == o_pn).all() and (g_pn == pns).all(), (mode, use_ws)
+
+
+@pytest.mark.parametrize("lmin,lmax,n,n_keys", [
+    (21, 90, 3001, 1),     # G = 1 (one round of 64 packets per wave), a ragged last wave
+    (21, 140, 2000, 3),    # G = 1 / 2 by wave, three key rows
+    (130, 290, 1500, 1),   # G = 2
+    (290, 600, 1200, 2),   # G = 4
+    (21, 640, 4000, 1),    # every G, waves of mixed sizes
+])
+def test_narrow_flat_vs_oracle(orc, lmin, lmax, n, n_keys):
+    keys, arena, sd, od, pns = short_batch(n, lmin, lmax, n_keys, seed=lmin * 7 + lmax)
+    roundtrip_vs_oracle(orc, keys, arena, sd, od, pns)
+
+
+@pytest.mark.parametrize("lead", [0, 5, 13])
+def test_narrow_uniform_alignments(orc, lead):
+    # uniform 64-B / 256-B batches (the len_sweep shapes) shifted by `lead` bytes: every packet at
+    # a fixed misalignment, the arena's last chunk partial
+    for L in (64, 256):
+        w = workload.uniform(777, CHACHA, L=L, pn_len=1 + L % 4)
+        arena = np.concatenate([np.full(lead, 0x5A, np.uint8), w.arena])
+        sd, od = w.seal_desc.copy(), w.open_desc.copy()
+        sd["offset"] += lead
+        od["offset"] += lead
+        roundtrip_vs_oracle(orc, w.keys, arena, sd, od, w.pns, modes=(None, "0"))
+
+
+def test_narrow_forced_on_long_packets(orc):
+    # MQ_CC_NARROW=1 on packets up to 2048 B: waves choose G = 8 rounds (the octet layout without
+    # the pool), rounds over the LDS budget run on HBM (direct)
+    keys, arena, sd, od, pns = short_batch(700, 21, 2048, 2, seed=99)
+    roundtrip_vs_oracle(orc, keys, arena, sd, od, pns, modes=("1",))
+
+
+def test_narrow_failures_match_oracle(orc):
+    keys, arena, sd, od, pns = short_batch(2500, 21, 400, 2, seed=5)
+    sealed, st, _ = oracle_run(orc, keys, arena, sd)
+    assert (st == 0).all()
+    rng = np.random.default_rng(8)
+    bad = sealed.copy()
+    for v in rng.choice(len(sd), size=300, replace=False):  # one flipped bit anywhere in the packet
+        o, L = int(sd["offset"][v]), int(sd["len"][v])
+        bad[o + int(rng.integers(0, L))] ^= 1 << int(rng.integers(0, 8))
+    od = od.copy()
+    od["key_id"][3] = 77                   # key id out of range
+    od["len"][4] = 24                      # sample out of range -> Crypto
+    od["offset"][6] = len(bad) - 10        # past the arena end
+    od["pn"][9] = (1 << 62) - 2            # decode_pn above 2^62 - 1 -> ProtocolViolation
+    o_out, o_st, o_pn = oracle_run(orc, keys, bad, od, open_=True)
+    assert (o_st != 0).sum() >= 250
+    for mode in (None, "0"):
+        with _Env(mode):
+            for use_ws in (True, False):
+                g_out, g_st, g_pn = gpu_run(keys, bad, od, open_=True, use_ws=use_ws)
+                assert (g_st == o_st).all(), (mode, use_ws, np.nonzero(g_st != o_st)[0][:8])
+                assert g_out.tobytes() == o_out.tobytes(), (mode, use_ws)
+                ok = o_st == 0
+                assert (g_pn[ok] == o_pn[ok]).all()
+    sd = sd.copy()
+    sd["pn_len"][3] = 0
+    sd["len"][9] = 20
+    sd["key_id"][10] = 1 << 20
+    o_out, o_st, _ = oracle_run(orc, keys, arena, sd)
+    g_out, g_st, _ = gpu_run(keys, arena, sd)
+    assert (g_st == o_st).all() and g_out.tobytes() == o_out.tobytes()
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 255, 257])
+def test_narrow_counts(orc, n):
+    # waves with one packet, exactly full waves, a partial last wave and a partial workgroup
+    keys, arena, sd, od, pns = short_batch(n, 21, 200, 1, seed=n)
+    roundtrip_vs_oracle(orc, keys, arena, sd, od, pns, modes=(None,))
