@@ -744,7 +744,7 @@ struct NarrowPolicy {
     // a single-key tile keeps its key in SGPRs
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      if (SINGLE) asm volatile("" : "+s"(key[k]));
+      if (SINGLE) key[k] = __builtin_amdgcn_readfirstlane(key[k]);
       else pin(key[k]);
     }
     pin(n0); pin(n1); pin(n2);
@@ -764,8 +764,6 @@ struct NarrowPolicy {
       const uint32_t ctr = is_otk ? 0u : slot + 1;  // keystream block of the slot
       const bool a = c.act && ctr < nblk;            // a keystream block (or the one-time key)
       const bool is_hp = hp_in && slot == nblk;
-      uint32_t w[17];
-      if (it > 0) ChaChaPolicy::load_block(sp, pay, a && !is_otk ? ctr : 0u, w);
       uint32_t ks[16];
       if (wave_any(is_hp)) {  // the HP lanes run the HP key on the sample (ciphertext by now)
         uint32_t smp[4], kh[8], kk[8];
@@ -784,8 +782,10 @@ struct NarrowPolicy {
           if (rec && j == 0) write_record_header(sp, pkt, d);
           wave_sync();
         }
-        ChaChaPolicy::load_block(sp, pay, a && !is_otk ? ctr : 0u, w);
       }
+      // the block's raw LDS words after the rounds (not in flight during them: 17 VGPRs fewer)
+      uint32_t w[17];
+      ChaChaPolicy::load_block(sp, pay, a && !is_otk ? ctr : 0u, w);
       if (is_otk) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) otk[k] = ks[k];
@@ -970,13 +970,46 @@ using namespace mq;
 // tb: the workgroup's block of W tiles (blockIdx.x, or the persistent kernels' current block)
 // tid: threadIdx.x (the persistent list kernels pass an opaque copy per tile, so nothing derived
 // from it is hoisted out of their loop and held across every tile — that pressure spilled)
+// A partition list's narrow regions (mq_partition.hip: reg = tiles of G = 8, 4, 2, 1, then the first
+// entries of the G = 4, 2, 1 regions): list tile u >= T8 is narrow tile u - T8 of the G = 4 region,
+// and so on. Runs it, if there is one.
 template <bool OPEN, bool SINGLE>
+__device__ __forceinline__ void chacha_narrow_list(uint8_t* wsm, uint32_t u, const uint32_t* __restrict__ reg,
+                                                   const KeyRow* __restrict__ kt, uint32_t n_rows,
+                                                   uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                   const mq_pkt_desc* __restrict__ desc,
+                                                   const uint32_t* __restrict__ index, uint8_t* __restrict__ status,
+                                                   uint64_t* __restrict__ pn_out, const uint2* __restrict__ hpm) {
+  const uint32_t T8 = reg[0], T4 = reg[1], T2 = reg[2], T1 = reg[3], R4 = reg[4], R2 = reg[5], R1 = reg[6];
+  if (u < T8) return;
+  uint32_t v = u - T8;
+  if (v < T4) {
+    narrow_tile<4, OPEN, SINGLE>(wsm, kt, n_rows, arena, arena_len, desc, R4 + 16 * v, R4 + 16 * T4, index, status,
+                                 pn_out, hpm);
+    return;
+  }
+  v -= T4;
+  if (v < T2) {
+    narrow_tile<2, OPEN, SINGLE>(wsm, kt, n_rows, arena, arena_len, desc, R2 + 32 * v, R2 + 32 * T2, index, status,
+                                 pn_out, hpm);
+    return;
+  }
+  v -= T2;
+  if (v < T1)
+    narrow_tile<1, OPEN, SINGLE>(wsm, kt, n_rows, arena, arena_len, desc, R1 + 64 * v, R1 + 64 * T1, index, status,
+                                 pn_out, hpm);
+}
+
+// LIST: a partition list with narrow regions (reg): the octet tiles are the G = 8 region's (count =
+// its entries), a workgroup with an octet tile runs the pool's barriers on every wave (its narrow
+// waves run their tile first), one without any runs its narrow tiles with no barrier.
+template <bool OPEN, bool SINGLE, bool LIST = false>
 __device__ __forceinline__ void chacha_tile(uint32_t tb, uint32_t tid, const KeyRow* __restrict__ kt, uint32_t n_rows,
                                             uint8_t* __restrict__ arena, uint64_t arena_len,
                                             const mq_pkt_desc* __restrict__ desc, uint32_t n,
                                             const uint32_t* __restrict__ index, const uint32_t* __restrict__ n_dev,
                                             uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,
-                                            const uint2* __restrict__ hpm) {
+                                            const uint2* __restrict__ hpm, const uint32_t* __restrict__ reg = nullptr) {
   constexpr uint32_t W = kCcWaves;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t w = tid >> 6;
@@ -986,11 +1019,24 @@ __device__ __forceinline__ void chacha_tile(uint32_t tb, uint32_t tid, const Key
   PktCtx c;
   const KeyRow* row;
   CcPool pool{false, smem, w * kLdsBytes, (uint32_t*)(wsm + kDataBudget + 32u * (uint32_t)p), kt};
+  if (LIST) {  // the octet region's entries
+    n = kPktsPerTile * __builtin_amdgcn_readfirstlane(reg[0]);
+    n_dev = nullptr;
+  }
   if (!tile_ctx<MQ_SUITE_CHACHA20, OPEN, SINGLE>(tile_id, kt, n_rows, arena_len, desc, n, index, n_dev, hpm,
                                                  TilePrefetch{false, 0u, 0u}, c, row, tid)) {
     // past the batch (list capacities exceed the count): a whole workgroup leaves at once, a
     // wave of a live workgroup only joins its barriers and pool
-    if (tb * W * kPktsPerTile >= (n_dev ? *n_dev : n)) return;  // workgroup-uniform
+    if (tb * W * kPktsPerTile >= (n_dev ? *n_dev : n)) {  // workgroup-uniform
+      if (LIST) chacha_narrow_list<OPEN, SINGLE>(wsm, tile_id, reg, kt, n_rows, arena, arena_len, desc, index, status,
+                                                 pn_out, hpm);
+      return;
+    }
+    if (LIST) {  // this wave's narrow tile, before the barriers (its records are reset after it)
+      chacha_narrow_list<OPEN, SINGLE>(wsm, tile_id, reg, kt, n_rows, arena, arena_len, desc, index, status, pn_out,
+                                       hpm);
+      wave_sync();
+    }
     if (j == 0) pool.rec[0] = 0;
     __syncthreads();
     cc_pool_run<SINGLE>(pool, tid);
@@ -1047,6 +1093,27 @@ __device__ __forceinline__ void chacha_tile(uint32_t tb, uint32_t tid, const Key
 MQ_CHACHA_KERNELS(mq_chacha_seal_kernel, mq_chacha_open_kernel, false)
 MQ_CHACHA_KERNELS(mq_chacha_seal1_kernel, mq_chacha_open1_kernel, true)
 
+// One-shot grids over a partition list with narrow regions (reg, mq_partition.hip): tile
+// tb * W + w is an octet tile of the G = 8 region or a narrow tile after it
+#define MQ_CHACHA_LGRID_KERNELS(NAME_SEAL, NAME_OPEN, SINGLE)                                             \
+  extern "C" __global__ __launch_bounds__(64 * kCcWaves) __attribute__((amdgpu_waves_per_eu(4))) void NAME_SEAL( \
+      const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
+      const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
+      const uint32_t* __restrict__ reg, uint8_t* __restrict__ status) {                                   \
+    chacha_tile<false, SINGLE, true>(blockIdx.x, threadIdx.x, kt, n_rows, arena, arena_len, desc, n, index, nullptr, \
+                                     status, nullptr, nullptr, reg);                                      \
+  }                                                                                                       \
+  extern "C" __global__ __launch_bounds__(64 * kCcWaves) __attribute__((amdgpu_waves_per_eu(4))) void NAME_OPEN( \
+      const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
+      const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
+      const uint32_t* __restrict__ reg, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,      \
+      const uint2* __restrict__ hpm) {                                                                    \
+    chacha_tile<true, SINGLE, true>(blockIdx.x, threadIdx.x, kt, n_rows, arena, arena_len, desc, n, index, nullptr, \
+                                    status, pn_out, hpm, reg);                                            \
+  }
+MQ_CHACHA_LGRID_KERNELS(mq_chacha_seal_lgrid_kernel, mq_chacha_open_lgrid_kernel, false)
+MQ_CHACHA_LGRID_KERNELS(mq_chacha_seal_lgrid1_kernel, mq_chacha_open_lgrid1_kernel, true)
+
 // Partition lists (index != null) run on PERSISTENT workgroups (r04): the list's length is a
 // device count, so a grid covering the list capacity (1.6 x the batch in tiles of W) was mostly
 // workgroups that read the count and left — config E's ChaCha list has ~15k blocks of work in a
@@ -1063,7 +1130,8 @@ __device__ __forceinline__ void chacha_list(const KeyRow* __restrict__ kt, uint3
                                             uint64_t arena_len, const mq_pkt_desc* __restrict__ desc, uint32_t n,
                                             const uint32_t* __restrict__ index, const uint32_t* __restrict__ n_dev,
                                             uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,
-                                            const uint2* __restrict__ hpm, uint32_t* __restrict__ sched) {
+                                            const uint2* __restrict__ hpm, uint32_t* __restrict__ sched,
+                                            const uint32_t* __restrict__ reg) {
   constexpr uint32_t W = kCcWaves;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   // the next block goes to every wave through word 7 of wave 0's first pool record, free between
@@ -1072,6 +1140,7 @@ __device__ __forceinline__ void chacha_list(const KeyRow* __restrict__ kt, uint3
   uint32_t* next_slot = (uint32_t*)(smem + kDataBudget) + 7;
   uint32_t tb = blockIdx.x, pend = 0;
   if (threadIdx.x == 0 && sched) pend = __hip_atomic_fetch_add(sched, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  (void)reg;  // the receive passes' partitions have no narrow regions (mq_partition.hip, skip_unkeyed)
   for (;;) {
     const uint32_t count = n_dev ? *n_dev : n;
     if (tb * W * kPktsPerTile >= count) break;  // workgroup-uniform
@@ -1105,15 +1174,16 @@ __device__ __forceinline__ void chacha_list(const KeyRow* __restrict__ kt, uint3
   extern "C" __global__ __launch_bounds__(64 * kCcWaves) __attribute__((amdgpu_waves_per_eu(4))) void NAME_SEAL( \
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,     \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,                \
-      const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint32_t* __restrict__ sched) {    \
-    chacha_list<false, SINGLE>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr, nullptr, sched); \
+      const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint32_t* __restrict__ sched,      \
+      const uint32_t* __restrict__ reg) {                                                                  \
+    chacha_list<false, SINGLE>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr, nullptr, sched, reg); \
   }                                                                                                        \
   extern "C" __global__ __launch_bounds__(64 * kCcWaves) __attribute__((amdgpu_waves_per_eu(4))) void NAME_OPEN( \
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,     \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,                \
       const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,     \
-      const uint2* __restrict__ hpm, uint32_t* __restrict__ sched) {                                       \
-    chacha_list<true, SINGLE>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm, sched); \
+      const uint2* __restrict__ hpm, uint32_t* __restrict__ sched, const uint32_t* __restrict__ reg) {   \
+    chacha_list<true, SINGLE>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm, sched, reg); \
   }
 MQ_CHACHA_LIST_KERNELS(mq_chacha_seal_list_kernel, mq_chacha_open_list_kernel, false)
 MQ_CHACHA_LIST_KERNELS(mq_chacha_seal_list1_kernel, mq_chacha_open_list1_kernel, true)
@@ -1386,7 +1456,7 @@ hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_
                             uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
                             const uint32_t* index, const uint32_t* n_dev, uint8_t* status,
                             uint64_t* pn_out, uint2* hpm, bool own_hp, hipStream_t s, int cus, uint32_t* sched,
-                            int64_t single_row, bool persistent) {
+                            int64_t single_row, bool persistent, const uint32_t* reg) {
   const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
   if (tiles == 0) return hipSuccess;
   if (open && hpm && own_hp) {  // !own_hp: mq_launch_mixed_hp covers both suites' lists
@@ -1400,10 +1470,8 @@ hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_
   // list then costs 1024 workgroups, not a grid over the list capacity), else on the one-shot grid,
   // which measured 1.1 % faster on config E (r04q: 557.9 vs 551.6 GiB/s, three alternating runs).
   // MQ_CC_LIST=0 / 1 (diagnostic) forces either.
-  static const int forced = [] {
-    const char* e = std::getenv("MQ_CC_LIST");
-    return e ? (e[0] == '0' ? 0 : 1) : -1;
-  }();
+  const char* fe = std::getenv("MQ_CC_LIST");  // read per call: tests run both grids on one batch
+  const int forced = fe ? (fe[0] == '0' ? 0 : 1) : -1;
   if (forced >= 0) persistent = forced == 1;
   // single_row >= 0: every packet of the list is on that row (the single-key kernels)
   const bool one = index && single_row >= 0 && (uint64_t)single_row < n_rows;
@@ -1413,11 +1481,22 @@ hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_
     if (open)
       hipLaunchKernelGGL(one ? mq_chacha_open_list1_kernel : mq_chacha_open_list_kernel, dim3(grid),
                          dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kl, n_rows, arena, arena_len, desc, n, index,
-                         n_dev, status, pn_out, hpm, sched);
+                         n_dev, status, pn_out, hpm, sched, reg);
     else
       hipLaunchKernelGGL(one ? mq_chacha_seal_list1_kernel : mq_chacha_seal_list_kernel, dim3(grid),
                          dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kl, n_rows, arena, arena_len, desc, n, index,
-                         n_dev, status, sched);
+                         n_dev, status, sched, reg);
+    return hipGetLastError();
+  }
+  if (index) {  // one-shot grid over the list capacity (every region's tiles fit: a tile holds >= 8 entries)
+    if (open)
+      hipLaunchKernelGGL(one ? mq_chacha_open_lgrid1_kernel : mq_chacha_open_lgrid_kernel, dim3(blocks),
+                         dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kl, n_rows, arena, arena_len, desc, n, index,
+                         reg, status, pn_out, hpm);
+    else
+      hipLaunchKernelGGL(one ? mq_chacha_seal_lgrid1_kernel : mq_chacha_seal_lgrid_kernel, dim3(blocks),
+                         dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kl, n_rows, arena, arena_len, desc, n, index,
+                         reg, status);
     return hipGetLastError();
   }
   // Flat batches of short packets run the narrow kernels (r05): the arena's bytes per packet bound

@@ -26,7 +26,8 @@ hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_
                             uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
                             const uint32_t* index, const uint32_t* n_dev, uint8_t* status,
                             uint64_t* pn_out, uint2* hpm, bool own_hp, hipStream_t s, int cus, uint32_t* sched,
-                            int64_t single_row, bool persistent);
+                            int64_t single_row, bool persistent, const uint32_t* reg);
+const uint32_t* mq_partition_regions(const uint32_t* counts);
 hipError_t mq_launch_chacha_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t* key_ids,
                                const uint8_t* samples, uint8_t* masks, uint32_t n, hipStream_t s);
 hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena,
@@ -475,7 +476,7 @@ int run_one(Scratch& sc, const KeyRow& row, const uint8_t* aad, uint32_t aad_len
   // protection pass to launch (own_hp false)
   hipError_t e = row.suite == MQ_SUITE_CHACHA20
                      ? mq_launch_chacha(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, st, pn, nullptr, false, sc.stream,
-                                        0, nullptr, -1, false)
+                                        0, nullptr, -1, false, nullptr)
                      : mq_launch_aes(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, nullptr, st, pn, nullptr, false,
                                      sc.stream, sc.stream, devices().cus(sc.device), nullptr, nullptr, nullptr);
   if (e != hipSuccess) return MQ_ERR_HIP;
@@ -903,7 +904,7 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
   uint2* hpm = (open && ws) ? (uint2*)ws : nullptr;
   if (suite_hint == MQ_SUITE_CHACHA20) {
     e = mq_launch_chacha(open, kt->dev, kt->rows, arena, arena_len, desc, n, nullptr, nullptr, status, pn_out, hpm, true,
-                         s, cus, nullptr, -1, false);
+                         s, cus, nullptr, -1, false, nullptr);
   } else if (suite_hint == MQ_SUITE_AES128GCM && (kt->rows == 1 || !ws || n > (1u << 30))) {
     e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, n, nullptr, nullptr, nullptr, status, pn_out,
                       hpm, true, s, s, cus, nullptr, sched_slot(kt->device, s), nullptr);
@@ -957,7 +958,7 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
     else if (e == hipSuccess)
       e = mq_launch_chacha(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list + cap, counts + 1, status,
                            pn_out, hpm, false, s_list1, cus, sched_slot(kt->device, s_list1), kt->single_row(),
-                           recv_pass);
+                           recv_pass, mq_partition_regions(counts));
     // join even after a failed launch, so no side stream runs ahead of s
     if (!fork.join() && e == hipSuccess) e = hipErrorUnknown;
   } else {

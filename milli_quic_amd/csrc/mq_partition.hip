@@ -31,6 +31,8 @@
 // 2^20-packet partition.)
 #include "mq_tile.h"
 
+#include <cstdlib>
+
 using namespace mq;
 
 namespace {
@@ -131,6 +133,21 @@ __device__ __forceinline__ uint32_t class_ppt(uint32_t c, uint32_t cmax) {
   const uint32_t x = kBudgetChunks / need;
   return x >= kPktsPerTile ? kPktsPerTile : (x >= kMinPpt ? x : kPktsPerTile);
 }
+// Narrow tiles of list 1 (r05, mq_chacha.hip narrow_tile): a class whose largest image lets at least
+// 3/4 of a narrow tile's Q = 64 / G packets fit the wave's image budget (kNarrowChunks, no pool
+// scratch) runs G lanes per packet: G = 1, 2 or 4, the smallest that qualifies; else the octet
+// layout (G = 8). cmax = 0: an empty class, G = 1 (it constrains no neighbour).
+constexpr uint32_t kNarrowImageChunks = (kLdsBytes - 64) / 16;  // mq_chacha.hip kNarrowChunks
+__device__ __forceinline__ uint32_t class_g(uint32_t b, uint32_t cmax) {
+  if (cmax == 0) return 1;
+  if (b == kLenClasses - 1) return kPktsPerTile;
+#pragma unroll
+  for (uint32_t g = 1; g <= 4; g <<= 1) {
+    const uint32_t q = kWave / g, fit = kNarrowImageChunks / cmax;
+    if (4 * min(fit, q) >= 3 * q) return g;
+  }
+  return kPktsPerTile;
+}
 }  // namespace
 
 // Entries of one suite's list: every class segment is whole tiles of 8 entries, holes included.
@@ -138,8 +155,13 @@ __device__ __forceinline__ uint32_t class_ppt(uint32_t c, uint32_t cmax) {
 // list of n packets spread over its classes needs at most 8n / kMinPpt + 8 per class. List 0 holds
 // two class groups (hot AES key, other AES keys: 2 * kLenClasses classes), list 1 one; the cap
 // covers the larger.
+// Narrow ChaCha20 classes (tiles of Q = 16, 32 or 64 entries, at least 3Q/4 packets each) take at
+// most 4c/3 + Q entries, and the regions' starts are aligned to their tile size: kNarrowSlack more
+// per list covers both.
+constexpr uint32_t kNarrowCapSlack = kWave * kLenClasses + 128;
 uint32_t mq_partition_list_cap(uint32_t n) {
-  const uint64_t c = ((uint64_t)n * kPktsPerTile + kMinPpt - 1) / kMinPpt + kPktsPerTile * 2 * kLenClasses;
+  const uint64_t c = ((uint64_t)n * kPktsPerTile + kMinPpt - 1) / kMinPpt + kPktsPerTile * 2 * kLenClasses +
+                     kNarrowCapSlack;
   return (uint32_t)((c + kPktsPerTile - 1) & ~(uint64_t)(kPktsPerTile - 1));
 }
 
@@ -265,9 +287,13 @@ extern "C" __global__ __launch_bounds__(64 * kScanWaves) void mq_part_scan_kerne
                                                                                  uint32_t n_rows,
                                                                                  uint32_t* __restrict__ rowseg,
                                                                                  const uint32_t* __restrict__ live,
-                                                                                 const uint32_t* __restrict__ cmax) {
-  if (pass_empty(live)) {  // empty lists: no hot key, no row segments
+                                                                                 const uint32_t* __restrict__ cmax,
+                                                                                 uint32_t* __restrict__ cls,
+                                                                                 uint32_t* __restrict__ reg,
+                                                                                 uint32_t narrow) {
+  if (pass_empty(live)) {  // empty lists: no hot key, no row segments, no regions
     if (threadIdx.x == 0) { counts[0] = 0; counts[1] = 0; counts[2] = kNoKey; counts[3] = 0; }
+    if (threadIdx.x < 8) reg[threadIdx.x] = 0;
     if (rowseg)
       for (uint32_t r = threadIdx.x; r < n_rows; r += blockDim.x) *(uint2*)(rowseg + 2 * (size_t)r) = make_uint2(0, 0);
     return;
@@ -310,20 +336,59 @@ extern "C" __global__ __launch_bounds__(64 * kScanWaves) void mq_part_scan_kerne
   }
   __syncthreads();
   static_assert(2 * kLenClasses == kWave && kClasses - 2 * kLenClasses <= kWave, "one wave per list");
-  if (wave < 2) {  // wave s lays out list s: lane = class (list 0: classes 0..63, list 1: 64..95)
-    const uint32_t s = (uint32_t)wave, c = (s == 0 ? 0u : 2 * kLenClasses) + (uint32_t)lane;
-    const bool in = c < (s == 0 ? 2 * kLenClasses : kClasses);
-    const uint32_t ppt = in ? class_ppt(c, c >= 2 * kLenClasses ? cmax[c - 2 * kLenClasses] : 0u) : 1u;
-    const uint32_t ent = in ? kPktsPerTile * ((s_tot[c] + ppt - 1) / ppt) : 0u;
+  if (wave == 0) {  // list 0 (AES): lane = class 0..63, tiles of 8 entries
+    const uint32_t c = (uint32_t)lane;
+    const uint32_t ppt = class_ppt(c, 0u);
+    const uint32_t ent = kPktsPerTile * ((s_tot[c] + ppt - 1) / ppt);
     const uint32_t incl = wave_incl_scan(ent), e = lane_u32(incl, kWave - 1);
-    if (in) seg[c] = s * cap + incl - ent;
+    seg[c] = incl - ent;
     const uint32_t hot_e = lane_u32(incl, kLenClasses - 1);  // list 0: the hot key's classes first
     if (lane == 0) {
-      if (s == 0) counts[3] = hot_e;
+      counts[3] = hot_e;
       // mq_partition_list_cap bounds e; the clamp only keeps a broken bound from running a suite
       // kernel over the other list
-      counts[s] = min(e, cap);
-      if (s == 0) s_list0 = e;
+      counts[0] = min(e, cap);
+      s_list0 = e;
+    }
+  } else if (wave == 1) {
+    // list 1 (ChaCha20 and the rest): lane l = class 2 kLenClasses + l, longest first. Each class
+    // runs G lanes per packet (class_g; made non-increasing along the list by a suffix maximum, so
+    // the list is four regions — G = 8, 4, 2, 1 — each a run of whole tiles of Q = 64 / G entries
+    // starting at a multiple of Q); a class's tiles hold ppt <= Q packets, the rest holes.
+    const bool in = lane < (int)kLenClasses;
+    const uint32_t c = 2 * kLenClasses + (uint32_t)lane, b = kLenClasses - 1 - (uint32_t)lane;
+    const uint32_t cm = in ? cmax[lane] : 0u, tot = in ? s_tot[c] : 0u;
+    // the receive composite's passes (skip_unkeyed) keep octet tiles only: their persistent list
+    // kernels carry no narrow path (it spilled their registers)
+    uint32_t g = in ? (narrow ? class_g(b, tot ? cm : 0u) : (tot ? kPktsPerTile : 1u)) : 0u;
+#pragma unroll
+    for (int d = 1; d < (int)kLenClasses; d <<= 1) {  // suffix maximum over the classes after this one
+      const uint32_t v = (uint32_t)__shfl_down((int)g, d, kWave);
+      if (lane + d < (int)kLenClasses) g = max(g, v);
+    }
+    const uint32_t Q = in ? kWave / g : 1u;
+    const uint32_t ppt = !in ? 1u : (g == kPktsPerTile ? class_ppt(c, cm) : min(Q, kNarrowImageChunks / max(cm, 1u)));
+    const uint32_t ent = in && tot ? Q * ((tot + ppt - 1) / ppt) : 0u;
+    uint32_t E[4];  // entries of the regions G = 8, 4, 2, 1
+#pragma unroll
+    for (int r = 0; r < 4; ++r) E[r] = lane_u32(wave_incl_scan(in && g == (8u >> r) ? ent : 0u), kWave - 1);
+    const uint32_t R4 = (E[0] + 15) & ~15u, R2 = (R4 + E[1] + 31) & ~31u, R1 = (R2 + E[2] + 63) & ~63u;
+    // the list ends with its last non-empty region (no padding after it); every 8 entries of it also
+    // form a valid octet tile (holes skipped), so a kernel that ignores the regions (the persistent
+    // list kernels, MQ_CC_LIST=1) still processes every packet
+    const uint32_t end = E[3] ? R1 + E[3] : E[2] ? R2 + E[2] : E[1] ? R4 + E[1] : E[0];
+    const uint32_t incl = wave_incl_scan(ent), excl = incl - ent;
+    const uint32_t start = g == 8 ? excl : g == 4 ? R4 + excl - E[0] : g == 2 ? R2 + excl - E[0] - E[1]
+                                                                         : R1 + excl - E[0] - E[1] - E[2];
+    if (in) {
+      seg[c] = cap + start;
+      cls[lane] = ppt | Q << 8;
+    }
+    if (lane == 0) {
+      counts[1] = min(end, cap);
+      // the regions (list-relative): tiles of each, then the narrow regions' first entries
+      reg[0] = E[0] / 8; reg[1] = E[1] / 16; reg[2] = E[2] / 32; reg[3] = E[3] / 64;
+      reg[4] = R4; reg[5] = R2; reg[6] = R1; reg[7] = reg[0] + reg[1] + reg[2] + reg[3];
     }
   }
   if (bins) {  // keyed layout: the other AES keys' segments follow (workgroup-uniform)
@@ -404,13 +469,13 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_scatter_kerne
     const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_pkt_desc* __restrict__ desc, uint32_t n,
     uint32_t nblocks, const uint32_t* __restrict__ hot_p, const uint32_t* __restrict__ hist,
     const uint32_t* __restrict__ seg, uint32_t* __restrict__ list, uint32_t* __restrict__ bins,
-    uint32_t skip_unkeyed, const uint32_t* __restrict__ live, const uint32_t* __restrict__ cmax) {
+    uint32_t skip_unkeyed, const uint32_t* __restrict__ live, const uint32_t* __restrict__ cls) {
   if (pass_empty(live)) return;
   __shared__ uint32_t s_rank[kClasses];
-  __shared__ uint32_t s_cmax[kLenClasses];
+  __shared__ uint32_t s_cls[kLenClasses];  // list 1's classes: ppt | Q << 8 (the scan's layout)
   __shared__ uint32_t s_bcnt[kBinSlots];
   const bool lds_bins = bins_in_lds(bins, n_rows);  // kernel-uniform
-  if (threadIdx.x < kLenClasses) s_cmax[threadIdx.x] = cmax[threadIdx.x];
+  if (threadIdx.x < kLenClasses) s_cls[threadIdx.x] = cls[threadIdx.x];
   if (lds_bins)
     for (uint32_t q = threadIdx.x; q < n_rows * kKeyClasses; q += blockDim.x) s_bcnt[q] = 0;
   PartItem it[kPartItems];
@@ -479,8 +544,10 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_scatter_kerne
     const int leader = in ? __ffsll((unsigned long long)peers) - 1 : lane;
     base = (uint32_t)__shfl((int)base, leader, kWave);
     if (in) {
-      const uint32_t r = base + rank, ppt = class_ppt(c, c >= 2 * kLenClasses ? s_cmax[c - 2 * kLenClasses] : 0u);
-      list[seg[c] + kPktsPerTile * (r / ppt) + r % ppt] = i;
+      const uint32_t r = base + rank;
+      const uint32_t x = c >= 2 * kLenClasses ? s_cls[c - 2 * kLenClasses] : (class_ppt(c, 0u) | kPktsPerTile << 8);
+      const uint32_t ppt = x & 0xffu, Q = x >> 8;
+      list[seg[c] + Q * (r / ppt) + r % ppt] = i;
     }
   }
 }
@@ -495,8 +562,13 @@ static bool keyed_layout(uint32_t n, uint32_t n_rows) {
 }
 
 // meta: counts[0..1] | hot row | hot segment entries | seg[kClasses] | slice votes (kVoteSlices pairs) |
-// cmax[kLenClasses] (list 1's largest image per class, chunks)
-constexpr uint32_t kMetaWords = 4 + kClasses + 2 * kVoteSlices + kLenClasses;  // + list 1's class maxima
+// cmax[kLenClasses] (list 1's largest image per class, chunks) | cls[kLenClasses] (list 1's classes:
+// ppt | Q << 8) | reg[8] (list 1's regions: tiles of G = 8, 4, 2, 1, first entries of G = 4, 2, 1,
+// all tiles; mq_chacha.hip chacha_list_tile)
+constexpr uint32_t kMetaCmax = 4 + kClasses + 2 * kVoteSlices;
+constexpr uint32_t kMetaCls = kMetaCmax + kLenClasses;
+constexpr uint32_t kMetaReg = kMetaCls + kLenClasses;
+constexpr uint32_t kMetaWords = kMetaReg + 8;
 
 // list (2 x cap entries) | class histograms (kClasses per block) |
 // meta (2 totals, hot row, hot segment entries, kClasses segment starts) | keyed bins, 256-B aligned pieces
@@ -514,12 +586,21 @@ hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_d
                                uint32_t* list, uint32_t* hist, uint32_t* counts, hipStream_t s, bool skip_unkeyed,
                                const uint32_t* live) {
   const uint32_t nblocks = (n + kPartBlock - 1) / kPartBlock;
-  if (nblocks == 0) return hipMemsetAsync(counts, 0, 4 * sizeof(uint32_t), s);
+  // narrow ChaCha20 regions: not for the receive passes (skip_unkeyed); MQ_CC_NARROW=0 (read per call,
+  // diagnostic / A-B) turns them off as it turns off the flat narrow kernels
+  const char* ne = std::getenv("MQ_CC_NARROW");
+  const bool narrow = !skip_unkeyed && !(ne && ne[0] == '0');
+  if (nblocks == 0) {  // no lists, no regions
+    const hipError_t e = hipMemsetAsync(counts, 0, 4 * sizeof(uint32_t), s);
+    return e != hipSuccess ? e : hipMemsetAsync(counts + kMetaReg, 0, 8 * sizeof(uint32_t), s);
+  }
   const uint32_t cap = mq_partition_list_cap(n);
   uint32_t* hot = counts + 2;  // meta (kMetaWords): counts[0..1] | hot row | hot entries | seg | votes
   uint32_t* seg = counts + 4;
   uint2* votes = (uint2*)(counts + 4 + kClasses);
-  uint32_t* cmax = counts + 4 + kClasses + 2 * kVoteSlices;
+  uint32_t* cmax = counts + kMetaCmax;
+  uint32_t* cls = counts + kMetaCls;
+  uint32_t* reg = counts + kMetaReg;
   uint32_t* bins = keyed_layout(n, n_rows) ? (uint32_t*)((uint8_t*)counts + part_align(sizeof(uint32_t) * kMetaWords))
                                            : nullptr;
   const uint32_t list_q = cap / 2, bins_q = bins ? kKeyClasses / 4 * n_rows : 0u;  // 16-B words
@@ -532,11 +613,14 @@ hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_d
   hipLaunchKernelGGL(mq_part_count_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, kt, n_rows, desc, n,
                      nblocks, votes, max(nv, used), hot, hist, bins, (uint32_t)skip_unkeyed, live, cmax);
   hipLaunchKernelGGL(mq_part_scan_kernel, dim3(1), dim3(64 * kScanWaves), 0, s, hist, nblocks, cap, counts, seg,
-                     bins, n_rows, bins ? bins + key_bins(n) : nullptr, live, cmax);
+                     bins, n_rows, bins ? bins + key_bins(n) : nullptr, live, cmax, cls, reg, (uint32_t)narrow);
   hipLaunchKernelGGL(mq_part_scatter_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, kt, n_rows, desc, n,
-                     nblocks, hot, hist, seg, list, bins, (uint32_t)skip_unkeyed, live, cmax);
+                     nblocks, hot, hist, seg, list, bins, (uint32_t)skip_unkeyed, live, cls);
   return hipGetLastError();
 }
+
+// list 1's region words (reg[8], see kMetaWords) of a partition whose meta is `counts`
+const uint32_t* mq_partition_regions(const uint32_t* counts) { return counts + kMetaReg; }
 
 size_t mq_partition_workspace(uint32_t n) {
   const size_t nblocks = (n + kPartBlock - 1) / kPartBlock;

@@ -190,3 +190,31 @@ def test_narrow_counts(orc, n):
     # waves with one packet, exactly full waves, a partial last wave and a partial workgroup
     keys, arena, sd, od, pns = short_batch(n, 21, 200, 1, seed=n)
     roundtrip_vs_oracle(orc, keys, arena, sd, od, pns, modes=(None,))
+
+
+@pytest.mark.parametrize("lmin,lmax,n", [(21, 150, 30000), (64, 700, 30000), (21, 2000, 20000), (64, 1350, 4097)])
+@pytest.mark.parametrize("grid", [None, "1"])
+def test_mixed_batches_narrow_regions(orc, lmin, lmax, n, grid):
+    # mixed batches (MQ_SUITE_MIXED: the device partition) whose ChaCha20 list has narrow regions
+    # (mq_partition.hip: classes of G = 4, 2, 1 after the octet classes; workgroups with and
+    # without octet tiles, region boundaries inside a workgroup); grid "1" forces the persistent
+    # list kernels, which walk the same list as octet tiles
+    w = workload.config_e(n, seed=lmin * 31 + lmax, lmin=lmin, lmax=lmax)
+    hint = _lib.MQ_SUITE_MIXED
+    old = os.environ.get("MQ_CC_LIST")
+    try:
+        if grid is not None:
+            os.environ["MQ_CC_LIST"] = grid
+        g_out, g_st, _ = gpu_run(w.keys, w.arena, w.seal_desc, hint=hint)
+        o_out, o_st, _ = oracle_run(orc, w.keys, w.arena, w.seal_desc, hint=hint)
+        assert (o_st == 0).all() and (g_st == o_st).all()
+        assert g_out.tobytes() == o_out.tobytes()
+        g_back, g_st, g_pn = gpu_run(w.keys, g_out, w.open_desc, open_=True, hint=hint)
+        o_back, o_st, o_pn = oracle_run(orc, w.keys, o_out, w.open_desc, open_=True, hint=hint)
+        assert (g_st == 0).all() and (g_st == o_st).all() and (g_pn == o_pn).all()
+        assert g_back.tobytes() == o_back.tobytes()
+    finally:
+        if old is None:
+            os.environ.pop("MQ_CC_LIST", None)
+        else:
+            os.environ["MQ_CC_LIST"] = old
