@@ -211,14 +211,15 @@ struct CcPool {
   const KeyRow* kt;
 };
 
-template <bool SINGLE>
+// IMG: bytes of LDS per wave (kLdsBytes; the long-packet kernels' larger images, chacha_tile)
+template <bool SINGLE, uint32_t IMG = kLdsBytes>
 __device__ __forceinline__ void cc_pool_run(const CcPool& pool, uint32_t tid = threadIdx.x) {
   constexpr uint32_t kQ = kPktsPerTile * kCcWaves;  // packets of the workgroup
   static_assert(kQ <= kWave, "one packet per lane in the pool scan");
   const int lane = tid & (kWave - 1);
   const uint32_t w = tid >> 6;
   auto rec = [&](uint32_t q) -> uint32_t* {
-    return (uint32_t*)(pool.wg + (q >> 3) * kLdsBytes + kDataBudget + 32u * (q & 7));
+    return (uint32_t*)(pool.wg + (q >> 3) * IMG + (IMG - kScratchBytes) + 32u * (q & 7));
   };
   const uint32_t r0l = (uint32_t)lane < kQ ? rec((uint32_t)lane)[0] : 0u;  // lane q: packet q
   const uint32_t nq = (r0l & 0xffu) + ((r0l >> 8) ? 1u : 0u);
@@ -320,7 +321,7 @@ struct ChaChaPolicy {
   // iteration ctr / 8 (ctr 0 = the Poly1305 key); with the pool, blocks >= 16 and the
   // header-protection block (its sample is ciphertext of block 1) run in the workgroup's pool
   // before the MACs, and the mask is applied once the MAC has read the unprotected header.
-  template <bool SINGLE, class S, class G>
+  template <bool SINGLE, class S, class G, uint32_t IMG = kLdsBytes>
   static __device__ __forceinline__ void seal(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j,
                                               G& stg, const CcPool& pool) {
     const mq_pkt_desc& d = c.d;
@@ -378,7 +379,7 @@ struct ChaChaPolicy {
       }
     }
     __syncthreads();  // every wave's records
-    cc_pool_run<SINGLE>(pool);
+    cc_pool_run<SINGLE, IMG>(pool);
     __syncthreads();  // every pooled block (and mask) is in place before any MAC reads it
     MQ_STAMP(c.tile, 3);
     uint32_t tag[4];
@@ -406,7 +407,7 @@ struct ChaChaPolicy {
   }
 
   // receive composite (recv.rs:340-421 / 953-1025): HP removal, decode_pn, open.
-  template <bool SINGLE, class S, class G>
+  template <bool SINGLE, class S, class G, uint32_t IMG = kLdsBytes>
   static __device__ __forceinline__ void open(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j,
                               bool direct, G& stg, const CcPool& pool) {
     const mq_pkt_desc& d = c.d;
@@ -483,7 +484,7 @@ struct ChaChaPolicy {
       }
     }
     __syncthreads();  // every wave's MAC has read its ciphertext
-    cc_pool_run<SINGLE>(pool);
+    cc_pool_run<SINGLE, IMG>(pool);
     __syncthreads();
     MQ_STAMP(c.tile, 5);
     if (direct && hdr_written && !c.act) {  // direct path writes HBM in place: undo the unmask
@@ -1003,7 +1004,7 @@ __device__ __forceinline__ void chacha_narrow_list(uint8_t* wsm, uint32_t u, con
 // LIST: a partition list with narrow regions (reg): the octet tiles are the G = 8 region's (count =
 // its entries), a workgroup with an octet tile runs the pool's barriers on every wave (its narrow
 // waves run their tile first), one without any runs its narrow tiles with no barrier.
-template <bool OPEN, bool SINGLE, bool LIST = false>
+template <bool OPEN, bool SINGLE, bool LIST = false, uint32_t IMG = kLdsBytes>
 __device__ __forceinline__ void chacha_tile(uint32_t tb, uint32_t tid, const KeyRow* __restrict__ kt, uint32_t n_rows,
                                             uint8_t* __restrict__ arena, uint64_t arena_len,
                                             const mq_pkt_desc* __restrict__ desc, uint32_t n,
@@ -1013,12 +1014,13 @@ __device__ __forceinline__ void chacha_tile(uint32_t tb, uint32_t tid, const Key
   constexpr uint32_t W = kCcWaves;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t w = tid >> 6;
-  uint8_t* wsm = smem + w * kLdsBytes;
+  uint8_t* wsm = smem + w * IMG;
   const int lane = tid & (kWave - 1), p = lane / kLanesPerPkt, j = lane % kLanesPerPkt;
   const uint32_t tile_id = tb * W + w;
   PktCtx c;
   const KeyRow* row;
-  CcPool pool{false, smem, w * kLdsBytes, (uint32_t*)(wsm + kDataBudget + 32u * (uint32_t)p), kt};
+  constexpr uint32_t kBudget = IMG - kScratchBytes;  // packet images (9728 B at 10 KiB)
+  CcPool pool{false, smem, w * IMG, (uint32_t*)(wsm + kBudget + 32u * (uint32_t)p), kt};
   if (LIST) {  // the octet region's entries
     n = kPktsPerTile * __builtin_amdgcn_readfirstlane(reg[0]);
     n_dev = nullptr;
@@ -1039,12 +1041,12 @@ __device__ __forceinline__ void chacha_tile(uint32_t tb, uint32_t tid, const Key
     }
     if (j == 0) pool.rec[0] = 0;
     __syncthreads();
-    cc_pool_run<SINGLE>(pool, tid);
+    cc_pool_run<SINGLE, IMG>(pool, tid);
     __syncthreads();
     return;
   }
   MQ_STAMP(tile_id, 0);
-  c.otk = (uint32_t*)(wsm + kLdsBytes - 32u * kPktsPerTile + 32u * (uint32_t)p);
+  c.otk = (uint32_t*)(wsm + IMG - 32u * kPktsPerTile + 32u * (uint32_t)p);
   const uint64_t off = c.act ? c.d.offset : 0;
   Placement pl;
   pl.off = off;
@@ -1053,15 +1055,15 @@ __device__ __forceinline__ void chacha_tile(uint32_t tb, uint32_t tid, const Key
   const uint32_t nch = (uint32_t)(nch64 < 0xFFFFu ? nch64 : 0xFFFFu);
   const uint32_t incl = oct_incl_scan(nch);
   const uint32_t total = lane_u32(incl, kWave - 1);
-  if (total * 16u <= kDataBudget) {
+  if (total * 16u <= kBudget) {
     pl.slot = incl - nch;
     pool.on = true;
     DmaStager stg{wsm, arena, arena_len, lane, j, pl};
     LdsSpace sp{wsm};
     MQ_STAMP(tile_id, 1);
     const uint32_t pkt = pl.slot * 16u + pl.head();
-    if (OPEN) ChaChaPolicy::template open<SINGLE, LdsSpace>(sp, pkt, c, row, j, false, stg, pool);
-    else ChaChaPolicy::template seal<SINGLE, LdsSpace>(sp, pkt, c, row, j, stg, pool);
+    if (OPEN) ChaChaPolicy::template open<SINGLE, LdsSpace, DmaStager, IMG>(sp, pkt, c, row, j, false, stg, pool);
+    else ChaChaPolicy::template seal<SINGLE, LdsSpace, DmaStager, IMG>(sp, pkt, c, row, j, stg, pool);
     MQ_STAMP(tile_id, 6);
     wave_sync();
     stage_out(wsm, arena, lane, c.act, pl);
@@ -1069,8 +1071,8 @@ __device__ __forceinline__ void chacha_tile(uint32_t tb, uint32_t tid, const Key
   } else {
     GlobalSpace sp{arena, arena_len};
     NoStager stg;
-    if (OPEN) ChaChaPolicy::template open<SINGLE, GlobalSpace>(sp, off, c, row, j, true, stg, pool);
-    else ChaChaPolicy::template seal<SINGLE, GlobalSpace>(sp, off, c, row, j, stg, pool);
+    if (OPEN) ChaChaPolicy::template open<SINGLE, GlobalSpace, NoStager, IMG>(sp, off, c, row, j, true, stg, pool);
+    else ChaChaPolicy::template seal<SINGLE, GlobalSpace, NoStager, IMG>(sp, off, c, row, j, stg, pool);
   }
   tile_status<OPEN>(c, j, status, pn_out);
 }
@@ -1092,6 +1094,32 @@ __device__ __forceinline__ void chacha_tile(uint32_t tb, uint32_t tid, const Key
   }
 MQ_CHACHA_KERNELS(mq_chacha_seal_kernel, mq_chacha_open_kernel, false)
 MQ_CHACHA_KERNELS(mq_chacha_seal1_kernel, mq_chacha_open1_kernel, true)
+
+// Flat batches of long packets (r05): the same octet tiles and keystream pool with
+// larger LDS images, so eight packets over ~1216 B stay staged instead of running on HBM (direct:
+// 358-409 GiB/s at 1232-2048 B, against 1034 at 1200): 13 KiB per wave (12 waves per CU: eight
+// images of up to 100 chunks, packets up to ~1585 B at any alignment) or 20 KiB (8 waves per CU: up
+// to 156 chunks, ~2480 B). The waves-per-EU hint gives them the registers of that occupancy.
+constexpr uint32_t kLongImg = 13312, kLongerImg = 20480;
+static_assert(kCcWaves * kLongImg * 3 <= kCuLdsBytes && kCcWaves * kLongerImg * 2 <= kCuLdsBytes, "long images per CU");
+#define MQ_CHACHA_LONG_KERNELS(NAME_SEAL, NAME_OPEN, SINGLE, IMG, WPE)                                      \
+  extern "C" __global__ __launch_bounds__(64 * kCcWaves) __attribute__((amdgpu_waves_per_eu(WPE))) void NAME_SEAL( \
+      const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
+      const mq_pkt_desc* __restrict__ desc, uint32_t n, uint8_t* __restrict__ status) {                   \
+    chacha_tile<false, SINGLE, false, IMG>(blockIdx.x, threadIdx.x, kt, n_rows, arena, arena_len, desc, n, nullptr, \
+                                           nullptr, status, nullptr, nullptr);                            \
+  }                                                                                                       \
+  extern "C" __global__ __launch_bounds__(64 * kCcWaves) __attribute__((amdgpu_waves_per_eu(WPE))) void NAME_OPEN( \
+      const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
+      const mq_pkt_desc* __restrict__ desc, uint32_t n, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out, \
+      const uint2* __restrict__ hpm) {                                                                    \
+    chacha_tile<true, SINGLE, false, IMG>(blockIdx.x, threadIdx.x, kt, n_rows, arena, arena_len, desc, n, nullptr, \
+                                          nullptr, status, pn_out, hpm);                                  \
+  }
+MQ_CHACHA_LONG_KERNELS(mq_chacha_seal_long_kernel, mq_chacha_open_long_kernel, false, kLongImg, 3)
+MQ_CHACHA_LONG_KERNELS(mq_chacha_seal_long1_kernel, mq_chacha_open_long1_kernel, true, kLongImg, 3)
+MQ_CHACHA_LONG_KERNELS(mq_chacha_seal_longer_kernel, mq_chacha_open_longer_kernel, false, kLongerImg, 2)
+MQ_CHACHA_LONG_KERNELS(mq_chacha_seal_longer1_kernel, mq_chacha_open_longer1_kernel, true, kLongerImg, 2)
 
 // One-shot grids over a partition list with narrow regions (reg, mq_partition.hip): tile
 // tb * W + w is an octet tile of the G = 8 region or a narrow tile after it
@@ -1505,6 +1533,9 @@ hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_
   // kernels on the same batch) forces either.
   if (!index) {
     constexpr uint64_t kNarrowAvg = 640;
+    // above kLongAvg0 bytes per packet eight images overflow the 10-KiB image (config B: 1200);
+    // above kLongAvg1 they overflow 13 KiB
+    constexpr uint64_t kLongAvg0 = 1216, kLongAvg1 = 1584;
     bool narrow = arena_len <= kNarrowAvg * (uint64_t)n;
     const char* ne = std::getenv("MQ_CC_NARROW");
     if (ne) narrow = ne[0] == '1';
@@ -1520,9 +1551,29 @@ hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_
                            status);
       return hipGetLastError();
     }
+    // long packets (r05): larger LDS images; MQ_CC_LONG=0 / 1 / 2 (read per call) forces the
+    // 10-KiB, 13-KiB or 20-KiB kernels
+    int img = arena_len > kLongAvg1 * (uint64_t)n ? 2 : arena_len > kLongAvg0 * (uint64_t)n ? 1 : 0;
+    const char* le = std::getenv("MQ_CC_LONG");
+    if (le) img = le[0] == '2' ? 2 : le[0] == '1' ? 1 : 0;
+    if (img) {
+      const uint32_t lds = (img == 2 ? kLongerImg : kLongImg) * kCcWaves;
+      const bool o1 = n_rows == 1;
+      if (open)
+        hipLaunchKernelGGL(img == 2 ? (o1 ? mq_chacha_open_longer1_kernel : mq_chacha_open_longer_kernel)
+                                    : (o1 ? mq_chacha_open_long1_kernel : mq_chacha_open_long_kernel),
+                           dim3(blocks), dim3(kWave * kCcWaves), lds, s, kt, n_rows, arena, arena_len, desc, n, status,
+                           pn_out, hpm);
+      else
+        hipLaunchKernelGGL(img == 2 ? (o1 ? mq_chacha_seal_longer1_kernel : mq_chacha_seal_longer_kernel)
+                                    : (o1 ? mq_chacha_seal_long1_kernel : mq_chacha_seal_long_kernel),
+                           dim3(blocks), dim3(kWave * kCcWaves), lds, s, kt, n_rows, arena, arena_len, desc, n, status);
+      return hipGetLastError();
+    }
   }
   if (open)
     hipLaunchKernelGGL(n_rows == 1 || one ? mq_chacha_open1_kernel : mq_chacha_open_kernel, dim3(blocks),
+
                        dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kl, n_rows, arena, arena_len, desc, n, index,
                        n_dev, status, pn_out, hpm);
   if (open) return hipGetLastError();

@@ -218,3 +218,31 @@ def test_mixed_batches_narrow_regions(orc, lmin, lmax, n, grid):
             os.environ.pop("MQ_CC_LIST", None)
         else:
             os.environ["MQ_CC_LIST"] = old
+
+
+class _EnvLong(_Env):
+    def __enter__(self):
+        self.old = os.environ.get("MQ_CC_LONG")
+        if self.v is None:
+            os.environ.pop("MQ_CC_LONG", None)
+        else:
+            os.environ["MQ_CC_LONG"] = self.v
+
+    def __exit__(self, *a):
+        if self.old is None:
+            os.environ.pop("MQ_CC_LONG", None)
+        else:
+            os.environ["MQ_CC_LONG"] = self.old
+
+
+@pytest.mark.parametrize("lmin,lmax,n", [(1150, 1600, 3000), (1500, 2600, 2000), (21, 2600, 2500)])
+@pytest.mark.parametrize("mode", [None, "0", "1", "2"])
+def test_long_images_vs_oracle(orc, lmin, lmax, n, mode):
+    # flat ChaCha20 batches of long packets (r05): the 13-KiB (12 waves per CU) and 20-KiB (8 per CU)
+    # image kernels, picked by the arena's bytes per packet or forced (MQ_CC_LONG); tiles over the
+    # image budget take the direct path inside them. Open over 2048 B with MQ_PKT_NO_RECV_LIMIT.
+    keys, arena, sd, od, pns = short_batch(n, lmin, lmax, 2, seed=lmax + n)
+    od = od.copy()
+    od["flags"] |= _lib.MQ_PKT_NO_RECV_LIMIT
+    with _EnvLong(mode):
+        roundtrip_vs_oracle(orc, keys, arena, sd, od, pns, modes=(None,))

@@ -423,13 +423,15 @@ def test_full_size_roundtrip(orc, cfg):
     assert v.tobytes() == w.arena.reshape(w.n, 1200)[:, :1184].tobytes()
 
 
-@pytest.mark.parametrize("cfg", ["b", "c", "ck", "e"])
+@pytest.mark.parametrize("cfg", ["b", "c", "ck", "e", "b1350"])
 def test_full_size_byte_exact(orc, cfg):
     # BASELINE configs[1], configs[2] (also with 1024 keys, key_id = g mod 1024: the key-segmented
     # AES kernels) and configs[4] at the bench's full 2^20 packets, every byte of the arena, every
-    # status and PN against the oracle (16 threads), sealed and then opened — not a sample.
+    # status and PN against the oracle (16 threads), sealed and then opened — not a sample. b1350:
+    # 2^20 x 1350-B ChaCha20 packets, the long-image kernels (r05).
     w = {"b": lambda: workload.config_b(1 << 20), "c": lambda: workload.config_c(1 << 20),
-         "ck": lambda: workload.config_c(1 << 20, n_keys=1024), "e": lambda: workload.config_e(1 << 20)}[cfg]()
+         "ck": lambda: workload.config_c(1 << 20, n_keys=1024), "e": lambda: workload.config_e(1 << 20),
+         "b1350": lambda: workload.uniform(1 << 20, _lib.MQ_SUITE_CHACHA20, L=1350)}[cfg]()
     g_out, g_st, _ = gpu_run(w.keys, w.arena, w.seal_desc, w.suite_hint)
     o_out = w.arena.copy()
     o_st = orc.batch_seal(w.keys, o_out, w.seal_desc, w.suite_hint, threads=16)
