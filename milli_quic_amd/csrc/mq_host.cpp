@@ -60,13 +60,15 @@ hipError_t mq_launch_chacha_protect(const KeyRow* kt, uint32_t n_rows, const mq_
                                     const mq_send_req* req, uint32_t n, uint32_t suite_hint, uint8_t* status,
                                     uint32_t* pkt_len, hipStream_t s);
 size_t mq_recv_workspace(uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_conns, size_t open_ws_bytes);
+void mq_recv_trace(const char* what, uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_conns, void* ws_ptr,
+                   size_t open_ws_bytes, hipStream_t s);
 hipError_t mq_recv_front(const KeyRow* kt, uint32_t n_rows, mq_conn_recv* conns, uint32_t n_conns, uint8_t* arena,
                          uint64_t arena_len, const mq_dgram* dg, uint32_t n_dgrams, uint32_t max_pkts,
                          uint32_t* n_pkts, mq_recv_pkt* out, void* ws_ptr, size_t open_ws_bytes, mq::MQRecvPass* pass,
                          hipStream_t s);
 hipError_t mq_recv_walk(const KeyRow* kt, uint32_t n_rows, mq_conn_recv* conns, uint32_t n_conns,
                         uint32_t n_dgrams, uint32_t max_pkts, mq_recv_pkt* out, void* ws_ptr, size_t open_ws_bytes,
-                        bool final_walk, hipStream_t s);
+                        bool final_walk, bool verify, uint32_t walk_idx, hipStream_t s);
 hipError_t mq_recv_retry(uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_conns, void* ws_ptr, size_t open_ws_bytes,
                          hipStream_t s);
 hipError_t mq_recv_outcomes(uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_conns, void* ws_ptr,
@@ -1127,6 +1129,7 @@ int mq_batch_recv(const mq_keytable* kt, mq_conn_recv* conns, uint32_t n_conns, 
                     workspace, open_ws, &p, s) != hipSuccess)
     return MQ_ERR_HIP;
   if (!max_pkts) return MQ_OK;
+  mq_recv_trace("walk 1", n_dgrams, max_pkts, n_conns, workspace, open_ws, s);
   // walk -> AEAD passes -> walk ...: the first walk speculates that every packet opens, later walks
   // re-attempt what the real outcomes changed (rare: after a failed packet); the last walk defers
   // anything still unresolved. Fixed rounds keep the call asynchronous (no host read-back).
@@ -1143,8 +1146,9 @@ int mq_batch_recv(const mq_keytable* kt, mq_conn_recv* conns, uint32_t n_conns, 
     if (r != MQ_OK) return r;
     if (mq_recv_outcomes(n_dgrams, max_pkts, n_conns, workspace, open_ws, s) != hipSuccess) return MQ_ERR_HIP;
     if (mq_recv_walk(kt->dev, kt->rows, conns, n_conns, n_dgrams, max_pkts, pkts, workspace, open_ws,
-                     round + 1 == kRounds, s) != hipSuccess)
+                     round + 1 == kRounds, true, (uint32_t)round + 1, s) != hipSuccess)
       return MQ_ERR_HIP;
+    mq_recv_trace(round + 1 == kRounds ? "final walk" : "walk 2", n_dgrams, max_pkts, n_conns, workspace, open_ws, s);
   }
   // Re-seal pass: a packet that opened under the speculation's inputs but fails under the
   // reference's (MQ_ERR_CRYPTO) holds plaintext; the final walk left its opening key row and PN in

@@ -22,6 +22,10 @@
 //           MQ_ERR_DEFERRED (untouched, to be resubmitted)
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+
 #include "mq_device.h"
 
 using namespace mq;
@@ -426,33 +430,158 @@ __device__ __forceinline__ uint64_t excl_max_u64(uint64_t v, uint32_t lane, uint
   return lane == 0 ? 0ull : e;
 }
 
-extern "C" __global__ __launch_bounds__(kWalkThreads) void mq_recv_walk_kernel(
-    const mq_conn_recv* __restrict__ conn0, mq_conn_recv* __restrict__ conns, uint32_t n_conns,
-    const RecvWork* __restrict__ work, const uint32_t* __restrict__ svals, const uint32_t* __restrict__ seg_lo,
-    const uint32_t* __restrict__ seg_hi, const RecvPlan* __restrict__ hdr, uint32_t n_rows,
-    RecvPlan* __restrict__ tried, const uint8_t* __restrict__ outcome, mq_pkt_desc* __restrict__ d1,
-    mq_pkt_desc* __restrict__ d2, mq_recv_pkt* __restrict__ out, uint32_t* __restrict__ attempts, int final_walk,
-    uint2* __restrict__ hpm) {
-  __shared__ WalkIn s_in[kWalkThreads];
-  __shared__ WalkOut s_out[kWalkThreads];
-  const uint32_t wv = threadIdx.x / kWave, q = threadIdx.x % kWave;
-  const uint32_t ci = blockIdx.x * kWalkConns + wv;
-  if (ci >= n_conns) return;  // wave-uniform; the kernel has no workgroup barrier
-  const uint32_t lo = seg_lo[ci], hi = seg_hi[ci];
+// Long runs across waves (r05): a connection's run is cut into SEGMENTS of at most
+// kSeg packets, one wave each, so 2^20 packets over one connection are walked by 512 waves instead
+// of one (12.5 GiB/s in r04: 16 k sequential chunk steps per walk). Segment 0 starts from the
+// connection's state; a later segment starts from a guess — the state at the batch start with the
+// largest PN of its first packet's level set just below that packet's PN, decoded against the
+// batch-start largest PN plus the packets before it in the run (exact for in-order runs whose PNs
+// stay inside the PN window of the guess). Its walk is then the usual exact chunk walk from that
+// state. After a walk a verify pass re-walks every later segment from the end state its
+// predecessor recorded and compares each packet's decision with the records: if every segment of a
+// connection agrees, the chained walk equals the sequential one (induction over the segments);
+// otherwise (a key update, a PN gap or reordering across a segment boundary outside the window)
+// the connection is flagged and walked again sequentially from its batch-start state by one wave
+// (fallback). The earlier walks only speculate (their attempts are checked by the AEAD passes
+// and the final walk), so they take the guessed starts unverified.
+constexpr uint32_t kSeg = 1024;
+constexpr uint32_t kNoSeg = 0xFFFFFFFFu;  // one segment per run
+// the segment length in packets: kSeg, or MQ_RECV_SEG (diagnostic; 0 = one segment per run, the
+// r04 walk), read per call
+uint32_t recv_seg() {
+  const char* e = std::getenv("MQ_RECV_SEG");
+  if (!e) return kSeg;
+  const unsigned long v = std::strtoul(e, nullptr, 10);
+  return v == 0 ? kNoSeg : (uint32_t)(v < 64 ? 64 : v & ~63ul);  // whole walk chunks
+}
+struct SegState { uint64_t largest[3]; uint32_t row[3]; uint32_t misc; };  // misc: phase | flags << 8 | updates << 16
+
+__device__ __forceinline__ SegState pack_state(const ConnState& s) {
+  SegState x;
+  for (int l = 0; l < 3; ++l) { x.largest[l] = s.largest[l]; x.row[l] = s.row[l]; }
+  x.misc = s.phase | (uint32_t)s.flags << 8 | (uint32_t)s.updates << 16;
+  return x;
+}
+__device__ __forceinline__ ConnState unpack_state(const SegState& x) {
+  ConnState s;
+  for (int l = 0; l < 3; ++l) { s.largest[l] = x.largest[l]; s.row[l] = x.row[l]; }
+  s.phase = (uint8_t)x.misc;
+  s.flags = (uint8_t)(x.misc >> 8);
+  s.updates = (uint8_t)(x.misc >> 16);
+  return s;
+}
+__device__ __forceinline__ bool same_state(const ConnState& a, const ConnState& b) {
+  bool eq = a.phase == b.phase && a.flags == b.flags && a.updates == b.updates;
+  for (int l = 0; l < 3; ++l) eq = eq && a.largest[l] == b.largest[l] && a.row[l] == b.row[l];
+  return eq;
+}
+
+enum : int { kWalkMode = 0, kVerifyMode = 1, kFallbackMode = 2 };
+
+// A segment: its connection ci, its packets [lo, hi) in sorted order, the connection's run
+// [run_lo, run_hi), its index g (its end-state slot) and its predecessor's (pred). Segment j of a
+// run covers [run_lo + j*seg, run_lo + (j+1)*seg), so a run of at most seg packets is one segment.
+// The table is arithmetic (no per-batch segment table): index g < n_conns is connection g's segment
+// 0; index n_conns + e stands for sorted position P = (e + 1) * seg, and takes segment m of the run
+// holding P, m = the number of multiples of seg in (run_lo, P] — every window of seg positions holds
+// exactly one multiple, so each later segment gets exactly one index (a run's last multiple may be
+// spare: then there is no segment g).
+struct SegGeo { uint32_t ci, lo, hi, run_lo, run_hi, g, pred; bool first, last; };
+
+// the number of segments after the first in a run
+__device__ __forceinline__ uint32_t later_segs(uint32_t run_lo, uint32_t run_hi, uint32_t seg) {
+  return run_hi > run_lo ? (run_hi - run_lo - 1) / seg : 0u;
+}
+
+__device__ __forceinline__ bool seg_geo(uint32_t g, uint32_t n_conns, uint32_t seg, uint32_t max_pkts,
+                                        const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ seg_lo,
+                                        const uint32_t* __restrict__ seg_hi, SegGeo& x) {
+  if (g < n_conns) {
+    x.ci = g;
+    x.run_lo = seg_lo[g];
+    x.run_hi = seg_hi[g];
+    x.lo = x.run_lo;
+    x.hi = seg == kNoSeg ? x.run_hi : (uint32_t)min((uint64_t)x.run_hi, (uint64_t)x.run_lo + seg);
+    x.first = true;
+    x.pred = 0;
+  } else {
+    if (seg == kNoSeg) return false;
+    const uint64_t P = (uint64_t)(g - n_conns + 1) * seg;
+    if (P >= max_pkts) return false;
+    const uint32_t ci = skeys[P];  // the sorted connection keys (padding past the count: all ones)
+    if (ci >= n_conns) return false;
+    x.ci = ci;
+    x.run_lo = seg_lo[ci];
+    x.run_hi = seg_hi[ci];
+    const uint32_t m = (uint32_t)(P / seg) - x.run_lo / seg;
+    if (m == 0 || m > later_segs(x.run_lo, x.run_hi, seg)) return false;
+    x.lo = x.run_lo + m * seg;
+    x.hi = min(x.run_hi, x.lo + seg);
+    x.first = false;
+    x.pred = m == 1 ? ci : g - 1;
+  }
+  x.g = g;
+  x.last = x.hi == x.run_hi;
+  return true;
+}
+// the slot of segment j of connection ci's run
+__device__ __forceinline__ uint32_t seg_slot(uint32_t j, uint32_t ci, uint32_t run_lo, uint32_t n_conns,
+                                             uint32_t seg) {
+  return j == 0 ? ci : n_conns + run_lo / seg + j - 1;
+}
+
+// One wave walks segment x. Walk: from the connection's state (first segment), the previous walk's
+// end state of the predecessor (later segments, walks after the first) or the guessed start (later
+// segments, first walk). Verify: from this walk's recorded end state of the predecessor; returns
+// whether any decision or the end state differs. Fallback: the whole run from the connection's
+// state, recording the exact end state of every segment for the next walk.
+template <int MODE>
+__device__ __forceinline__ bool recv_walk(const mq_conn_recv* __restrict__ conn0, mq_conn_recv* __restrict__ conns,
+                                          uint32_t n_conns, const RecvWork* __restrict__ work,
+                                          const uint32_t* __restrict__ svals, const RecvPlan* __restrict__ hdr,
+                                          uint32_t n_rows, const RecvPlan* __restrict__ tried,
+                                          RecvPlan* __restrict__ tried2,
+                                          const uint8_t* __restrict__ outcome, mq_pkt_desc* __restrict__ d1,
+                                          mq_pkt_desc* __restrict__ d2, mq_recv_pkt* __restrict__ out,
+                                          uint32_t* __restrict__ attempts, int final_walk, uint2* __restrict__ hpm,
+                                          SegState* __restrict__ segend, const SegState* __restrict__ segprev,
+                                          uint32_t seg, uint32_t walk_idx, const SegGeo& x, WalkIn* sin,
+                                          WalkOut* sout) {
+  const uint32_t q = threadIdx.x % kWave;
+  const uint32_t ci = x.ci, lo = x.lo, hi = x.hi;
   const mq_conn_recv c = conn0[ci];  // every lane: the state is kept wave-uniform
   ConnState s = load_state(c);
+  if (MODE == kVerifyMode) {
+    s = unpack_state(segend[x.pred]);  // the predecessor's recorded end state
+  } else if (MODE == kWalkMode && !x.first && walk_idx > 0) {
+    s = unpack_state(segprev[x.pred]);  // the previous walk's end state of the segment before
+  } else if (MODE == kWalkMode && !x.first) {
+    // the guessed start: the first packet's PN decoded against the batch-start largest PN plus
+    // the packets before it in the run, minus one, as its level's largest PN
+    const RecvWork w0 = work[lo];
+    if (w0.pre == kPending) {
+      const RecvPlan p0 = hdr[lo];
+      const uint32_t l0 = w0.level;
+      const uint64_t base = largest_of(s, l0) + (uint64_t)(lo - x.run_lo);
+      const uint64_t est = decode_pn(p0.trunc, p0.pn_len, base);
+      if (est > 0) raise_largest(s, l0, est - 1);
+    }
+  }
   uint32_t new_attempts = 0;
-  WalkIn* sin = s_in + wv * kWave;
-  WalkOut* sout = s_out + wv * kWave;
+  bool mismatch = false;
   // Settled prefix (walks after the first): while every packet so far OPENED with the keys the
   // speculation chose (outcome kOk1, no key update), the reference's decisions are exactly the
   // speculation's — same state, same inputs — so the previous walk's records stand; the walk only
   // clears the chunk's descriptors (nothing to attempt) and raises the largest PNs. The first chunk
-  // that is not settled switches the connection to the full path for the rest of its run.
-  bool settled = true;
+  // that is not settled switches the connection to the full path for the rest of its run. The
+  // verify and fallback passes decide every packet.
+  bool settled = MODE == kWalkMode;
   for (uint32_t k0 = lo; k0 < hi; k0 += kWave) {  // wave-uniform
     const uint32_t m = min((uint32_t)kWave, hi - k0), k = k0 + q;
     const bool mine = q < m;
+    // a segment boundary (seg is a multiple of kWave): the exact state, the next walk's start there
+    if (MODE == kFallbackMode && seg != kNoSeg && k0 > lo && (k0 - lo) % seg == 0 && q == 0)
+      segend[seg_slot((k0 - lo) / seg - 1, ci, x.run_lo, n_conns, seg)] = pack_state(s);
     if (settled) {
       uint8_t so = kOk1;
       RecvPlan st{};
@@ -546,6 +675,23 @@ extern "C" __global__ __launch_bounds__(kWalkThreads) void mq_recv_walk_kernel(
       s.updates = (uint8_t)__builtin_amdgcn_readfirstlane((int)s.updates);
       wave_sync();  // the entries are read before the next round overwrites them
     }
+    if (MODE == kVerifyMode) {
+      // the walk's records of this packet: the output record, whether d1 holds an attempt or a
+      // re-seal, and an attempt's inputs
+      bool diff = false;
+      if (mine) {
+        const mq_recv_pkt rec = out[i];
+        diff = rec.status != r.st || (r.st == MQ_OK && (rec.pn != r.pn ||
+               rec.key_gen != ((w.level == MQ_LEVEL_APPLICATION) ? r.gen : 0))) ||
+               ((d1[k].key_id != kNoRow) != (r.mode != 0));
+        if (!diff && r.mode == 1) {
+          const RecvPlan ta = tried2[k];  // the attempt this walk made
+          diff = ta.pn != r.pn || ta.row != r.row || ta.retry != r.retry || ta.gen != r.pgen;
+        }
+      }
+      mismatch = mismatch || wave_any(diff);
+      continue;
+    }
     bool att = false;
     if (mine) {
       mq_pkt_desc a;
@@ -555,9 +701,11 @@ extern "C" __global__ __launch_bounds__(kWalkThreads) void mq_recv_walk_kernel(
       if (r.mode == 1) {
         RecvPlan tp;
         tp.pn = r.pn; tp.lbefore = r.lbefore; tp.row = r.row; tp.retry = r.retry; tp.trunc = p.trunc;
-        // tried entries: status = the packet's level (the settled prefix's largest PNs)
+        // tried entries: status = the packet's level (the settled prefix's largest PNs). Written
+        // as PENDING (tried2): the outcome kernel commits them to tried[] with their outcome, so a
+        // fallback walk that drops this attempt (d1 unkeyed) leaves tried[] matching outcome[]
         tp.status = w.level; tp.gen = r.pgen; tp.phase = p.phase; tp.pn_len = p.pn_len;
-        tried[k] = tp;
+        tried2[k] = tp;
         a.key_id = r.row;
         b.key_id = r.retry;
         // the open pre-pass value of both passes (prepass_decode: truncated PN, unmasked first
@@ -581,14 +729,76 @@ extern "C" __global__ __launch_bounds__(kWalkThreads) void mq_recv_walk_kernel(
     }
     new_attempts += (uint32_t)__popcll(__ballot(att));
   }
-  if (q != 0) return;
+  if (MODE == kVerifyMode) return mismatch || !same_state(s, unpack_state(segend[x.g]));
+  if (q != 0) return false;
   if (new_attempts) atomicAdd(attempts, new_attempts);
+  if (MODE == kWalkMode) segend[x.g] = pack_state(s);
+  if (MODE == kFallbackMode && seg != kNoSeg && hi > lo) segend[seg_slot((hi - lo - 1) / seg, ci, x.run_lo, n_conns, seg)] = pack_state(s);
+  if (!x.last) return false;  // the connection's state: its last segment's (or the fallback's)
   mq_conn_recv u = c;
   for (int l = 0; l < 3; ++l) { u.largest_pn[l] = s.largest[l]; u.app_row[l] = s.row[l]; }
   u.key_phase = s.phase;
   u.flags = s.flags;
   u.key_updates = s.updates;
   conns[ci] = u;
+  return false;
+}
+
+#define MQ_RECV_WALK_PARAMS                                                                                  \
+  const mq_conn_recv *__restrict__ conn0, mq_conn_recv *__restrict__ conns, uint32_t n_conns,               \
+      const RecvWork *__restrict__ work, const uint32_t *__restrict__ svals, const uint32_t *__restrict__ skeys, \
+      const uint32_t *__restrict__ seg_lo, const uint32_t *__restrict__ seg_hi, const RecvPlan *__restrict__ hdr, \
+      uint32_t n_rows, const RecvPlan *__restrict__ tried, RecvPlan *__restrict__ tried2,                   \
+      const uint8_t *__restrict__ outcome, mq_pkt_desc *__restrict__ d1, mq_pkt_desc *__restrict__ d2,      \
+      mq_recv_pkt *__restrict__ out, uint32_t *__restrict__ attempts, int final_walk, uint2 *__restrict__ hpm, \
+      SegState *__restrict__ segend_all, uint32_t *__restrict__ vstate, uint32_t max_segs, uint32_t seg,    \
+      uint32_t max_pkts, uint32_t walk_idx
+#define MQ_RECV_WALK_ARGS(MODE, X)                                                                           \
+  recv_walk<MODE>(conn0, conns, n_conns, work, svals, hdr, n_rows, tried, tried2, outcome, d1, d2, out, attempts, \
+                  final_walk, hpm, segend, segprev, seg, walk_idx, X, s_in + wv * kWave, s_out + wv * kWave)
+#define MQ_RECV_WALK_PROLOGUE                                                                                \
+  __shared__ WalkIn s_in[kWalkThreads];                                                                      \
+  __shared__ WalkOut s_out[kWalkThreads];                                                                    \
+  const uint32_t wv = threadIdx.x / kWave, q = threadIdx.x % kWave;                                          \
+  (void)q;                                                                                                   \
+  /* this walk's end states, and the previous walk's (the starts of this walk's later segments) */         \
+  SegState* segend = segend_all + (size_t)(walk_idx & 1) * max_segs;                                         \
+  const SegState* segprev = segend_all + (size_t)((walk_idx & 1) ^ 1) * max_segs;
+
+// the walk: one wave per segment (every connection's first segment, then the later ones)
+extern "C" __global__ __launch_bounds__(kWalkThreads) void mq_recv_walk_kernel(MQ_RECV_WALK_PARAMS) {
+  MQ_RECV_WALK_PROLOGUE
+  SegGeo x;
+  if (!seg_geo(blockIdx.x * kWalkConns + wv, n_conns, seg, max_pkts, skeys, seg_lo, seg_hi, x)) return;
+  (void)vstate;
+  (void)MQ_RECV_WALK_ARGS(kWalkMode, x);
+}
+
+// verify + fallback: one wave per later segment re-walks it from its predecessor's recorded end
+// state; vstate[2c] collects connection c's verdicts and vstate[2c + 1] counts its finished
+// segments. The wave finishing a connection's last check resets both and, when a segment disagreed,
+// walks the whole run again from the connection's state (no further launch: a batch whose runs fit
+// one segment each costs one early-exit launch per walk).
+extern "C" __global__ __launch_bounds__(kWalkThreads) void mq_recv_verify_kernel(MQ_RECV_WALK_PARAMS) {
+  MQ_RECV_WALK_PROLOGUE
+  SegGeo x;
+  if (!seg_geo(n_conns + blockIdx.x * kWalkConns + wv, n_conns, seg, max_pkts, skeys, seg_lo, seg_hi, x)) return;
+  const bool differs = MQ_RECV_WALK_ARGS(kVerifyMode, x);
+  uint32_t redo = 0;
+  if (q == 0) {
+    if (differs) atomicOr(&vstate[2 * x.ci], 1u);
+    __threadfence();  // the verdict is visible before the count that releases it
+    if (atomicAdd(&vstate[2 * x.ci + 1], 1u) + 1 == later_segs(x.run_lo, x.run_hi, seg)) {
+      redo = atomicExch(&vstate[2 * x.ci], 0u);
+      vstate[2 * x.ci + 1] = 0;
+      if (redo) atomicAdd(&vstate[2 * n_conns], 1u);  // fallbacks run (MQ_RECV_TRACE)
+    }
+  }
+  if (!__builtin_amdgcn_readfirstlane((int)redo)) return;
+  SegGeo f;
+  f.ci = x.ci; f.lo = f.run_lo = x.run_lo; f.hi = f.run_hi = x.run_hi; f.g = f.pred = x.ci;
+  f.first = f.last = true;
+  (void)MQ_RECV_WALK_ARGS(kFallbackMode, f);
 }
 
 // retry pass descriptors: only 1-RTT packets whose current keys failed (recv.rs:441-474); live[1]
@@ -613,12 +823,15 @@ extern "C" __global__ __launch_bounds__(256) void mq_recv_outcome_kernel(const m
                                                                          const uint8_t* __restrict__ st1,
                                                                          const uint8_t* __restrict__ st2,
                                                                          uint8_t* __restrict__ outcome,
+                                                                         RecvPlan* __restrict__ tried,
+                                                                         const RecvPlan* __restrict__ tried2,
                                                                          uint32_t max_pkts,
                                                                          const uint32_t* __restrict__ live) {
   if (live[0] == 0) return;  // nothing attempted this round
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= max_pkts || d1[i].key_id == kNoRow) return;
   outcome[i] = st1[i] == MQ_OK ? kOk1 : (d2[i].key_id != kNoRow && st2[i] == MQ_OK) ? kOk0 : kFail;
+  tried[i] = tried2[i];  // the attempt's inputs, with its outcome
 }
 
 // ---- stable sort of the records by connection (r04) ----------------------------------------------
@@ -701,8 +914,11 @@ size_t al(size_t b) { return (b + 255) & ~(size_t)255; }
 struct RecvWs {
   uint32_t *counts, *base, *total, *keys, *vals, *skeys, *svals, *seg_lo, *seg_hi, *attempts;
   uint32_t *shist, *tkeys, *tvals;  // the sort's digit histograms and ping-pong buffers
+  uint32_t* vstate;  // per connection: verify verdicts, finished checks
+  SegState* segend;
+  uint32_t max_segs;
   RecvWork *work, *work_s;
-  RecvPlan *hdr_s, *tried;
+  RecvPlan *hdr_s, *tried, *tried2;
   mq_conn_recv* conn0;
   uint2* hpm;
   mq_pkt_desc *d1, *d2;
@@ -740,11 +956,16 @@ RecvWs layout(uint8_t* p, uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_conns
   w.tvals = (uint32_t*)take(4ull * max_pkts);
   w.seg_lo = (uint32_t*)take(4ull * n_conns);
   w.seg_hi = (uint32_t*)take(4ull * n_conns);
+  const size_t max_segs = (size_t)n_conns + ((size_t)max_pkts + 63) / 64;  // segments of >= 64 packets
+  w.vstate = (uint32_t*)take(8ull * n_conns + 8);
+  w.segend = (SegState*)take(2 * sizeof(SegState) * max_segs);  // this walk's and the previous walk's
+  w.max_segs = (uint32_t)max_segs;
   w.conn0 = (mq_conn_recv*)take(sizeof(mq_conn_recv) * (size_t)n_conns);
   w.work = (RecvWork*)take(sizeof(RecvWork) * (size_t)max_pkts);
   w.work_s = (RecvWork*)take(sizeof(RecvWork) * (size_t)max_pkts);
   w.hdr_s = (RecvPlan*)take(sizeof(RecvPlan) * (size_t)max_pkts);
   w.tried = (RecvPlan*)take(sizeof(RecvPlan) * (size_t)max_pkts);
+  w.tried2 = (RecvPlan*)take(sizeof(RecvPlan) * (size_t)max_pkts);
   w.hpm = (uint2*)take(8ull * max_pkts);
   w.d1 = (mq_pkt_desc*)take(sizeof(mq_pkt_desc) * (size_t)max_pkts);
   w.d2 = (mq_pkt_desc*)take(sizeof(mq_pkt_desc) * (size_t)max_pkts);
@@ -770,7 +991,7 @@ hipError_t mq_launch_aes_prepass(const KeyRow* kt, uint32_t n_rows, const uint8_
 
 hipError_t mq_recv_walk(const KeyRow* kt, uint32_t n_rows, mq_conn_recv* conns, uint32_t n_conns,
                         uint32_t n_dgrams, uint32_t max_pkts, mq_recv_pkt* out, void* ws_ptr, size_t open_ws_bytes,
-                        bool final_walk, hipStream_t s);
+                        bool final_walk, bool verify, uint32_t walk_idx, hipStream_t s);
 
 // split, header-protection masks, sort, first walk (mq_host.cpp then runs the AEAD passes)
 hipError_t mq_recv_front(const KeyRow* kt, uint32_t n_rows, mq_conn_recv* conns, uint32_t n_conns, uint8_t* arena,
@@ -831,24 +1052,35 @@ hipError_t mq_recv_front(const KeyRow* kt, uint32_t n_rows, mq_conn_recv* conns,
     if ((e = hipMemsetAsync(w.seg_lo, 0, 4ull * n_conns, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(w.seg_hi, 0, 4ull * n_conns, s)) != hipSuccess) return e;
   }
+  if ((e = hipMemsetAsync(w.vstate, 0, 8ull * n_conns + 8, s)) != hipSuccess) return e;
   hipLaunchKernelGGL(mq_recv_seg_kernel, dim3((max_pkts + 255) / 256), b256, 0, s, w.skeys, max_pkts, n_conns, w.seg_lo,
                      w.seg_hi);
   hipLaunchKernelGGL(mq_recv_gather_kernel, dim3((max_pkts + 255) / 256), b256, 0, s, w.total, max_pkts, w.svals, w.work,
                      arena, w.hpm, w.work_s, w.hdr_s, w.outcome);
-  return mq_recv_walk(kt, n_rows, conns, n_conns, n_dgrams, max_pkts, out, ws_ptr, open_ws_bytes, false, s);
+  return mq_recv_walk(kt, n_rows, conns, n_conns, n_dgrams, max_pkts, out, ws_ptr, open_ws_bytes, false, false, 0, s);
 }
 
 // one walk (after the first, the previous round's AEAD outcomes are folded in first)
 hipError_t mq_recv_walk(const KeyRow* /*kt*/, uint32_t n_rows, mq_conn_recv* conns, uint32_t n_conns,
                         uint32_t n_dgrams, uint32_t max_pkts, mq_recv_pkt* out, void* ws_ptr, size_t open_ws_bytes,
-                        bool final_walk, hipStream_t s) {
+                        bool final_walk, bool verify, uint32_t walk_idx, hipStream_t s) {
   RecvWs w = layout((uint8_t*)ws_ptr, n_dgrams, max_pkts, n_conns, open_ws_bytes);
   hipError_t e;
   if ((e = hipMemsetAsync(w.attempts, 0, 4, s)) != hipSuccess) return e;
-  if (n_conns)
-    hipLaunchKernelGGL(mq_recv_walk_kernel, dim3((n_conns + kWalkConns - 1) / kWalkConns), dim3(kWalkThreads), 0, s,
-                       w.conn0, conns, n_conns, w.work_s, w.svals, w.seg_lo, w.seg_hi, w.hdr_s, n_rows, w.tried,
-                       w.outcome, w.d1, w.d2, out, w.attempts, (int)final_walk, (uint2*)w.open_ws);
+  if (!n_conns) return hipGetLastError();
+  const uint32_t seg = recv_seg();
+  const uint32_t later = seg == kNoSeg ? 0u : (max_pkts + seg - 1) / seg;  // bound on later segments
+#define MQ_RECV_WALK_LAUNCH(KERNEL, GRID)                                                                     \
+  hipLaunchKernelGGL(KERNEL, dim3(GRID), dim3(kWalkThreads), 0, s, (const mq_conn_recv*)w.conn0, conns, n_conns,  \
+                     (const RecvWork*)w.work_s, (const uint32_t*)w.svals, (const uint32_t*)w.skeys,             \
+                     (const uint32_t*)w.seg_lo, (const uint32_t*)w.seg_hi, (const RecvPlan*)w.hdr_s, n_rows,   \
+                     (const RecvPlan*)w.tried, w.tried2, (const uint8_t*)w.outcome, w.d1, w.d2, out, w.attempts, \
+                     (int)final_walk, (uint2*)w.open_ws, w.segend, w.vstate, w.max_segs, seg, max_pkts, walk_idx)
+  MQ_RECV_WALK_LAUNCH(mq_recv_walk_kernel, (n_conns + later + kWalkConns - 1) / kWalkConns);
+  // later segments (none when no run can exceed one segment): the walk's chained starts are
+  // verified, and connections whose segments disagree are walked again sequentially
+  if (verify && later > 1) MQ_RECV_WALK_LAUNCH(mq_recv_verify_kernel, (later + kWalkConns - 1) / kWalkConns);
+#undef MQ_RECV_WALK_LAUNCH
   return hipGetLastError();
 }
 
@@ -869,6 +1101,24 @@ hipError_t mq_recv_outcomes(uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_con
   RecvWs w = layout((uint8_t*)ws_ptr, n_dgrams, max_pkts, n_conns, open_ws_bytes);
   if (max_pkts)
     hipLaunchKernelGGL(mq_recv_outcome_kernel, dim3((max_pkts + 255) / 256), dim3(256), 0, s, w.d1, w.d2, w.st1, w.st2,
-                       w.outcome, max_pkts, (const uint32_t*)w.attempts);
+                       w.outcome, w.tried, (const RecvPlan*)w.tried2, max_pkts, (const uint32_t*)w.attempts);
   return hipGetLastError();
+}
+
+// MQ_RECV_TRACE=1 (diagnostic): after each walk, the segment count, flagged connections and
+// attempts, printed to stderr (synchronizes the stream)
+void mq_recv_trace(const char* what, uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_conns, void* ws_ptr,
+                   size_t open_ws_bytes, hipStream_t s) {
+  static const bool on = [] {
+    const char* e = std::getenv("MQ_RECV_TRACE");
+    return e && e[0] == '1';
+  }();
+  if (!on) return;
+  RecvWs w = layout((uint8_t*)ws_ptr, n_dgrams, max_pkts, n_conns, open_ws_bytes);
+  (void)hipStreamSynchronize(s);
+  uint32_t nfb = 0, att[2] = {0, 0};
+  (void)hipMemcpy(&nfb, w.vstate + 2ull * n_conns, 4, hipMemcpyDeviceToHost);
+  (void)hipMemcpy(att, w.attempts, 8, hipMemcpyDeviceToHost);
+  std::fprintf(stderr, "[recv %s] segment %u fallbacks so far %u attempts %u retries %u\n", what, recv_seg(), nfb,
+               att[0], att[1]);
 }

@@ -824,6 +824,88 @@ static int orc_recv_aead(const mq_key_material* km, uint8_t* pkt, size_t len, si
   return rc;
 }
 
+/* One datagram of the receive loop (recv.rs:189-265): its packets in order, records out[np..) (those
+ * below max_pkts). upd0: the connection's key_updates at batch start. Returns the packets seen. */
+static uint32_t orc_recv_dgram(const mq_key_material* rows, uint32_t n_rows, mq_conn_recv* c, uint8_t upd0,
+                               uint8_t* arena, const mq_dgram* d, uint32_t g, mq_recv_pkt* out, uint32_t max_pkts,
+                               uint32_t np) {
+  const uint32_t np0 = np;
+  uint8_t* base = arena + d->offset;
+  size_t off = 0;
+  while (off < d->len) {
+    size_t plen = 0, pn_off = 0;
+    uint64_t length = 0;
+    int kind;
+    if (orc_next_packet(base + off, d->len - off, &plen, &kind, &pn_off, &length)) break;
+    uint8_t* pkt = base + off;
+    off += plen;
+    if (kind == 1 || kind == 3 || kind == 5) continue; /* 0-RTT, Retry, VN skipped (:221-226) */
+    mq_recv_pkt r;
+    memset(&r, 0, sizeof r);
+    r.offset = (uint64_t)(pkt - arena); r.len = (uint32_t)plen; r.dgram = g;
+    int st = MQ_OK, lvl = kind == 0 ? MQ_LEVEL_INITIAL : kind == 2 ? MQ_LEVEL_HANDSHAKE : MQ_LEVEL_APPLICATION;
+    r.level = (uint8_t)lvl;
+    uint64_t pn = 0;
+    size_t poff = 0;
+    if (lvl != MQ_LEVEL_APPLICATION) { /* recv_initial / recv_handshake -> decrypt_long_packet */
+      uint32_t row = lvl == MQ_LEVEL_INITIAL ? c->initial_row : c->handshake_row;
+      int has = c->flags & (lvl == MQ_LEVEL_INITIAL ? MQ_RECV_HAS_INITIAL : MQ_RECV_HAS_HANDSHAKE);
+      size_t total = pn_off + (size_t)length;
+      if (!has || row >= n_rows) st = MQ_ERR_CRYPTO;
+      else if (total > 2048) st = MQ_ERR_BUFFER_TOO_SMALL; /* :963-965 */
+      else st = orc_recv_open(&rows[row], pkt, total, pn_off, 1, c->largest_pn[lvl], &pn, &poff, NULL);
+      if (st == MQ_OK) st = orc_recv_aead(&rows[row], pkt, total, pn_off, 1, pn);
+      r.len = (uint32_t)total;
+    } else { /* recv_short (:340-510) */
+      size_t dl = c->dcid_len;
+      int phase = 0;
+      if (plen < 1 + dl) st = MQ_ERR_BUFFER_TOO_SMALL;                       /* parse_short_header */
+      else if (!(c->flags & MQ_RECV_HAS_APP) || c->app_row[1] >= n_rows) st = MQ_ERR_CRYPTO;
+      else if (plen > 2048) st = MQ_ERR_BUFFER_TOO_SMALL;                    /* :356-360 */
+      else st = orc_recv_open(&rows[c->app_row[1]], pkt, plen, 1 + dl, 0, c->largest_pn[2], &pn, &poff, &phase);
+      if (st == MQ_OK) {
+        if (phase == c->key_phase) {
+          st = orc_recv_aead(&rows[c->app_row[1]], pkt, plen, 1 + dl, 0, pn);
+          r.key_gen = 1;
+          if (st != MQ_OK) { /* :441-474: previous keys, else Error::Crypto */
+            st = MQ_ERR_CRYPTO;
+            if ((c->flags & MQ_RECV_HAS_PREV) && c->app_row[0] < n_rows) {
+              st = orc_recv_aead(&rows[c->app_row[0]], pkt, plen, 1 + dl, 0, pn);
+              r.key_gen = 0;
+            }
+          }
+        } else { /* :476-509: next generation, rotate on success */
+          /* no next-generation keys installed: Crypto (derive_next_recv_keys without a secret);
+           * after a rotation inside this batch the next-next keys need the host: Deferred */
+          st = c->key_updates != upd0 ? MQ_ERR_DEFERRED : MQ_ERR_CRYPTO;
+          if ((c->flags & MQ_RECV_HAS_NEXT) && c->app_row[2] < n_rows) {
+            st = orc_recv_aead(&rows[c->app_row[2]], pkt, plen, 1 + dl, 0, pn);
+            r.key_gen = 2;
+            if (st == MQ_OK) {
+              c->app_row[0] = c->app_row[1]; c->app_row[1] = c->app_row[2];
+              c->flags = (uint8_t)((c->flags | MQ_RECV_HAS_PREV) & ~MQ_RECV_HAS_NEXT);
+              c->key_phase ^= 1; c->key_updates++;
+            }
+          }
+        }
+      }
+    }
+    if (st != MQ_OK) r.key_gen = 0; /* only meaningful for opened 1-RTT packets */
+    if (st == MQ_OK) {
+      r.pn = pn; r.payload_offset = (uint16_t)poff;
+      if (pn > c->largest_pn[lvl]) c->largest_pn[lvl] = pn; /* :239-247 */
+    }
+    r.status = (uint8_t)st;
+    if (np < max_pkts) out[np] = r;
+    ++np;
+  }
+  return np - np0;
+}
+
+static int orc_dgram_ok(const mq_dgram* d, uint32_t n_conns, uint64_t arena_len) {
+  return d->conn < n_conns && d->offset + (uint64_t)d->len <= arena_len;
+}
+
 void orc_batch_recv(const mq_key_material* rows, uint32_t n_rows, mq_conn_recv* conns, uint32_t n_conns,
                     uint8_t* arena, uint64_t arena_len, const mq_dgram* dg, uint32_t n_dgrams,
                     mq_recv_pkt* out, uint32_t max_pkts, uint32_t* n_pkts) {
@@ -831,79 +913,71 @@ void orc_batch_recv(const mq_key_material* rows, uint32_t n_rows, mq_conn_recv* 
   uint8_t* upd0 = (uint8_t*)malloc(n_conns ? n_conns : 1);
   for (uint32_t k = 0; k < n_conns; ++k) upd0[k] = conns[k].key_updates;
   for (uint32_t g = 0; g < n_dgrams; ++g) {
-    if (dg[g].conn >= n_conns || dg[g].offset + (uint64_t)dg[g].len > arena_len) continue;
-    mq_conn_recv* c = &conns[dg[g].conn];
-    uint8_t* base = arena + dg[g].offset;
+    if (!orc_dgram_ok(&dg[g], n_conns, arena_len)) continue;
+    np += orc_recv_dgram(rows, n_rows, &conns[dg[g].conn], upd0[dg[g].conn], arena, &dg[g], g, out, max_pkts, np);
+  }
+  free(upd0);
+  *n_pkts = np;
+}
+
+/* The same loop on `threads` threads: connections are independent (each one's state and packets
+ * are its own; its datagrams keep their arrival order), so thread t takes the datagrams of the
+ * connections c with c % threads == t. Each datagram's first record index comes from a sequential
+ * pass that only parses (CoalescedPackets does not depend on decryption). Identical records,
+ * connection table and arena as orc_batch_recv. */
+typedef struct {
+  const mq_key_material* rows; uint32_t n_rows; mq_conn_recv* conns; uint32_t n_conns; uint8_t* arena;
+  uint64_t arena_len; const mq_dgram* dg; uint32_t n_dgrams; mq_recv_pkt* out; uint32_t max_pkts;
+  const uint32_t* base; const uint8_t* upd0; int t, threads;
+} orc_recv_job;
+
+static void* orc_recv_run(void* arg) {
+  orc_recv_job* j = (orc_recv_job*)arg;
+  for (uint32_t g = 0; g < j->n_dgrams; ++g) {
+    const mq_dgram* d = &j->dg[g];
+    if (!orc_dgram_ok(d, j->n_conns, j->arena_len) || (int)(d->conn % (uint32_t)j->threads) != j->t) continue;
+    (void)orc_recv_dgram(j->rows, j->n_rows, &j->conns[d->conn], j->upd0[d->conn], j->arena, d, g, j->out,
+                         j->max_pkts, j->base[g]);
+  }
+  return NULL;
+}
+
+void orc_batch_recv_mt(const mq_key_material* rows, uint32_t n_rows, mq_conn_recv* conns, uint32_t n_conns,
+                       uint8_t* arena, uint64_t arena_len, const mq_dgram* dg, uint32_t n_dgrams,
+                       mq_recv_pkt* out, uint32_t max_pkts, uint32_t* n_pkts, int threads) {
+  if (threads < 1) threads = 1;
+  uint32_t* base = (uint32_t*)malloc(sizeof(uint32_t) * (n_dgrams ? n_dgrams : 1));
+  uint8_t* upd0 = (uint8_t*)malloc(n_conns ? n_conns : 1);
+  for (uint32_t k = 0; k < n_conns; ++k) upd0[k] = conns[k].key_updates;
+  uint32_t np = 0;
+  for (uint32_t g = 0; g < n_dgrams; ++g) {  /* parse-only pass: packets per datagram */
+    base[g] = np;
+    if (!orc_dgram_ok(&dg[g], n_conns, arena_len)) continue;
+    const uint8_t* b = arena + dg[g].offset;
     size_t off = 0;
     while (off < dg[g].len) {
       size_t plen = 0, pn_off = 0;
       uint64_t length = 0;
       int kind;
-      if (orc_next_packet(base + off, dg[g].len - off, &plen, &kind, &pn_off, &length)) break;
-      uint8_t* pkt = base + off;
+      if (orc_next_packet(b + off, dg[g].len - off, &plen, &kind, &pn_off, &length)) break;
       off += plen;
-      if (kind == 1 || kind == 3 || kind == 5) continue; /* 0-RTT, Retry, VN skipped (:221-226) */
-      mq_recv_pkt r;
-      memset(&r, 0, sizeof r);
-      r.offset = (uint64_t)(pkt - arena); r.len = (uint32_t)plen; r.dgram = g;
-      int st = MQ_OK, lvl = kind == 0 ? MQ_LEVEL_INITIAL : kind == 2 ? MQ_LEVEL_HANDSHAKE : MQ_LEVEL_APPLICATION;
-      r.level = (uint8_t)lvl;
-      uint64_t pn = 0;
-      size_t poff = 0;
-      if (lvl != MQ_LEVEL_APPLICATION) { /* recv_initial / recv_handshake -> decrypt_long_packet */
-        uint32_t row = lvl == MQ_LEVEL_INITIAL ? c->initial_row : c->handshake_row;
-        int has = c->flags & (lvl == MQ_LEVEL_INITIAL ? MQ_RECV_HAS_INITIAL : MQ_RECV_HAS_HANDSHAKE);
-        size_t total = pn_off + (size_t)length;
-        if (!has || row >= n_rows) st = MQ_ERR_CRYPTO;
-        else if (total > 2048) st = MQ_ERR_BUFFER_TOO_SMALL; /* :963-965 */
-        else st = orc_recv_open(&rows[row], pkt, total, pn_off, 1, c->largest_pn[lvl], &pn, &poff, NULL);
-        if (st == MQ_OK) st = orc_recv_aead(&rows[row], pkt, total, pn_off, 1, pn);
-        r.len = (uint32_t)total;
-      } else { /* recv_short (:340-510) */
-        size_t dl = c->dcid_len;
-        int phase = 0;
-        if (plen < 1 + dl) st = MQ_ERR_BUFFER_TOO_SMALL;                       /* parse_short_header */
-        else if (!(c->flags & MQ_RECV_HAS_APP) || c->app_row[1] >= n_rows) st = MQ_ERR_CRYPTO;
-        else if (plen > 2048) st = MQ_ERR_BUFFER_TOO_SMALL;                    /* :356-360 */
-        else st = orc_recv_open(&rows[c->app_row[1]], pkt, plen, 1 + dl, 0, c->largest_pn[2], &pn, &poff, &phase);
-        if (st == MQ_OK) {
-          if (phase == c->key_phase) {
-            st = orc_recv_aead(&rows[c->app_row[1]], pkt, plen, 1 + dl, 0, pn);
-            r.key_gen = 1;
-            if (st != MQ_OK) { /* :441-474: previous keys, else Error::Crypto */
-              st = MQ_ERR_CRYPTO;
-              if ((c->flags & MQ_RECV_HAS_PREV) && c->app_row[0] < n_rows) {
-                st = orc_recv_aead(&rows[c->app_row[0]], pkt, plen, 1 + dl, 0, pn);
-                r.key_gen = 0;
-              }
-            }
-          } else { /* :476-509: next generation, rotate on success */
-            /* no next-generation keys installed: Crypto (derive_next_recv_keys without a secret);
-             * after a rotation inside this batch the next-next keys need the host: Deferred */
-            st = c->key_updates != upd0[dg[g].conn] ? MQ_ERR_DEFERRED : MQ_ERR_CRYPTO;
-            if ((c->flags & MQ_RECV_HAS_NEXT) && c->app_row[2] < n_rows) {
-              st = orc_recv_aead(&rows[c->app_row[2]], pkt, plen, 1 + dl, 0, pn);
-              r.key_gen = 2;
-              if (st == MQ_OK) {
-                c->app_row[0] = c->app_row[1]; c->app_row[1] = c->app_row[2];
-                c->flags = (uint8_t)((c->flags | MQ_RECV_HAS_PREV) & ~MQ_RECV_HAS_NEXT);
-                c->key_phase ^= 1; c->key_updates++;
-              }
-            }
-          }
-        }
-      }
-      if (st != MQ_OK) r.key_gen = 0; /* only meaningful for opened 1-RTT packets */
-      if (st == MQ_OK) {
-        r.pn = pn; r.payload_offset = (uint16_t)poff;
-        if (pn > c->largest_pn[lvl]) c->largest_pn[lvl] = pn; /* :239-247 */
-      }
-      r.status = (uint8_t)st;
-      if (np < max_pkts) out[np] = r;
+      if (kind == 1 || kind == 3 || kind == 5) continue;
       ++np;
     }
   }
-  free(upd0);
+  orc_recv_job* jobs = (orc_recv_job*)calloc((size_t)threads, sizeof(orc_recv_job));
+  pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+  for (int t = 0; t < threads; ++t) {
+    orc_recv_job jb = {rows, n_rows, conns, n_conns, arena, arena_len, dg, n_dgrams, out, max_pkts, base, upd0, t,
+                       threads};
+    jobs[t] = jb;
+  }
+  if (threads == 1) orc_recv_run(&jobs[0]);
+  else {
+    for (int t = 0; t < threads; ++t) pthread_create(&th[t], NULL, orc_recv_run, &jobs[t]);
+    for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+  }
+  free(jobs); free(th); free(base); free(upd0);
   *n_pkts = np;
 }
 

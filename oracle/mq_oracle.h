@@ -88,6 +88,10 @@ void orc_batch_protect(const mq_key_material* rows, uint32_t n_rows, const mq_co
 void orc_batch_recv(const mq_key_material* rows, uint32_t n_rows, mq_conn_recv* conns, uint32_t n_conns,
                     uint8_t* arena, uint64_t arena_len, const mq_dgram* dg, uint32_t n_dgrams,
                     mq_recv_pkt* out, uint32_t max_pkts, uint32_t* n_pkts);
+/* the same on `threads` threads (connections split over them; identical results) */
+void orc_batch_recv_mt(const mq_key_material* rows, uint32_t n_rows, mq_conn_recv* conns, uint32_t n_conns,
+                    uint8_t* arena, uint64_t arena_len, const mq_dgram* dg, uint32_t n_dgrams,
+                    mq_recv_pkt* out, uint32_t max_pkts, uint32_t* n_pkts, int threads);
 
 /* batch drivers with the product's descriptor semantics; `threads` <= 1 runs serially */
 void orc_batch_seal(const mq_key_material* rows, uint32_t n_rows, uint8_t* arena,

@@ -172,16 +172,20 @@ def batch_protect(rows, conns, frames, out, req, suite_hint):
     return status, pkt_len
 
 
-def batch_recv(rows, conns, arena, dgrams, max_pkts):
+def batch_recv(rows, conns, arena, dgrams, max_pkts, threads=1):
     """Receive composite over datagrams (recv.rs:189-510) on the host copies `arena` / `conns`
-    (numpy, milli_quic_amd.recv dtypes; both updated in place); returns the packet records."""
+    (numpy, milli_quic_amd.recv dtypes; both updated in place); returns the packet records.
+    threads > 1: connections split over threads (orc_batch_recv_mt, the same results)."""
     from milli_quic_amd.recv import PKT_DTYPE
     arr, nr = _rows(rows)
     out = np.zeros(max(max_pkts, 1), dtype=PKT_DTYPE)
     n = ctypes.c_uint32(0)
-    load().orc_batch_recv(arr, ctypes.c_uint32(nr), _p(conns), ctypes.c_uint32(len(conns)), _p(arena),
-                          ctypes.c_uint64(arena.size), _p(dgrams), ctypes.c_uint32(len(dgrams)), _p(out),
-                          ctypes.c_uint32(max_pkts), ctypes.byref(n))
+    args = (arr, ctypes.c_uint32(nr), _p(conns), ctypes.c_uint32(len(conns)), _p(arena), ctypes.c_uint64(arena.size),
+            _p(dgrams), ctypes.c_uint32(len(dgrams)), _p(out), ctypes.c_uint32(max_pkts), ctypes.byref(n))
+    if threads > 1:
+        load().orc_batch_recv_mt(*args, ctypes.c_int(threads))
+    else:
+        load().orc_batch_recv(*args)
     return out[:min(n.value, max_pkts)], n.value
 
 

@@ -155,3 +155,113 @@ def build_pn_jump(orc, suites=(_lib.MQ_SUITE_CHACHA20, _lib.MQ_SUITE_AES128GCM),
     for o, b in blobs:
         arena[o:o + len(b)] = np.frombuffer(b, dtype=np.uint8)
     return keys, conns, arena, dgrams
+
+
+def long_runs(orc, n_conns, n_per_conn, seed=1, frame_min=20, frame_max=300, gap_p=0.02, big_gap_p=0.001,
+              reorder_p=0.01, tamper_p=0.005, flip_at=0.5, lag_max=100, interleave=True):
+    """Long 1-RTT runs for the segmented receive walk (r05, mq_recv.hip kSeg): n_conns connections
+    of n_per_conn one-packet datagrams each, built by the oracle's send composite in one batch.
+    PNs mostly step by 1, with gaps (2..300, rarely ~40000: the sender's largest acknowledged PN
+    then lags behind the gap, so its PN length covers it, number.rs:9-26), adjacent packets swapped
+    in flight (in-window reordering), a peer key update (phase 1, next-generation keys) from
+    packet flip_at * n on, and tampered packets (one flipped bit). Suites alternate ChaCha20 /
+    AES-128-GCM by connection. Returns keys, conns, arena, dgrams."""
+    rng = np.random.default_rng(seed)
+    keys = [_lib.KeyMaterial()]
+    rconns = np.zeros(n_conns, dtype=recv.CONN_DTYPE)
+    sconns = []
+    reqs = []
+    frames = []
+    fpos = 0
+    per_conn_order = []
+    for c in range(n_conns):
+        suite = _lib.MQ_SUITE_CHACHA20 if c % 2 == 0 else _lib.MQ_SUITE_AES128GCM
+        dcid = rng.bytes(8)
+        g0 = key_material(suite, rng.bytes(32))
+        g1 = key_material(suite, rng.bytes(32))
+        g1.hp[:] = g0.hp[:]  # HP keys survive key updates (keys.rs:386-414)
+        r0 = len(keys); keys.append(g0)
+        r1 = len(keys); keys.append(g1)
+        rconns[c]["app_row"] = [0, r0, r1]
+        rconns[c]["dcid_len"] = 8
+        rconns[c]["flags"] = recv.HAS_APP | recv.HAS_NEXT
+        s0 = len(sconns)
+        sconns.append((dcid, r0, 0))
+        sconns.append((dcid, r1, 1))
+        inc = np.ones(n_per_conn, dtype=np.int64)
+        u = rng.random(n_per_conn)
+        inc[u < gap_p] = rng.integers(2, 300, size=int((u < gap_p).sum()))
+        inc[u < big_gap_p] = 40000 + rng.integers(0, 1000, size=int((u < big_gap_p).sum()))
+        pns = np.cumsum(inc) + int(rng.integers(0, 1 << 20))
+        rconns[c]["largest_pn"][2] = int(pns[0]) - 1  # the run continues what the receiver has seen
+        flip = int(flip_at * n_per_conn)
+        order = np.arange(n_per_conn)
+        for k in range(1, n_per_conn - 1):  # adjacent swaps in flight
+            if rng.random() < reorder_p and order[k] == k and order[k + 1] == k + 1:
+                order[k], order[k + 1] = k + 1, k
+        if 2 <= flip < n_per_conn - 1:  # the first new-phase packet overtakes the last old-phase one
+            order[flip - 2:flip + 2] = [flip - 2, flip, flip - 1, flip + 1]
+        lag = rng.integers(1, lag_max + 1, size=n_per_conn)
+        tamper = set(int(x) for x in np.nonzero(rng.random(n_per_conn) < tamper_p)[0])
+        idx0 = len(reqs)
+        acked = int(pns[0]) - 1  # the largest PN the receiver accepted so far (what ACKs could report)
+        for k in range(n_per_conn):
+            pn = int(pns[k])
+            prev = int(pns[k - 1]) if k else pn - 1
+            # the sender's largest acknowledged PN: behind the last sent, never past what the
+            # receiver accepted (a tampered packet is never acknowledged)
+            la = max(0, min(prev - int(lag[k]), acked))
+            if k not in tamper:
+                acked = max(acked, pn)
+            fl = int(rng.integers(frame_min, frame_max + 1))
+            frames.append(rng.bytes(fl))
+            reqs.append((fpos, pn, la, fl, s0 + (1 if k >= flip else 0)))
+            fpos += fl
+        per_conn_order.append([(c, idx0 + int(k), int(k) in tamper) for k in order])
+    sc = send.make_conns([d for d, _, _ in sconns], [b"\x01\x02\x03\x04"] * len(sconns),
+                         [[r, r, r] for _, r, _ in sconns], 0)
+    sc["key_phase"] = [p for _, _, p in sconns]
+    n = len(reqs)
+    req = np.zeros(n, dtype=send.REQ_DTYPE)
+    cap = frame_max + 64
+    req["frames_offset"] = [r[0] for r in reqs]
+    req["out_offset"] = np.arange(n, dtype=np.uint64) * np.uint64(cap)
+    req["pn"] = [r[1] for r in reqs]
+    req["largest_acked"] = [r[2] for r in reqs]
+    req["frame_len"] = [r[3] for r in reqs]
+    req["out_cap"] = cap
+    req["conn"] = [r[4] for r in reqs]
+    req["level"] = send.APPLICATION
+    fr = np.frombuffer(b"".join(frames) + b"\0", dtype=np.uint8)
+    out = np.zeros(n * cap, dtype=np.uint8)
+    st, ln = orc.batch_protect(keys, sc, fr, out, req, _lib.MQ_SUITE_MIXED)
+    assert (st == 0).all()
+    # arrival order: the connections' (reordered) sequences, interleaved at random or one after another
+    seqs = [list(s) for s in per_conn_order]
+    arrival = []
+    if interleave:
+        pos = [0] * n_conns
+        left = [len(s) for s in seqs]
+        while sum(left):
+            c = int(rng.choice([k for k in range(n_conns) if left[k]]))
+            take = min(left[c], int(rng.integers(1, 64)))
+            arrival += seqs[c][pos[c]:pos[c] + take]
+            pos[c] += take
+            left[c] -= take
+    else:
+        for s in seqs:
+            arrival += s
+    dgrams = np.zeros(n, dtype=recv.DGRAM_DTYPE)
+    total = int(ln.astype(np.int64).sum()) + 16 * n
+    arena = np.zeros(total + 64, dtype=np.uint8)
+    p = 0
+    for i, (c, r, tam) in enumerate(arrival):
+        L = int(ln[r])
+        b = out[r * cap:r * cap + L].copy()
+        if tam:
+            b[L - 20] ^= 0x10
+        p = (p + 7) // 8 * 8 if i % 3 else p
+        arena[p:p + L] = b
+        dgrams[i]["offset"], dgrams[i]["len"], dgrams[i]["conn"] = p, L, c
+        p += L
+    return keys, rconns, arena, dgrams

@@ -50,3 +50,21 @@ def test_oracle_recv_traffic(orc, tamper_flip):
     for r in bad:
         o, L = int(r["offset"]), int(r["len"])
         assert a2[o:o + L].tobytes() == arena[o:o + L].tobytes()
+
+
+@pytest.mark.parametrize("threads", [2, 5, 16])
+def test_oracle_recv_threads_identical(orc, threads):
+    # orc_batch_recv_mt (connections split over threads; record indices from a parse-only pass)
+    # gives the serial loop's records, connection table and arena exactly — what lets the full-size
+    # GPU receive parity tests check 2^20 datagrams against the oracle on 16 threads
+    keys, conns, scripts = build_traffic(orc, seed=7, n_conns=9, n_app=40, tamper_flip=True)
+    arena, dgrams = assemble(orc, keys, conns, scripts, seed=7)
+    c1, a1 = conns.copy(), arena.copy()
+    p1, n1 = orc.batch_recv(keys, c1, a1, dgrams, 4096)
+    c2, a2 = conns.copy(), arena.copy()
+    p2, n2 = orc.batch_recv(keys, c2, a2, dgrams, 4096, threads=threads)
+    assert n1 == n2 and p1.tobytes() == p2.tobytes()
+    assert c1.tobytes() == c2.tobytes() and a1.tobytes() == a2.tobytes()
+    c3, a3 = conns.copy(), arena.copy()  # max_pkts below the packet count: the same prefix kept
+    p3, n3 = orc.batch_recv(keys, c3, a3, dgrams, 50, threads=threads)
+    assert n3 == n1 and p3.tobytes() == p1[:50].tobytes() and a3.tobytes() == a1.tobytes()

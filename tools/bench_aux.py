@@ -3,7 +3,8 @@ stream; median of `reps`). Prints one JSON object; the round's copy lives in pro
 
   derive   mq_batch_derive_initial: 2^20 client DCIDs (8 B) -> 2^21 key-table rows
   protect  mq_batch_protect: 2^20 x 1171-B frames -> 1200-B 1-RTT packets (ChaCha20, 4096 keys)
-  recv     mq_batch_recv: the same 2^20 packets as one-packet datagrams of 4096 connections
+  recv     mq_batch_recv: the same 2^20 packets as one-packet datagrams of 4096 connections (and of
+           1024, 64, 4, 1 connections); a 4096-datagram sample byte-checked against the oracle
   records  mq_batch_seal_records / open_records: 2^20 x 1200-B and 2^16 x 16 KiB TLS records
            (AES-128-GCM)
   hp_mask  mq_batch_hp_mask (SURVEY §8d "mask-only timing"): 2^20 16-B samples -> 5-B masks,
@@ -94,11 +95,41 @@ def bench_protect_recv(reps, n=1 << 20, n_conns=4096, only="both"):
     ms_r = timed(one_recv, reps) - copy_ms
     got = pk.cpu().numpy().view(recv.PKT_DTYPE)
     assert int(cnt[0]) == n and (got["status"] == 0).all()
+    checked = sample_check(kt_rows=w.keys, rc=rc, sealed=sealed, opened=out, got=got, dg=dg)
     wire = n * 1200
     return ({"packets": n, "connections": n_conns, "ms": round(ms_p, 4),
              "GiB_per_s_wire": round(wire / ms_p * 1e3 / 2 ** 30, 1)},
             {"packets": n, "connections": n_conns, "ms": round(ms_r, 4),
-             "GiB_per_s_wire": round(wire / ms_r * 1e3 / 2 ** 30, 1)})
+             "GiB_per_s_wire": round(wire / ms_r * 1e3 / 2 ** 30, 1), "sample_checked": checked})
+
+
+def sample_check(kt_rows, rc, sealed, opened, got, dg, k=4096, seed=12):
+    """Byte check of a sample of the receive run: the oracle's receive composite
+    (the checker) on k sampled datagrams, from the sealed bytes, must give the same records and
+    the same opened bytes as the GPU's full run. The PNs are 4-byte encoded, so a sampled packet
+    decodes the same without its connection's earlier packets."""
+    from oracle import oracle
+    oracle.load()
+    rng = np.random.default_rng(seed)
+    n = len(dg)
+    idx = np.sort(rng.choice(n, size=min(k, n), replace=False))
+    sd = dg[idx].copy()
+    L = int(dg["len"][0])
+    arena = np.zeros(len(idx) * L, dtype=np.uint8)
+    sealed_np = sealed.cpu().numpy()
+    opened_np = opened.cpu().numpy()
+    for j, g in enumerate(idx):
+        o = int(dg["offset"][g])
+        arena[j * L:(j + 1) * L] = sealed_np[o:o + L]
+    sd["offset"] = np.arange(len(idx), dtype=np.uint64) * np.uint64(L)
+    o_pk, o_n = oracle.batch_recv(kt_rows, rc.copy(), arena, sd, len(idx), threads=16)
+    assert o_n == len(idx) and (o_pk["status"] == 0).all(), "oracle sample failed"
+    gp = got[idx]  # one packet per datagram: record index = datagram index
+    assert (gp["pn"] == o_pk["pn"]).all() and (gp["status"] == o_pk["status"]).all()
+    for j, g in enumerate(idx):
+        o = int(dg["offset"][g])
+        assert opened_np[o:o + L].tobytes() == arena[j * L:(j + 1) * L].tobytes(), f"datagram {g} differs"
+    return len(idx)
 
 
 def bench_records(reps, n, L):
@@ -134,10 +165,20 @@ def bench_hp_mask(reps, suite, n=1 << 20):
 
 
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "recv":  # receive runs only: recv REPS CONNS...
+        assert _lib.load().mq_device_init(0) == 0
+        reps = int(sys.argv[2])
+        res = {f"recv_{nc}_connections": bench_protect_recv(reps, n_conns=nc, only="recv")[1]
+               for nc in map(int, sys.argv[3:])}
+        print(json.dumps(res), flush=True)
+        return
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
     assert _lib.load().mq_device_init(0) == 0
     res = {"device": torch.cuda.get_device_name(0), "derive": bench_derive(reps)}
     res["protect"], res["recv"] = bench_protect_recv(reps)
+    # the receive walk over few connections (r05: runs cut into segments of kSeg packets per wave)
+    for nc in (1024, 64, 4, 1):
+        res[f"recv_{nc}_connections"] = bench_protect_recv(reps, n_conns=nc, only="recv")[1]
     res["records_1200"] = bench_records(reps, 1 << 20, 1200)
     res["records_16k"] = bench_records(reps, 1 << 16, 16384 + 5 + 17)
     res["hp_mask_aes"] = bench_hp_mask(reps, _lib.MQ_SUITE_AES128GCM)
