@@ -900,7 +900,7 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
   if (n == 0) return MQ_OK;
   const int cus = devices().cus(kt->device);
   hipStream_t s = (hipStream_t)stream;
-  hipError_t e;
+  hipError_t e = hipSuccess;
   uint8_t* ws = (uint8_t*)workspace;
   // open with a workspace: header-protection masks come from the one-lane-per-packet pre-pass
   uint2* hpm = (open && ws) ? (uint2*)ws : nullptr;
@@ -926,13 +926,21 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
     uint32_t* counts = (uint32_t*)(pw + counts_off);
     // list mode: the grids cover the list capacity; the kernels read the real lengths from counts
     const uint32_t cap = mq_partition_list_cap(n);
-    e = mq_launch_partition(kt->dev, kt->rows, desc, n, list, hist, counts, s, recv_pass, live);
     // open: one header-protection pre-pass over the whole batch in descriptor order, both suites,
-    // before the tiles (seal needs none: the tiles mask their own packets). r03f ran it on a side
-    // stream beside the partition: no gain (E open 1.279 -> 1.280 ms), its blocks delayed the
-    // partition's single-workgroup scan (27 -> 85 us)
-    if (e == hipSuccess && open && hpm && !hpm_ready)
-      e = mq_launch_mixed_open_hp(kt->dev, kt->rows, arena, arena_len, desc, n, hpm, s);
+    // before the tiles (seal needs none: the tiles mask their own packets). It runs on a side
+    // stream beside the partition (r05: the partition no longer has a single-workgroup launch for
+    // its blocks to delay — r03f measured that scan 27 -> 85 us and no gain); MQ_HP_FORK=0
+    // (diagnostic, read per call) runs it on s after the partition, as r04 did.
+    {
+      const bool hp = open && hpm && !hpm_ready;
+      const char* hf = std::getenv("MQ_HP_FORK");
+      auto hfork = hp && fork_enabled() && !(hf && hf[0] == '0') ? side_streams().fork(kt->device, s, 1)
+                                                                   : mq::SideStreams<HipBackend>::Fork();
+      if (hp && hfork) e = mq_launch_mixed_open_hp(kt->dev, kt->rows, arena, arena_len, desc, n, hpm, hfork.side(0));
+      if (e == hipSuccess) e = mq_launch_partition(kt->dev, kt->rows, desc, n, list, hist, counts, s, recv_pass, live);
+      if (e == hipSuccess && hp && !hfork) e = mq_launch_mixed_open_hp(kt->dev, kt->rows, arena, arena_len, desc, n, hpm, s);
+      if (!hfork.join() && e == hipSuccess) e = hipErrorUnknown;
+    }  // the fork's entry lock is released before the AES fork below takes it
     if (e != hipSuccess) return MQ_ERR_HIP;
     // The hot AES key's segment (counts + 2: its row and segment length, list 0's front;
     // single-key kernel) runs on a side stream beside the other AES keys' tiles on s: each CU moves

@@ -192,6 +192,18 @@ __device__ __forceinline__ uint32_t fold_votes(const uint2* __restrict__ votes, 
   const uint32_t x = __builtin_amdgcn_readfirstlane(v.x), y = __builtin_amdgcn_readfirstlane(v.y);
   return y ? x : kNoKey;
 }
+// meta: counts[0..1] | hot row | hot segment entries | seg[kClasses] | slice votes (kVoteSlices pairs) |
+// cmax[kLenClasses] (list 1's largest image per class, chunks) | cls[kLenClasses] (list 1's classes:
+// ppt | Q << 8) | reg[8] (list 1's regions: tiles of G = 8, 4, 2, 1, first entries of G = 4, 2, 1,
+// all tiles; mq_chacha.hip chacha_list_tile) | ctot[kClasses] | ccur[kClasses] | done
+constexpr uint32_t kMetaCmax = 4 + kClasses + 2 * kVoteSlices;
+constexpr uint32_t kMetaCls = kMetaCmax + kLenClasses;
+constexpr uint32_t kMetaReg = kMetaCls + kLenClasses;
+constexpr uint32_t kMetaCtot = kMetaReg + 8;       // class totals (count kernel)
+constexpr uint32_t kMetaCcur = kMetaCtot + kClasses;  // class cursors (scatter)
+constexpr uint32_t kMetaDone = kMetaCcur + kClasses;  // count blocks finished
+constexpr uint32_t kMetaWords = kMetaDone + 1;
+
 // First launch: fills the lists with holes and zeroes the keyed bins (grid-stride, 16-B stores);
 // blocks 0 .. nv-1 also vote a sample slice each.
 extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_init_kernel(
@@ -200,6 +212,8 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_init_kernel(
     uint32_t bins_q, const uint32_t* __restrict__ live, uint32_t* __restrict__ cmax) {
   if (pass_empty(live)) return;
   if (blockIdx.x == 0 && threadIdx.x < kLenClasses) cmax[threadIdx.x] = 0;
+  // ctot | ccur | done follow reg in the meta (kMetaCtot .. kMetaDone)
+  if (blockIdx.x == 0 && threadIdx.x < 2 * kClasses + 1) cmax[kMetaCtot - kMetaCmax + threadIdx.x] = 0;
   if (blockIdx.x < nv) {  // block-uniform
     const uint2 v = vote_slice(kt, n_rows, desc, n, blockIdx.x);
     if (threadIdx.x == 0) votes[blockIdx.x] = v;
@@ -210,17 +224,47 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_init_kernel(
   for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < bins_q; q += stride) bins[q] = make_uint4(0, 0, 0, 0);
 }
 
-// Per block: the class histogram of its kPartBlock descriptors; keyed (bins != nullptr):
-// non-majority AES packets are counted per (row, class) bin instead.
+// Keyed-layout words (after the meta): bins[16 R] (per (row, class) packet counts), fill[16 R] (the
+// scatter's cursors inside each bin), rowtot[R, padded to 4] (per-row packet counts), rowseg[2 R]
+// (per row: first list entry, entries including the tile padding). Init zeroes bins..rowtot.
+struct KeyedWs { uint32_t *bins, *fill, *rowtot, *rowseg; };
+__host__ __device__ __forceinline__ KeyedWs keyed_ws(uint32_t* base, uint32_t n_rows) {
+  KeyedWs k;
+  k.bins = base;
+  k.fill = base ? base + 16ull * n_rows : nullptr;
+  k.rowtot = base ? base + 32ull * n_rows : nullptr;
+  k.rowseg = base ? base + 32ull * n_rows + ((n_rows + 3) & ~3u) : nullptr;
+  return k;
+}
+__host__ __device__ __forceinline__ size_t keyed_zero_quads(uint32_t n_rows) { return (32ull * n_rows + ((n_rows + 3) & ~3u)) / 4; }
+
+__device__ void part_layout(uint32_t cap, uint32_t* __restrict__ counts, uint32_t* __restrict__ seg,
+                            const uint32_t* __restrict__ ctot, const KeyedWs& kw, uint32_t n_rows,
+                            const uint32_t* __restrict__ cmax, uint32_t* __restrict__ cls, uint32_t* __restrict__ reg,
+                            uint32_t narrow);
+__device__ void part_empty(uint32_t* __restrict__ counts, uint32_t* __restrict__ reg, const KeyedWs& kw,
+                           uint32_t n_rows);
+
+// Per block: the class counts of its kPartBlock descriptors, added to the batch's class totals
+// (ctot); keyed (bins != nullptr): non-majority AES packets are counted per (row, class) bin and
+// per row instead. The block that finishes last lays the lists out (part_layout): no single-
+// workgroup scan launch (r05: the r04 scan kernel took 32-35 us for config E, 19 of them scanning
+// the 4098 rows' bins; the row totals are now counted directly).
 extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_count_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_pkt_desc* __restrict__ desc, uint32_t n,
-    uint32_t nblocks, const uint2* __restrict__ votes, uint32_t nv, uint32_t* __restrict__ hot_p,
-    uint32_t* __restrict__ hist, uint32_t* __restrict__ bins, uint32_t skip_unkeyed,
-    const uint32_t* __restrict__ live, uint32_t* __restrict__ cmax) {
-  if (pass_empty(live)) return;
+    const uint2* __restrict__ votes, uint32_t nv, uint32_t* __restrict__ hot_p, uint32_t* __restrict__ bins,
+    uint32_t skip_unkeyed, const uint32_t* __restrict__ live, uint32_t* __restrict__ cmax,
+    uint32_t* __restrict__ ctot, uint32_t* __restrict__ done, uint32_t cap, uint32_t* __restrict__ counts,
+    uint32_t* __restrict__ seg, uint32_t* __restrict__ cls, uint32_t* __restrict__ reg, uint32_t narrow) {
+  const KeyedWs kw = keyed_ws(bins, n_rows);
+  if (pass_empty(live)) {  // empty lists: no hot key, no row segments, no regions
+    if (blockIdx.x == 0) part_empty(counts, reg, kw, n_rows);
+    return;
+  }
   __shared__ uint32_t s_cnt[kClasses];
   __shared__ uint32_t s_max[kLenClasses];  // list 1's classes: the largest image, in chunks
   __shared__ uint32_t s_bcnt[kBinSlots];
+  __shared__ uint32_t s_last;
   const bool lds_bins = bins_in_lds(bins, n_rows);  // kernel-uniform
   PartItem it[kPartItems];
   part_fetch(kt, n_rows, desc, n, it);
@@ -256,84 +300,59 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_count_kernel(
       if (j < k && same) first = false;
       if (j > k && same) ++cnt;
     }
-    if (first) atomicAdd(lds_bins ? &s_bcnt[kb[k]] : &bins[kb[k]], cnt);
+    if (first && lds_bins) atomicAdd(&s_bcnt[kb[k]], cnt);
+    if (first && !lds_bins) {
+      atomicAdd(&kw.bins[kb[k]], cnt);
+      atomicAdd(&kw.rowtot[kb[k] / kKeyClasses], cnt);
+    }
   }
   __syncthreads();
   if (lds_bins)
     for (uint32_t q = threadIdx.x; q < n_rows * kKeyClasses; q += blockDim.x)
-      if (s_bcnt[q]) atomicAdd(&bins[q], s_bcnt[q]);
-  if (threadIdx.x < kClasses) hist[(size_t)threadIdx.x * nblocks + blockIdx.x] = s_cnt[threadIdx.x];
+      if (s_bcnt[q]) {
+        atomicAdd(&kw.bins[q], s_bcnt[q]);
+        atomicAdd(&kw.rowtot[q / kKeyClasses], s_bcnt[q]);
+      }
+  if (threadIdx.x < kClasses && s_cnt[threadIdx.x]) atomicAdd(&ctot[threadIdx.x], s_cnt[threadIdx.x]);
   if (threadIdx.x < kLenClasses && s_max[threadIdx.x]) atomicMax(&cmax[threadIdx.x], s_max[threadIdx.x]);
+  // The last block to finish lays the lists out. Each thread waits until its atomics above are
+  // performed (vmcnt counts them on gfx950) before the barrier that precedes the block's count, so
+  // the block's totals are in when the count is. No __threadfence: on gfx950 a device-scope release
+  // also writes back the XCD's L2 (measured: the count kernel 26 -> 108 us with one per block).
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;  // block-uniform
+  part_layout(cap, counts, seg, ctot, kw, n_rows, cmax, cls, reg, narrow);
 }
 
-// Single workgroup: per class, the exclusive scan of its per-block counts (in place: the rank of
-// the block's first packet inside the class); then the class segments (whole tiles) are laid out
-// list by list (groups 0 and 1: list 0, group 2: list 1 at `cap`): seg[c] = first list entry of
-// class c, counts[s] = entries of list s, holes included; counts[3] = entries of the hot key's
-// classes (the front of list 0, whole tiles).
-// Latency-bound work (a few thousand counts): each wave owns kClasses / 16 classes and issues
-// all their loads before any scan (4 consecutive blocks per lane per 256-block chunk), so the
-// kernel waits on memory once instead of once per class (r01: 26 us per partition, rocprof).
-constexpr int kScanWaves = 16, kClassesPerWave = kClasses / kScanWaves;
-static_assert(kClasses % kScanWaves == 0, "classes per scan wave");
-__device__ void key_scan(uint32_t* __restrict__ bins, uint32_t n_rows, uint32_t* __restrict__ counts, uint32_t base,
-                         uint32_t* __restrict__ rowseg);
+__device__ __forceinline__ uint32_t ld_fresh(const uint32_t* p) {  // past this CU's L1: other blocks' atomics
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
-extern "C" __global__ __launch_bounds__(64 * kScanWaves) void mq_part_scan_kernel(uint32_t* __restrict__ hist,
-                                                                                 uint32_t nblocks, uint32_t cap,
-                                                                                 uint32_t* __restrict__ counts,
-                                                                                 uint32_t* __restrict__ seg,
-                                                                                 uint32_t* __restrict__ bins,
-                                                                                 uint32_t n_rows,
-                                                                                 uint32_t* __restrict__ rowseg,
-                                                                                 const uint32_t* __restrict__ live,
-                                                                                 const uint32_t* __restrict__ cmax,
-                                                                                 uint32_t* __restrict__ cls,
-                                                                                 uint32_t* __restrict__ reg,
-                                                                                 uint32_t narrow) {
-  if (pass_empty(live)) {  // empty lists: no hot key, no row segments, no regions
-    if (threadIdx.x == 0) { counts[0] = 0; counts[1] = 0; counts[2] = kNoKey; counts[3] = 0; }
-    if (threadIdx.x < 8) reg[threadIdx.x] = 0;
-    if (rowseg)
-      for (uint32_t r = threadIdx.x; r < n_rows; r += blockDim.x) *(uint2*)(rowseg + 2 * (size_t)r) = make_uint2(0, 0);
-    return;
-  }
+__device__ void part_empty(uint32_t* __restrict__ counts, uint32_t* __restrict__ reg, const KeyedWs& kw,
+                           uint32_t n_rows) {
+  if (threadIdx.x == 0) { counts[0] = 0; counts[1] = 0; counts[2] = kNoKey; counts[3] = 0; }
+  if (threadIdx.x < 8) reg[threadIdx.x] = 0;
+  if (kw.rowseg)
+    for (uint32_t r = threadIdx.x; r < n_rows; r += blockDim.x) *(uint2*)(kw.rowseg + 2 * (size_t)r) = make_uint2(0, 0);
+}
+
+__device__ void row_scan(const KeyedWs& kw, uint32_t n_rows, uint32_t* __restrict__ counts, uint32_t base);
+
+// The lists' layout (the count kernel's last block, 16 waves) from the class totals: the class
+// segments (whole tiles) list by list (groups 0 and 1: list 0, group 2: list 1 at `cap`): seg[c] =
+// first list entry of class c, counts[s] = entries of list s, holes included; counts[3] = entries of
+// the hot key's classes (the front of list 0, whole tiles); keyed, the rows' segments after them.
+__device__ void part_layout(uint32_t cap, uint32_t* __restrict__ counts, uint32_t* __restrict__ seg,
+                            const uint32_t* __restrict__ ctot, const KeyedWs& kw, uint32_t n_rows,
+                            const uint32_t* __restrict__ cmax, uint32_t* __restrict__ cls, uint32_t* __restrict__ reg,
+                            uint32_t narrow) {
   __shared__ uint32_t s_list0;
   __shared__ uint32_t s_tot[kClasses];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t carry[kClassesPerWave];
-#pragma unroll
-  for (int q = 0; q < kClassesPerWave; ++q) carry[q] = 0;
-  for (uint32_t k0 = 0; k0 < nblocks; k0 += 4 * kWave) {  // one chunk for n <= 2^20 descriptors
-    uint32_t v[kClassesPerWave][4];
-#pragma unroll
-    for (int q = 0; q < kClassesPerWave; ++q) {
-      const uint32_t* h = hist + (size_t)(wave + kScanWaves * q) * nblocks;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const uint32_t k = k0 + 4 * lane + e;
-        v[q][e] = k < nblocks ? h[k] : 0u;
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < kClassesPerWave; ++q) {
-      uint32_t* h = hist + (size_t)(wave + kScanWaves * q) * nblocks;
-      const uint32_t lsum = v[q][0] + v[q][1] + v[q][2] + v[q][3];
-      const uint32_t incl = wave_incl_scan(lsum);
-      uint32_t run = carry[q] + incl - lsum;  // exclusive prefix of this lane's first block
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const uint32_t k = k0 + 4 * lane + e;
-        if (k < nblocks) h[k] = run;
-        run += v[q][e];
-      }
-      carry[q] += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    }
-  }
-  if (lane == 0) {
-#pragma unroll
-    for (int q = 0; q < kClassesPerWave; ++q) s_tot[wave + kScanWaves * q] = carry[q];
-  }
+  if (threadIdx.x < kClasses) s_tot[threadIdx.x] = ld_fresh(ctot + threadIdx.x);
   __syncthreads();
   static_assert(2 * kLenClasses == kWave && kClasses - 2 * kLenClasses <= kWave, "one wave per list");
   if (wave == 0) {  // list 0 (AES): lane = class 0..63, tiles of 8 entries
@@ -357,7 +376,7 @@ extern "C" __global__ __launch_bounds__(64 * kScanWaves) void mq_part_scan_kerne
     // starting at a multiple of Q); a class's tiles hold ppt <= Q packets, the rest holes.
     const bool in = lane < (int)kLenClasses;
     const uint32_t c = 2 * kLenClasses + (uint32_t)lane, b = kLenClasses - 1 - (uint32_t)lane;
-    const uint32_t cm = in ? cmax[lane] : 0u, tot = in ? s_tot[c] : 0u;
+    const uint32_t cm = in ? ld_fresh(cmax + lane) : 0u, tot = in ? s_tot[c] : 0u;
     // the receive composite's passes (skip_unkeyed) keep octet tiles only: their persistent list
     // kernels carry no narrow path (it spilled their registers)
     uint32_t g = in ? (narrow ? class_g(b, tot ? cm : 0u) : (tot ? kPktsPerTile : 1u)) : 0u;
@@ -391,43 +410,30 @@ extern "C" __global__ __launch_bounds__(64 * kScanWaves) void mq_part_scan_kerne
       reg[4] = R4; reg[5] = R2; reg[6] = R1; reg[7] = reg[0] + reg[1] + reg[2] + reg[3];
     }
   }
-  if (bins) {  // keyed layout: the other AES keys' segments follow (workgroup-uniform)
+  if (kw.bins) {  // keyed layout: the other AES keys' segments follow (workgroup-uniform)
     __syncthreads();
-    key_scan(bins, n_rows, counts, s_list0, rowseg);
+    row_scan(kw, n_rows, counts, s_list0);
   }
 }
 
-// Keyed layout (the scan kernel's workgroup, after the class segments): each row's segment (its
-// bins' packets, whole tiles) follows the majority key's classes in list 0, which end on a tile
-// boundary at `base`; bins[b] becomes the list position of bin b's first packet (the scatter's
-// cursor), rowseg[2r], rowseg[2r + 1] = row r's segment (first entry, entries including the tile
-// padding) and counts[0] the list's entries. Each thread takes kKeyRowsPerThread consecutive rows
-// (their bins are one contiguous 256-B read), so a 4096-row table is one pass of two barriers
-// (r02/r03 took one row per thread: five passes of three barriers for config E's 4098 rows). Five
-// rows per thread (one pass for E's 4098) spill at 128 VGPRs and measured 34 -> 45 us (r03y).
+// Keyed layout (the layout block, after the class segments): each row's segment (its packets,
+// whole tiles) follows the majority key's classes in list 0, which end on a tile boundary at
+// `base`: rowseg[2r], rowseg[2r + 1] = row r's first entry and entries (tile padding included),
+// counts[0] = the list's entries. Each thread takes kKeyRowsPerThread consecutive rows' totals (one
+// 16-B read): 4096 rows per pass of two barriers. The scatter places a bin's packets at its row's
+// start plus the packets of the row's longer classes (read from bins) plus its cursor (fill).
 constexpr int kKeyRowsPerThread = 4;
-static_assert(64 * kScanWaves == 1024, "key scan: a 1024-thread workgroup");
-__device__ void key_scan(uint32_t* __restrict__ bins, uint32_t n_rows, uint32_t* __restrict__ counts, uint32_t base,
-                         uint32_t* __restrict__ rowseg) {
-  constexpr int kThreads = 64 * kScanWaves, R = kKeyRowsPerThread;
-  __shared__ uint32_t s_wave[kScanWaves];
+__device__ void row_scan(const KeyedWs& kw, uint32_t n_rows, uint32_t* __restrict__ counts, uint32_t base) {
+  constexpr int kThreads = kPartThreads, R = kKeyRowsPerThread;
+  __shared__ uint32_t s_wave[kPartThreads / kWave];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t run_base = base;  // entries of list 0 before this pass (the same in every thread)
   for (uint32_t r0 = 0; r0 < n_rows; r0 += kThreads * R) {  // workgroup-uniform
-    const uint32_t rt = r0 + (uint32_t)threadIdx.x * R;  // this thread's first row
-    uint4 v[R][kKeyClasses / 4];
-#pragma unroll
-    for (int q = 0; q < R; ++q) {
-      const uint4* src = (const uint4*)(bins + (size_t)(rt + q) * kKeyClasses);
-#pragma unroll
-      for (int k = 0; k < (int)kKeyClasses / 4; ++k) v[q][k] = rt + q < n_rows ? src[k] : make_uint4(0, 0, 0, 0);
-    }
+    const uint32_t rt = r0 + (uint32_t)threadIdx.x * R;  // this thread's first row (rowtot is padded to 4)
     uint32_t ent[R], sum = 0;
 #pragma unroll
     for (int q = 0; q < R; ++q) {
-      uint32_t tot = 0;
-#pragma unroll
-      for (int k = 0; k < (int)kKeyClasses / 4; ++k) tot += v[q][k].x + v[q][k].y + v[q][k].z + v[q][k].w;
+      const uint32_t tot = rt + q < n_rows ? ld_fresh(kw.rowtot + rt + q) : 0u;
       ent[q] = (tot + kPktsPerTile - 1) & ~(kPktsPerTile - 1);  // the row's segment: whole tiles
       sum += ent[q];
     }
@@ -436,27 +442,14 @@ __device__ void key_scan(uint32_t* __restrict__ bins, uint32_t n_rows, uint32_t*
     __syncthreads();
     uint32_t at = run_base + incl - sum, pass = 0;
 #pragma unroll
-    for (int q = 0; q < kScanWaves; ++q) {
+    for (int q = 0; q < kThreads / kWave; ++q) {
       const uint32_t t = s_wave[q];
       if (q < wave) at += t;
       pass += t;
     }
 #pragma unroll
     for (int q = 0; q < R; ++q) {
-      if (rt + q >= n_rows) break;
-      // the row's segment of list 0 (the key-segmented AES kernels walk these)
-      *(uint2*)(rowseg + 2 * (size_t)(rt + q)) = make_uint2(at, ent[q]);
-      uint4* dst = (uint4*)(bins + (size_t)(rt + q) * kKeyClasses);
-      uint32_t p = at;
-#pragma unroll
-      for (int k = 0; k < (int)kKeyClasses / 4; ++k) {
-        uint4 o;
-        o.x = p; p += v[q][k].x;
-        o.y = p; p += v[q][k].y;
-        o.z = p; p += v[q][k].z;
-        o.w = p; p += v[q][k].w;
-        dst[k] = o;
-      }
+      if (rt + q < n_rows) *(uint2*)(kw.rowseg + 2 * (size_t)(rt + q)) = make_uint2(at, ent[q]);
       at += ent[q];
     }
     run_base += pass;
@@ -465,37 +458,62 @@ __device__ void key_scan(uint32_t* __restrict__ bins, uint32_t n_rows, uint32_t*
   if (threadIdx.x == 0) counts[0] = run_base;
 }
 
+// first list entry of keyed bin kb: its row's start plus the row's packets in longer classes
+__device__ __forceinline__ uint32_t bin_start(const KeyedWs& kw, uint32_t kb) {
+  const uint32_t row = kb / kKeyClasses, c = kb % kKeyClasses;
+  const uint4* b = (const uint4*)(kw.bins + (size_t)row * kKeyClasses);
+  uint32_t p = kw.rowseg[2 * (size_t)row];
+#pragma unroll
+  for (uint32_t k = 0; k < kKeyClasses / 4; ++k) {
+    const uint4 v = b[k];
+    p += (4 * k < c ? v.x : 0u) + (4 * k + 1 < c ? v.y : 0u) + (4 * k + 2 < c ? v.z : 0u) + (4 * k + 3 < c ? v.w : 0u);
+  }
+  return p;
+}
+
+// Each block counts its packets per class again and reserves their ranks inside each class with
+// one global atomic per class (ccur): the block's packets of a class take consecutive ranks (the
+// order of blocks inside a class is whichever reserved first — packets are independent, so only
+// the tile composition can change between runs, never a result). Keyed packets reserve their
+// places inside their bin the same way (fill) and sit at bin_start + that rank.
 extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_scatter_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_pkt_desc* __restrict__ desc, uint32_t n,
-    uint32_t nblocks, const uint32_t* __restrict__ hot_p, const uint32_t* __restrict__ hist,
-    const uint32_t* __restrict__ seg, uint32_t* __restrict__ list, uint32_t* __restrict__ bins,
-    uint32_t skip_unkeyed, const uint32_t* __restrict__ live, const uint32_t* __restrict__ cls) {
+    const uint32_t* __restrict__ hot_p, uint32_t* __restrict__ ccur, const uint32_t* __restrict__ seg,
+    uint32_t* __restrict__ list, uint32_t* __restrict__ bins, uint32_t skip_unkeyed, const uint32_t* __restrict__ live,
+    const uint32_t* __restrict__ cls) {
   if (pass_empty(live)) return;
+  const KeyedWs kw = keyed_ws(bins, n_rows);
   __shared__ uint32_t s_rank[kClasses];
-  __shared__ uint32_t s_cls[kLenClasses];  // list 1's classes: ppt | Q << 8 (the scan's layout)
+  __shared__ uint32_t s_cls[kLenClasses];  // list 1's classes: ppt | Q << 8 (the layout's)
   __shared__ uint32_t s_bcnt[kBinSlots];
   const bool lds_bins = bins_in_lds(bins, n_rows);  // kernel-uniform
   if (threadIdx.x < kLenClasses) s_cls[threadIdx.x] = cls[threadIdx.x];
+  if (threadIdx.x < kClasses) s_rank[threadIdx.x] = 0;
   if (lds_bins)
     for (uint32_t q = threadIdx.x; q < n_rows * kKeyClasses; q += blockDim.x) s_bcnt[q] = 0;
   PartItem it[kPartItems];
   part_fetch(kt, n_rows, desc, n, it);
   const uint32_t hot = *hot_p;
   const int lane = threadIdx.x & 63;
-  if (threadIdx.x < kClasses) s_rank[threadIdx.x] = hist[(size_t)threadIdx.x * nblocks + blockIdx.x];
-  __syncthreads();
-  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  // keyed bins: the thread's items of one bin claim their positions with one atomic (as counted)
-  uint32_t kb[kPartItems], kpos[kPartItems];
-  bool kd[kPartItems], skp[kPartItems];
+  uint32_t kb[kPartItems], cl[kPartItems];
+  bool kd[kPartItems], in[kPartItems];
 #pragma unroll
   for (int k = 0; k < kPartItems; ++k) {
     const uint32_t i = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
-    skp[k] = skip_unkeyed && it[k].key >= n_rows;  // in no list (never AES: not keyed either)
-    const uint32_t c = i < n ? part_class(hot, it[k]) : 0u;
-    kd[k] = bins && i < n && c / kLenClasses == 1;
+    const bool skp = skip_unkeyed && it[k].key >= n_rows;  // in no list (never AES: not keyed either)
+    cl[k] = i < n ? part_class(hot, it[k]) : 0u;
+    kd[k] = bins && i < n && cl[k] / kLenClasses == 1;
     kb[k] = kd[k] ? key_bin(it[k]) : 0u;
+    in[k] = i < n && !kd[k] && !skp;
   }
+  __syncthreads();  // s_rank, s_bcnt zeroed
+  // the block's counts per class (as the count kernel made them), then one global reservation each
+#pragma unroll
+  for (int k = 0; k < kPartItems; ++k)
+    if (in[k]) atomicAdd(&s_rank[cl[k]], 1u);
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  // keyed bins: the thread's items of one bin claim their places with one atomic
+  uint32_t kpos[kPartItems];
 #pragma unroll
   for (int k = 0; k < kPartItems; ++k) {
     int lead = k;
@@ -507,31 +525,33 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_scatter_kerne
       if (j > k && same) ++cnt;
     }
     uint32_t base = 0;
-    if (kd[k] && lead == k) base = atomicAdd(lds_bins ? &s_bcnt[kb[k]] : &bins[kb[k]], cnt);
-    // a follower takes the leader's position (its base: the leader comes first in k order) + rank
+    if (kd[k] && lead == k) base = atomicAdd(lds_bins ? &s_bcnt[kb[k]] : &kw.fill[kb[k]], cnt);
+    // a follower takes the leader's place (its base: the leader comes first in k order) + rank
 #pragma unroll
     for (int j = 0; j < kPartItems; ++j)
       if (j == lead && j < k) base = kpos[j];
     kpos[k] = kd[k] ? base + rank : 0u;  // lds_bins: the rank inside the block's count of the bin
-    if (kd[k] && !lds_bins) list[kpos[k]] = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;  // any order in a bin
+    if (kd[k] && !lds_bins)
+      list[bin_start(kw, kb[k]) + kpos[k]] = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
   }
-  if (lds_bins) {  // kernel-uniform: the block's base in each bin, one global atomic per bin
-    __syncthreads();
+  __syncthreads();
+  if (threadIdx.x < kClasses && s_rank[threadIdx.x]) s_rank[threadIdx.x] = atomicAdd(&ccur[threadIdx.x], s_rank[threadIdx.x]);
+  if (lds_bins)  // kernel-uniform: the block's base in each bin, one global atomic per bin
     for (uint32_t q = threadIdx.x; q < n_rows * kKeyClasses; q += blockDim.x)
-      if (s_bcnt[q]) s_bcnt[q] = atomicAdd(&bins[q], s_bcnt[q]);
-    __syncthreads();
+      if (s_bcnt[q]) s_bcnt[q] = atomicAdd(&kw.fill[q], s_bcnt[q]);
+  __syncthreads();
+  if (lds_bins) {
 #pragma unroll
     for (int k = 0; k < kPartItems; ++k)
-      if (kd[k]) list[s_bcnt[kb[k]] + kpos[k]] = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
+      if (kd[k])
+        list[bin_start(kw, kb[k]) + s_bcnt[kb[k]] + kpos[k]] = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
   }
 #pragma unroll
   for (int k = 0; k < kPartItems; ++k) {
     const uint32_t i = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
-    const uint32_t c = i < n ? part_class(hot, it[k]) : 0u;
-    const bool keyed = kd[k];
-    const bool in = i < n && !keyed && !skp[k];
+    const uint32_t c = cl[k];
     // lanes of this wave with the same class (7 ballots), rank among them = peers below
-    uint64_t peers = __ballot(in);
+    uint64_t peers = __ballot(in[k]);
 #pragma unroll
     for (int bit = 0; bit < 7; ++bit) {
       const uint64_t b = __ballot((c >> bit) & 1u);
@@ -539,11 +559,11 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_scatter_kerne
     }
     const uint32_t rank = (uint32_t)__popcll(peers & below);
     uint32_t base = 0;
-    if (in && rank == 0) base = atomicAdd(&s_rank[c], (uint32_t)__popcll(peers));
+    if (in[k] && rank == 0) base = atomicAdd(&s_rank[c], (uint32_t)__popcll(peers));
     // the leader (lowest lane of the peer group) hands its base to the group
-    const int leader = in ? __ffsll((unsigned long long)peers) - 1 : lane;
+    const int leader = in[k] ? __ffsll((unsigned long long)peers) - 1 : lane;
     base = (uint32_t)__shfl((int)base, leader, kWave);
-    if (in) {
+    if (in[k]) {
       const uint32_t r = base + rank;
       const uint32_t x = c >= 2 * kLenClasses ? s_cls[c - 2 * kLenClasses] : (class_ppt(c, 0u) | kPktsPerTile << 8);
       const uint32_t ppt = x & 0xffu, Q = x >> 8;
@@ -561,25 +581,17 @@ static bool keyed_layout(uint32_t n, uint32_t n_rows) {
          (uint64_t)n + kPktsPerTile * kLenClasses + (uint64_t)(kPktsPerTile - 1) * n_rows <= mq_partition_list_cap(n);
 }
 
-// meta: counts[0..1] | hot row | hot segment entries | seg[kClasses] | slice votes (kVoteSlices pairs) |
-// cmax[kLenClasses] (list 1's largest image per class, chunks) | cls[kLenClasses] (list 1's classes:
-// ppt | Q << 8) | reg[8] (list 1's regions: tiles of G = 8, 4, 2, 1, first entries of G = 4, 2, 1,
-// all tiles; mq_chacha.hip chacha_list_tile)
-constexpr uint32_t kMetaCmax = 4 + kClasses + 2 * kVoteSlices;
-constexpr uint32_t kMetaCls = kMetaCmax + kLenClasses;
-constexpr uint32_t kMetaReg = kMetaCls + kLenClasses;
-constexpr uint32_t kMetaWords = kMetaReg + 8;
 
 // list (2 x cap entries) | class histograms (kClasses per block) |
 // meta (2 totals, hot row, hot segment entries, kClasses segment starts) | keyed bins, 256-B aligned pieces
 static size_t part_align(size_t b) { return (b + 255) & ~(size_t)255; }
 
-// The per-row segments of a keyed partition (rowseg, 2 words per row after the keyed bins), or
-// null when mq_launch_partition(n, n_rows) does not lay the list out keyed. counts: the
-// partition's meta (as passed to mq_launch_partition).
+// The per-row segments of a keyed partition (rowseg, 2 words per row, keyed_ws), or null when
+// mq_launch_partition(n, n_rows) does not lay the list out keyed. counts: the partition's meta (as
+// passed to mq_launch_partition).
 const uint32_t* mq_partition_rowseg(uint32_t n, uint32_t n_rows, const uint32_t* counts) {
   if (!keyed_layout(n, n_rows)) return nullptr;
-  return (const uint32_t*)((const uint8_t*)counts + part_align(sizeof(uint32_t) * kMetaWords)) + key_bins(n);
+  return keyed_ws((uint32_t*)((uint8_t*)counts + part_align(sizeof(uint32_t) * kMetaWords)), n_rows).rowseg;
 }
 
 hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_desc* desc, uint32_t n,
@@ -603,19 +615,18 @@ hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_d
   uint32_t* reg = counts + kMetaReg;
   uint32_t* bins = keyed_layout(n, n_rows) ? (uint32_t*)((uint8_t*)counts + part_align(sizeof(uint32_t) * kMetaWords))
                                            : nullptr;
-  const uint32_t list_q = cap / 2, bins_q = bins ? kKeyClasses / 4 * n_rows : 0u;  // 16-B words
+  const uint32_t list_q = cap / 2, bins_q = bins ? (uint32_t)keyed_zero_quads(n_rows) : 0u;  // 16-B words
   const uint32_t init_blocks = max(1u, min(256u, (list_q + bins_q + kPartThreads - 1) / kPartThreads));
   const uint32_t nv = min(kVoteSlices, init_blocks);
   const uint32_t S = min(n, kVoteSample), used = (S + kVoteSlice - 1) / kVoteSlice;  // slices with samples
   const uint32_t grid = max(init_blocks, used);
   hipLaunchKernelGGL(mq_part_init_kernel, dim3(grid), dim3(kPartThreads), 0, s, kt, n_rows, desc, n, votes,
                      max(nv, used), (uint4*)list, list_q, (uint4*)bins, bins_q, live, cmax);
-  hipLaunchKernelGGL(mq_part_count_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, kt, n_rows, desc, n,
-                     nblocks, votes, max(nv, used), hot, hist, bins, (uint32_t)skip_unkeyed, live, cmax);
-  hipLaunchKernelGGL(mq_part_scan_kernel, dim3(1), dim3(64 * kScanWaves), 0, s, hist, nblocks, cap, counts, seg,
-                     bins, n_rows, bins ? bins + key_bins(n) : nullptr, live, cmax, cls, reg, (uint32_t)narrow);
-  hipLaunchKernelGGL(mq_part_scatter_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, kt, n_rows, desc, n,
-                     nblocks, hot, hist, seg, list, bins, (uint32_t)skip_unkeyed, live, cls);
+  hipLaunchKernelGGL(mq_part_count_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, kt, n_rows, desc, n, votes,
+                     max(nv, used), hot, bins, (uint32_t)skip_unkeyed, live, cmax, counts + kMetaCtot,
+                     counts + kMetaDone, cap, counts, seg, cls, reg, (uint32_t)narrow);
+  hipLaunchKernelGGL(mq_part_scatter_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, kt, n_rows, desc, n, hot,
+                     counts + kMetaCcur, seg, list, bins, (uint32_t)skip_unkeyed, live, cls);
   return hipGetLastError();
 }
 
@@ -624,9 +635,10 @@ const uint32_t* mq_partition_regions(const uint32_t* counts) { return counts + k
 
 size_t mq_partition_workspace(uint32_t n) {
   const size_t nblocks = (n + kPartBlock - 1) / kPartBlock;
+  // keyed words (keyed_ws): at most 34 per row plus padding, rows <= key_bins(n) / 16
   return part_align(sizeof(uint32_t) * 2 * (size_t)mq_partition_list_cap(n)) +
          part_align(sizeof(uint32_t) * kClasses * nblocks) + part_align(sizeof(uint32_t) * kMetaWords) +
-         part_align(sizeof(uint32_t) * (key_bins(n) + key_bins(n) / 8));  // keyed bins + rowseg
+         part_align(sizeof(uint32_t) * (key_bins(n) / 16 * 34 + 8));
 }
 
 // offsets of the pieces inside the partition workspace

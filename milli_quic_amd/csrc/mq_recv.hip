@@ -786,8 +786,10 @@ extern "C" __global__ __launch_bounds__(kWalkThreads) void mq_recv_verify_kernel
   const bool differs = MQ_RECV_WALK_ARGS(kVerifyMode, x);
   uint32_t redo = 0;
   if (q == 0) {
+    // the verdict is in before the count that releases it: the wave waits until its atomic is
+    // performed (no __threadfence, which on gfx950 also writes back the XCD's L2)
     if (differs) atomicOr(&vstate[2 * x.ci], 1u);
-    __threadfence();  // the verdict is visible before the count that releases it
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (atomicAdd(&vstate[2 * x.ci + 1], 1u) + 1 == later_segs(x.run_lo, x.run_hi, seg)) {
       redo = atomicExch(&vstate[2 * x.ci], 0u);
       vstate[2 * x.ci + 1] = 0;

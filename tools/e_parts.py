@@ -1,5 +1,5 @@
 """Config-E cost split (diagnostic): seal / open medians of the whole mixed batch and of its parts
-run on their own — the ChaCha20 packets, the hot 1-RTT AES key's packets, the Initial packets on
+run on their own (E_NOCHECK=1: no status check, for MQ_LIB phase-cost variants) — the ChaCha20 packets, the hot 1-RTT AES key's packets, the Initial packets on
 their 4096 per-connection keys, and the Initial packets moved onto the hot row (what the
 per-connection keys cost). Every part goes through the same call the batch makes (mixed hint, the
 device partition). MQ_* environment switches apply to every line (e.g. MQ_FORK=0).
@@ -35,7 +35,7 @@ def timeit(torch, batch, kt, w, sd_np, od_np, hint, reps=8):
             e1.record()
             torch.cuda.synchronize()
             bad = int((st != 0).sum())
-            if bad:
+            if bad and not os.environ.get("E_NOCHECK"):  # phase-cost variants (MQ_LIB) compute garbage
                 raise SystemExit(f"{which}: {bad} packets failed")
             if rep >= 2:
                 res[which].append(e0.elapsed_time(e1))
