@@ -131,6 +131,25 @@ __device__ __forceinline__ void patch_header(uint32_t (&m)[4], uint32_t at, uint
   }
 }
 
+// Seal: the original values of the header bytes that header protection masks — byte 0 (bits 0-7
+// of hv, present: bit 8) and PN byte q (byte q of pn, present: bit 9 + q) — from the AAD block at
+// packet offset `at` that this lane absorbs,
+// so that the masked bytes are stored at the end without reading the header back from HBM (r05:
+// that dependent read-modify-write cost the C seal 3-6 %, E's 4.6 %, profiles/r05n_phase_aes_hdr.txt)
+__device__ __forceinline__ void save_header(const uint32_t (&m)[4], uint32_t at, uint32_t pn_off, uint32_t pn_len,
+                                            uint32_t& hv, uint32_t& pn) {
+  if (at == 0) hv |= (m[0] & 0xffu) | 0x100u;
+#pragma unroll
+  for (uint32_t q = 0; q < 4; ++q) {
+    const uint32_t x = pn_off + q - at;  // the PN byte's offset in this block (wraps when before it)
+    if (q < pn_len && x < 16u) {
+      const uint32_t w = x < 4 ? m[0] : x < 8 ? m[1] : x < 12 ? m[2] : m[3];
+      pn |= ((w >> (8 * (x & 3))) & 0xffu) << (8 * q);
+      hv |= 0x200u << q;
+    }
+  }
+}
+
 // How a streaming tile multiplies by H^8: the workgroup's full table (single-key kernels), the
 // wave's half table (multi-key kernels, key-uniform tile) or the bit-holed product (mixed keys)
 enum GhMode { kGhWorkgroup, kGhWave, kGhProduct };
@@ -281,6 +300,8 @@ struct AesStream {
     const uint32_t dl = 0;
 #endif
     uint32_t dct[4] = {0, 0, 0, 0}, dn = 0, doff = 0;  // this lane's deferred bytes (one block at most)
+    uint32_t hs_v = 0, hs_pn = 0;                      // this lane's header bytes to mask (save_header)
+    MQ_STAMP(c.tile, 1);
 #pragma nounroll
     for (int it = it_lo; it < it_hi; ++it) {
       const int b = j + kLanesPerPkt * it;
@@ -338,6 +359,7 @@ struct AesStream {
         uint32_t m[4];
         u4w(cur, m);
         if (k.rec) { m[0] = 23u | 3u << 8 | 3u << 16 | (rlen >> 8 & 0xffu) << 24; m[1] = rlen & 0xffu; }
+        if (k.hp) save_header(m, 16u * (uint32_t)((int)k.A + b - 1), d.pn_offset, d.pn_len, hs_v, hs_pn);
         gh_block(m, k.aad_len - 16u * (uint32_t)((int)k.A + b - 1), x);
         has = true;
       } else if (k.act && ub == k.nblk) {  // length block
@@ -358,10 +380,13 @@ struct AesStream {
       }
       gh_step(acc, m8, has, b + kLanesPerPkt > (int)k.nblk && !fin8, x);
       cur = nxt;
+      if (it == 0) MQ_STAMP(c.tile, 2);
     }
+    MQ_STAMP(c.tile, 3);
     uint32_t tag[4];
     finish(acc, row, j, k, ej0, tag);
     if (k.act && j == 0) st16(arena + k.pay + k.P, tag);
+    MQ_STAMP(c.tile, 4);
     if (dn) st_range(arena + k.pay + doff, dct, 0, dn);  // the first line's deferred bytes
     // packets of fewer than 7 CTR blocks (no free slot for the HP block; a sample that may reach
     // into the tag): one more AES block for the wave once ciphertext and tag are stored — length-
@@ -378,12 +403,21 @@ struct AesStream {
       aes128_enc(RkLds{kl + 44}, L, s);
       if (late && j == 0) { m0 = bswap32(s[0]); m1 = s[1] >> 24; have_mask = true; }
     }
-    if (have_mask) {  // after the MAC read the unprotected header (RFC 9001 §5.4.1)
+    // the masked header (RFC 9001 §5.4.1; the MAC read it unprotected): the mask from its one lane
+    // to the octet, then each lane stores the header bytes it saved from its AAD blocks
+    const uint32_t mk0 = oct_xor(have_mask ? m0 : 0u), mk1 = oct_xor(have_mask ? m1 : 0u);
+#if MQ_PROF_SKIP & 128  // phase-cost diagnostic build only: no header mask writes
+    hs_v = 0;
+#endif
+    if (hs_v) {
       uint8_t* h = arena + k.pkt;
-      h[0] ^= (uint8_t)m0 & ((d.flags & MQ_PKT_LONG_HEADER) ? 0x0f : 0x1f);
-      const uint32_t mk = (m0 >> 8) | (m1 << 24);
-      for (uint32_t q = 0; q < d.pn_len; ++q) h[d.pn_offset + q] ^= (uint8_t)(mk >> (8 * q));
+      if (hs_v & 0x100u) h[0] = (uint8_t)(hs_v ^ (mk0 & ((d.flags & MQ_PKT_LONG_HEADER) ? 0x0fu : 0x1fu)));
+      const uint32_t mk = (mk0 >> 8) | (mk1 << 24);
+#pragma unroll
+      for (uint32_t q = 0; q < 4; ++q)
+        if (hs_v & (0x200u << q)) h[d.pn_offset + q] = (uint8_t)((hs_pn ^ mk) >> (8 * q));
     }
+    MQ_STAMP(c.tile, 5);
   }
 
   // receive composite (recv.rs:340-421 / 953-1025): HP removal, decode_pn, open. Plaintext is
@@ -440,6 +474,7 @@ struct AesStream {
     uint4 cur = data(j + kLanesPerPkt * it_lo);
     const int it_lean = lean_end(k.act, k.P);
     const bool fin8 = fin_in_loop(k, j);
+    MQ_STAMP(c.tile, 1);
 #pragma nounroll
     for (int it = it_lo; it < it_hi; ++it) {
       const int b = j + kLanesPerPkt * it;
@@ -485,9 +520,12 @@ struct AesStream {
       }
       gh_step(acc, m8, has, b + kLanesPerPkt > (int)k.nblk && !fin8, x);
       cur = nxt;
+      if (it == 0) MQ_STAMP(c.tile, 2);
     }
+    MQ_STAMP(c.tile, 3);
     uint32_t tag[4];
     finish(acc, row, j, k, ej0, tag);
+    MQ_STAMP(c.tile, 4);
     const bool bad = k.act && ((tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) | (tag[3] ^ got[3])) != 0;
     if (bad) {  // Error::Crypto (rustcrypto.rs:60-94)
       c.st = MQ_ERR_CRYPTO;

@@ -59,7 +59,7 @@ def main():
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
     libs = [("product", os.path.join(ROOT, "milli_quic_amd", "libmq_aead.so"))]
     names = {1: "no chacha rounds", 2: "no MAC", 4: "no store", 8: "no staging", 16: "no AES rounds",
-             12: "no store+staging", 32: "all direct", 64: "no AES final mul", 128: "ks stride 68"}
+             12: "no store+staging", 32: "all direct", 64: "no AES final mul", 128: "ks stride 68 (ChaCha) / no AES header mask"}
     for m, nm in names.items():
         p = os.path.join(BUILD, f"prof_{m}.so")
         if os.path.exists(p):

@@ -3,7 +3,7 @@
 Each tile's lane 0 records s_memtime (shader clock) at: 0 start, 1 staged (table ready), 2 DMA
 landed, 3/4/5 policy phases, 6 policy done, 7 stored. Reports the median / mean cycles of each
 phase for seal and open, plus tiles resident per CU. Diagnostic only: never quote its times.
-Usage: python tools/stamps.py [b|c|e] [packets]
+Usage: python tools/stamps.py [b|c|e|a<L>|ak<L>] [packets]   (a<L>: AES n x L B, ak<L>: with 1024 keys)
 """
 import ctypes
 import os
@@ -22,8 +22,8 @@ from milli_quic_amd.batch import KeyTable  # noqa: E402
 
 NAMES = {"seal": ["setup", "dma+blk0", "chacha", "poly+tag", "hp", "-", "store"],
          "open": ["setup", "dma", "hp+unmask", "blk0+poly+verify", "xor", "-", "store"]}
-AES_NAMES = {"seal": ["setup", "dma+ctr0", "ctr", "ghash+tag", "hp", "-", "store"],
-             "open": ["setup", "dma", "hp+unmask", "ghash", "ej0+blk0+verify", "ctr", "store"]}
+AES_NAMES = {"seal": ["setup", "iteration 0", "iterations 1+", "finish+tag", "late hp+mask", "-", "status"],
+             "open": ["hp+setup", "iteration 0", "iterations 1+", "finish", "-", "-", "verify+restore+status"]}
 
 
 def main():
@@ -32,8 +32,12 @@ def main():
     lib = _lib.load()
     lib.mq_debug_set_stamps.argtypes = [ctypes.c_void_p]
     assert lib.mq_device_init(0) == 0
-    w = {"b": workload.config_b, "c": workload.config_c, "e": workload.config_e}[cfg](n)
-    names = AES_NAMES if cfg == "c" else NAMES
+    if cfg.startswith("a"):  # a<L>: AES-128-GCM, n x L bytes, one key; ak<L>: 1024 keys
+        kk = 1024 if cfg.startswith("ak") else 1
+        w = workload.uniform(n, _lib.MQ_SUITE_AES128GCM, L=int(cfg.lstrip("ak")), n_keys=kk)
+    else:
+        w = {"b": workload.config_b, "c": workload.config_c, "e": workload.config_e}[cfg](n)
+    names = AES_NAMES if cfg[0] in "ca" else NAMES
     dev = torch.device("cuda", 0)
     kt = KeyTable(w.keys)
     arena = torch.from_numpy(w.arena).to(dev)
