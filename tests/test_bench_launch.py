@@ -100,9 +100,9 @@ def test_roofline_seal_composite_traffic():
     assert bench.seal_kernels("b", 1) == ("mq_chacha_seal1_kernel",)  # HP inside the tile (r03)
     assert bench.seal_kernels("b", 1024) == ("mq_chacha_seal_kernel",)
     assert bench.seal_kernels("c", 1) == ("mq_aes_seal1_kernel",)
-    assert bench.seal_kernels("e", 4098) == bench.PARTITION + bench.AES_LIST0 + ("mq_chacha_seal_kernel",)
+    assert bench.seal_kernels("e", 4098) == bench.PARTITION + bench.AES_LIST0 + ("mq_chacha_seal_lgrid_kernel",)
     # config E's table has one non-AES row: its ChaCha20 list runs on the single-key kernel
-    assert bench.seal_kernels("e", 4098, 1 << 20, 1) == bench.PARTITION + bench.AES_LIST0 + ("mq_chacha_seal1_kernel",)
+    assert bench.seal_kernels("e", 4098, 1 << 20, 1) == bench.PARTITION + bench.AES_LIST0 + ("mq_chacha_seal_lgrid1_kernel",)
     # 1024 keys over 2^20 packets (>= 512 per row): the key-segmented kernel runs list 0 (r03);
     # 4096 keys: the hot split and the multi-key kernel
     assert bench.seal_kernels("c", 1024) == bench.PARTITION + ("mq_aes_seals_kernel", "mq_aes_seal_kernel")
