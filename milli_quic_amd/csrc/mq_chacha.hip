@@ -211,10 +211,11 @@ struct CcPool {
   const KeyRow* kt;
 };
 
-// IMG: bytes of LDS per wave (kLdsBytes; the long-packet kernels' larger images, chacha_tile)
-template <bool SINGLE, uint32_t IMG = kLdsBytes>
+// IMG: bytes of LDS per wave (kLdsBytes; the long-packet kernels' larger images, chacha_tile);
+// W: waves of the workgroup sharing the pool
+template <bool SINGLE, uint32_t IMG = kLdsBytes, uint32_t W = kCcWaves>
 __device__ __forceinline__ void cc_pool_run(const CcPool& pool, uint32_t tid = threadIdx.x) {
-  constexpr uint32_t kQ = kPktsPerTile * kCcWaves;  // packets of the workgroup
+  constexpr uint32_t kQ = kPktsPerTile * W;  // packets of the workgroup
   static_assert(kQ <= kWave, "one packet per lane in the pool scan");
   const int lane = tid & (kWave - 1);
   const uint32_t w = tid >> 6;
@@ -226,7 +227,7 @@ __device__ __forceinline__ void cc_pool_run(const CcPool& pool, uint32_t tid = t
   const uint32_t incl = wave_incl_scan(nq), excl = incl - nq;
   const uint32_t T = lane_u32(incl, kWave - 1);
   const LdsSpace sp{pool.wg};
-  for (uint32_t e0 = kWave * w; e0 < T; e0 += kWave * kCcWaves) {  // wave-uniform
+  for (uint32_t e0 = kWave * w; e0 < T; e0 += kWave * W) {  // wave-uniform
     const uint32_t e = e0 + (uint32_t)lane;
     uint32_t q = 0;  // the packet of entry e: the last q with excl[q] <= e
 #pragma unroll
@@ -321,7 +322,7 @@ struct ChaChaPolicy {
   // iteration ctr / 8 (ctr 0 = the Poly1305 key); with the pool, blocks >= 16 and the
   // header-protection block (its sample is ciphertext of block 1) run in the workgroup's pool
   // before the MACs, and the mask is applied once the MAC has read the unprotected header.
-  template <bool SINGLE, class S, class G, uint32_t IMG = kLdsBytes>
+  template <bool SINGLE, class S, class G, uint32_t IMG = kLdsBytes, uint32_t W = kCcWaves>
   static __device__ __forceinline__ void seal(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j,
                                               G& stg, const CcPool& pool) {
     const mq_pkt_desc& d = c.d;
@@ -379,7 +380,7 @@ struct ChaChaPolicy {
       }
     }
     __syncthreads();  // every wave's records
-    cc_pool_run<SINGLE, IMG>(pool);
+    cc_pool_run<SINGLE, IMG, W>(pool);
     __syncthreads();  // every pooled block (and mask) is in place before any MAC reads it
     MQ_STAMP(c.tile, 3);
     uint32_t tag[4];
@@ -407,7 +408,7 @@ struct ChaChaPolicy {
   }
 
   // receive composite (recv.rs:340-421 / 953-1025): HP removal, decode_pn, open.
-  template <bool SINGLE, class S, class G, uint32_t IMG = kLdsBytes>
+  template <bool SINGLE, class S, class G, uint32_t IMG = kLdsBytes, uint32_t W = kCcWaves>
   static __device__ __forceinline__ void open(const S& sp, typename S::off_t pkt, PktCtx& c, const KeyRow* row, int j,
                               bool direct, G& stg, const CcPool& pool) {
     const mq_pkt_desc& d = c.d;
@@ -484,7 +485,7 @@ struct ChaChaPolicy {
       }
     }
     __syncthreads();  // every wave's MAC has read its ciphertext
-    cc_pool_run<SINGLE, IMG>(pool);
+    cc_pool_run<SINGLE, IMG, W>(pool);
     __syncthreads();
     MQ_STAMP(c.tile, 5);
     if (direct && hdr_written && !c.act) {  // direct path writes HBM in place: undo the unmask
@@ -1004,14 +1005,13 @@ __device__ __forceinline__ void chacha_narrow_list(uint8_t* wsm, uint32_t u, con
 // LIST: a partition list with narrow regions (reg): the octet tiles are the G = 8 region's (count =
 // its entries), a workgroup with an octet tile runs the pool's barriers on every wave (its narrow
 // waves run their tile first), one without any runs its narrow tiles with no barrier.
-template <bool OPEN, bool SINGLE, bool LIST = false, uint32_t IMG = kLdsBytes>
+template <bool OPEN, bool SINGLE, bool LIST = false, uint32_t IMG = kLdsBytes, uint32_t W = kCcWaves>
 __device__ __forceinline__ void chacha_tile(uint32_t tb, uint32_t tid, const KeyRow* __restrict__ kt, uint32_t n_rows,
                                             uint8_t* __restrict__ arena, uint64_t arena_len,
                                             const mq_pkt_desc* __restrict__ desc, uint32_t n,
                                             const uint32_t* __restrict__ index, const uint32_t* __restrict__ n_dev,
                                             uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out,
                                             const uint2* __restrict__ hpm, const uint32_t* __restrict__ reg = nullptr) {
-  constexpr uint32_t W = kCcWaves;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t w = tid >> 6;
   uint8_t* wsm = smem + w * IMG;
@@ -1041,7 +1041,7 @@ __device__ __forceinline__ void chacha_tile(uint32_t tb, uint32_t tid, const Key
     }
     if (j == 0) pool.rec[0] = 0;
     __syncthreads();
-    cc_pool_run<SINGLE, IMG>(pool, tid);
+    cc_pool_run<SINGLE, IMG, W>(pool, tid);
     __syncthreads();
     return;
   }
@@ -1055,15 +1055,24 @@ __device__ __forceinline__ void chacha_tile(uint32_t tb, uint32_t tid, const Key
   const uint32_t nch = (uint32_t)(nch64 < 0xFFFFu ? nch64 : 0xFFFFu);
   const uint32_t incl = oct_incl_scan(nch);
   const uint32_t total = lane_u32(incl, kWave - 1);
+  // Packets of one even image size (lengths a multiple of 32 B at one alignment: 1600, 2048 B...)
+  // start their images an even number of chunks apart, so the same keystream dword of every packet
+  // sits on one LDS bank: 8-way conflicts in the XOR passes at 2048 B. A 16-B gap after each image
+  // staggers them when the budget has room (r05; odd sizes such as config B's 75 chunks get none).
+#ifndef MQ_CC_NOPAD  // diagnostic A/B build only: no gaps
+  const uint32_t pad = (lane_u32(nch, 0) & 1u) == 0 && (total + kPktsPerTile) * 16u <= kBudget ? 1u : 0u;
+#else
+  const uint32_t pad = 0;
+#endif
   if (total * 16u <= kBudget) {
-    pl.slot = incl - nch;
+    pl.slot = incl - nch + (uint32_t)p * pad;
     pool.on = true;
     DmaStager stg{wsm, arena, arena_len, lane, j, pl};
     LdsSpace sp{wsm};
     MQ_STAMP(tile_id, 1);
     const uint32_t pkt = pl.slot * 16u + pl.head();
-    if (OPEN) ChaChaPolicy::template open<SINGLE, LdsSpace, DmaStager, IMG>(sp, pkt, c, row, j, false, stg, pool);
-    else ChaChaPolicy::template seal<SINGLE, LdsSpace, DmaStager, IMG>(sp, pkt, c, row, j, stg, pool);
+    if (OPEN) ChaChaPolicy::template open<SINGLE, LdsSpace, DmaStager, IMG, W>(sp, pkt, c, row, j, false, stg, pool);
+    else ChaChaPolicy::template seal<SINGLE, LdsSpace, DmaStager, IMG, W>(sp, pkt, c, row, j, stg, pool);
     MQ_STAMP(tile_id, 6);
     wave_sync();
     stage_out(wsm, arena, lane, c.act, pl);
@@ -1071,8 +1080,8 @@ __device__ __forceinline__ void chacha_tile(uint32_t tb, uint32_t tid, const Key
   } else {
     GlobalSpace sp{arena, arena_len};
     NoStager stg;
-    if (OPEN) ChaChaPolicy::template open<SINGLE, GlobalSpace, NoStager, IMG>(sp, off, c, row, j, true, stg, pool);
-    else ChaChaPolicy::template seal<SINGLE, GlobalSpace, NoStager, IMG>(sp, off, c, row, j, stg, pool);
+    if (OPEN) ChaChaPolicy::template open<SINGLE, GlobalSpace, NoStager, IMG, W>(sp, off, c, row, j, true, stg, pool);
+    else ChaChaPolicy::template seal<SINGLE, GlobalSpace, NoStager, IMG, W>(sp, off, c, row, j, stg, pool);
   }
   tile_status<OPEN>(c, j, status, pn_out);
 }
@@ -1097,29 +1106,31 @@ MQ_CHACHA_KERNELS(mq_chacha_seal1_kernel, mq_chacha_open1_kernel, true)
 
 // Flat batches of long packets (r05): the same octet tiles and keystream pool with
 // larger LDS images, so eight packets over ~1216 B stay staged instead of running on HBM (direct:
-// 358-409 GiB/s at 1232-2048 B, against 1034 at 1200): 13 KiB per wave (12 waves per CU: eight
-// images of up to 100 chunks, packets up to ~1585 B at any alignment) or 20 KiB (8 waves per CU: up
-// to 156 chunks, ~2480 B). The waves-per-EU hint gives them the registers of that occupancy.
+// 358-409 GiB/s at 1232-2048 B, against 1034 at 1200): 13 KiB per wave (4-wave workgroups, 12
+// waves per CU: eight images of up to 100 chunks, packets up to ~1570 B at any alignment) or 20 KiB
+// (8 waves per CU: 156 chunks, ~2480 B). The waves-per-EU hint gives them the registers of that
+// occupancy. (Measured and dropped: 16 KiB in 2-wave workgroups, 10 waves per CU — the pool shared
+// by two waves lost more than the occupancy gained: 1800 B 833 vs 945 GiB/s, gpurun_out/r05p.)
 constexpr uint32_t kLongImg = 13312, kLongerImg = 20480;
 static_assert(kCcWaves * kLongImg * 3 <= kCuLdsBytes && kCcWaves * kLongerImg * 2 <= kCuLdsBytes, "long images per CU");
-#define MQ_CHACHA_LONG_KERNELS(NAME_SEAL, NAME_OPEN, SINGLE, IMG, WPE)                                      \
-  extern "C" __global__ __launch_bounds__(64 * kCcWaves) __attribute__((amdgpu_waves_per_eu(WPE))) void NAME_SEAL( \
+#define MQ_CHACHA_LONG_KERNELS(NAME_SEAL, NAME_OPEN, SINGLE, IMG, WPE, W)                                   \
+  extern "C" __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE))) void NAME_SEAL( \
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, uint8_t* __restrict__ status) {                   \
-    chacha_tile<false, SINGLE, false, IMG>(blockIdx.x, threadIdx.x, kt, n_rows, arena, arena_len, desc, n, nullptr, \
-                                           nullptr, status, nullptr, nullptr);                            \
+    chacha_tile<false, SINGLE, false, IMG, W>(blockIdx.x, threadIdx.x, kt, n_rows, arena, arena_len, desc, n, nullptr, \
+                                              nullptr, status, nullptr, nullptr);                         \
   }                                                                                                       \
-  extern "C" __global__ __launch_bounds__(64 * kCcWaves) __attribute__((amdgpu_waves_per_eu(WPE))) void NAME_OPEN( \
+  extern "C" __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE))) void NAME_OPEN( \
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, uint8_t* __restrict__ status, uint64_t* __restrict__ pn_out, \
       const uint2* __restrict__ hpm) {                                                                    \
-    chacha_tile<true, SINGLE, false, IMG>(blockIdx.x, threadIdx.x, kt, n_rows, arena, arena_len, desc, n, nullptr, \
-                                          nullptr, status, pn_out, hpm);                                  \
+    chacha_tile<true, SINGLE, false, IMG, W>(blockIdx.x, threadIdx.x, kt, n_rows, arena, arena_len, desc, n, nullptr, \
+                                             nullptr, status, pn_out, hpm);                               \
   }
-MQ_CHACHA_LONG_KERNELS(mq_chacha_seal_long_kernel, mq_chacha_open_long_kernel, false, kLongImg, 3)
-MQ_CHACHA_LONG_KERNELS(mq_chacha_seal_long1_kernel, mq_chacha_open_long1_kernel, true, kLongImg, 3)
-MQ_CHACHA_LONG_KERNELS(mq_chacha_seal_longer_kernel, mq_chacha_open_longer_kernel, false, kLongerImg, 2)
-MQ_CHACHA_LONG_KERNELS(mq_chacha_seal_longer1_kernel, mq_chacha_open_longer1_kernel, true, kLongerImg, 2)
+MQ_CHACHA_LONG_KERNELS(mq_chacha_seal_long_kernel, mq_chacha_open_long_kernel, false, kLongImg, 3, kCcWaves)
+MQ_CHACHA_LONG_KERNELS(mq_chacha_seal_long1_kernel, mq_chacha_open_long1_kernel, true, kLongImg, 3, kCcWaves)
+MQ_CHACHA_LONG_KERNELS(mq_chacha_seal_longer_kernel, mq_chacha_open_longer_kernel, false, kLongerImg, 2, kCcWaves)
+MQ_CHACHA_LONG_KERNELS(mq_chacha_seal_longer1_kernel, mq_chacha_open_longer1_kernel, true, kLongerImg, 2, kCcWaves)
 
 // One-shot grids over a partition list with narrow regions (reg, mq_partition.hip): tile
 // tb * W + w is an octet tile of the G = 8 region or a narrow tile after it
@@ -1556,9 +1567,9 @@ hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_
     int img = arena_len > kLongAvg1 * (uint64_t)n ? 2 : arena_len > kLongAvg0 * (uint64_t)n ? 1 : 0;
     const char* le = std::getenv("MQ_CC_LONG");
     if (le) img = le[0] == '2' ? 2 : le[0] == '1' ? 1 : 0;
+    const bool o1 = n_rows == 1;
     if (img) {
       const uint32_t lds = (img == 2 ? kLongerImg : kLongImg) * kCcWaves;
-      const bool o1 = n_rows == 1;
       if (open)
         hipLaunchKernelGGL(img == 2 ? (o1 ? mq_chacha_open_longer1_kernel : mq_chacha_open_longer_kernel)
                                     : (o1 ? mq_chacha_open_long1_kernel : mq_chacha_open_long_kernel),

@@ -235,7 +235,7 @@ class _EnvLong(_Env):
             os.environ["MQ_CC_LONG"] = self.old
 
 
-@pytest.mark.parametrize("lmin,lmax,n", [(1150, 1600, 3000), (1500, 2600, 2000), (21, 2600, 2500)])
+@pytest.mark.parametrize("lmin,lmax,n", [(1150, 1600, 3000), (1600, 1950, 3001), (1500, 2600, 2000), (21, 2600, 2500)])
 @pytest.mark.parametrize("mode", [None, "0", "1", "2"])
 def test_long_images_vs_oracle(orc, lmin, lmax, n, mode):
     # flat ChaCha20 batches of long packets (r05): the 13-KiB (12 waves per CU) and 20-KiB (8 per CU)
@@ -244,5 +244,14 @@ def test_long_images_vs_oracle(orc, lmin, lmax, n, mode):
     keys, arena, sd, od, pns = short_batch(n, lmin, lmax, 2, seed=lmax + n)
     od = od.copy()
     od["flags"] |= _lib.MQ_PKT_NO_RECV_LIMIT
+    with _EnvLong(mode):
+        roundtrip_vs_oracle(orc, keys, arena, sd, od, pns, modes=(None,))
+
+
+@pytest.mark.parametrize("mode", [None, "1", "2"])
+def test_long_images_single_key_vs_oracle(orc, mode):
+    # the single-key (key material in SGPRs) long-image kernels, 1600-1950-B packets, a partial
+    # last workgroup
+    keys, arena, sd, od, pns = short_batch(4093, 1600, 1950, 1, seed=77)
     with _EnvLong(mode):
         roundtrip_vs_oracle(orc, keys, arena, sd, od, pns, modes=(None,))
