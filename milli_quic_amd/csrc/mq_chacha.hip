@@ -525,6 +525,7 @@ struct NarrowStager {
   uint32_t slot;   // this lane's packet: first chunk (group-uniform)
   uint64_t base;   // its image start in the arena (16-B aligned)
   int lane;
+  uint32_t nch;    // its image chunks (a gap may follow them: narrow_tile)
   uint32_t tail_c = 0xFFFFFFFFu;  // a chunk that would read past the arena end: guarded load
   uint64_t tail_src = 0;
 
@@ -550,7 +551,8 @@ struct NarrowStager {
       const uint64_t bq = (uint64_t)(uint32_t)__shfl((int)(uint32_t)(base >> 32), G * (int)q, kWave) << 32 |
                           (uint32_t)__shfl((int)(uint32_t)base, G * (int)q, kWave);
       const uint64_t src = bq + 16ull * (c - sq);
-      if (c < total) {
+      const uint32_t nq = (uint32_t)__shfl((int)nch, G * (int)q, kWave);
+      if (c < total && c - sq < nq) {  // not a gap chunk
         if (src + 16 <= arena_len)
           __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(arena + src),
                                            (__attribute__((address_space(3))) void*)(smem + 16u * k), 16, 0, 0);
@@ -937,12 +939,20 @@ __device__ __forceinline__ void narrow_tile(uint8_t* wsm, const KeyRow* __restri
   pl.len = c.act ? c.d.len : 0u;
   const uint64_t nch64 = c.act ? ((pl.off & 15) + (uint64_t)c.d.len + 15) >> 4 : 0u;
   const uint32_t nch = (uint32_t)(nch64 < 0xFFFFu ? nch64 : 0xFFFFu);
-  const uint32_t incl = wave_incl_scan(j == 0 ? nch : 0u);  // the groups' inclusive prefix
+  // equal even image sizes (e.g. 256-B packets: 16 chunks) would put every packet's blocks on the
+  // same LDS banks: a one-chunk gap after each image when packet 0's size is even and the budget
+  // has room (as chacha_tile)
+#ifndef MQ_CC_NOPAD  // diagnostic A/B build only: no gaps
+  const uint32_t t0 = lane_u32(wave_incl_scan(j == 0 ? nch : 0u), kWave - 1);
+  const uint32_t pad = (lane_u32(nch, 0) & 1u) == 0 && t0 + (uint32_t)Q <= kNarrowChunks ? 1u : 0u;
+#else
+  const uint32_t pad = 0;
+#endif
+  const uint32_t incl = pad ? wave_incl_scan(j == 0 ? nch + 1u : 0u) : wave_incl_scan(j == 0 ? nch : 0u);
   const uint32_t total = lane_u32(incl, kWave - 1);
-  (void)Q;
   if (total <= kNarrowChunks) {
-    pl.slot = incl - nch;
-    NarrowStager<G> stg{wsm, arena, arena_len, total, pl.slot, pl.base(), lane};
+    pl.slot = incl - nch - pad;
+    NarrowStager<G> stg{wsm, arena, arena_len, total, pl.slot, pl.base(), lane, nch};
     LdsSpace sp{wsm};
     const uint32_t pkt = pl.slot * 16u + pl.head();
     if (OPEN) NarrowPolicy<G, SINGLE>::template open<LdsSpace>(sp, pkt, c, row, j, false, stg);
