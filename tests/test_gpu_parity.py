@@ -284,6 +284,32 @@ def test_mixed_batch_vs_oracle(orc, n, lmin, lmax):
         assert g_back.tobytes() == o_back.tobytes()
 
 
+@pytest.mark.parametrize("n,lmin,lmax", [(6000, 21, 450), (5000, 21, 1500)])
+def test_mixed_short_tampered_vs_oracle(orc, n, lmin, lmax):
+    # VERDICT r04 #1's cases: short packets of both suites (21-450 B: ChaCha20 narrow regions, AES
+    # short classes; long Initial headers and short 1-RTT ones), alone and mixed with long ones,
+    # sealed, then ~10 % tampered (one byte anywhere: header, payload, tag) and opened — statuses,
+    # PNs and every byte (failed packets restored) against the oracle
+    w = workload.config_e(n, seed=0x5150 + lmax, lmin=lmin, lmax=lmax)
+    g_out, g_st, _ = gpu_run(w.keys, w.arena, w.seal_desc, w.suite_hint)
+    o_out, o_st, _ = oracle_run(orc, w.keys, w.arena, w.seal_desc, w.suite_hint)
+    assert (o_st == 0).all() and (g_st == o_st).all() and g_out.tobytes() == o_out.tobytes()
+    rng = np.random.default_rng(lmax)
+    bad = o_out.copy()
+    for v in rng.choice(w.n, size=w.n // 10, replace=False):
+        o, L = int(w.seal_desc["offset"][v]), int(w.seal_desc["len"][v])
+        bad[o + int(rng.integers(0, L))] ^= 1 << int(rng.integers(0, 8))
+    od = w.open_desc.copy()
+    od["flags"] |= _lib.MQ_PKT_NO_RECV_LIMIT
+    g_back, g_st, g_pn = gpu_run(w.keys, bad, od, w.suite_hint, open_=True)
+    o_back, o_st, o_pn = oracle_run(orc, w.keys, bad, od, w.suite_hint, open_=True)
+    assert (o_st != 0).sum() >= w.n // 20
+    assert (g_st == o_st).all()
+    ok = o_st == 0
+    assert (g_pn[ok] == o_pn[ok]).all()
+    assert g_back.tobytes() == o_back.tobytes()
+
+
 @pytest.mark.parametrize("suite,mixed", [(1, False), (2, False), (1, True), (2, True)])
 def test_failures_match_oracle(orc, suite, mixed):
     # mixed: the same failures through MQ_SUITE_MIXED (partition; invalid key ids land in the
