@@ -12,7 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # MQ_ASAN=1 (tools/asan_cpu_tests.sh, CPU only): the build whose host code carries AddressSanitizer +
 # UBSan (`make -C milli_quic_amd/csrc asan`); the kernels are the same
 LIB_PATH = os.path.join(_HERE, "asan" if os.environ.get("MQ_ASAN") == "1" else "", "libmq_aead.so")
-# diagnostic A/B of library builds (tools/ab_libs/*.so, tools/gpu_r04*.sh); never set by the product
+# diagnostic A/B of library builds (tools/ab_libs/*.so, tools/runs/gpu_r0*.sh); never set by the product
 if os.environ.get("MQ_LIB"):
     LIB_PATH = os.environ["MQ_LIB"]
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "mq_aead.h")
