@@ -184,7 +184,11 @@ struct AesStream {
     return;
 #endif
     uint32_t t[4] = {acc[0], acc[1], acc[2], acc[3]};
+#if MQ_AES_NIBBLE
+    if (GH == kGhWorkgroup) gh_mul_half(t, (const uint8_t*)g_aes_gh8);
+#else
     if (GH == kGhWorkgroup) gh_mul_tab8(t);
+#endif
     else if (GH == kGhWave) gh_mul_half(t, (const uint8_t*)g_aes_wtab + kGhHalfBytes * wave_id());
     else gf_mul(t, m8);
 #pragma unroll
@@ -604,7 +608,12 @@ __device__ __forceinline__ void aes_key_tables(const KeyRow* __restrict__ kt) {
     uint32_t h8[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) h8[q] = brev(kt[0].H[7][q]);
+#if MQ_AES_NIBBLE  // diagnostic A/B build only: the Horner multiply by H^8 through a nibble half table
+    if (w == 7) build_gh_half((uint8_t*)g_aes_gh8, h8, (int)(threadIdx.x & (kWave - 1)));
+    __syncthreads();
+#else
     build_gh8(h8, threadIdx.x, blockDim.x);  // ends with a barrier
+#endif
 }
 
 template <bool SINGLE>
