@@ -667,18 +667,38 @@ struct Resident {
   std::mutex mu;
 };
 
+// A device's servers (r05): kResLanes independent mailboxes, each with its own
+// resident workgroup, so up to that many threads' per-packet calls run at once instead of one at
+// a time behind one mutex. A lane's kernel holds one CU while it lives (it leaves after 2 ms
+// without a call), so a device busy with per-packet calls from T threads holds min(T, lanes) CUs.
+// MQ_RESIDENT_LANES (read once, 1..16) sets the count.
+struct ResidentSet {
+  std::vector<Resident*> lanes;
+  std::atomic<uint32_t> last{0};  // the lane of the latest completed call (mq_resident_phases)
+};
 std::mutex g_res_mu;
-std::vector<Resident*> g_res;  // per device; never freed (the kernel may outlive static destructors)
+std::vector<ResidentSet*> g_res;  // per device; never freed (the kernels may outlive static destructors)
+
+uint32_t resident_lanes() {
+  static const uint32_t k = [] {
+    const char* e = std::getenv("MQ_RESIDENT_LANES");
+    const unsigned long v = e ? std::strtoul(e, nullptr, 10) : 4ul;
+    return (uint32_t)(v < 1 ? 1 : v > 16 ? 16 : v);
+  }();
+  return k;
+}
 
 void stop_all() {  // atexit: ask every resident kernel to leave (plain stores, no HIP call)
-  for (Resident* r : g_res) {
-    if (r && r->host) __atomic_store_n(&r->host->hdr[kHwStop], (uint64_t)1, __ATOMIC_SEQ_CST);
-    if (r)
+  for (ResidentSet* set : g_res) {
+    if (!set) continue;
+    for (Resident* r : set->lanes) {
+      if (r->host) __atomic_store_n(&r->host->hdr[kHwStop], (uint64_t)1, __ATOMIC_SEQ_CST);
       for (ResArea* x : r->abandoned) __atomic_store_n(&x->hdr[kHwStop], (uint64_t)1, __ATOMIC_SEQ_CST);
+    }
   }
 }
 
-Resident* resident(int dev) {
+ResidentSet* resident_set(int dev) {
   std::lock_guard<std::mutex> lk(g_res_mu);
   if ((size_t)dev >= g_res.size()) g_res.resize((size_t)dev + 1, nullptr);
   if (!g_res[(size_t)dev]) {
@@ -687,8 +707,12 @@ Resident* resident(int dev) {
       hooked = true;
       std::atexit(stop_all);
     }
-    g_res[(size_t)dev] = new Resident();
-    g_res[(size_t)dev]->dev = dev;
+    ResidentSet* set = new ResidentSet();
+    for (uint32_t k = 0; k < resident_lanes(); ++k) {
+      set->lanes.push_back(new Resident());
+      set->lanes.back()->dev = dev;
+    }
+    g_res[(size_t)dev] = set;
   }
   return g_res[(size_t)dev];
 }
@@ -712,8 +736,27 @@ std::chrono::microseconds resident_timeout() {
 // is MQ_OK, mask = the header-protection mask words), else an MQ_ERR_* of the transport.
 int mq_resident_call(int dev, const ResReq& q, uint64_t uid, const uint8_t* aad, const uint8_t* body, uint8_t* out,
                      size_t out_off, size_t out_len, int* status, uint32_t* mask) {
-  Resident* r = resident(dev);
-  std::lock_guard<std::mutex> lk(r->mu);
+  // a free lane, trying the thread's own first (a thread keeps its lane, and with it its context's
+  // GHASH powers in the mailbox, while no other thread takes it); all busy: wait for the own lane
+  ResidentSet* set = resident_set(dev);
+  const uint32_t K = (uint32_t)set->lanes.size();
+  const uint32_t home = (uint32_t)(std::hash<std::thread::id>()(std::this_thread::get_id()) % K);
+  Resident* r = nullptr;
+  uint32_t lane = home;
+  std::unique_lock<std::mutex> lk;
+  for (uint32_t k = 0; k < K && !r; ++k) {
+    Resident* c = set->lanes[(home + k) % K];
+    std::unique_lock<std::mutex> t(c->mu, std::try_to_lock);
+    if (t.owns_lock()) {
+      r = c;
+      lane = (home + k) % K;
+      lk = std::move(t);
+    }
+  }
+  if (!r) {
+    r = set->lanes[home];
+    lk = std::unique_lock<std::mutex>(r->mu);
+  }
   if (!r->host) {
     if (hipHostMalloc((void**)&r->host, sizeof(ResArea), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
       r->host = nullptr;
@@ -824,6 +867,7 @@ int mq_resident_call(int dev, const ResReq& q, uint64_t uid, const uint8_t* aad,
   r->host_ns[0] = ns(t0 - h0);
   r->host_ns[1] = relaunched ? 0u : ns(t1 - t0);
   r->host_ns[2] = ns(t2 - t1);
+  set->last.store(lane, std::memory_order_relaxed);
   return MQ_OK;
 }
 
@@ -832,7 +876,8 @@ int mq_resident_call(int dev, const ResReq& q, uint64_t uid, const uint8_t* aad,
 // before any call.
 extern "C" int mq_resident_phases(int dev, uint32_t* ns, int n) {
   if (dev < 0 || !ns || n <= 0) return 0;
-  Resident* r = resident(dev);
+  ResidentSet* set = resident_set(dev);
+  Resident* r = set->lanes[set->last.load(std::memory_order_relaxed) % set->lanes.size()];
   std::lock_guard<std::mutex> lk(r->mu);
   if (!r->host || !r->seq) return 0;
   int m = 0;

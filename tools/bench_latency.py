@@ -35,7 +35,47 @@ def main():
         os.environ["MQ_PER_PACKET_COPY"] = "1" if mode == "copy" else "0"
         out[mode] = measure(lib, _lib, args.calls)
     os.environ.pop("MQ_RESIDENT", None)
+    out["resident_throughput"] = throughput(lib, _lib)
     print(json.dumps(out), flush=True)
+
+
+def throughput(lib, _lib, seconds=0.5):
+    """Per-packet seal calls per second from T host threads at once (resident mode): each thread its
+    own ChaCha20 context and 1200-B packet; ctypes drops the GIL during the call, so the calls meet
+    in the library (r05: one server lane per thread up to MQ_RESIDENT_LANES)."""
+    import threading
+    res = {}
+    for T in (1, 2, 4, 8):
+        counts = [0] * T
+        stop = threading.Event()
+
+        def work(t):
+            ctx = ctypes.c_void_p()
+            assert lib.mq_aead_new(_lib.MQ_SUITE_CHACHA20, bytes(range(32)), 32, ctypes.byref(ctx)) == 0
+            nonce = (ctypes.c_uint8 * 12)(*range(12))
+            aad = (ctypes.c_uint8 * 13)(*range(13))
+            buf = (ctypes.c_uint8 * 1200)()
+            ol, nd = ctypes.c_size_t(), ctypes.c_size_t()
+            while not stop.is_set():
+                assert lib.mq_aead_seal_in_place(ctx, nonce, 12, aad, 13, buf, 1200, 1171, ctypes.byref(ol),
+                                                 ctypes.byref(nd)) == 0
+                counts[t] += 1
+            lib.mq_aead_free(ctx)
+        th = [threading.Thread(target=work, args=(t,)) for t in range(T)]
+        for x in th:
+            x.start()
+        time.sleep(0.1)  # every lane's server up
+        c0 = sum(counts)
+        t0 = time.perf_counter()
+        time.sleep(seconds)
+        c1 = sum(counts)
+        t1 = time.perf_counter()
+        stop.set()
+        for x in th:
+            x.join()
+        res[f"threads_{T}"] = round((c1 - c0) / (t1 - t0))
+    res["unit"] = "seal calls per second (ChaCha20-Poly1305, 1200 B), all threads"
+    return res
 
 
 def measure(lib, _lib, calls):
