@@ -349,12 +349,12 @@ def end_to_end(torch, batch, kt, w, sd, od, dev, reps=3):
 # The seal composite of a single-suite, single-key batch is its tile kernel (the "1" variant: key
 # material in SGPRs, n_rows == 1); the tiles apply header protection themselves (ChaCha20 and AES,
 # r03), so no pass follows. seal_ms (HIP events around mq_batch_seal) spans the composite.
-# A mixed batch (config E) or a multi-key AES batch goes through the partition (three launches
-# since r05: the count kernel's last block lays the lists out),
+# A mixed batch (config E) or a multi-key AES batch goes through the partition (four launches
+# since r05: the count kernel's last block lays the classes out, the row blocks the keyed rows),
 # then list 0's AES tiles — the hot key's segment on the single-key kernel beside the multi-key
 # kernel — then list 1 (ChaCha20, or the AES hint's leftovers on the multi-key kernel again).
 # mq_host.cpp batch() makes the same launches.
-PARTITION = ("mq_part_init_kernel", "mq_part_count_kernel", "mq_part_scatter_kernel")
+PARTITION = ("mq_part_init_kernel", "mq_part_count_kernel", "mq_part_rows_kernel", "mq_part_scatter_kernel")
 AES_LIST0 = ("mq_aes_seal1_kernel", "mq_aes_seal_kernel")
 
 

@@ -42,10 +42,10 @@ hipError_t mq_launch_mixed_open_hp(const KeyRow* kt, uint32_t n_rows, const uint
 hipError_t mq_launch_aes_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t* key_ids,
                             const uint8_t* samples, uint8_t* masks, uint32_t n, hipStream_t s);
 hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_desc* desc, uint32_t n,
-                               uint32_t* list, uint32_t* hist, uint32_t* counts, hipStream_t s, bool skip_unkeyed,
+                               uint32_t* list, uint32_t* codes, uint32_t* counts, hipStream_t s, bool skip_unkeyed,
                                const uint32_t* live);
 size_t mq_partition_workspace(uint32_t n);
-void mq_partition_layout(uint32_t n, size_t* hist_off, size_t* counts_off);
+void mq_partition_layout(uint32_t n, size_t* codes_off, size_t* counts_off);
 uint32_t mq_partition_list_cap(uint32_t n);
 hipError_t mq_launch_derive_initial(const mq::MQDeriveConsts& k, const uint8_t* dcids, const uint8_t* dcid_lens,
                                     uint32_t n, KeyRow* rows, mq_key_material* km_out, uint8_t* status,
@@ -80,6 +80,7 @@ int mq_resident_call(int dev, const mq::ResReq& q, uint64_t uid, const uint8_t* 
 #ifdef MQ_STAMPS
 void mq_stamps_set_chacha(uint64_t* p);
 void mq_stamps_set_aes(uint64_t* p);
+void mq_stamps_set_part(uint64_t* p);
 #endif
 
 namespace {
@@ -920,9 +921,9 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
     const bool aes_only = suite_hint == MQ_SUITE_AES128GCM;
     uint8_t* pw = ws + ws_align(8 * (size_t)n);
     uint32_t* list = (uint32_t*)pw;
-    size_t hist_off, counts_off;
-    mq_partition_layout(n, &hist_off, &counts_off);
-    uint32_t* hist = (uint32_t*)(pw + hist_off);
+    size_t codes_off, counts_off;
+    mq_partition_layout(n, &codes_off, &counts_off);
+    uint32_t* codes = (uint32_t*)(pw + codes_off);
     uint32_t* counts = (uint32_t*)(pw + counts_off);
     // list mode: the grids cover the list capacity; the kernels read the real lengths from counts
     const uint32_t cap = mq_partition_list_cap(n);
@@ -937,7 +938,7 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
       auto hfork = hp && fork_enabled() && !(hf && hf[0] == '0') ? side_streams().fork(kt->device, s, 1)
                                                                    : mq::SideStreams<HipBackend>::Fork();
       if (hp && hfork) e = mq_launch_mixed_open_hp(kt->dev, kt->rows, arena, arena_len, desc, n, hpm, hfork.side(0));
-      if (e == hipSuccess) e = mq_launch_partition(kt->dev, kt->rows, desc, n, list, hist, counts, s, recv_pass, live);
+      if (e == hipSuccess) e = mq_launch_partition(kt->dev, kt->rows, desc, n, list, codes, counts, s, recv_pass, live);
       if (e == hipSuccess && hp && !hfork) e = mq_launch_mixed_open_hp(kt->dev, kt->rows, arena, arena_len, desc, n, hpm, s);
       if (!hfork.join() && e == hipSuccess) e = hipErrorUnknown;
     }  // the fork's entry lock is released before the AES fork below takes it
@@ -1282,6 +1283,8 @@ void mq_debug_set_stamps(uint64_t* dev) {
   mq_stamps_set_chacha(dev);
   mq_stamps_set_aes(dev);
 }
+// the partition kernels' stamps (2 x blocks x 8 uint64: count, then scatter; mq_partition.hip)
+void mq_debug_set_part_stamps(uint64_t* dev) { mq_stamps_set_part(dev); }
 #endif
 
 }  // extern "C"

@@ -24,11 +24,10 @@
 // majority key does. With no majority the vote's candidate is just some key: results are the
 // same either way, only the tile composition changes.
 //
-// Launches: fill + sliced sample vote (mq_part_init_kernel); per-block class histograms
-// (class-major) and, keyed, per-(row, class) counts (one global atomic per packet); one workgroup
-// for the exclusive scan of the histograms and, keyed, the scan of the per-row counts into bin
-// bases; scatter. (r02 start: eight operations with a full vote pass, ~126 us per mixed
-// 2^20-packet partition.)
+// Launches: fill + sliced sample vote (mq_part_init_kernel); class counts and, keyed, per-(row,
+// class) counts and ranks, with the lists' layout by the last block (mq_part_count_kernel);
+// scatter from the count kernel's per-packet codes. (r02 start: eight operations with a full vote
+// pass, ~126 us per mixed 2^20-packet partition.)
 #include "mq_tile.h"
 
 #include <cstdlib>
@@ -54,6 +53,22 @@ constexpr uint32_t kKeyClasses = 16;  // keyed layout: per row, min(len / 128, 1
 // open costs a few launches instead of four passes over the batch's descriptors (r04: ~110 us per
 // empty pass, four such passes per receive batch, profiles/r04k2_kernel_trace_recv.csv).
 __device__ __forceinline__ bool pass_empty(const uint32_t* live) { return live && *live == 0; }
+
+// Diagnostic phase stamps (-DMQ_STAMPS build only, tools/part_count_stamps.py): thread 0 of each
+// block records s_memrealtime (100 MHz, one clock for all XCDs) at phase boundaries into
+// buf[row * 8 + slot]; count kernel rows 0 .. grid-1, scatter rows grid .. 2 grid-1.
+#ifdef MQ_STAMPS
+static __device__ uint64_t* mq_part_stamp_buf;
+#define MQ_PSTAMP(row, slot)                                                        \
+  do {                                                                              \
+    __builtin_amdgcn_sched_barrier(0);                                              \
+    uint64_t _t = __builtin_amdgcn_s_memrealtime();                                 \
+    if (threadIdx.x == 0 && mq_part_stamp_buf) mq_part_stamp_buf[(size_t)(row) * 8 + (slot)] = _t; \
+    __builtin_amdgcn_sched_barrier(0);                                              \
+  } while (0)
+#else
+#define MQ_PSTAMP(row, slot) do { } while (0)
+#endif
 
 // What the partition reads of a descriptor: key row, length, and whether the row is AES-128-GCM.
 // A thread's kPartItems descriptors are fetched together (fields first, then the rows' suites),
@@ -224,19 +239,28 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_init_kernel(
   for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < bins_q; q += stride) bins[q] = make_uint4(0, 0, 0, 0);
 }
 
-// Keyed-layout words (after the meta): bins[16 R] (per (row, class) packet counts), fill[16 R] (the
-// scatter's cursors inside each bin), rowtot[R, padded to 4] (per-row packet counts), rowseg[2 R]
-// (per row: first list entry, entries including the tile padding). Init zeroes bins..rowtot.
-struct KeyedWs { uint32_t *bins, *fill, *rowtot, *rowseg; };
+// Keyed-layout words (after the meta): bins[16 R] (per (row, class) packet counts; the count
+// kernel's atomics hand each packet its rank inside its bin), rowseg[2 R] (per row: first list
+// entry, entries including the tile padding), rowrel[R] (a row's first entry relative to its row
+// block), btot[kRowBlocksMax] (row blocks' entries) and base (list 0's first keyed entry). Init
+// zeroes the bins.
+constexpr uint32_t kRowThreads = 256, kRowBlocksMax = 256;
+struct KeyedWs { uint32_t *bins, *rowseg, *rowrel, *btot; };
 __host__ __device__ __forceinline__ KeyedWs keyed_ws(uint32_t* base, uint32_t n_rows) {
   KeyedWs k;
   k.bins = base;
-  k.fill = base ? base + 16ull * n_rows : nullptr;
-  k.rowtot = base ? base + 32ull * n_rows : nullptr;
-  k.rowseg = base ? base + 32ull * n_rows + ((n_rows + 3) & ~3u) : nullptr;
+  k.rowseg = base ? base + 16ull * n_rows : nullptr;
+  k.rowrel = base ? base + 18ull * n_rows : nullptr;
+  k.btot = base ? base + 19ull * n_rows : nullptr;
   return k;
 }
-__host__ __device__ __forceinline__ size_t keyed_zero_quads(uint32_t n_rows) { return (32ull * n_rows + ((n_rows + 3) & ~3u)) / 4; }
+__host__ __device__ __forceinline__ size_t keyed_zero_quads(uint32_t n_rows) { return 4ull * n_rows; }
+// row blocks of mq_part_rows_kernel: kRowThreads threads of R consecutive rows, at most
+// kRowBlocksMax blocks
+__host__ __device__ __forceinline__ uint32_t rows_per_thread(uint32_t n_rows) {
+  const uint32_t per = kRowThreads * kRowBlocksMax;
+  return n_rows > per ? (n_rows + per - 1) / per : 1u;
+}
 
 __device__ void part_layout(uint32_t cap, uint32_t* __restrict__ counts, uint32_t* __restrict__ seg,
                             const uint32_t* __restrict__ ctot, const KeyedWs& kw, uint32_t n_rows,
@@ -247,15 +271,22 @@ __device__ void part_empty(uint32_t* __restrict__ counts, uint32_t* __restrict__
 
 // Per block: the class counts of its kPartBlock descriptors, added to the batch's class totals
 // (ctot); keyed (bins != nullptr): non-majority AES packets are counted per (row, class) bin and
-// per row instead. The block that finishes last lays the lists out (part_layout): no single-
-// workgroup scan launch (r05: the r04 scan kernel took 32-35 us for config E, 19 of them scanning
-// the 4098 rows' bins; the row totals are now counted directly).
+// per row instead, and each keyed packet's rank inside its bin comes back from the bin's atomic.
+// Every packet's code (its class, or its bin and rank) goes to code[i] for the scatter, which then
+// reads 8 B per packet instead of the descriptor and key row, and makes no keyed atomics (r05:
+// the scatter's returning per-bin atomics took ~10 us of config E's and ~22 us of C/1024's scatter,
+// tools/part_count_stamps.py). The block that finishes last lays the lists out (part_layout): no
+// single-workgroup scan launch (r05: the r04 scan kernel took 32-35 us for config E, 19 of them
+// scanning the 4098 rows' bins; the row totals are now counted directly).
+constexpr uint32_t kCodeClass = 1u << 31;  // code.x: class item (| class), else keyed bin (< 2^26)
+constexpr uint32_t kCodeNone = 0xFFFFFFFFu;  // in no list (skip_unkeyed)
 extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_count_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_pkt_desc* __restrict__ desc, uint32_t n,
     const uint2* __restrict__ votes, uint32_t nv, uint32_t* __restrict__ hot_p, uint32_t* __restrict__ bins,
     uint32_t skip_unkeyed, const uint32_t* __restrict__ live, uint32_t* __restrict__ cmax,
     uint32_t* __restrict__ ctot, uint32_t* __restrict__ done, uint32_t cap, uint32_t* __restrict__ counts,
-    uint32_t* __restrict__ seg, uint32_t* __restrict__ cls, uint32_t* __restrict__ reg, uint32_t narrow) {
+    uint32_t* __restrict__ seg, uint32_t* __restrict__ cls, uint32_t* __restrict__ reg, uint32_t narrow,
+    uint2* __restrict__ code) {
   const KeyedWs kw = keyed_ws(bins, n_rows);
   if (pass_empty(live)) {  // empty lists: no hot key, no row segments, no regions
     if (blockIdx.x == 0) part_empty(counts, reg, kw, n_rows);
@@ -266,6 +297,7 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_count_kernel(
   __shared__ uint32_t s_bcnt[kBinSlots];
   __shared__ uint32_t s_last;
   const bool lds_bins = bins_in_lds(bins, n_rows);  // kernel-uniform
+  MQ_PSTAMP(blockIdx.x, 0);
   PartItem it[kPartItems];
   part_fetch(kt, n_rows, desc, n, it);
   if (threadIdx.x < kClasses) s_cnt[threadIdx.x] = 0;
@@ -273,58 +305,73 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_count_kernel(
   if (lds_bins)
     for (uint32_t q = threadIdx.x; q < n_rows * kKeyClasses; q += blockDim.x) s_bcnt[q] = 0;
   const uint32_t hot = fold_votes(votes, nv);  // the same in every wave of every block
-  if (blockIdx.x == 0 && threadIdx.x == 0) *hot_p = hot;  // for the scatter
+  if (blockIdx.x == 0 && threadIdx.x == 0) *hot_p = hot;
   __syncthreads();
-  uint32_t kb[kPartItems];
-  bool kd[kPartItems];
+  MQ_PSTAMP(blockIdx.x, 1);
+  uint32_t kb[kPartItems], cl[kPartItems];
+  bool kd[kPartItems], in[kPartItems];
 #pragma unroll
   for (int k = 0; k < kPartItems; ++k) {
     const uint32_t i = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
-    const bool in = i < n && !(skip_unkeyed && it[k].key >= n_rows);
-    const uint32_t c = in ? part_class(hot, it[k]) : 0u;
-    kd[k] = bins && in && c / kLenClasses == 1;
+    in[k] = i < n && !(skip_unkeyed && it[k].key >= n_rows);
+    const uint32_t c = in[k] ? part_class(hot, it[k]) : 0u;
+    cl[k] = c;
+    kd[k] = bins && in[k] && c / kLenClasses == 1;
     kb[k] = kd[k] ? key_bin(it[k]) : 0u;
-    if (in && !kd[k]) atomicAdd(&s_cnt[c], 1u);
-    if (in && c >= 2 * kLenClasses) atomicMax(&s_max[c - 2 * kLenClasses], it[k].nch);
+    if (in[k] && !kd[k]) atomicAdd(&s_cnt[c], 1u);
+    if (in[k] && c >= 2 * kLenClasses) atomicMax(&s_max[c - 2 * kLenClasses], it[k].nch);
   }
-  // keyed bins: one global atomic per distinct bin of the thread's items (a thread's items are
-  // kPartThreads descriptors apart: with keys assigned round-robin over 1024 rows, as in config C
-  // with 1024 keys, all four share a bin — 4x fewer atomics on the 1024 hot addresses)
+  // keyed bins: the thread's items of one bin claim their places with one atomic (a thread's items
+  // are kPartThreads descriptors apart: with keys assigned round-robin over 1024 rows, as in config
+  // C with 1024 keys, all four share a bin — 4x fewer atomics on the 1024 hot addresses); the
+  // leader's returned count is the group's first rank, a follower's rank adds the items before it
+  uint32_t kpos[kPartItems];
 #pragma unroll
   for (int k = 0; k < kPartItems; ++k) {
-    bool first = kd[k];
-    uint32_t cnt = 1;
+    int lead = k;
+    uint32_t cnt = 1, rank = 0;
 #pragma unroll
     for (int j = 0; j < kPartItems; ++j) {
       const bool same = kd[j] && kb[j] == kb[k];
-      if (j < k && same) first = false;
+      if (j < k && same) { rank += 1; lead = lead == k ? j : lead; }
       if (j > k && same) ++cnt;
     }
-    if (first && lds_bins) atomicAdd(&s_bcnt[kb[k]], cnt);
-    if (first && !lds_bins) {
-      atomicAdd(&kw.bins[kb[k]], cnt);
-      atomicAdd(&kw.rowtot[kb[k] / kKeyClasses], cnt);
-    }
+    uint32_t base = 0;
+    if (kd[k] && lead == k) base = atomicAdd(lds_bins ? &s_bcnt[kb[k]] : &kw.bins[kb[k]], cnt);
+#pragma unroll
+    for (int j = 0; j < kPartItems; ++j)
+      if (j == lead && j < k) base = kpos[j];
+    kpos[k] = kd[k] ? base + rank : 0u;  // lds_bins: the rank inside the block's count of the bin
   }
+  MQ_PSTAMP(blockIdx.x, 2);
   __syncthreads();
-  if (lds_bins)
+  if (lds_bins) {  // kernel-uniform: the block's base in each bin, one global atomic per bin
     for (uint32_t q = threadIdx.x; q < n_rows * kKeyClasses; q += blockDim.x)
-      if (s_bcnt[q]) {
-        atomicAdd(&kw.bins[q], s_bcnt[q]);
-        atomicAdd(&kw.rowtot[q / kKeyClasses], s_bcnt[q]);
-      }
+      if (s_bcnt[q]) s_bcnt[q] = atomicAdd(&kw.bins[q], s_bcnt[q]);
+  }
   if (threadIdx.x < kClasses && s_cnt[threadIdx.x]) atomicAdd(&ctot[threadIdx.x], s_cnt[threadIdx.x]);
   if (threadIdx.x < kLenClasses && s_max[threadIdx.x]) atomicMax(&cmax[threadIdx.x], s_max[threadIdx.x]);
+  if (lds_bins) __syncthreads();  // kernel-uniform
+#pragma unroll
+  for (int k = 0; k < kPartItems; ++k) {
+    const uint32_t i = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
+    if (i < n)
+      code[i] = kd[k] ? make_uint2(kb[k], kpos[k] + (lds_bins ? s_bcnt[kb[k]] : 0u))
+                      : make_uint2(in[k] ? kCodeClass | cl[k] : kCodeNone, 0u);
+  }
   // The last block to finish lays the lists out. Each thread waits until its atomics above are
   // performed (vmcnt counts them on gfx950) before the barrier that precedes the block's count, so
   // the block's totals are in when the count is. No __threadfence: on gfx950 a device-scope release
   // also writes back the XCD's L2 (measured: the count kernel 26 -> 108 us with one per block).
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  MQ_PSTAMP(blockIdx.x, 3);
   if (threadIdx.x == 0) s_last = atomicAdd(done, 1u) == gridDim.x - 1;
   __syncthreads();
+  MQ_PSTAMP(blockIdx.x, 4);
   if (!s_last) return;  // block-uniform
   part_layout(cap, counts, seg, ctot, kw, n_rows, cmax, cls, reg, narrow);
+  MQ_PSTAMP(blockIdx.x, 6);
 }
 
 __device__ __forceinline__ uint32_t ld_fresh(const uint32_t* p) {  // past this CU's L1: other blocks' atomics
@@ -339,8 +386,6 @@ __device__ void part_empty(uint32_t* __restrict__ counts, uint32_t* __restrict__
     for (uint32_t r = threadIdx.x; r < n_rows; r += blockDim.x) *(uint2*)(kw.rowseg + 2 * (size_t)r) = make_uint2(0, 0);
 }
 
-__device__ void row_scan(const KeyedWs& kw, uint32_t n_rows, uint32_t* __restrict__ counts, uint32_t base);
-
 // The lists' layout (the count kernel's last block, 16 waves) from the class totals: the class
 // segments (whole tiles) list by list (groups 0 and 1: list 0, group 2: list 1 at `cap`): seg[c] =
 // first list entry of class c, counts[s] = entries of list s, holes included; counts[3] = entries of
@@ -349,7 +394,6 @@ __device__ void part_layout(uint32_t cap, uint32_t* __restrict__ counts, uint32_
                             const uint32_t* __restrict__ ctot, const KeyedWs& kw, uint32_t n_rows,
                             const uint32_t* __restrict__ cmax, uint32_t* __restrict__ cls, uint32_t* __restrict__ reg,
                             uint32_t narrow) {
-  __shared__ uint32_t s_list0;
   __shared__ uint32_t s_tot[kClasses];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (threadIdx.x < kClasses) s_tot[threadIdx.x] = ld_fresh(ctot + threadIdx.x);
@@ -365,9 +409,9 @@ __device__ void part_layout(uint32_t cap, uint32_t* __restrict__ counts, uint32_
     if (lane == 0) {
       counts[3] = hot_e;
       // mq_partition_list_cap bounds e; the clamp only keeps a broken bound from running a suite
-      // kernel over the other list
+      // kernel over the other list (keyed: the scatter adds the rows' segments)
       counts[0] = min(e, cap);
-      s_list0 = e;
+      if (kw.btot) kw.btot[kRowBlocksMax] = e;  // keyed: the rows' segments follow
     }
   } else if (wave == 1) {
     // list 1 (ChaCha20 and the rest): lane l = class 2 kLenClasses + l, longest first. Each class
@@ -410,59 +454,65 @@ __device__ void part_layout(uint32_t cap, uint32_t* __restrict__ counts, uint32_
       reg[4] = R4; reg[5] = R2; reg[6] = R1; reg[7] = reg[0] + reg[1] + reg[2] + reg[3];
     }
   }
-  if (kw.bins) {  // keyed layout: the other AES keys' segments follow (workgroup-uniform)
-    __syncthreads();
-    row_scan(kw, n_rows, counts, s_list0);
-  }
+  MQ_PSTAMP(blockIdx.x, 5);
 }
 
-// Keyed layout (the layout block, after the class segments): each row's segment (its packets,
-// whole tiles) follows the majority key's classes in list 0, which end on a tile boundary at
-// `base`: rowseg[2r], rowseg[2r + 1] = row r's first entry and entries (tile padding included),
-// counts[0] = the list's entries. Each thread takes kKeyRowsPerThread consecutive rows' totals (one
-// 16-B read): 4096 rows per pass of two barriers. The scatter places a bin's packets at its row's
-// start plus the packets of the row's longer classes (read from bins) plus its cursor (fill).
-constexpr int kKeyRowsPerThread = 4;
-__device__ void row_scan(const KeyedWs& kw, uint32_t n_rows, uint32_t* __restrict__ counts, uint32_t base) {
-  constexpr int kThreads = kPartThreads, R = kKeyRowsPerThread;
-  __shared__ uint32_t s_wave[kPartThreads / kWave];
+// Keyed layout, after the count kernel: each row's segment (its packets, whole tiles) follows the
+// majority key's classes in list 0, which end on a tile boundary at `base`. Row blocks of
+// kRowThreads threads sum their rows' 16 bins each (64 B), scan the rows' entries (rounded up to
+// whole tiles) inside the block: rowseg[2r + 1] = entries, rowrel[r] = first entry relative to the
+// row block, btot[block] = the block's entries; the scatter adds the row blocks' prefix and writes
+// rowseg[2r] = first entry. (r05: the count kernel's last block scanned all rows alone: 15 us for
+// config E's 4098 rows, one CU's reads of lines the atomics had just updated, and before that a
+// per-row counter cost one more global atomic per keyed packet, tools/part_count_stamps.py.)
+extern "C" __global__ __launch_bounds__(kRowThreads) void mq_part_rows_kernel(uint32_t* __restrict__ bins,
+                                                                           uint32_t n_rows,
+                                                                           const uint32_t* __restrict__ live) {
+  if (pass_empty(live)) return;
+  __shared__ uint32_t s_w[kRowThreads / kWave];
+  const KeyedWs kw = keyed_ws(bins, n_rows);
+  const uint32_t R = rows_per_thread(n_rows);
+  const uint32_t r0 = (blockIdx.x * kRowThreads + threadIdx.x) * R;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t run_base = base;  // entries of list 0 before this pass (the same in every thread)
-  for (uint32_t r0 = 0; r0 < n_rows; r0 += kThreads * R) {  // workgroup-uniform
-    const uint32_t rt = r0 + (uint32_t)threadIdx.x * R;  // this thread's first row (rowtot is padded to 4)
-    uint32_t ent[R], sum = 0;
+  uint32_t sum = 0;
+  for (uint32_t q = 0; q < R; ++q) {
+    const uint32_t r = r0 + q;
+    if (r >= n_rows) break;
+    const uint4* b = (const uint4*)(kw.bins + (size_t)r * kKeyClasses);
+    uint32_t tot = 0;
 #pragma unroll
-    for (int q = 0; q < R; ++q) {
-      const uint32_t tot = rt + q < n_rows ? ld_fresh(kw.rowtot + rt + q) : 0u;
-      ent[q] = (tot + kPktsPerTile - 1) & ~(kPktsPerTile - 1);  // the row's segment: whole tiles
-      sum += ent[q];
+    for (int j = 0; j < (int)kKeyClasses / 4; ++j) {
+      const uint4 v = b[j];
+      tot += v.x + v.y + v.z + v.w;
     }
-    const uint32_t incl = wave_incl_scan(sum);
-    if (lane == 63) s_wave[wave] = incl;
-    __syncthreads();
-    uint32_t at = run_base + incl - sum, pass = 0;
-#pragma unroll
-    for (int q = 0; q < kThreads / kWave; ++q) {
-      const uint32_t t = s_wave[q];
-      if (q < wave) at += t;
-      pass += t;
-    }
-#pragma unroll
-    for (int q = 0; q < R; ++q) {
-      if (rt + q < n_rows) *(uint2*)(kw.rowseg + 2 * (size_t)(rt + q)) = make_uint2(at, ent[q]);
-      at += ent[q];
-    }
-    run_base += pass;
-    __syncthreads();  // s_wave is rewritten by the next pass
+    const uint32_t ent = (tot + kPktsPerTile - 1) & ~(kPktsPerTile - 1);  // whole tiles
+    kw.rowseg[2 * (size_t)r + 1] = ent;
+    sum += ent;
   }
-  if (threadIdx.x == 0) counts[0] = run_base;
+  const uint32_t incl = wave_incl_scan(sum);
+  if (lane == 63) s_w[wave] = incl;
+  __syncthreads();
+  uint32_t at = incl - sum, blk = 0;
+#pragma unroll
+  for (int w = 0; w < (int)(kRowThreads / kWave); ++w) {
+    at += w < wave ? s_w[w] : 0u;
+    blk += s_w[w];
+  }
+  for (uint32_t q = 0; q < R; ++q) {
+    const uint32_t r = r0 + q;
+    if (r >= n_rows) break;
+    kw.rowrel[r] = at;
+    at += kw.rowseg[2 * (size_t)r + 1];
+  }
+  if (threadIdx.x == 0) kw.btot[blockIdx.x] = blk;
 }
 
-// first list entry of keyed bin kb: its row's start plus the row's packets in longer classes
-__device__ __forceinline__ uint32_t bin_start(const KeyedWs& kw, uint32_t kb) {
+// first list entry of keyed bin kb: its row's start (the row block's prefix s_bpre, the row's
+// offset inside its block) plus the row's packets in longer classes
+__device__ __forceinline__ uint32_t bin_start(const KeyedWs& kw, uint32_t kb, const uint32_t* s_bpre, uint32_t rpb) {
   const uint32_t row = kb / kKeyClasses, c = kb % kKeyClasses;
   const uint4* b = (const uint4*)(kw.bins + (size_t)row * kKeyClasses);
-  uint32_t p = kw.rowseg[2 * (size_t)row];
+  uint32_t p = s_bpre[row / rpb] + kw.rowrel[row];
 #pragma unroll
   for (uint32_t k = 0; k < kKeyClasses / 4; ++k) {
     const uint4 v = b[k];
@@ -471,81 +521,79 @@ __device__ __forceinline__ uint32_t bin_start(const KeyedWs& kw, uint32_t kb) {
   return p;
 }
 
-// Each block counts its packets per class again and reserves their ranks inside each class with
-// one global atomic per class (ccur): the block's packets of a class take consecutive ranks (the
-// order of blocks inside a class is whichever reserved first — packets are independent, so only
-// the tile composition can change between runs, never a result). Keyed packets reserve their
-// places inside their bin the same way (fill) and sit at bin_start + that rank.
+// Each block counts its packets per class again (from the count kernel's codes) and reserves
+// their ranks inside each class with one global atomic per class (ccur): the block's packets of a
+// class take consecutive ranks (the order of blocks inside a class is whichever reserved first —
+// packets are independent, so only the tile composition can change between runs, never a result).
+// Keyed packets sit at bin_start + the rank their count-kernel atomic returned.
 extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_scatter_kernel(
-    const KeyRow* __restrict__ kt, uint32_t n_rows, const mq_pkt_desc* __restrict__ desc, uint32_t n,
-    const uint32_t* __restrict__ hot_p, uint32_t* __restrict__ ccur, const uint32_t* __restrict__ seg,
-    uint32_t* __restrict__ list, uint32_t* __restrict__ bins, uint32_t skip_unkeyed, const uint32_t* __restrict__ live,
-    const uint32_t* __restrict__ cls) {
+    const uint2* __restrict__ code, uint32_t n, uint32_t n_rows, uint32_t* __restrict__ ccur,
+    const uint32_t* __restrict__ seg, uint32_t* __restrict__ list, uint32_t* __restrict__ bins,
+    const uint32_t* __restrict__ live, const uint32_t* __restrict__ cls, uint32_t* __restrict__ counts,
+    uint32_t cap) {
   if (pass_empty(live)) return;
+  MQ_PSTAMP(gridDim.x + blockIdx.x, 0);
   const KeyedWs kw = keyed_ws(bins, n_rows);
   __shared__ uint32_t s_rank[kClasses];
   __shared__ uint32_t s_cls[kLenClasses];  // list 1's classes: ppt | Q << 8 (the layout's)
-  __shared__ uint32_t s_bcnt[kBinSlots];
-  const bool lds_bins = bins_in_lds(bins, n_rows);  // kernel-uniform
+  __shared__ uint32_t s_bpre[kRowBlocksMax];  // keyed: first list entry of each row block
+  __shared__ uint32_t s_bw[kRowBlocksMax / kWave];
   if (threadIdx.x < kLenClasses) s_cls[threadIdx.x] = cls[threadIdx.x];
   if (threadIdx.x < kClasses) s_rank[threadIdx.x] = 0;
-  if (lds_bins)
-    for (uint32_t q = threadIdx.x; q < n_rows * kKeyClasses; q += blockDim.x) s_bcnt[q] = 0;
-  PartItem it[kPartItems];
-  part_fetch(kt, n_rows, desc, n, it);
-  const uint32_t hot = *hot_p;
-  const int lane = threadIdx.x & 63;
-  uint32_t kb[kPartItems], cl[kPartItems];
-  bool kd[kPartItems], in[kPartItems];
+  const uint32_t rpb = kRowThreads * rows_per_thread(n_rows);  // rows per row block
+  if (bins) {  // kernel-uniform: the row blocks' exclusive prefix, from list 0's keyed base
+    const uint32_t nrb = (n_rows + rpb - 1) / rpb;
+    const uint32_t t = threadIdx.x;
+    const uint32_t v = t < nrb ? kw.btot[t] : 0u;
+    const uint32_t incl = wave_incl_scan(v);
+    if (t < kRowBlocksMax && (t & 63) == 63) s_bw[t >> 6] = incl;
+    __syncthreads();
+    if (t < kRowBlocksMax) {
+      uint32_t x = kw.btot[kRowBlocksMax] + incl - v, all = kw.btot[kRowBlocksMax];
+#pragma unroll
+      for (int w = 0; w < (int)(kRowBlocksMax / kWave); ++w) {
+        x += w < (int)(t >> 6) ? s_bw[w] : 0u;
+        all += s_bw[w];
+      }
+      s_bpre[t] = x;
+      if (blockIdx.x == 0 && t == 0) counts[0] = min(all, cap);  // list 0: hot classes + rows
+    }
+  }
+  uint2 x[kPartItems];
 #pragma unroll
   for (int k = 0; k < kPartItems; ++k) {
     const uint32_t i = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
-    const bool skp = skip_unkeyed && it[k].key >= n_rows;  // in no list (never AES: not keyed either)
-    cl[k] = i < n ? part_class(hot, it[k]) : 0u;
-    kd[k] = bins && i < n && cl[k] / kLenClasses == 1;
-    kb[k] = kd[k] ? key_bin(it[k]) : 0u;
-    in[k] = i < n && !kd[k] && !skp;
+    x[k] = i < n ? code[i] : make_uint2(kCodeNone, 0u);
   }
-  __syncthreads();  // s_rank, s_bcnt zeroed
+  const int lane = threadIdx.x & 63;
+  uint32_t cl[kPartItems];
+  bool in[kPartItems];
+#pragma unroll
+  for (int k = 0; k < kPartItems; ++k) {
+    in[k] = (x[k].x & kCodeClass) && x[k].x != kCodeNone;
+    cl[k] = in[k] ? x[k].x & ~kCodeClass : 0u;
+  }
+  __syncthreads();  // s_rank zeroed, s_bpre
+  MQ_PSTAMP(gridDim.x + blockIdx.x, 1);
+  if (bins) {  // kernel-uniform: this block's share of the rows' absolute first entries
+    const uint32_t share = (n_rows + gridDim.x - 1) / gridDim.x;
+    const uint32_t lo = blockIdx.x * share, hi = min(n_rows, lo + share);
+    for (uint32_t r = lo + threadIdx.x; r < hi; r += blockDim.x) kw.rowseg[2 * (size_t)r] = s_bpre[r / rpb] + kw.rowrel[r];
+  }
   // the block's counts per class (as the count kernel made them), then one global reservation each
 #pragma unroll
   for (int k = 0; k < kPartItems; ++k)
     if (in[k]) atomicAdd(&s_rank[cl[k]], 1u);
-  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  // keyed bins: the thread's items of one bin claim their places with one atomic
-  uint32_t kpos[kPartItems];
 #pragma unroll
-  for (int k = 0; k < kPartItems; ++k) {
-    int lead = k;
-    uint32_t cnt = 1, rank = 0;
-#pragma unroll
-    for (int j = 0; j < kPartItems; ++j) {
-      const bool same = kd[j] && kb[j] == kb[k];
-      if (j < k && same) { rank += 1; lead = lead == k ? j : lead; }
-      if (j > k && same) ++cnt;
-    }
-    uint32_t base = 0;
-    if (kd[k] && lead == k) base = atomicAdd(lds_bins ? &s_bcnt[kb[k]] : &kw.fill[kb[k]], cnt);
-    // a follower takes the leader's place (its base: the leader comes first in k order) + rank
-#pragma unroll
-    for (int j = 0; j < kPartItems; ++j)
-      if (j == lead && j < k) base = kpos[j];
-    kpos[k] = kd[k] ? base + rank : 0u;  // lds_bins: the rank inside the block's count of the bin
-    if (kd[k] && !lds_bins)
-      list[bin_start(kw, kb[k]) + kpos[k]] = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
-  }
+  for (int k = 0; k < kPartItems; ++k)
+    if (!(x[k].x & kCodeClass))  // keyed
+      list[bin_start(kw, x[k].x, s_bpre, rpb) + x[k].y] = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
+  MQ_PSTAMP(gridDim.x + blockIdx.x, 2);
   __syncthreads();
   if (threadIdx.x < kClasses && s_rank[threadIdx.x]) s_rank[threadIdx.x] = atomicAdd(&ccur[threadIdx.x], s_rank[threadIdx.x]);
-  if (lds_bins)  // kernel-uniform: the block's base in each bin, one global atomic per bin
-    for (uint32_t q = threadIdx.x; q < n_rows * kKeyClasses; q += blockDim.x)
-      if (s_bcnt[q]) s_bcnt[q] = atomicAdd(&kw.fill[q], s_bcnt[q]);
   __syncthreads();
-  if (lds_bins) {
-#pragma unroll
-    for (int k = 0; k < kPartItems; ++k)
-      if (kd[k])
-        list[bin_start(kw, kb[k]) + s_bcnt[kb[k]] + kpos[k]] = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
-  }
+  MQ_PSTAMP(gridDim.x + blockIdx.x, 3);
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 #pragma unroll
   for (int k = 0; k < kPartItems; ++k) {
     const uint32_t i = blockIdx.x * kPartBlock + k * kPartThreads + threadIdx.x;
@@ -565,11 +613,12 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_scatter_kerne
     base = (uint32_t)__shfl((int)base, leader, kWave);
     if (in[k]) {
       const uint32_t r = base + rank;
-      const uint32_t x = c >= 2 * kLenClasses ? s_cls[c - 2 * kLenClasses] : (class_ppt(c, 0u) | kPktsPerTile << 8);
-      const uint32_t ppt = x & 0xffu, Q = x >> 8;
+      const uint32_t y = c >= 2 * kLenClasses ? s_cls[c - 2 * kLenClasses] : (class_ppt(c, 0u) | kPktsPerTile << 8);
+      const uint32_t ppt = y & 0xffu, Q = y >> 8;
       list[seg[c] + Q * (r / ppt) + r % ppt] = i;
     }
   }
+  MQ_PSTAMP(gridDim.x + blockIdx.x, 4);
 }
 
 // keyed layout bins: one counter per (row, class), within a budget of 2 per packet (at least
@@ -582,7 +631,7 @@ static bool keyed_layout(uint32_t n, uint32_t n_rows) {
 }
 
 
-// list (2 x cap entries) | class histograms (kClasses per block) |
+// list (2 x cap entries) | codes (8 B per packet, the count kernel's) |
 // meta (2 totals, hot row, hot segment entries, kClasses segment starts) | keyed bins, 256-B aligned pieces
 static size_t part_align(size_t b) { return (b + 255) & ~(size_t)255; }
 
@@ -595,7 +644,7 @@ const uint32_t* mq_partition_rowseg(uint32_t n, uint32_t n_rows, const uint32_t*
 }
 
 hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_desc* desc, uint32_t n,
-                               uint32_t* list, uint32_t* hist, uint32_t* counts, hipStream_t s, bool skip_unkeyed,
+                               uint32_t* list, uint32_t* codes, uint32_t* counts, hipStream_t s, bool skip_unkeyed,
                                const uint32_t* live) {
   const uint32_t nblocks = (n + kPartBlock - 1) / kPartBlock;
   // narrow ChaCha20 regions: not for the receive passes (skip_unkeyed); MQ_CC_NARROW=0 (read per call,
@@ -624,9 +673,13 @@ hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_d
                      max(nv, used), (uint4*)list, list_q, (uint4*)bins, bins_q, live, cmax);
   hipLaunchKernelGGL(mq_part_count_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, kt, n_rows, desc, n, votes,
                      max(nv, used), hot, bins, (uint32_t)skip_unkeyed, live, cmax, counts + kMetaCtot,
-                     counts + kMetaDone, cap, counts, seg, cls, reg, (uint32_t)narrow);
-  hipLaunchKernelGGL(mq_part_scatter_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, kt, n_rows, desc, n, hot,
-                     counts + kMetaCcur, seg, list, bins, (uint32_t)skip_unkeyed, live, cls);
+                     counts + kMetaDone, cap, counts, seg, cls, reg, (uint32_t)narrow, (uint2*)codes);
+  if (bins && n_rows) {
+    const uint32_t rpb = kRowThreads * rows_per_thread(n_rows);
+    hipLaunchKernelGGL(mq_part_rows_kernel, dim3((n_rows + rpb - 1) / rpb), dim3(kRowThreads), 0, s, bins, n_rows, live);
+  }
+  hipLaunchKernelGGL(mq_part_scatter_kernel, dim3(nblocks), dim3(kPartThreads), 0, s, (const uint2*)codes, n, n_rows,
+                     counts + kMetaCcur, seg, list, bins, live, cls, counts, cap);
   return hipGetLastError();
 }
 
@@ -634,16 +687,18 @@ hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_d
 const uint32_t* mq_partition_regions(const uint32_t* counts) { return counts + kMetaReg; }
 
 size_t mq_partition_workspace(uint32_t n) {
-  const size_t nblocks = (n + kPartBlock - 1) / kPartBlock;
-  // keyed words (keyed_ws): at most 34 per row plus padding, rows <= key_bins(n) / 16
+  // keyed words (keyed_ws): 19 per row, rows <= key_bins(n) / 16, then btot and base
   return part_align(sizeof(uint32_t) * 2 * (size_t)mq_partition_list_cap(n)) +
-         part_align(sizeof(uint32_t) * kClasses * nblocks) + part_align(sizeof(uint32_t) * kMetaWords) +
-         part_align(sizeof(uint32_t) * (key_bins(n) / 16 * 34 + 8));
+         part_align(sizeof(uint2) * (size_t)n) + part_align(sizeof(uint32_t) * kMetaWords) +
+         part_align(sizeof(uint32_t) * (key_bins(n) / 16 * 19 + kRowBlocksMax + 8));
 }
 
 // offsets of the pieces inside the partition workspace
-void mq_partition_layout(uint32_t n, size_t* hist_off, size_t* counts_off) {
-  const size_t nblocks = (n + kPartBlock - 1) / kPartBlock;
-  *hist_off = part_align(sizeof(uint32_t) * 2 * (size_t)mq_partition_list_cap(n));
-  *counts_off = *hist_off + part_align(sizeof(uint32_t) * kClasses * nblocks);
+void mq_partition_layout(uint32_t n, size_t* codes_off, size_t* counts_off) {
+  *codes_off = part_align(sizeof(uint32_t) * 2 * (size_t)mq_partition_list_cap(n));
+  *counts_off = *codes_off + part_align(sizeof(uint2) * (size_t)n);
 }
+
+#ifdef MQ_STAMPS
+void mq_stamps_set_part(uint64_t* p) { (void)hipMemcpyToSymbol(HIP_SYMBOL(mq_part_stamp_buf), &p, sizeof p); }
+#endif
