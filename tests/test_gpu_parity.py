@@ -449,6 +449,25 @@ def test_full_size_roundtrip(orc, cfg):
     assert v.tobytes() == w.arena.reshape(w.n, 1200)[:, :1184].tobytes()
 
 
+@pytest.mark.parametrize("hint", [_lib.MQ_SUITE_AES128GCM, _lib.MQ_SUITE_MIXED])
+def test_keyed_partition_many_rows(orc, hint):
+    # A keyed partition over more than 65536 key rows (r05, mq_partition.hip): the row blocks take
+    # two rows per thread (rows_per_thread), the scatter's prefix spans 129 row blocks (three waves
+    # of the scan) and the hot key is a minority row. 800 000 x 64-B AES-128-GCM packets over 66 000
+    # keys, every byte, status and PN against the oracle, sealed and then opened.
+    keys = workload.uniform_keys(_lib.MQ_SUITE_AES128GCM, 66000)
+    w = workload.uniform(800000, _lib.MQ_SUITE_AES128GCM, L=64, keys=keys)
+    g_out, g_st, _ = gpu_run(w.keys, w.arena, w.seal_desc, hint)
+    o_out = w.arena.copy()
+    o_st = orc.batch_seal(w.keys, o_out, w.seal_desc, w.suite_hint, threads=16)
+    assert (o_st == 0).all() and (g_st == o_st).all()
+    assert g_out.tobytes() == o_out.tobytes()
+    g_back, g_st, g_pn = gpu_run(w.keys, g_out, w.open_desc, hint, open_=True)
+    assert (g_st == 0).all() and (g_pn == w.pns).all()
+    v = g_back.reshape(w.n, 64)[:, :48]
+    assert v.tobytes() == w.arena.reshape(w.n, 64)[:, :48].tobytes()
+
+
 @pytest.mark.parametrize("cfg", ["b", "c", "ck", "e", "b1350"])
 def test_full_size_byte_exact(orc, cfg):
     # BASELINE configs[1], configs[2] (also with 1024 keys, key_id = g mod 1024: the key-segmented
