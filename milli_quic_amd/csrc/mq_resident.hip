@@ -91,12 +91,18 @@ __device__ __forceinline__ uint64_t poll_read(uint32_t k, int lane) {
 // chunks) from waves 1..3 (wave 0's first half must not wait for them); completes at the next
 // fenced barrier (s_waitcnt vmcnt(0)).
 // (t: the thread's index among the loading threads, a multiple of 64 of them: kResThreads - 64)
+// Mailbox bytes (host memory) -> LDS, system-coherent like the polls (sc0 sc1): the same mailbox
+// lines were read by earlier requests, and a cached copy must never serve a new one. (Until late
+// r05 these loads were cached and relied on wave 0's `buffer_inv` before the barrier, which waves
+// 1..3 could pass before the invalidation had completed: one AES open of 12 000 resident calls
+// failed its tag on stale packet bytes, gpurun_out/r05zd.)
 __device__ __forceinline__ void dma_chunks(const uint8_t* src, uint8_t* dst, uint32_t nch, int t) {
   const uint32_t w = (uint32_t)t >> 6, lane = (uint32_t)t & 63;
   for (uint32_t b = 64 * w; b < nch; b += kResThreads - 64)  // wave-uniform
     if (b + lane < nch)
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 16u * (b + lane)),
-                                       (__attribute__((address_space(3))) void*)(dst + 16u * b), 16, 0, 0);
+                                       (__attribute__((address_space(3))) void*)(dst + 16u * b), 16, 0,
+                                       17 /* sc0 sc1: system coherent */);
 }
 
 // the octet of a keystream word from a quad of lanes (chacha20_block4) to all lanes: word k of
