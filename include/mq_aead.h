@@ -213,6 +213,19 @@ void mq_stream_release(void* stream);
  * Writes min(n, 9) values and returns that count; 0 before any resident call. */
 int mq_resident_phases(int device, uint32_t* ns, int n);
 const char* mq_status_str(int status);
+/* Diagnostic switches (A/B measurements and tests that run two kernel paths on one batch; no
+ * switch changes a result): MQ_CC_NARROW, MQ_CC_LONG, MQ_CC_LIST, MQ_HP_FORK, MQ_AES_SEG,
+ * MQ_PROTECT_FUSED, MQ_RESIDENT, MQ_RESIDENT_TIMEOUT_US, MQ_RECV_SEG. Each starts from the
+ * environment variable of that name (read once, at the first use of any switch); value < 0 unsets
+ * it (the product behaviour). MQ_OK, or MQ_ERR_INVALID_ARG for an unknown name. A batch reads each
+ * switch once per call. */
+int mq_debug_option(const char* name, long value);
+/* The switch's value: -1 unset, -2 unknown name. */
+long mq_debug_option_get(const char* name);
+/* The kernel family a flat single-suite ChaCha20 batch of n packets over arena_len bytes runs with
+ * this suite_hint (MQ_BATCH_LEN_HINT included): 0 narrow tiles (short packets), 1 octet tiles over
+ * 10-KiB images, 2 over 13-KiB, 3 over 20-KiB images; -1 for n = 0. (Diagnostic switches aside.) */
+int mq_debug_chacha_flat_kind(uint64_t arena_len, uint32_t n, uint32_t suite_hint);
 
 /* ---- CryptoProvider::aead / Aead (per packet, host buffers; runs the HIP kernels) ----------- */
 /* provider.aead(key): key_len must equal KEY_LEN of the suite (rustcrypto.rs:234-236, 267-269) */
@@ -285,6 +298,15 @@ int mq_batch_derive_initial(mq_keytable* kt, uint32_t first_row, const uint8_t* 
                             uint8_t* status, void* stream);
 
 /* ---- batch API (device pointers, stream-ordered, asynchronous) ------------------------------ */
+/* Optional length hint, OR-ed into suite_hint of mq_batch_seal / mq_batch_open and the record
+ * variants: the batch's typical (average) protected packet length in bytes (saturating at 65535).
+ * Flat ChaCha20 batches choose their tile geometry from it (LDS image per 8-packet tile, or the
+ * narrow tiles of short packets: mq_debug_chacha_flat_kind). Without it the library takes
+ * arena_len / n, which is the batch's own figure only when the arena holds just this batch: a
+ * batch over part of a larger arena (a ring buffer, one chunk of a pipeline) should pass the hint,
+ * or it may run a kernel sized for longer packets. Results never depend on it. */
+#define MQ_BATCH_LEN_HINT(len) ((uint32_t)((len) > 0xFFFF ? 0xFFFF : (len)) << 16)
+
 /* `arena` is device memory of `arena_len` bytes holding the packets; `desc` (n entries) and
  * `status` (n bytes, written with MQ_* per packet) are device memory; `pn_out` (open only,
  * may be NULL) receives each packet's decoded packet number. `suite_hint` is

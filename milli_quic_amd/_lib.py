@@ -32,6 +32,11 @@ MQ_SUITE_AES128GCM = 1
 MQ_SUITE_CHACHA20 = 2
 MQ_SUITE_MIXED = 0xFF
 
+
+def MQ_BATCH_LEN_HINT(length):
+    """suite_hint bits: the batch's typical packet length (include/mq_aead.h)."""
+    return min(int(length), 0xFFFF) << 16
+
 MQ_PKT_LONG_HEADER = 0x01
 MQ_PKT_NO_HP = 0x02
 MQ_PKT_TLS_RECORD = 0x06  # implies MQ_PKT_NO_HP
@@ -88,6 +93,9 @@ SIGNATURES = {
     "mq_stream_release": (None, [_vp]),
     "mq_resident_phases": (ctypes.c_int, [ctypes.c_int, _vp, ctypes.c_int]),
     "mq_status_str": (ctypes.c_char_p, [ctypes.c_int]),
+    "mq_debug_option": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_long]),
+    "mq_debug_option_get": (ctypes.c_long, [ctypes.c_char_p]),
+    "mq_debug_chacha_flat_kind": (ctypes.c_int, [_u64, _u32, _u32]),
     "mq_aead_new": (ctypes.c_int, [_u32, _vp, _sz, ctypes.POINTER(_vp)]),
     "mq_aead_free": (None, [_vp]),
     "mq_aead_key_len": (_sz, [_u32]),
@@ -149,6 +157,26 @@ def load():
             fn.argtypes = args
         _lib = lib
         return lib
+
+
+class option:
+    """Context manager / setter of a diagnostic switch (mq_debug_option; None unsets it):
+    ``with _lib.option("MQ_CC_NARROW", 0): ...`` restores the previous value on exit."""
+
+    def __init__(self, name, value):
+        self.name, self.value = name.encode(), -1 if value is None else int(value)
+        self.old = None
+
+    def __enter__(self):
+        lib = load()
+        self.old = lib.mq_debug_option_get(self.name)
+        assert self.old != -2, self.name
+        assert lib.mq_debug_option(self.name, self.value) == MQ_OK
+        return self
+
+    def __exit__(self, *exc):
+        load().mq_debug_option(self.name, self.old)
+        return False
 
 
 def status_str(code):

@@ -170,3 +170,9 @@ def time_seal_open(kt, arena, desc, status, pn_out, suite_hint, iters, workspace
         _stream_ptr(stream), iters, ctypes.byref(s_ms), ctypes.byref(o_ms))
     _raise(rc)
     return s_ms.value, o_ms.value
+
+
+def flat_kind(arena_len, n, suite_hint):
+    """The flat ChaCha20 kernel family a batch would run (mq_debug_chacha_flat_kind): 0 narrow,
+    1 / 2 / 3 octet tiles over 10- / 13- / 20-KiB images."""
+    return _lib.load().mq_debug_chacha_flat_kind(int(arena_len), int(n), int(suite_hint))

@@ -14,6 +14,7 @@
 //         keystream XOR (held first block + the rest); failed packets are never stored.
 #include "mq_tile.h"
 #include "mq_build.h"
+#include "mq_opts.h"
 
 #include <cstdlib>
 
@@ -1501,11 +1502,22 @@ __global__ __launch_bounds__(256) void mq_chacha_open_hp_kernel(
 // ---- host-side launchers (called from mq_host.cpp) -------------------------------------------
 // index != null (a partition list, length on the device): the persistent list kernels, cus x 4
 // workgroups, sched = the stream's schedule slot (null: static stride)
+// Flat batches (no partition list): the kernel family from the batch's bytes per packet `bpp` —
+// the caller's length hint (MQ_BATCH_LEN_HINT), else arena_len / n. 0: narrow tiles (a batch
+// averaging at most 640 B per packet: short packets, G = 8 / 4 / 2 / 1 lanes chosen per wave;
+// configs B and E never), 1: octet tiles over 10-KiB images (config B: 1200), 2: 13-KiB images (eight
+// images over 1216 B), 3: 20-KiB images (over 1584 B). Tiles whose images overflow the kernel's LDS
+// image take the direct HBM path: right, only slower.
+int mq_chacha_flat_kind(uint64_t bpp) {
+  constexpr uint64_t kNarrowAvg = 640, kLongAvg0 = 1216, kLongAvg1 = 1584;
+  return bpp <= kNarrowAvg ? 0 : bpp <= kLongAvg0 ? 1 : bpp <= kLongAvg1 ? 2 : 3;
+}
+
 hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena,
                             uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
                             const uint32_t* index, const uint32_t* n_dev, uint8_t* status,
                             uint64_t* pn_out, uint2* hpm, bool own_hp, hipStream_t s, int cus, uint32_t* sched,
-                            int64_t single_row, bool persistent, const uint32_t* reg) {
+                            int64_t single_row, bool persistent, const uint32_t* reg, uint64_t bpp) {
   const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
   if (tiles == 0) return hipSuccess;
   if (open && hpm && own_hp) {  // !own_hp: mq_launch_mixed_hp covers both suites' lists
@@ -1518,10 +1530,9 @@ hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_
   // Lists run on the persistent grid when asked for (the receive composite's passes: an empty
   // list then costs 1024 workgroups, not a grid over the list capacity), else on the one-shot grid,
   // which measured 1.1 % faster on config E (r04q: 557.9 vs 551.6 GiB/s, three alternating runs).
-  // MQ_CC_LIST=0 / 1 (diagnostic) forces either.
-  const char* fe = std::getenv("MQ_CC_LIST");  // read per call: tests run both grids on one batch
-  const int forced = fe ? (fe[0] == '0' ? 0 : 1) : -1;
-  if (forced >= 0) persistent = forced == 1;
+  // MQ_CC_LIST=0 / 1 (diagnostic, mq_opts.h: tests run both grids on one batch) forces either.
+  const long forced = mq::opt(mq::Opt::CcList);
+  if (forced >= 0) persistent = forced != 0;
   // single_row >= 0: every packet of the list is on that row (the single-key kernels)
   const bool one = index && single_row >= 0 && (uint64_t)single_row < n_rows;
   const KeyRow* kl = one ? kt + single_row : kt;
@@ -1548,18 +1559,14 @@ hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_
                          reg, status);
     return hipGetLastError();
   }
-  // Flat batches of short packets run the narrow kernels (r05): the arena's bytes per packet bound
-  // the average packet length from above, so a batch averaging at most kNarrowAvg bytes per packet
-  // takes them (configs B and E never do). MQ_CC_NARROW=0 / 1 (read per call: tests run both
-  // kernels on the same batch) forces either.
+  // Flat batches: the kernel family from the bytes per packet (mq_chacha_flat_kind). MQ_CC_NARROW=0 / 1
+  // and MQ_CC_LONG=0 / 1 / 2 (diagnostic, mq_opts.h: tests run several kernels on one batch) force
+  // the wide / narrow kernels and the 10-, 13- or 20-KiB images.
   if (!index) {
-    constexpr uint64_t kNarrowAvg = 640;
-    // above kLongAvg0 bytes per packet eight images overflow the 10-KiB image (config B: 1200);
-    // above kLongAvg1 they overflow 13 KiB
-    constexpr uint64_t kLongAvg0 = 1216, kLongAvg1 = 1584;
-    bool narrow = arena_len <= kNarrowAvg * (uint64_t)n;
-    const char* ne = std::getenv("MQ_CC_NARROW");
-    if (ne) narrow = ne[0] == '1';
+    const int kind = mq_chacha_flat_kind(bpp);
+    bool narrow = kind == 0;
+    const long fn = mq::opt(mq::Opt::CcNarrow);
+    if (fn >= 0) narrow = fn == 1;
     if (narrow) {
       const uint32_t nb = (uint32_t)(((uint64_t)n + kWave * kCcWaves - 1) / (kWave * kCcWaves));
       if (open)
@@ -1572,11 +1579,9 @@ hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_
                            status);
       return hipGetLastError();
     }
-    // long packets (r05): larger LDS images; MQ_CC_LONG=0 / 1 / 2 (read per call) forces the
-    // 10-KiB, 13-KiB or 20-KiB kernels
-    int img = arena_len > kLongAvg1 * (uint64_t)n ? 2 : arena_len > kLongAvg0 * (uint64_t)n ? 1 : 0;
-    const char* le = std::getenv("MQ_CC_LONG");
-    if (le) img = le[0] == '2' ? 2 : le[0] == '1' ? 1 : 0;
+    int img = kind >= 2 ? kind - 1 : 0;  // 0: 10 KiB, 1: 13 KiB, 2: 20 KiB
+    const long fl = mq::opt(mq::Opt::CcLong);
+    if (fl >= 0) img = fl >= 2 ? 2 : (int)fl;
     const bool o1 = n_rows == 1;
     if (img) {
       const uint32_t lds = (img == 2 ? kLongerImg : kLongImg) * kCcWaves;
@@ -1594,7 +1599,6 @@ hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_
   }
   if (open)
     hipLaunchKernelGGL(n_rows == 1 || one ? mq_chacha_open1_kernel : mq_chacha_open_kernel, dim3(blocks),
-
                        dim3(kWave * kCcWaves), kLdsBytes * kCcWaves, s, kl, n_rows, arena, arena_len, desc, n, index,
                        n_dev, status, pn_out, hpm);
   if (open) return hipGetLastError();

@@ -16,17 +16,72 @@
 #include <vector>
 
 #include "mq_device.h"
+#include "mq_opts.h"
 #include "mq_resident.h"
 #include "mq_runtime.h"
 
 using mq::KeyRow;
+
+int mq_chacha_flat_kind(uint64_t bpp);  // mq_chacha.hip
+
+// ---- diagnostic switches (mq_opts.h) ---------------------------------------------------------
+namespace {
+const char* const kOptNames[(int)mq::Opt::Count] = {
+    "MQ_CC_NARROW", "MQ_CC_LONG",  "MQ_CC_LIST",           "MQ_HP_FORK", "MQ_AES_SEG",
+    "MQ_PROTECT_FUSED", "MQ_RESIDENT", "MQ_RESIDENT_TIMEOUT_US", "MQ_RECV_SEG"};
+std::atomic<long> g_opts[(int)mq::Opt::Count];
+std::once_flag g_opts_once;
+void opts_init() {  // once: the environment's values (shell-driven diagnostics keep working)
+  std::call_once(g_opts_once, [] {
+    for (int k = 0; k < (int)mq::Opt::Count; ++k) {
+      const char* e = std::getenv(kOptNames[k]);
+      long v = -1;
+      if (e && *e) {
+        char* end = nullptr;
+        v = std::strtol(e, &end, 10);
+        if (end == e || v < 0) v = -1;  // not a number: unset
+      }
+      g_opts[k].store(v, std::memory_order_relaxed);
+    }
+  });
+}
+}  // namespace
+
+long mq::opt(mq::Opt o) {
+  opts_init();
+  return g_opts[(int)o].load(std::memory_order_relaxed);
+}
+
+extern "C" int mq_debug_option(const char* name, long value) {
+  if (!name) return MQ_ERR_INVALID_ARG;
+  opts_init();
+  for (int k = 0; k < (int)mq::Opt::Count; ++k)
+    if (std::strcmp(name, kOptNames[k]) == 0) {
+      g_opts[k].store(value < 0 ? -1 : value, std::memory_order_relaxed);
+      return MQ_OK;
+    }
+  return MQ_ERR_INVALID_ARG;
+}
+
+extern "C" int mq_debug_chacha_flat_kind(uint64_t arena_len, uint32_t n, uint32_t suite_hint) {
+  const uint64_t len_hint = suite_hint >> 16;
+  if (n == 0) return -1;
+  return mq_chacha_flat_kind(len_hint ? len_hint : (arena_len + n - 1) / n);
+}
+
+extern "C" long mq_debug_option_get(const char* name) {
+  if (!name) return -2;
+  for (int k = 0; k < (int)mq::Opt::Count; ++k)
+    if (std::strcmp(name, kOptNames[k]) == 0) return mq::opt((mq::Opt)k);
+  return -2;
+}
 
 // launchers defined in the .hip translation units
 hipError_t mq_launch_chacha(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena,
                             uint64_t arena_len, const mq_pkt_desc* desc, uint32_t n,
                             const uint32_t* index, const uint32_t* n_dev, uint8_t* status,
                             uint64_t* pn_out, uint2* hpm, bool own_hp, hipStream_t s, int cus, uint32_t* sched,
-                            int64_t single_row, bool persistent, const uint32_t* reg);
+                            int64_t single_row, bool persistent, const uint32_t* reg, uint64_t bpp);
 const uint32_t* mq_partition_regions(const uint32_t* counts);
 hipError_t mq_launch_chacha_hp(const KeyRow* kt, uint32_t n_rows, const uint32_t* key_ids,
                                const uint8_t* samples, uint8_t* masks, uint32_t n, hipStream_t s);
@@ -61,14 +116,15 @@ hipError_t mq_launch_chacha_protect(const KeyRow* kt, uint32_t n_rows, const mq_
                                     uint32_t* pkt_len, hipStream_t s);
 size_t mq_recv_workspace(uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_conns, size_t open_ws_bytes);
 void mq_recv_trace(const char* what, uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_conns, void* ws_ptr,
-                   size_t open_ws_bytes, hipStream_t s);
+                   size_t open_ws_bytes, uint32_t seg, hipStream_t s);
+uint32_t mq_recv_seg_len();
 hipError_t mq_recv_front(const KeyRow* kt, uint32_t n_rows, mq_conn_recv* conns, uint32_t n_conns, uint8_t* arena,
                          uint64_t arena_len, const mq_dgram* dg, uint32_t n_dgrams, uint32_t max_pkts,
                          uint32_t* n_pkts, mq_recv_pkt* out, void* ws_ptr, size_t open_ws_bytes, mq::MQRecvPass* pass,
-                         hipStream_t s);
+                         uint32_t seg, hipStream_t s);
 hipError_t mq_recv_walk(const KeyRow* kt, uint32_t n_rows, mq_conn_recv* conns, uint32_t n_conns,
                         uint32_t n_dgrams, uint32_t max_pkts, mq_recv_pkt* out, void* ws_ptr, size_t open_ws_bytes,
-                        bool final_walk, bool verify, uint32_t walk_idx, hipStream_t s);
+                        bool final_walk, bool verify, uint32_t walk_idx, uint32_t seg, hipStream_t s);
 hipError_t mq_recv_retry(uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_conns, void* ws_ptr, size_t open_ws_bytes,
                          hipStream_t s);
 hipError_t mq_recv_outcomes(uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_conns, void* ws_ptr,
@@ -479,7 +535,7 @@ int run_one(Scratch& sc, const KeyRow& row, const uint8_t* aad, uint32_t aad_len
   // protection pass to launch (own_hp false)
   hipError_t e = row.suite == MQ_SUITE_CHACHA20
                      ? mq_launch_chacha(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, st, pn, nullptr, false, sc.stream,
-                                        0, nullptr, -1, false, nullptr)
+                                        0, nullptr, -1, false, nullptr, bytes)
                      : mq_launch_aes(open, kt, 1, sc.dev, bytes, dd, 1, nullptr, nullptr, nullptr, st, pn, nullptr, false,
                                      sc.stream, sc.stream, devices().cus(sc.device), nullptr, nullptr, nullptr);
   if (e != hipSuccess) return MQ_ERR_HIP;
@@ -493,8 +549,8 @@ int run_one(Scratch& sc, const KeyRow& row, const uint8_t* aad, uint32_t aad_len
 // Per-packet calls go to the device's resident kernel (mq_resident.hip: no launch per call) unless
 // MQ_RESIDENT=0 or the packet exceeds its buffer; then run_one's batch of one.
 bool resident_enabled(size_t bytes) {
-  const char* e = std::getenv("MQ_RESIDENT");  // per call: tests and tools/bench_latency.py switch it
-  return !(e && e[0] == '0') && bytes + 31 <= mq::kResMaxPkt;  // + the body's alignment pad and the tag
+  // tests and tools/bench_latency.py switch it (mq_debug_option)
+  return mq::opt(mq::Opt::Resident) != 0 && bytes + 31 <= mq::kResMaxPkt;  // + the body's alignment pad and the tag
 }
 
 // The resident request image of a context: suite and key material (and for AES-128-GCM the GHASH
@@ -899,6 +955,11 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
   DeviceGuard g(kt->device);  // the table's device; `stream` must belong to it
   if (!g.ok()) return MQ_ERR_NO_DEVICE;
   if (n == 0) return MQ_OK;
+  // MQ_BATCH_LEN_HINT in the high half; without it the arena's bytes per packet stand in for the
+  // batch's (right when the arena holds just this batch)
+  const uint64_t len_hint = suite_hint >> 16;
+  suite_hint &= 0xFFFFu;
+  const uint64_t bpp = len_hint ? len_hint : (arena_len + n - 1) / n;
   const int cus = devices().cus(kt->device);
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = hipSuccess;
@@ -907,7 +968,7 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
   uint2* hpm = (open && ws) ? (uint2*)ws : nullptr;
   if (suite_hint == MQ_SUITE_CHACHA20) {
     e = mq_launch_chacha(open, kt->dev, kt->rows, arena, arena_len, desc, n, nullptr, nullptr, status, pn_out, hpm, true,
-                         s, cus, nullptr, -1, false, nullptr);
+                         s, cus, nullptr, -1, false, nullptr, bpp);
   } else if (suite_hint == MQ_SUITE_AES128GCM && (kt->rows == 1 || !ws || n > (1u << 30))) {
     e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, n, nullptr, nullptr, nullptr, status, pn_out,
                       hpm, true, s, s, cus, nullptr, sched_slot(kt->device, s), nullptr);
@@ -931,12 +992,11 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
     // before the tiles (seal needs none: the tiles mask their own packets). It runs on a side
     // stream beside the partition (r05: the partition no longer has a single-workgroup launch for
     // its blocks to delay — r03f measured that scan 27 -> 85 us and no gain); MQ_HP_FORK=0
-    // (diagnostic, read per call) runs it on s after the partition, as r04 did.
+    // (diagnostic, mq_opts.h) runs it on s after the partition, as r04 did.
     {
       const bool hp = open && hpm && !hpm_ready;
-      const char* hf = std::getenv("MQ_HP_FORK");
-      auto hfork = hp && fork_enabled() && !(hf && hf[0] == '0') ? side_streams().fork(kt->device, s, 1)
-                                                                   : mq::SideStreams<HipBackend>::Fork();
+      auto hfork = hp && fork_enabled() && mq::opt(mq::Opt::HpFork) != 0 ? side_streams().fork(kt->device, s, 1)
+                                                                          : mq::SideStreams<HipBackend>::Fork();
       if (hp && hfork) e = mq_launch_mixed_open_hp(kt->dev, kt->rows, arena, arena_len, desc, n, hpm, hfork.side(0));
       if (e == hipSuccess) e = mq_launch_partition(kt->dev, kt->rows, desc, n, list, codes, counts, s, recv_pass, live);
       if (e == hipSuccess && hp && !hfork) e = mq_launch_mixed_open_hp(kt->dev, kt->rows, arena, arena_len, desc, n, hpm, s);
@@ -953,9 +1013,9 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
     // Keys with many packets each (on average >= kSegPackets per row, keyed layout): the
     // key-segmented single-key kernels run list 0 whole, no fork (mq_aes.hip aes_seg_tiles)
     constexpr uint32_t kSegPackets = 512;
-    const char* seg_env = std::getenv("MQ_AES_SEG");  // diagnostic: 0 = never
-    const bool seg_force = seg_env && seg_env[0] == '1';  // diagnostic: 1 = whenever keyed
-    const uint32_t* rowseg = (seg_env && seg_env[0] == '0') || (!seg_force && (uint64_t)n < (uint64_t)kSegPackets * kt->rows)
+    const long seg_opt = mq::opt(mq::Opt::AesSeg);  // diagnostic: 0 = never, 1 = whenever keyed
+    const bool seg_force = seg_opt == 1;
+    const uint32_t* rowseg = seg_opt == 0 || (!seg_force && (uint64_t)n < (uint64_t)kSegPackets * kt->rows)
                                  ? nullptr
                                  : mq_partition_rowseg(n, kt->rows, counts);
     auto fork = fork_enabled() && !rowseg ? side_streams().fork(kt->device, s, 1) : mq::SideStreams<HipBackend>::Fork();
@@ -969,7 +1029,7 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
     else if (e == hipSuccess)
       e = mq_launch_chacha(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list + cap, counts + 1, status,
                            pn_out, hpm, false, s_list1, cus, sched_slot(kt->device, s_list1), kt->single_row(),
-                           recv_pass, mq_partition_regions(counts));
+                           recv_pass, mq_partition_regions(counts), bpp);
     // join even after a failed launch, so no side stream runs ahead of s
     if (!fork.join() && e == hipSuccess) e = hipErrorUnknown;
   } else {
@@ -1065,16 +1125,16 @@ int mq_batch_protect(const mq_keytable* kt, const mq_conn_send* conns, uint32_t 
                      uint8_t* status, uint32_t* pkt_len, uint32_t suite_hint, void* workspace, void* stream) {
   if (!kt || (n && (!conns || !frames || !out || !req || !status || !pkt_len || !workspace)))
     return MQ_ERR_INVALID_ARG;
+  suite_hint &= 0xFFFFu;  // a length hint (MQ_BATCH_LEN_HINT) is not used here
   if (((uintptr_t)out & 15) != 0) return MQ_ERR_INVALID_ARG;
   DeviceGuard g(kt->device);
   if (!g.ok()) return MQ_ERR_NO_DEVICE;
   if (n == 0) return MQ_OK;
   hipStream_t s = (hipStream_t)stream;
   // ChaCha20 batches (r04): one fused kernel builds each tile's packets into LDS and seals them
-  // there (mq_chacha.hip); MQ_PROTECT_FUSED=0 (diagnostic, read per call so tests compare both)
-  // keeps the two-kernel composite below
-  const char* fe = std::getenv("MQ_PROTECT_FUSED");
-  if (!(fe && fe[0] == '0') && suite_hint == MQ_SUITE_CHACHA20)
+  // there (mq_chacha.hip); MQ_PROTECT_FUSED=0 (diagnostic, mq_opts.h: tests compare both) keeps
+  // the two-kernel composite below
+  if (mq::opt(mq::Opt::ProtectFused) != 0 && suite_hint == MQ_SUITE_CHACHA20)
     return mq_launch_chacha_protect(kt->dev, kt->rows, conns, n_conns, frames, frames_len, out, out_len, req, n,
                                     suite_hint, status, pkt_len, s) == hipSuccess
                ? MQ_OK
@@ -1134,11 +1194,12 @@ int mq_batch_recv(const mq_keytable* kt, mq_conn_recv* conns, uint32_t n_conns, 
   hipStream_t s = (hipStream_t)stream;
   const size_t open_ws = mq_batch_workspace_size(max_pkts);
   mq::MQRecvPass p;
+  const uint32_t seg = mq_recv_seg_len();  // once per batch: every walk uses the same segment layout
   if (mq_recv_front(kt->dev, kt->rows, conns, n_conns, arena, arena_len, dgrams, n_dgrams, max_pkts, n_pkts, pkts,
-                    workspace, open_ws, &p, s) != hipSuccess)
+                    workspace, open_ws, &p, seg, s) != hipSuccess)
     return MQ_ERR_HIP;
   if (!max_pkts) return MQ_OK;
-  mq_recv_trace("walk 1", n_dgrams, max_pkts, n_conns, workspace, open_ws, s);
+  mq_recv_trace("walk 1", n_dgrams, max_pkts, n_conns, workspace, open_ws, seg, s);
   // walk -> AEAD passes -> walk ...: the first walk speculates that every packet opens, later walks
   // re-attempt what the real outcomes changed (rare: after a failed packet); the last walk defers
   // anything still unresolved. Fixed rounds keep the call asynchronous (no host read-back).
@@ -1155,9 +1216,10 @@ int mq_batch_recv(const mq_keytable* kt, mq_conn_recv* conns, uint32_t n_conns, 
     if (r != MQ_OK) return r;
     if (mq_recv_outcomes(n_dgrams, max_pkts, n_conns, workspace, open_ws, s) != hipSuccess) return MQ_ERR_HIP;
     if (mq_recv_walk(kt->dev, kt->rows, conns, n_conns, n_dgrams, max_pkts, pkts, workspace, open_ws,
-                     round + 1 == kRounds, true, (uint32_t)round + 1, s) != hipSuccess)
+                     round + 1 == kRounds, true, (uint32_t)round + 1, seg, s) != hipSuccess)
       return MQ_ERR_HIP;
-    mq_recv_trace(round + 1 == kRounds ? "final walk" : "walk 2", n_dgrams, max_pkts, n_conns, workspace, open_ws, s);
+    mq_recv_trace(round + 1 == kRounds ? "final walk" : "walk 2", n_dgrams, max_pkts, n_conns, workspace, open_ws,
+                  seg, s);
   }
   // Re-seal pass: a packet that opened under the speculation's inputs but fails under the
   // reference's (MQ_ERR_CRYPTO) holds plaintext; the final walk left its opening key row and PN in

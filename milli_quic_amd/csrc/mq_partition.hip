@@ -29,6 +29,7 @@
 // scatter from the count kernel's per-packet codes. (r02 start: eight operations with a full vote
 // pass, ~126 us per mixed 2^20-packet partition.)
 #include "mq_tile.h"
+#include "mq_opts.h"
 
 #include <cstdlib>
 
@@ -363,6 +364,13 @@ extern "C" __global__ __launch_bounds__(kPartThreads) void mq_part_count_kernel(
   // performed (vmcnt counts them on gfx950) before the barrier that precedes the block's count, so
   // the block's totals are in when the count is. No __threadfence: on gfx950 a device-scope release
   // also writes back the XCD's L2 (measured: the count kernel 26 -> 108 us with one per block).
+  // This is the hand-off the MI355X guide lists as measured-valid on gfx950 / ROCm 7.2 without a
+  // release/acquire pair (MI355X_MICROARCH.md "Valid forms", first table row: every storing wave's
+  // vmcnt(0), the barrier, ONE lane's agent-scope add to one counter, the block whose add came last
+  // told by its returned value, every load of the handed-off words past L1 — ld_fresh — and the
+  // handed-off words themselves written only by agent-scope atomics). It is outside the HIP memory
+  // model, so tests/test_gpu_parity.py::test_partition_handoff_stress re-runs keyed partitions over
+  // every XCD and checks each result byte for byte.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   MQ_PSTAMP(blockIdx.x, 3);
@@ -647,10 +655,9 @@ hipError_t mq_launch_partition(const KeyRow* kt, uint32_t n_rows, const mq_pkt_d
                                uint32_t* list, uint32_t* codes, uint32_t* counts, hipStream_t s, bool skip_unkeyed,
                                const uint32_t* live) {
   const uint32_t nblocks = (n + kPartBlock - 1) / kPartBlock;
-  // narrow ChaCha20 regions: not for the receive passes (skip_unkeyed); MQ_CC_NARROW=0 (read per call,
-  // diagnostic / A-B) turns them off as it turns off the flat narrow kernels
-  const char* ne = std::getenv("MQ_CC_NARROW");
-  const bool narrow = !skip_unkeyed && !(ne && ne[0] == '0');
+  // narrow ChaCha20 regions: not for the receive passes (skip_unkeyed); MQ_CC_NARROW=0 (diagnostic /
+  // A-B, mq_opts.h) turns them off as it turns off the flat narrow kernels
+  const bool narrow = !skip_unkeyed && mq::opt(mq::Opt::CcNarrow) != 0;
   if (nblocks == 0) {  // no lists, no regions
     const hipError_t e = hipMemsetAsync(counts, 0, 4 * sizeof(uint32_t), s);
     return e != hipSuccess ? e : hipMemsetAsync(counts + kMetaReg, 0, 8 * sizeof(uint32_t), s);

@@ -27,6 +27,7 @@
 #include <cstdlib>
 
 #include "mq_device.h"
+#include "mq_opts.h"
 
 using namespace mq;
 
@@ -446,13 +447,13 @@ __device__ __forceinline__ uint64_t excl_max_u64(uint64_t v, uint32_t lane, uint
 // and the final walk), so they take the guessed starts unverified.
 constexpr uint32_t kSeg = 1024;
 constexpr uint32_t kNoSeg = 0xFFFFFFFFu;  // one segment per run
-// the segment length in packets: kSeg, or MQ_RECV_SEG (diagnostic; 0 = one segment per run, the
-// r04 walk), read per call
-uint32_t recv_seg() {
-  const char* e = std::getenv("MQ_RECV_SEG");
-  if (!e) return kSeg;
-  const unsigned long v = std::strtoul(e, nullptr, 10);
-  return v == 0 ? kNoSeg : (uint32_t)(v < 64 ? 64 : v & ~63ul);  // whole walk chunks
+// the segment length in packets: kSeg, or MQ_RECV_SEG (diagnostic, mq_opts.h; 0 = one segment per
+// run, the r04 walk). Read ONCE per batch (mq_batch_recv) and handed to every walk: segprev[] slots
+// are indexed by the segment layout, which must not change between the walks of a batch.
+uint32_t mq_recv_seg_len() {
+  const long v = mq::opt(mq::Opt::RecvSeg);
+  if (v < 0) return kSeg;
+  return v == 0 ? kNoSeg : (uint32_t)(v < 64 ? 64 : (unsigned long)v & ~63ul);  // whole walk chunks
 }
 struct SegState { uint64_t largest[3]; uint32_t row[3]; uint32_t misc; };  // misc: phase | flags << 8 | updates << 16
 
@@ -567,7 +568,12 @@ __device__ __forceinline__ bool recv_walk(const mq_conn_recv* __restrict__ conn0
       if (est > 0) raise_largest(s, l0, est - 1);
     }
   }
-  uint32_t new_attempts = 0;
+  // attempts = keyed d1 entries of the pass. A fallback re-walks a run whose segment walks already
+  // counted their keyed entries in this walk: it takes those back and counts its own.
+  uint32_t new_attempts = 0, prior = 0;
+  if (MODE == kFallbackMode)
+    for (uint32_t k0 = lo; k0 < hi; k0 += kWave)  // wave-uniform
+      prior += (uint32_t)__popcll(__ballot(k0 + q < hi && d1[k0 + q].key_id != kNoRow));
   bool mismatch = false;
   // Settled prefix (walks after the first): while every packet so far OPENED with the keys the
   // speculation chose (outcome kOk1, no key update), the reference's decisions are exactly the
@@ -725,13 +731,13 @@ __device__ __forceinline__ bool recv_walk(const mq_conn_recv* __restrict__ conn0
       rec.key_gen = (w.level == MQ_LEVEL_APPLICATION && r.st == MQ_OK) ? r.gen : 0;
       rec.reserved[0] = rec.reserved[1] = rec.reserved[2] = 0;
       out[i] = rec;
-      att = r.mode != 0;  // keyed d1 entry: an attempt, or a re-seal (final walk)
+      att = a.key_id != kNoRow;  // keyed d1 entry: an attempt, or a re-seal (final walk)
     }
     new_attempts += (uint32_t)__popcll(__ballot(att));
   }
   if (MODE == kVerifyMode) return mismatch || !same_state(s, unpack_state(segend[x.g]));
   if (q != 0) return false;
-  if (new_attempts) atomicAdd(attempts, new_attempts);
+  if (new_attempts != prior) atomicAdd(attempts, new_attempts - prior);  // mod 2^32: the total stays >= 0
   if (MODE == kWalkMode) segend[x.g] = pack_state(s);
   if (MODE == kFallbackMode && seg != kNoSeg && hi > lo) segend[seg_slot((hi - lo - 1) / seg, ci, x.run_lo, n_conns, seg)] = pack_state(s);
   if (!x.last) return false;  // the connection's state: its last segment's (or the fallback's)
@@ -775,10 +781,14 @@ extern "C" __global__ __launch_bounds__(kWalkThreads) void mq_recv_walk_kernel(M
 }
 
 // verify + fallback: one wave per later segment re-walks it from its predecessor's recorded end
-// state; vstate[2c] collects connection c's verdicts and vstate[2c + 1] counts its finished
-// segments. The wave finishing a connection's last check resets both and, when a segment disagreed,
-// walks the whole run again from the connection's state (no further launch: a batch whose runs fit
-// one segment each costs one early-exit launch per walk).
+// state. Connection c's checks meet in ONE 64-bit word, vstate[2c..2c+1] read as a uint64: each
+// check adds 1 (low half: checks done) plus 2^32 when its segment disagreed (high half), so the
+// check whose add completes the count reads every other check's verdict in the value its own add
+// returns — one location, one modification order, no fence or ordering between two words needed
+// (r05 kept verdict and count in two words and relied on s_waitcnt between them). That
+// check resets the word and, when a segment disagreed, walks the whole run again from the
+// connection's state (no further launch: a batch whose runs fit one segment each costs one
+// early-exit launch per walk).
 extern "C" __global__ __launch_bounds__(kWalkThreads) void mq_recv_verify_kernel(MQ_RECV_WALK_PARAMS) {
   MQ_RECV_WALK_PROLOGUE
   SegGeo x;
@@ -786,13 +796,11 @@ extern "C" __global__ __launch_bounds__(kWalkThreads) void mq_recv_verify_kernel
   const bool differs = MQ_RECV_WALK_ARGS(kVerifyMode, x);
   uint32_t redo = 0;
   if (q == 0) {
-    // the verdict is in before the count that releases it: the wave waits until its atomic is
-    // performed (no __threadfence, which on gfx950 also writes back the XCD's L2)
-    if (differs) atomicOr(&vstate[2 * x.ci], 1u);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (atomicAdd(&vstate[2 * x.ci + 1], 1u) + 1 == later_segs(x.run_lo, x.run_hi, seg)) {
-      redo = atomicExch(&vstate[2 * x.ci], 0u);
-      vstate[2 * x.ci + 1] = 0;
+    unsigned long long* word = (unsigned long long*)(vstate + 2 * (size_t)x.ci);
+    const unsigned long long old = atomicAdd(word, 1ull + (differs ? (1ull << 32) : 0ull));
+    if ((uint32_t)old + 1 == later_segs(x.run_lo, x.run_hi, seg)) {
+      redo = (uint32_t)(old >> 32) + (differs ? 1u : 0u);
+      *word = 0ull;  // the next walk's verify launch (stream-ordered) starts from zero
       if (redo) atomicAdd(&vstate[2 * n_conns], 1u);  // fallbacks run (MQ_RECV_TRACE)
     }
   }
@@ -916,7 +924,7 @@ size_t al(size_t b) { return (b + 255) & ~(size_t)255; }
 struct RecvWs {
   uint32_t *counts, *base, *total, *keys, *vals, *skeys, *svals, *seg_lo, *seg_hi, *attempts;
   uint32_t *shist, *tkeys, *tvals;  // the sort's digit histograms and ping-pong buffers
-  uint32_t* vstate;  // per connection: verify verdicts, finished checks
+  uint32_t* vstate;  // per connection: one 64-bit word (checks done | disagreeing checks << 32)
   SegState* segend;
   uint32_t max_segs;
   RecvWork *work, *work_s;
@@ -993,13 +1001,13 @@ hipError_t mq_launch_aes_prepass(const KeyRow* kt, uint32_t n_rows, const uint8_
 
 hipError_t mq_recv_walk(const KeyRow* kt, uint32_t n_rows, mq_conn_recv* conns, uint32_t n_conns,
                         uint32_t n_dgrams, uint32_t max_pkts, mq_recv_pkt* out, void* ws_ptr, size_t open_ws_bytes,
-                        bool final_walk, bool verify, uint32_t walk_idx, hipStream_t s);
+                        bool final_walk, bool verify, uint32_t walk_idx, uint32_t seg, hipStream_t s);
 
 // split, header-protection masks, sort, first walk (mq_host.cpp then runs the AEAD passes)
 hipError_t mq_recv_front(const KeyRow* kt, uint32_t n_rows, mq_conn_recv* conns, uint32_t n_conns, uint8_t* arena,
                          uint64_t arena_len, const mq_dgram* dg, uint32_t n_dgrams, uint32_t max_pkts,
                          uint32_t* n_pkts, mq_recv_pkt* out, void* ws_ptr, size_t open_ws_bytes, MQRecvPass* pass,
-                         hipStream_t s) {
+                         uint32_t seg, hipStream_t s) {
   RecvWs w = layout((uint8_t*)ws_ptr, n_dgrams, max_pkts, n_conns, open_ws_bytes);
   pass->d1 = w.d1; pass->d2 = w.d2; pass->st1 = w.st1; pass->st2 = w.st2; pass->open_ws = w.open_ws;
   pass->live1 = w.attempts; pass->live2 = w.attempts + 1;
@@ -1059,18 +1067,17 @@ hipError_t mq_recv_front(const KeyRow* kt, uint32_t n_rows, mq_conn_recv* conns,
                      w.seg_hi);
   hipLaunchKernelGGL(mq_recv_gather_kernel, dim3((max_pkts + 255) / 256), b256, 0, s, w.total, max_pkts, w.svals, w.work,
                      arena, w.hpm, w.work_s, w.hdr_s, w.outcome);
-  return mq_recv_walk(kt, n_rows, conns, n_conns, n_dgrams, max_pkts, out, ws_ptr, open_ws_bytes, false, false, 0, s);
+  return mq_recv_walk(kt, n_rows, conns, n_conns, n_dgrams, max_pkts, out, ws_ptr, open_ws_bytes, false, false, 0, seg, s);
 }
 
 // one walk (after the first, the previous round's AEAD outcomes are folded in first)
 hipError_t mq_recv_walk(const KeyRow* /*kt*/, uint32_t n_rows, mq_conn_recv* conns, uint32_t n_conns,
                         uint32_t n_dgrams, uint32_t max_pkts, mq_recv_pkt* out, void* ws_ptr, size_t open_ws_bytes,
-                        bool final_walk, bool verify, uint32_t walk_idx, hipStream_t s) {
+                        bool final_walk, bool verify, uint32_t walk_idx, uint32_t seg, hipStream_t s) {
   RecvWs w = layout((uint8_t*)ws_ptr, n_dgrams, max_pkts, n_conns, open_ws_bytes);
   hipError_t e;
   if ((e = hipMemsetAsync(w.attempts, 0, 4, s)) != hipSuccess) return e;
   if (!n_conns) return hipGetLastError();
-  const uint32_t seg = recv_seg();
   const uint32_t later = seg == kNoSeg ? 0u : (max_pkts + seg - 1) / seg;  // bound on later segments
 #define MQ_RECV_WALK_LAUNCH(KERNEL, GRID)                                                                     \
   hipLaunchKernelGGL(KERNEL, dim3(GRID), dim3(kWalkThreads), 0, s, (const mq_conn_recv*)w.conn0, conns, n_conns,  \
@@ -1110,7 +1117,7 @@ hipError_t mq_recv_outcomes(uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_con
 // MQ_RECV_TRACE=1 (diagnostic): after each walk, the segment count, flagged connections and
 // attempts, printed to stderr (synchronizes the stream)
 void mq_recv_trace(const char* what, uint32_t n_dgrams, uint32_t max_pkts, uint32_t n_conns, void* ws_ptr,
-                   size_t open_ws_bytes, hipStream_t s) {
+                   size_t open_ws_bytes, uint32_t seg, hipStream_t s) {
   static const bool on = [] {
     const char* e = std::getenv("MQ_RECV_TRACE");
     return e && e[0] == '1';
@@ -1121,6 +1128,6 @@ void mq_recv_trace(const char* what, uint32_t n_dgrams, uint32_t max_pkts, uint3
   uint32_t nfb = 0, att[2] = {0, 0};
   (void)hipMemcpy(&nfb, w.vstate + 2ull * n_conns, 4, hipMemcpyDeviceToHost);
   (void)hipMemcpy(att, w.attempts, 8, hipMemcpyDeviceToHost);
-  std::fprintf(stderr, "[recv %s] segment %u fallbacks so far %u attempts %u retries %u\n", what, recv_seg(), nfb,
+  std::fprintf(stderr, "[recv %s] segment %u fallbacks so far %u attempts %u retries %u\n", what, seg, nfb,
                att[0], att[1]);
 }

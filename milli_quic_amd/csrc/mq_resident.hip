@@ -26,6 +26,7 @@
 // Dekker-style handshake on `state` / slot 0, so a request posted meanwhile is either served or
 // finds the kernel gone (the host then relaunches it).
 #include "mq_aes.h"
+#include "mq_opts.h"
 #include "mq_resident.h"
 
 #include <atomic>
@@ -725,11 +726,11 @@ ResidentSet* resident_set(int dev) {
 
 uint32_t load_acq(const uint32_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
 
-// How long a call waits for the resident kernel: 10 s, or MQ_RESIDENT_TIMEOUT_US (read per call;
+// How long a call waits for the resident kernel: 10 s, or MQ_RESIDENT_TIMEOUT_US (mq_opts.h;
 // tests force the timeout path with it)
 std::chrono::microseconds resident_timeout() {
-  const char* e = std::getenv("MQ_RESIDENT_TIMEOUT_US");
-  return std::chrono::microseconds(e ? std::strtoull(e, nullptr, 10) : 10000000ull);
+  const long v = opt(Opt::ResidentTimeoutUs);
+  return std::chrono::microseconds(v >= 0 ? (unsigned long long)v : 10000000ull);
 }
 
 }  // namespace

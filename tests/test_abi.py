@@ -86,3 +86,36 @@ def test_no_cpu_fallback_without_gpu(mqlib):
     from milli_quic_amd import crypto
     with pytest.raises(crypto.DeviceError):
         crypto.ChaCha20Provider().aead(bytes(32))
+
+
+def test_flat_chacha_kernel_choice(mqlib):
+    # a flat ChaCha20 batch picks its kernel family from the bytes per packet —
+    # the caller's MQ_BATCH_LEN_HINT, else arena_len / n. A sub-range batch over a large arena
+    # (bench.py --e2e chunks, ring buffers) with the hint gets the kernel of the same packets in a
+    # tight arena; without it, the arena's size misleads the choice (the r05 e2e runs: config B's
+    # 1200-B packets on the 20-KiB kernel).
+    kind = mqlib.mq_debug_chacha_flat_kind
+    C = _lib.MQ_SUITE_CHACHA20
+    n_all, n_chunk = 1 << 20, 1 << 15
+    tight = kind(1200 * n_chunk, n_chunk, C)
+    assert tight == 1                                        # 10-KiB octet images (config B)
+    assert kind(1200 * n_all, n_chunk, C) == 3               # the misled choice
+    assert kind(1200 * n_all, n_chunk, C | _lib.MQ_BATCH_LEN_HINT(1200)) == tight
+    for L, want in ((64, 0), (640, 0), (641, 1), (1216, 1), (1217, 2), (1584, 2), (1585, 3), (65535, 3), (1 << 20, 3)):
+        assert kind(L * 1000, 1000, C) == want, L
+        assert kind(1 << 40, 1000, C | _lib.MQ_BATCH_LEN_HINT(L)) == want, L
+    assert kind(0, 0, C) == -1
+
+
+def test_debug_options(mqlib):
+    # diagnostic switches: set, read back, unset; unknown names refused; a batch never reads the
+    # environment on its hot path (mq_opts.h)
+    assert mqlib.mq_debug_option_get(b"MQ_NO_SUCH") == -2
+    assert mqlib.mq_debug_option(b"MQ_NO_SUCH", 1) == _lib.MQ_ERR_INVALID_ARG
+    old = mqlib.mq_debug_option_get(b"MQ_RECV_SEG")
+    with _lib.option("MQ_RECV_SEG", 256):
+        assert mqlib.mq_debug_option_get(b"MQ_RECV_SEG") == 256
+        with _lib.option("MQ_RECV_SEG", None):
+            assert mqlib.mq_debug_option_get(b"MQ_RECV_SEG") == -1
+        assert mqlib.mq_debug_option_get(b"MQ_RECV_SEG") == 256
+    assert mqlib.mq_debug_option_get(b"MQ_RECV_SEG") == old

@@ -2,13 +2,11 @@
 oracle, byte for byte: flat batches of short packets (the narrow kernel, mq_chacha.hip
 chacha_narrow_flat) over random lengths, both header forms, 1..4-byte packet numbers, several key
 rows, packed back to back at every alignment; the same batches forced through the octet kernel
-(MQ_CC_NARROW=0) must give the same bytes, and long packets forced through the narrow kernel
-(MQ_CC_NARROW=1: G = 8 rounds, direct rounds over the LDS budget) as well. Tampered packets, bad
+(MQ_CC_NARROW 0) must give the same bytes, and long packets forced through the narrow kernel
+(MQ_CC_NARROW 1: G = 8 rounds, direct rounds over the LDS budget) as well. Tampered packets, bad
 key ids and a packet ending exactly at an arena end that is not 16-B aligned are included.
 Reference composites: transmit.rs:625-755 (seal + header protection), recv.rs:340-421 /
 953-1025 (header protection removal, decode_pn, open); rustcrypto.rs:111-165, 197-220."""
-import os
-
 import numpy as np
 import pytest
 
@@ -29,24 +27,9 @@ def _device(mqlib):
     assert mqlib.mq_device_init(0) == 0
 
 
-class _Env:
-    """MQ_CC_NARROW for the calls inside the block (read per call by mq_launch_chacha)."""
-
-    def __init__(self, v):
-        self.v = v
-
-    def __enter__(self):
-        self.old = os.environ.get("MQ_CC_NARROW")
-        if self.v is None:
-            os.environ.pop("MQ_CC_NARROW", None)
-        else:
-            os.environ["MQ_CC_NARROW"] = self.v
-
-    def __exit__(self, *a):
-        if self.old is None:
-            os.environ.pop("MQ_CC_NARROW", None)
-        else:
-            os.environ["MQ_CC_NARROW"] = self.old
+def _Env(v):
+    """MQ_CC_NARROW for the calls inside the block (mq_debug_option; None: the product choice)."""
+    return _lib.option("MQ_CC_NARROW", v)
 
 
 def to_dev(a):
@@ -201,10 +184,7 @@ def test_mixed_batches_narrow_regions(orc, lmin, lmax, n, grid):
     # list kernels, which walk the same list as octet tiles
     w = workload.config_e(n, seed=lmin * 31 + lmax, lmin=lmin, lmax=lmax)
     hint = _lib.MQ_SUITE_MIXED
-    old = os.environ.get("MQ_CC_LIST")
-    try:
-        if grid is not None:
-            os.environ["MQ_CC_LIST"] = grid
+    with _lib.option("MQ_CC_LIST", grid):
         g_out, g_st, _ = gpu_run(w.keys, w.arena, w.seal_desc, hint=hint)
         o_out, o_st, _ = oracle_run(orc, w.keys, w.arena, w.seal_desc, hint=hint)
         assert (o_st == 0).all() and (g_st == o_st).all()
@@ -213,26 +193,11 @@ def test_mixed_batches_narrow_regions(orc, lmin, lmax, n, grid):
         o_back, o_st, o_pn = oracle_run(orc, w.keys, o_out, w.open_desc, open_=True, hint=hint)
         assert (g_st == 0).all() and (g_st == o_st).all() and (g_pn == o_pn).all()
         assert g_back.tobytes() == o_back.tobytes()
-    finally:
-        if old is None:
-            os.environ.pop("MQ_CC_LIST", None)
-        else:
-            os.environ["MQ_CC_LIST"] = old
 
 
-class _EnvLong(_Env):
-    def __enter__(self):
-        self.old = os.environ.get("MQ_CC_LONG")
-        if self.v is None:
-            os.environ.pop("MQ_CC_LONG", None)
-        else:
-            os.environ["MQ_CC_LONG"] = self.v
-
-    def __exit__(self, *a):
-        if self.old is None:
-            os.environ.pop("MQ_CC_LONG", None)
-        else:
-            os.environ["MQ_CC_LONG"] = self.old
+def _EnvLong(v):
+    """MQ_CC_LONG for the calls inside the block (mq_debug_option)."""
+    return _lib.option("MQ_CC_LONG", v)
 
 
 @pytest.mark.parametrize("lmin,lmax,n", [(1150, 1600, 3000), (1600, 1950, 3001), (1500, 2600, 2000), (21, 2600, 2500)])
@@ -255,3 +220,25 @@ def test_long_images_single_key_vs_oracle(orc, mode):
     keys, arena, sd, od, pns = short_batch(4093, 1600, 1950, 1, seed=77)
     with _EnvLong(mode):
         roundtrip_vs_oracle(orc, keys, arena, sd, od, pns, modes=(None,))
+
+
+@pytest.mark.parametrize("hinted", [False, True])
+def test_subrange_batch_len_hint(orc, hinted):
+    # a batch over part of a larger arena (descriptors of 4000 packets out of 24 000
+    # 1200-B packets) — with MQ_BATCH_LEN_HINT it runs the 10-KiB octet kernel of a tight arena,
+    # without it the 20-KiB one; same bytes either way, only the packets of the batch touched
+    w = workload.config_b(24000)
+    lo, hi = 9000, 13000
+    assert batch.flat_kind(len(w.arena), hi - lo, CHACHA | (_lib.MQ_BATCH_LEN_HINT(1200) if hinted else 0)) == \
+        (1 if hinted else 3)
+    hint = CHACHA | (_lib.MQ_BATCH_LEN_HINT(1200) if hinted else 0)
+    sd, od = w.seal_desc[lo:hi], w.open_desc[lo:hi]
+    o_out, o_st, _ = oracle_run(orc, w.keys, w.arena, sd)
+    assert (o_st == 0).all()
+    g_out, g_st, _ = gpu_run(w.keys, w.arena, sd, hint=hint)
+    assert (g_st == 0).all() and g_out.tobytes() == o_out.tobytes()
+    assert g_out[:1200 * lo].tobytes() == w.arena[:1200 * lo].tobytes()
+    g_back, g_st, g_pn = gpu_run(w.keys, g_out, od, open_=True, hint=hint)
+    assert (g_st == 0).all() and (g_pn == w.pns[lo:hi]).all()
+    v = g_back.reshape(-1, 1200)[lo:hi, :1184]
+    assert v.tobytes() == w.arena.reshape(-1, 1200)[lo:hi, :1184].tobytes()

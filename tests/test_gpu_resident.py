@@ -4,8 +4,7 @@ no kernel launch per call (reference call sites transmit.rs:713-718, recv.rs:416
 rustcrypto.rs:38-220). Bit-exact against the oracle and the golden vectors over sizes from an
 empty payload to a 16-KiB TLS record, AAD from 0 to 300 B, tampering (Error::Crypto, buffer
 untouched), the exit / relaunch handshake after idling, threads sharing the server, and equal to
-the launch path (MQ_RESIDENT=0) call for call."""
-import os
+the launch path (MQ_RESIDENT 0) call for call."""
 import threading
 import time
 
@@ -24,9 +23,9 @@ def _device(mqlib):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     assert mqlib.mq_device_init(0) == 0
-    os.environ.pop("MQ_RESIDENT", None)
+    mqlib.mq_debug_option(b"MQ_RESIDENT", -1)
     yield
-    os.environ.pop("MQ_RESIDENT", None)
+    mqlib.mq_debug_option(b"MQ_RESIDENT", -1)
 
 
 def provider(suite):
@@ -72,7 +71,7 @@ def test_resident_sizes_vs_oracle(orc, suite, klen):
 
 def test_resident_vectors_and_launch_path_agree(aead_vectors, hp_vectors):
     for mode in ("1", "0", "1"):
-        os.environ["MQ_RESIDENT"] = mode
+        _lib.load().mq_debug_option(b"MQ_RESIDENT", int(mode))
         for c in aead_vectors:
             key, nonce, aad, pt = (bytes.fromhex(c[k]) for k in ("key", "nonce", "aad", "pt"))
             aead = provider(c["suite"]).aead(key)
@@ -83,7 +82,7 @@ def test_resident_vectors_and_launch_path_agree(aead_vectors, hp_vectors):
         for c in hp_vectors:
             hp = provider(c["suite"]).header_protection(bytes.fromhex(c["hp"]))
             assert hp.mask(bytes.fromhex(c["sample"])).hex() == c["mask"], (mode, c)
-    os.environ.pop("MQ_RESIDENT", None)
+    _lib.load().mq_debug_option(b"MQ_RESIDENT", -1)
 
 
 def test_resident_relaunch_after_idle(orc):
@@ -180,7 +179,7 @@ def test_resident_timeout_then_recovers(orc):
             for _ in range(6):
                 seal()
                 open_()
-            os.environ["MQ_RESIDENT_TIMEOUT_US"] = "100"
+            _lib.load().mq_debug_option(b"MQ_RESIDENT_TIMEOUT_US", 100)
             nonce, pt = bytes([k + 1]) * 12, bytes(range(256)) * 3
             buf = bytearray(pt) + bytearray(16)
             try:
@@ -190,7 +189,7 @@ def test_resident_timeout_then_recovers(orc):
             except crypto.DeviceError:
                 outcomes.append("timeout")
             finally:
-                os.environ.pop("MQ_RESIDENT_TIMEOUT_US", None)
+                _lib.load().mq_debug_option(b"MQ_RESIDENT_TIMEOUT_US", -1)
             print("resident timeout test: call", k, outcomes[-1], flush=True)
             # the next calls are served, byte-exact (both while the batch may still run and after)
             for q in range(4):
@@ -202,7 +201,7 @@ def test_resident_timeout_then_recovers(orc):
                 assert bytes(buf[:len(pt)]) == pt
             s.synchronize()
     finally:
-        os.environ.pop("MQ_RESIDENT_TIMEOUT_US", None)
+        _lib.load().mq_debug_option(b"MQ_RESIDENT_TIMEOUT_US", -1)
     assert (st.cpu().numpy() == 0).all()
     assert _plaintext_back(arena, w)  # seal + open rounds: every packet's plaintext back
     print("timeout outcomes", outcomes)

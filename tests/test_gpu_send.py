@@ -87,13 +87,13 @@ def test_protect_suite_hint_vs_oracle(orc, seed, hint):
     assert (o_st == 0).sum() > (1000 if hint == _lib.MQ_SUITE_CHACHA20 else 100)
 
 
-def test_protect_fused_matches_two_kernel(monkeypatch):
-    # the fused ChaCha20 kernel and the build-then-seal composite (MQ_PROTECT_FUSED=0) agree byte
+def test_protect_fused_matches_two_kernel():
+    # the fused ChaCha20 kernel and the build-then-seal composite (MQ_PROTECT_FUSED 0) agree byte
     # for byte, statuses and lengths included
     keys, conns, frames, req, out = chacha_heavy_batch(5000, 4)
     a = gpu_protect(keys, conns, frames, out, req, _lib.MQ_SUITE_CHACHA20)
-    monkeypatch.setenv("MQ_PROTECT_FUSED", "0")
-    b = gpu_protect(keys, conns, frames, out, req, _lib.MQ_SUITE_CHACHA20)
+    with _lib.option("MQ_PROTECT_FUSED", 0):
+        b = gpu_protect(keys, conns, frames, out, req, _lib.MQ_SUITE_CHACHA20)
     for x, y in zip(a, b):
         assert x.tobytes() == y.tobytes()
 

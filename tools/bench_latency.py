@@ -31,10 +31,10 @@ def main():
     assert lib.mq_device_init(0) == 0
     out = {"unit": "us per call", "packet": "1200 B (13 B AAD, 1171 B payload, 16 B tag)", "calls": args.calls}
     for mode in ("resident", "zero_copy", "copy"):
-        os.environ["MQ_RESIDENT"] = "1" if mode == "resident" else "0"
+        lib.mq_debug_option(b"MQ_RESIDENT", 1 if mode == "resident" else 0)
         os.environ["MQ_PER_PACKET_COPY"] = "1" if mode == "copy" else "0"
         out[mode] = measure(lib, _lib, args.calls)
-    os.environ.pop("MQ_RESIDENT", None)
+    lib.mq_debug_option(b"MQ_RESIDENT", -1)
     out["resident_throughput"] = throughput(lib, _lib)
     print(json.dumps(out), flush=True)
 
@@ -133,7 +133,7 @@ def measure(lib, _lib, calls):
             ts[k], to[k] = t1 - t0, t2 - t1b
         res["seal"] = {"median": round(float(np.median(ts)) * 1e6, 2), "p99": round(float(np.quantile(ts, 0.99)) * 1e6, 2)}
         res["open"] = {"median": round(float(np.median(to)) * 1e6, 2), "p99": round(float(np.quantile(to, 0.99)) * 1e6, 2)}
-        if os.environ.get("MQ_RESIDENT") == "1":  # device-side phases (mq_resident_phases), median us
+        if lib.mq_debug_option_get(b"MQ_RESIDENT") == 1:  # device-side phases (mq_resident_phases), median us
             names = ("header_broadcast", "first_half", "packet_wait", "second_half", "decrypt_applied", "written_back",
                      "host_request_written", "host_wait_done", "host_copy_out")
             res["phases_us"] = {

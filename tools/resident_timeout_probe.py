@@ -49,7 +49,7 @@ def main():
             for _ in range(6):
                 batch.seal(kt, arena, sd, st, w.suite_hint, ws, s.cuda_stream)
                 batch.open_(kt, arena, od, st, pn, w.suite_hint, ws, s.cuda_stream)
-        os.environ["MQ_RESIDENT_TIMEOUT_US"] = "100"
+        _lib.load().mq_debug_option(b"MQ_RESIDENT_TIMEOUT_US", 100)
         log(k, "call with a 100-us limit")
         buf = bytearray(100) + bytearray(16)
         try:
@@ -57,7 +57,7 @@ def main():
             log(k, "served")
         except crypto.DeviceError as e:
             log(k, "timeout:", e)
-        os.environ.pop("MQ_RESIDENT_TIMEOUT_US", None)
+        _lib.load().mq_debug_option(b"MQ_RESIDENT_TIMEOUT_US", -1)
         for q in range(3):
             buf = bytearray(100) + bytearray(16)
             aead.seal_in_place(bytes([k, q]) * 6, b"h", buf, 100)
