@@ -215,7 +215,7 @@ int mq_resident_phases(int device, uint32_t* ns, int n);
 const char* mq_status_str(int status);
 /* Diagnostic switches (A/B measurements and tests that run two kernel paths on one batch; no
  * switch changes a result): MQ_CC_NARROW, MQ_CC_LONG, MQ_CC_LIST, MQ_HP_FORK, MQ_AES_SEG,
- * MQ_PROTECT_FUSED, MQ_RESIDENT, MQ_RESIDENT_TIMEOUT_US, MQ_RECV_SEG. Each starts from the
+ * MQ_PROTECT_FUSED, MQ_RESIDENT, MQ_RESIDENT_TIMEOUT_US, MQ_RECV_SEG, MQ_AES_NARROW. Each starts from the
  * environment variable of that name (read once, at the first use of any switch); value < 0 unsets
  * it (the product behaviour). MQ_OK, or MQ_ERR_INVALID_ARG for an unknown name. A batch reads each
  * switch once per call. */
@@ -226,6 +226,9 @@ long mq_debug_option_get(const char* name);
  * this suite_hint (MQ_BATCH_LEN_HINT included): 0 narrow tiles (short packets), 1 octet tiles over
  * 10-KiB images, 2 over 13-KiB, 3 over 20-KiB images; -1 for n = 0. (Diagnostic switches aside.) */
 int mq_debug_chacha_flat_kind(uint64_t arena_len, uint32_t n, uint32_t suite_hint);
+/* The same for a flat single-key AES-128-GCM batch: 0 narrow tiles (16 short packets per wave),
+ * 1 octet tiles; -1 for n = 0. */
+int mq_debug_aes_flat_kind(uint64_t arena_len, uint32_t n, uint32_t suite_hint);
 
 /* ---- CryptoProvider::aead / Aead (per packet, host buffers; runs the HIP kernels) ----------- */
 /* provider.aead(key): key_len must equal KEY_LEN of the suite (rustcrypto.rs:234-236, 267-269) */

@@ -96,6 +96,7 @@ SIGNATURES = {
     "mq_debug_option": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_long]),
     "mq_debug_option_get": (ctypes.c_long, [ctypes.c_char_p]),
     "mq_debug_chacha_flat_kind": (ctypes.c_int, [_u64, _u32, _u32]),
+    "mq_debug_aes_flat_kind": (ctypes.c_int, [_u64, _u32, _u32]),
     "mq_aead_new": (ctypes.c_int, [_u32, _vp, _sz, ctypes.POINTER(_vp)]),
     "mq_aead_free": (None, [_vp]),
     "mq_aead_key_len": (_sz, [_u32]),

@@ -176,3 +176,9 @@ def flat_kind(arena_len, n, suite_hint):
     """The flat ChaCha20 kernel family a batch would run (mq_debug_chacha_flat_kind): 0 narrow,
     1 / 2 / 3 octet tiles over 10- / 13- / 20-KiB images."""
     return _lib.load().mq_debug_chacha_flat_kind(int(arena_len), int(n), int(suite_hint))
+
+
+def aes_flat_kind(arena_len, n, suite_hint):
+    """The flat single-key AES-128-GCM kernel family a batch would run (mq_debug_aes_flat_kind):
+    0 narrow tiles (16 short packets per wave), 1 octet tiles."""
+    return _lib.load().mq_debug_aes_flat_kind(int(arena_len), int(n), int(suite_hint))

@@ -31,6 +31,7 @@
 // keystream again, so every failed packet ends byte-identical to its input (recv.rs:416-421).
 #include "mq_aes.h"
 #include "mq_tile.h"
+#include "mq_opts.h"
 
 #include <cstdlib>
 
@@ -101,12 +102,13 @@ __device__ __forceinline__ void gh_block(const uint32_t (&m)[4], uint32_t rem, u
 }
 
 // End of the iterations in which every active packet's lanes all hold a whole payload block that
-// is not their last GHASH block (slots 8it .. 8it + 7 with 8it + 14 <= full blocks), the range
-// [1, lean_end) that the tile loops run without the edge cases (AAD, length block, partial block,
-// HP slot, last-block multiplier).
+// is not their last GHASH block (slots G it .. G it + G - 1 with G it + 2G - 2 <= full blocks), the
+// range [1, lean_end) that the tile loops run without the edge cases (AAD, length block, partial
+// block, HP slot, last-block multiplier). G: lanes per packet.
+template <int G>
 __device__ __forceinline__ int lean_end(bool act, uint32_t P) {
-  const uint32_t F = P >> 4;
-  return (int)wave_min_u32(!act ? 0xFFFFFFFFu : (F >= 14 ? (F - 14) / 8 + 1 : 0u));
+  const uint32_t F = P >> 4, E = 2u * G - 2u;
+  return (int)Grp<G>::wave_min(!act ? 0xFFFFFFFFu : (F >= E ? (F - E) / G + 1 : 0u));
 }
 
 // Per-packet, per-lane state of a streaming tile (octet-uniform fields are equal on the 8 lanes)
@@ -154,9 +156,13 @@ __device__ __forceinline__ void save_header(const uint32_t (&m)[4], uint32_t at,
 // wave's half table (multi-key kernels, key-uniform tile) or the bit-holed product (mixed keys)
 enum GhMode { kGhWorkgroup, kGhWave, kGhProduct };
 
-// The streaming tile of one wave.
-template <bool SINGLE, int GH>
+// The streaming tile of one wave: 8 packets on 8 lanes each (G = 8), or 16 on 4 (G = 4, the narrow
+// single-key kernels, r06): lane j of a packet holds slots j, j + G, j + 2G, ... and the Horner
+// multiplier is H^G (the workgroup's byte-position table holds H^G: aes_key_tables<G>).
+template <bool SINGLE, int GH, int G = kLanesPerPkt>
 struct AesStream {
+  static_assert(G == 8 || (G == 4 && GH == kGhWorkgroup), "narrow tiles: single-key kernels only");
+  using Gp = Grp<G>;
   // AES of slot b (b >= 0) from the CTR cache or full rounds; keystream as little-endian words
   template <bool CACHED, class K>
   static __device__ __forceinline__ void ctr(const K& key, const TwLane& L, const AesPkt& k,
@@ -187,7 +193,7 @@ struct AesStream {
 #if MQ_AES_NIBBLE
     if (GH == kGhWorkgroup) gh_mul_half(t, (const uint8_t*)g_aes_gh8);
 #else
-    if (GH == kGhWorkgroup) gh_mul_tab8(t);
+    if (GH == kGhWorkgroup) gh_mul_tab8(t);  // the workgroup's byte-position table of H^G
 #endif
     else if (GH == kGhWave) gh_mul_half(t, (const uint8_t*)g_aes_wtab + kGhHalfBytes * wave_id());
     else gf_mul(t, m8);
@@ -195,20 +201,20 @@ struct AesStream {
     for (int w = 0; w < 4; ++w) acc[w] = (has && !last) ? t[w] : acc[w];
   }
 
-  // tag = GHASH (final multiply by H^e, octet XOR) ^ E_K(J0) (lane 0's, broadcast)
+  // tag = GHASH (final multiply by H^e, group XOR) ^ E_K(J0) (lane 0's, broadcast)
   static __device__ __forceinline__ void finish(uint32_t (&acc)[4], const KeyRow* row, int j, const AesPkt& k,
                                                 const uint32_t (&ej0)[4], uint32_t (&tag)[4]) {
-    uint32_t e1 = (k.nblk + 8u - (uint32_t)j) & 7u;  // H^(e1 + 1): blocks after the lane's last
+    uint32_t e1 = (k.nblk + (uint32_t)G - (uint32_t)j) & (uint32_t)(G - 1);  // H^(e1 + 1): blocks after the lane's last
     pin(e1);  // keeps the H^e load and its preparation (36 VGPRs) after the tile loop
 #if MQ_PROF_SKIP & 64  // phase-cost diagnostic build only: no final multiply by H^e
     acc[0] ^= e1; acc[1] ^= row->H[0][1];
 #else
     if (GH == kGhWorkgroup) {  // single key: the workgroup's table of H^(e1 + 1), per lane
-      // e1 = 7 (H^8): the lane multiplied its last block in the Horner loop (fin_in_loop)
+      // e1 = G - 1 (H^G): the lane multiplied its last block in the Horner loop (fin_in_loop)
       uint32_t t[4] = {acc[0], acc[1], acc[2], acc[3]};
-      gh_mul_half(t, fin_table(min(e1, 6u)));
+      gh_mul_half(t, fin_table(min(e1, (uint32_t)G - 2u)));
 #pragma unroll
-      for (int w = 0; w < 4; ++w) acc[w] = e1 == 7 ? acc[w] : t[w];
+      for (int w = 0; w < 4; ++w) acc[w] = e1 == (uint32_t)G - 1u ? acc[w] : t[w];
     } else {
       uint32_t hp[4];
 #pragma unroll
@@ -218,13 +224,13 @@ struct AesStream {
     }
 #endif
 #pragma unroll
-    for (int w = 0; w < 4; ++w) tag[w] = bswap32(brev(oct_xor(acc[w]))) ^ oct_bcast0(ej0[w]);
+    for (int w = 0; w < 4; ++w) tag[w] = bswap32(brev(Gp::xr(acc[w]))) ^ Gp::bcast0(ej0[w]);
   }
 
-  // single-key kernels: the lane whose final multiplier would be H^8 (e1 = 7) takes it in its last
-  // Horner step instead, through the H^8 table (finish skips it): no final-multiply table of H^8
+  // single-key kernels: the lane whose final multiplier would be H^G (e1 = G - 1) takes it in its
+  // last Horner step instead, through the loop's table (finish skips it)
   static __device__ __forceinline__ bool fin_in_loop(const AesPkt& k, int j) {
-    return GH == kGhWorkgroup && ((k.nblk + 8u - (uint32_t)j) & 7u) == 7u;
+    return GH == kGhWorkgroup && ((k.nblk + (uint32_t)G - (uint32_t)j) & (uint32_t)(G - 1)) == (uint32_t)G - 1u;
   }
 
   static __device__ __forceinline__ GfOp prep_m8(const KeyRow* row) {
@@ -232,7 +238,7 @@ struct AesStream {
     if (GH == kGhProduct) {
       uint32_t h[4];
 #pragma unroll
-      for (int w = 0; w < 4; ++w) h[w] = brev(row->H[7][w]);
+      for (int w = 0; w < 4; ++w) h[w] = brev(row->H[G - 1][w]);
       m8 = gf_prepare(h);
     }
     return m8;
@@ -260,9 +266,9 @@ struct AesStream {
     k.A = (k.aad_len + 15) >> 4;
     k.nblk = 1 + ((k.P + 15) >> 4);
     k.hp = k.act && !(d.flags & MQ_PKT_NO_HP);
-    const bool hp_slot = k.hp && k.nblk >= (uint32_t)kLanesPerPkt;  // else after the tag
-    const int it_lo = -(int)wave_max_u32(k.act ? (k.A + 6) / 8 : 0u);
-    const int it_hi = (int)wave_max_u32(k.act ? k.nblk / 8 + 1 : 0u);
+    const bool hp_slot = k.hp && k.nblk >= (uint32_t)G;  // else after the tag
+    const int it_lo = -(int)Gp::wave_max(k.act ? (k.A + G - 2) / G : 0u);
+    const int it_hi = (int)Gp::wave_max(k.act ? k.nblk / G + 1 : 0u);
     nonce_be(row, c.pn, k.nb);
     AesCtrCache cc{};
     if (CACHED) cc = ctr_cache(key, L, k.nb);
@@ -284,8 +290,8 @@ struct AesStream {
     uint32_t acc[4] = {0, 0, 0, 0}, ej0[4] = {0, 0, 0, 0}, smp[4] = {0, 0, 0, 0};
     uint32_t m0 = 0, m1 = 0;
     bool have_mask = false;
-    uint4 cur = data(j + kLanesPerPkt * it_lo);
-    const int it_lean = lean_end(k.act, k.P);
+    uint4 cur = data(j + G * it_lo);
+    const int it_lean = lean_end<G>(k.act, k.P);
     const bool fin8 = fin_in_loop(k, j);
 #if MQ_AES_DEFER
     // First-line deferral (r04, build option, off in the product): the payload bytes in the rest of
@@ -297,7 +303,7 @@ struct AesStream {
     // VGPR in the tile loop and the split block's byte stores), so the product keeps the writes.
     // Single-key kernels only: the multi-key ones have no registers to spare (15 -> 41 spills).
     const uint32_t line_rest = 128u - (uint32_t)(k.pkt & 127u);
-    const uint32_t dl = (GH != kGhWorkgroup || !k.act || k.rec || line_rest <= k.aad_len)
+    const uint32_t dl = (GH != kGhWorkgroup || G != 8 || !k.act || k.rec || line_rest <= k.aad_len)
                             ? 0u
                             : min(min(line_rest - k.aad_len, 112u), k.P);
 #else
@@ -308,9 +314,9 @@ struct AesStream {
     MQ_STAMP(c.tile, 1);
 #pragma nounroll
     for (int it = it_lo; it < it_hi; ++it) {
-      const int b = j + kLanesPerPkt * it;
+      const int b = j + G * it;
       const uint32_t ub = (uint32_t)b;
-      const uint4 nxt = data(b + kLanesPerPkt);  // next iteration's block, in flight during this one
+      const uint4 nxt = data(b + G);  // next iteration's block, in flight during this one
       if (it >= 1 && it < it_lean) {  // interior iteration (wave-uniform)
         uint32_t ks[4], ct[4], x[4];
         ctr<CACHED>(key, L, k, cc, ub, ks);
@@ -377,12 +383,12 @@ struct AesStream {
       if (it == 0) {  // the HP sample: payload bytes [4 - pn_len, 20 - pn_len) from slots 1 and 2
         uint32_t src[8];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) { src[q] = oct_lane<1>(ct[q]); src[4 + q] = oct_lane<2>(ct[q]); }
+        for (int q = 0; q < 4; ++q) { src[q] = Gp::template lane<1>(ct[q]); src[4 + q] = Gp::template lane<2>(ct[q]); }
         const uint32_t o = 4u - (k.hp ? d.pn_len : 4u);
 #pragma unroll
         for (int q = 0; q < 4; ++q) smp[q] = __builtin_amdgcn_alignbyte(src[q + 1], src[q], o);
       }
-      gh_step(acc, m8, has, b + kLanesPerPkt > (int)k.nblk && !fin8, x);
+      gh_step(acc, m8, has, b + G > (int)k.nblk && !fin8, x);
       cur = nxt;
       if (it == 0) MQ_STAMP(c.tile, 2);
     }
@@ -409,7 +415,7 @@ struct AesStream {
     }
     // the masked header (RFC 9001 §5.4.1; the MAC read it unprotected): the mask from its one lane
     // to the octet, then each lane stores the header bytes it saved from its AAD blocks
-    const uint32_t mk0 = oct_xor(have_mask ? m0 : 0u), mk1 = oct_xor(have_mask ? m1 : 0u);
+    const uint32_t mk0 = Gp::xr(have_mask ? m0 : 0u), mk1 = Gp::xr(have_mask ? m1 : 0u);
 #if MQ_PROF_SKIP & 128  // phase-cost diagnostic build only: no header mask writes
     hs_v = 0;
 #endif
@@ -461,8 +467,8 @@ struct AesStream {
     k.pay = k.pkt + k.aad_len;
     k.A = (k.aad_len + 15) >> 4;
     k.nblk = 1 + ((k.P + 15) >> 4);
-    const int it_lo = -(int)wave_max_u32(k.act ? (k.A + 6) / 8 : 0u);
-    const int it_hi = (int)wave_max_u32(k.act ? k.nblk / 8 + 1 : 0u);
+    const int it_lo = -(int)Gp::wave_max(k.act ? (k.A + G - 2) / G : 0u);
+    const int it_hi = (int)Gp::wave_max(k.act ? k.nblk / G + 1 : 0u);
     uint32_t got[4] = {0, 0, 0, 0};
     if (k.act) u4w(ld16(arena + k.pay + k.P), got);
     nonce_be(row, c.pn, k.nb);
@@ -475,15 +481,15 @@ struct AesStream {
       return make_uint4(0, 0, 0, 0);
     };
     uint32_t acc[4] = {0, 0, 0, 0}, ej0[4] = {0, 0, 0, 0};
-    uint4 cur = data(j + kLanesPerPkt * it_lo);
-    const int it_lean = lean_end(k.act, k.P);
+    uint4 cur = data(j + G * it_lo);
+    const int it_lean = lean_end<G>(k.act, k.P);
     const bool fin8 = fin_in_loop(k, j);
     MQ_STAMP(c.tile, 1);
 #pragma nounroll
     for (int it = it_lo; it < it_hi; ++it) {
-      const int b = j + kLanesPerPkt * it;
+      const int b = j + G * it;
       const uint32_t ub = (uint32_t)b;
-      const uint4 nxt = data(b + kLanesPerPkt);
+      const uint4 nxt = data(b + G);
       if (it >= 1 && it < it_lean) {  // interior iteration (wave-uniform)
         uint32_t ks[4], pt[4], x[4];
         ctr<CACHED>(key, L, k, cc, ub, ks);
@@ -522,7 +528,7 @@ struct AesStream {
 #pragma unroll
         for (int q = 0; q < 4; ++q) ej0[q] = ks[q];
       }
-      gh_step(acc, m8, has, b + kLanesPerPkt > (int)k.nblk && !fin8, x);
+      gh_step(acc, m8, has, b + G > (int)k.nblk && !fin8, x);
       cur = nxt;
       if (it == 0) MQ_STAMP(c.tile, 2);
     }
@@ -538,7 +544,7 @@ struct AesStream {
     if (wave_any(bad)) {  // restore the ciphertext of failed packets
 #pragma nounroll
       for (int it = 0; it < it_hi; ++it) {
-        const uint32_t b = (uint32_t)j + kLanesPerPkt * (uint32_t)it;
+        const uint32_t b = (uint32_t)j + (uint32_t)G * (uint32_t)it;
         uint32_t ks[4];
         ctr<CACHED>(key, L, k, cc, b, ks);
         if (bad && b >= 1 && b < k.nblk) {
@@ -595,7 +601,10 @@ constexpr int aes_seg_waves() { return MQ_AES_SEG_WAVES; }
 __shared__ __attribute__((aligned(16))) uint32_t g_aes_keys[kAesMultiWaves * kPktsPerTile * kRkSlotBytes / 4];
 __shared__ __attribute__((aligned(16))) uint32_t g_aes_keys1[kRkSlotBytes / 4];
 
-// the key-dependent tables of a single-key workgroup (row kt[0]); ends with a barrier
+// the key-dependent tables of a single-key workgroup (row kt[0]); ends with a barrier. G: lanes per
+// packet of its tiles — the byte-position table holds the Horner multiplier H^G (H^8, or H^4 for the
+// narrow kernels)
+template <int G = kLanesPerPkt>
 __device__ __forceinline__ void aes_key_tables(const KeyRow* __restrict__ kt) {
     if (threadIdx.x < kRkSlotBytes / 4) g_aes_keys1[threadIdx.x] = kt[0].aes_rk[threadIdx.x];  // aes_rk || hp_rk
     const uint32_t w = wave_id();
@@ -607,7 +616,7 @@ __device__ __forceinline__ void aes_key_tables(const KeyRow* __restrict__ kt) {
     }
     uint32_t h8[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) h8[q] = brev(kt[0].H[7][q]);
+    for (int q = 0; q < 4; ++q) h8[q] = brev(kt[0].H[G - 1][q]);
 #if MQ_AES_NIBBLE  // diagnostic A/B build only: the Horner multiply by H^8 through a nibble half table
     if (w == 7) build_gh_half((uint8_t*)g_aes_gh8, h8, (int)(threadIdx.x & (kWave - 1)));
     __syncthreads();
@@ -616,21 +625,22 @@ __device__ __forceinline__ void aes_key_tables(const KeyRow* __restrict__ kt) {
 #endif
 }
 
-template <bool SINGLE>
+template <bool SINGLE, int G = kLanesPerPkt>
 __device__ __forceinline__ void aes_tables(const KeyRow* __restrict__ kt) {
   build_tw(threadIdx.x, blockDim.x);
-  if (SINGLE) aes_key_tables(kt);
+  if (SINGLE) aes_key_tables<G>(kt);
   else __syncthreads();
 }
 
-template <bool SINGLE, bool OPEN, int GH, bool CACHED, class K>
+template <bool SINGLE, bool OPEN, int GH, bool CACHED, int G, class K>
 __device__ __forceinline__ void aes_run(uint8_t* __restrict__ arena, PktCtx& c, const KeyRow* row, int j, const K& key,
                                         const uint32_t* kl) {
-  if (OPEN) AesStream<SINGLE, GH>::template open<CACHED>(arena, c, row, j, key, kl);
-  else AesStream<SINGLE, GH>::template seal<CACHED>(arena, c, row, j, key, kl);
+  if (OPEN) AesStream<SINGLE, GH, G>::template open<CACHED>(arena, c, row, j, key, kl);
+  else AesStream<SINGLE, GH, G>::template seal<CACHED>(arena, c, row, j, key, kl);
 }
 
-template <bool SINGLE, bool OPEN>
+// G: lanes per packet — 8 (tiles of 8 packets), or 4 (16 packets, single-key kernels only)
+template <bool SINGLE, bool OPEN, int G = kLanesPerPkt>
 __device__ __forceinline__ void aes_stream_tiles(const KeyRow* __restrict__ kt, uint32_t n_rows,
                                                  uint8_t* __restrict__ arena, uint64_t arena_len,
                                                  const mq_pkt_desc* __restrict__ desc, uint32_t n,
@@ -639,23 +649,24 @@ __device__ __forceinline__ void aes_stream_tiles(const KeyRow* __restrict__ kt, 
                                                  uint64_t* __restrict__ pn_out, const uint2* __restrict__ hpm,
                                                  uint32_t skip, const TileSched& ts) {
   const uint32_t w = wave_id();
-  const int lane = (int)(threadIdx.x & (kWave - 1)), j = lane & (kLanesPerPkt - 1);
+  static_assert(SINGLE || G == kLanesPerPkt, "narrow tiles: single-key kernels only");
+  const int lane = (int)(threadIdx.x & (kWave - 1)), j = lane & (G - 1);
   uint32_t wt_kid = 0xFFFFFFFFu;  // multi-key: the row whose half table and key schedules the wave holds
-  for_tiles<OPEN>(ts, desc, n, index, n_dev, hpm,
-                  [&](uint32_t t, const TilePrefetch& pf) __attribute__((always_inline)) {
+  for_tiles<OPEN, G>(ts, desc, n, index, n_dev, hpm,
+                     [&](uint32_t t, const TilePrefetch& pf) __attribute__((always_inline)) {
     PktCtx c;
     const KeyRow* row;
-    if (!tile_ctx<MQ_SUITE_AES128GCM, OPEN, SINGLE>(t, kt, n_rows, arena_len, desc, n, index, n_dev, hpm, pf, c,
-                                                    row))
+    if (!tile_ctx<MQ_SUITE_AES128GCM, OPEN, SINGLE, G>(t, kt, n_rows, arena_len, desc, n, index, n_dev, hpm, pf, c,
+                                                       row))
       return;
     MQ_STAMP(t, 0);
     // CTR caching needs every counter < 256: packets of at most 4080 bytes
     const bool cached = !wave_any(c.act && c.d.len > 4080u);
-    if (SINGLE) {
+    if constexpr (SINGLE) {
       AesRk rk;
       load_rk(kt[0].aes_rk, rk);  // wave-uniform: SGPRs
-      if (cached) aes_run<SINGLE, OPEN, kGhWorkgroup, true>(arena, c, row, j, RkRegs{rk}, g_aes_keys1);
-      else aes_run<SINGLE, OPEN, kGhWorkgroup, false>(arena, c, row, j, RkRegs{rk}, g_aes_keys1);
+      if (cached) aes_run<SINGLE, OPEN, kGhWorkgroup, true, G>(arena, c, row, j, RkRegs{rk}, g_aes_keys1);
+      else aes_run<SINGLE, OPEN, kGhWorkgroup, false, G>(arena, c, row, j, RkRegs{rk}, g_aes_keys1);
     } else {
       // a tile whose active packets share one row: round keys in SGPRs, that row's H^8 half table
       // (and key schedules for the HP block) in the wave's LDS, rebuilt only when the row changes
@@ -674,8 +685,8 @@ __device__ __forceinline__ void aes_stream_tiles(const KeyRow* __restrict__ kt, 
         }
         AesRk rk;
         load_rk(urow->aes_rk, rk);
-        if (cached) aes_run<SINGLE, OPEN, kGhWave, true>(arena, c, urow, j, RkRegs{rk}, kl);
-        else aes_run<SINGLE, OPEN, kGhWave, false>(arena, c, urow, j, RkRegs{rk}, kl);
+        if (cached) aes_run<SINGLE, OPEN, kGhWave, true, G>(arena, c, urow, j, RkRegs{rk}, kl);
+        else aes_run<SINGLE, OPEN, kGhWave, false, G>(arena, c, urow, j, RkRegs{rk}, kl);
       } else {
         // mixed keys: each packet's key schedules into its own LDS slot (lane j copies words
         // 11j .. 11j + 10 of aes_rk || hp_rk, contiguous in the row)
@@ -689,8 +700,8 @@ __device__ __forceinline__ void aes_stream_tiles(const KeyRow* __restrict__ kt, 
         for (int q = 0; q < 11; ++q) kl[11 * j + q] = v[q];
         wave_sync();
         wt_kid = 0xFFFFFFFFu;  // slot 0 no longer holds a key-uniform tile's schedules
-        if (cached) aes_run<SINGLE, OPEN, kGhProduct, true>(arena, c, row, j, RkLds{kl}, kl);
-        else aes_run<SINGLE, OPEN, kGhProduct, false>(arena, c, row, j, RkLds{kl}, kl);
+        if (cached) aes_run<SINGLE, OPEN, kGhProduct, true, G>(arena, c, row, j, RkLds{kl}, kl);
+        else aes_run<SINGLE, OPEN, kGhProduct, false, G>(arena, c, row, j, RkLds{kl}, kl);
       }
     }
     MQ_STAMP(t, 7);
@@ -701,7 +712,7 @@ __device__ __forceinline__ void aes_stream_tiles(const KeyRow* __restrict__ kt, 
 // hot (partition lists only, else null): hot[0] = the hot key's row, hot[1] = the entries of its
 // segment at the front of the list (whole tiles). A single-key kernel then runs that segment with
 // the hot row as its one-row table; the multi-key kernel starts after it.
-template <bool SINGLE>
+template <bool SINGLE, int G = kLanesPerPkt>
 __device__ __forceinline__ bool aes_hot_split(const uint32_t* __restrict__ hot, const KeyRow* __restrict__& kt,
                                               const uint32_t* __restrict__& n_dev, uint32_t& skip) {
   skip = 0;
@@ -710,7 +721,7 @@ __device__ __forceinline__ bool aes_hot_split(const uint32_t* __restrict__ hot, 
   if (SINGLE) {
     // workgroup-uniform, before any barrier: no segment (hot[0] may be no row), or no tile for
     // this workgroup (a small segment: skip the table builds)
-    if (blockIdx.x * (aes_waves(true) * kPktsPerTile) >= entries) return false;
+    if (blockIdx.x * (aes_waves(true) * (kWave / G)) >= entries) return false;
     kt += hot[0];
     n_dev = hot + 1;
   } else {
@@ -724,10 +735,10 @@ __device__ __forceinline__ bool aes_hot_split(const uint32_t* __restrict__ hot, 
 // usually empty, and 256 workgroups building their tables for nothing cost ~35 us). Its waves' first
 // tiles are skip + blockIdx.x * W + w; every later tile lies beyond all first tiles, so a
 // workgroup without a first tile has none at all.
-template <bool SINGLE>
+template <bool SINGLE, int G = kLanesPerPkt>
 __device__ __forceinline__ bool aes_wg_has_work(uint32_t n, const uint32_t* __restrict__ n_dev, uint32_t skip) {
   const uint32_t count = n_dev ? *n_dev : n;
-  const uint32_t tiles = (count + kPktsPerTile - 1) / kPktsPerTile;
+  const uint32_t tiles = (count + kWave / G - 1) / (kWave / G);
   return skip + blockIdx.x * aes_waves(SINGLE) < tiles;
 }
 
@@ -738,19 +749,19 @@ __device__ __forceinline__ TileSched aes_sched(uint32_t* sched, bool single) {
 
 // sched: the launch's schedule slot (dynamic tiles), null for the static stride. Every workgroup
 // reaches sched_done once: without work at its only exit, else after a barrier behind its tiles.
-#define MQ_AES_KERNELS(NAME_SEAL, NAME_OPEN, SINGLE)                                                      \
+#define MQ_AES_KERNELS(NAME_SEAL, NAME_OPEN, SINGLE, G)                                                   \
   extern "C" __global__ __launch_bounds__(64 * aes_waves(SINGLE)) void NAME_SEAL(                           \
       const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,    \
       const mq_pkt_desc* __restrict__ desc, uint32_t n, const uint32_t* __restrict__ index,               \
       const uint32_t* __restrict__ n_dev, const uint32_t* __restrict__ hot, uint8_t* __restrict__ status, \
       uint32_t* __restrict__ sched) {                                                                     \
     uint32_t skip;                                                                                        \
-    if (!aes_hot_split<SINGLE>(hot, kt, n_dev, skip) || !aes_wg_has_work<SINGLE>(n, n_dev, skip)) {       \
+    if (!aes_hot_split<SINGLE, G>(hot, kt, n_dev, skip) || !aes_wg_has_work<SINGLE, G>(n, n_dev, skip)) { \
       sched_done(sched);                                                                                  \
       return;                                                                                             \
     }                                                                                                     \
-    aes_tables<SINGLE>(kt);                                                                               \
-    aes_stream_tiles<SINGLE, false>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr,  \
+    aes_tables<SINGLE, G>(kt);                                                                            \
+    aes_stream_tiles<SINGLE, false, G>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, nullptr, \
                                     nullptr, skip, aes_sched(sched, SINGLE));                             \
     __syncthreads();                                                                                      \
     sched_done(sched);                                                                                    \
@@ -761,18 +772,20 @@ __device__ __forceinline__ TileSched aes_sched(uint32_t* sched, bool single) {
       const uint32_t* __restrict__ n_dev, const uint32_t* __restrict__ hot, uint8_t* __restrict__ status, \
       uint64_t* __restrict__ pn_out, const uint2* __restrict__ hpm, uint32_t* __restrict__ sched) {       \
     uint32_t skip;                                                                                        \
-    if (!aes_hot_split<SINGLE>(hot, kt, n_dev, skip) || !aes_wg_has_work<SINGLE>(n, n_dev, skip)) {       \
+    if (!aes_hot_split<SINGLE, G>(hot, kt, n_dev, skip) || !aes_wg_has_work<SINGLE, G>(n, n_dev, skip)) { \
       sched_done(sched);                                                                                  \
       return;                                                                                             \
     }                                                                                                     \
-    aes_tables<SINGLE>(kt);                                                                               \
-    aes_stream_tiles<SINGLE, true>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm, \
+    aes_tables<SINGLE, G>(kt);                                                                            \
+    aes_stream_tiles<SINGLE, true, G>(kt, n_rows, arena, arena_len, desc, n, index, n_dev, status, pn_out, hpm, \
                                    skip, aes_sched(sched, SINGLE));                                       \
     __syncthreads();                                                                                      \
     sched_done(sched);                                                                                    \
   }
-MQ_AES_KERNELS(mq_aes_seal_kernel, mq_aes_open_kernel, false)
-MQ_AES_KERNELS(mq_aes_seal1_kernel, mq_aes_open1_kernel, true)
+MQ_AES_KERNELS(mq_aes_seal_kernel, mq_aes_open_kernel, false, 8)
+MQ_AES_KERNELS(mq_aes_seal1_kernel, mq_aes_open1_kernel, true, 8)
+// narrow single-key kernels (r06): tiles of 16 short packets on 4 lanes each (AesStream G = 4)
+MQ_AES_KERNELS(mq_aes_seal1n_kernel, mq_aes_open1n_kernel, true, 4)
 
 // Key-segmented single-key kernels (r03): for a partition list in the keyed layout whose keys carry
 // many packets each (config C with 1024 keys: 128 tiles per key), every key's segment runs at
@@ -952,13 +965,47 @@ static uint32_t aes_grid(uint32_t tiles, uint32_t waves, int cus) {
 // list (hot key included) instead of the hot split + multi-key kernel.
 // sched_s / sched_hs: the schedule slots of streams s / hs (mq_runtime.h SchedSlots), null for the
 // static stride.
+// Flat single-key batches (bytes per packet bpp, 0 = unknown) up to MQ_AES_NARROW_MAX run the
+// narrow kernels: 16 packets per tile on 4 lanes each, so the per-tile fixed work (set-up, J0, the
+// final multiply, the header-protection block) is shared by twice the packets, the HP block of a
+// packet with at least 4 CTR blocks takes a free slot instead of a late extra round, and a packet's
+// slots fill whole iterations of 4 instead of 8 (1200 B: 76 slots in 19 iterations, not 80 in 10).
+// Measured (profiles/r06i_*): seal + open 64 B 150 -> 244 GiB/s, 256 B 421 -> 555, 700 B 651 -> 739,
+// 1200 B 732 -> 768 (config C: 3.18 -> 3.02 ms), 1500 B 758 -> 768; 1600 B 771 -> 759, 2048 B 796 -> 768
+// (r06j), so the octet kernels keep packets over 1536 B.
+#ifndef MQ_AES_NARROW_MAX
+#define MQ_AES_NARROW_MAX 1536
+#endif
+constexpr uint64_t kAesNarrowMaxBpp = MQ_AES_NARROW_MAX;
+int mq_aes_flat_narrow(uint64_t bpp) {
+  const long f = opt(Opt::AesNarrow);
+  if (f >= 0) return f != 0;
+  return bpp != 0 && bpp <= kAesNarrowMaxBpp;
+}
+
 hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena, uint64_t arena_len,
                          const mq_pkt_desc* desc, uint32_t n, const uint32_t* index, const uint32_t* n_dev,
                          const uint32_t* hot, uint8_t* status, uint64_t* pn_out, uint2* hpm, bool own_hp,
                          hipStream_t s, hipStream_t hs, int cus, const uint32_t* rowseg, uint32_t* sched_s,
-                         uint32_t* sched_hs) {
+                         uint32_t* sched_hs, uint64_t bpp) {
   const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
   if (tiles == 0) return hipSuccess;
+  if (n_rows == 1 && !index && !n_dev && !hot && mq_aes_flat_narrow(bpp)) {
+    const uint32_t waves = aes_waves(true), blocks = aes_grid((n + 15) / 16, waves, cus);
+    if (open && hpm && own_hp) {
+      hipLaunchKernelGGL(mq_aes_open_hp_kernel<true>, dim3((n + 255) / 256), dim3(256), 0, s, kt, n_rows, arena,
+                         arena_len, desc, n, index, n_dev, hpm);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+    if (open)
+      hipLaunchKernelGGL(mq_aes_open1n_kernel, dim3(blocks), dim3(64 * waves), 0, s, kt, n_rows, arena, arena_len, desc,
+                         n, index, n_dev, hot, status, pn_out, hpm, sched_s);
+    else
+      hipLaunchKernelGGL(mq_aes_seal1n_kernel, dim3(blocks), dim3(64 * waves), 0, s, kt, n_rows, arena, arena_len, desc,
+                         n, index, n_dev, hot, status, sched_s);
+    return hipGetLastError();
+  }
   if (rowseg && index && hot && n_rows > 1 && !own_hp) {
     const uint32_t blocks = (uint32_t)(cus > 0 ? cus : 256);
     if (open)
@@ -980,20 +1027,25 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
     if (e != hipSuccess) return e;
   }
   if (!hot) hs = s;
+  // the hot key's segment (a partition list: length classes up to 1350 B in config E) on the
+  // narrow kernels too, unless MQ_AES_NARROW=0
+  const bool hot_narrow = opt(Opt::AesNarrow) != 0;
   // the launch's own HP passes run on s: a forked hot kernel would race them
   if (own_hp && hs != s) return hipErrorInvalidValue;
   // two kernels at once on one stream's slot would share its heads
   if (hot && hs == s) sched_hs = nullptr;
   if (open) {
     if (hot)
-      hipLaunchKernelGGL(mq_aes_open1_kernel, dim3(hot_blocks), dim3(64 * aes_waves(true)), 0, hs, kt, n_rows,
-                         arena, arena_len, desc, n, index, n_dev, hot, status, pn_out, hpm, sched_hs);
+      hipLaunchKernelGGL(hot_narrow ? mq_aes_open1n_kernel : mq_aes_open1_kernel, dim3(hot_blocks),
+                         dim3(64 * aes_waves(true)), 0, hs, kt, n_rows, arena, arena_len, desc, n, index, n_dev, hot,
+                         status, pn_out, hpm, sched_hs);
     hipLaunchKernelGGL(n_rows == 1 ? mq_aes_open1_kernel : mq_aes_open_kernel, dim3(blocks), dim3(64 * waves),
                        0, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, hot, status, pn_out, hpm, sched_s);
   } else {
     if (hot)
-      hipLaunchKernelGGL(mq_aes_seal1_kernel, dim3(hot_blocks), dim3(64 * aes_waves(true)), 0, hs, kt, n_rows,
-                         arena, arena_len, desc, n, index, n_dev, hot, status, sched_hs);
+      hipLaunchKernelGGL(hot_narrow ? mq_aes_seal1n_kernel : mq_aes_seal1_kernel, dim3(hot_blocks),
+                         dim3(64 * aes_waves(true)), 0, hs, kt, n_rows, arena, arena_len, desc, n, index, n_dev, hot,
+                         status, sched_hs);
     hipLaunchKernelGGL(n_rows == 1 ? mq_aes_seal1_kernel : mq_aes_seal_kernel, dim3(blocks), dim3(64 * waves),
                        0, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, hot, status, sched_s);
   }

@@ -373,7 +373,33 @@ struct Grp {
     if (G == 4) return x;
     return x + half_mirror(x);
   }
+  static __device__ __forceinline__ uint32_t xr(uint32_t x) {  // XOR over the group
+    if (G == 1) return x;
+    x ^= quad_swap1(x);
+    if (G == 2) return x;
+    x ^= quad_swap2(x);
+    if (G == 4) return x;
+    return x ^ half_mirror(x);
+  }
+  template <int K>  // group lane K, to every lane of the group
+  static __device__ __forceinline__ uint32_t lane(uint32_t x) {
+    static_assert(K >= 0 && K < G, "lane of the group");
+    if (G == 1) return x;
+    if (G == 2) return qp<K | (K << 2) | ((K + 2) << 4) | ((K + 2) << 6)>(x);
+    if (G == 4) return qp<K | (K << 2) | (K << 4) | (K << 6)>(x);
+    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x18 | (K << 5));
+  }
+  // maximum over the wave of a GROUP-UNIFORM value (fold the groups of an octet, then the octets)
+  static __device__ __forceinline__ uint32_t wave_max(uint32_t x);
+  static __device__ __forceinline__ uint32_t wave_min(uint32_t x) { return ~wave_max(~x); }
 };
+template <int G>
+__device__ __forceinline__ uint32_t Grp<G>::wave_max(uint32_t x) {
+  if (G <= 2) x = max(x, quad_swap2(x));
+  if (G <= 4) x = max(x, half_mirror(x));
+  if (G == 1) x = max(x, quad_swap1(x));
+  return wave_max_u32(x);
+}
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t x) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) {

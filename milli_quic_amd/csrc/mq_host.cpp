@@ -23,12 +23,13 @@
 using mq::KeyRow;
 
 int mq_chacha_flat_kind(uint64_t bpp);  // mq_chacha.hip
+int mq_aes_flat_narrow(uint64_t bpp);   // mq_aes.hip
 
 // ---- diagnostic switches (mq_opts.h) ---------------------------------------------------------
 namespace {
 const char* const kOptNames[(int)mq::Opt::Count] = {
     "MQ_CC_NARROW", "MQ_CC_LONG",  "MQ_CC_LIST",           "MQ_HP_FORK", "MQ_AES_SEG",
-    "MQ_PROTECT_FUSED", "MQ_RESIDENT", "MQ_RESIDENT_TIMEOUT_US", "MQ_RECV_SEG"};
+    "MQ_PROTECT_FUSED", "MQ_RESIDENT", "MQ_RESIDENT_TIMEOUT_US", "MQ_RECV_SEG", "MQ_AES_NARROW"};
 std::atomic<long> g_opts[(int)mq::Opt::Count];
 std::once_flag g_opts_once;
 void opts_init() {  // once: the environment's values (shell-driven diagnostics keep working)
@@ -69,6 +70,12 @@ extern "C" int mq_debug_chacha_flat_kind(uint64_t arena_len, uint32_t n, uint32_
   return mq_chacha_flat_kind(len_hint ? len_hint : (arena_len + n - 1) / n);
 }
 
+extern "C" int mq_debug_aes_flat_kind(uint64_t arena_len, uint32_t n, uint32_t suite_hint) {
+  const uint64_t len_hint = suite_hint >> 16;
+  if (n == 0) return -1;
+  return mq_aes_flat_narrow(len_hint ? len_hint : (arena_len + n - 1) / n) ? 0 : 1;
+}
+
 extern "C" long mq_debug_option_get(const char* name) {
   if (!name) return -2;
   for (int k = 0; k < (int)mq::Opt::Count; ++k)
@@ -90,7 +97,7 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
                          const uint32_t* index, const uint32_t* n_dev, const uint32_t* hot,
                          uint8_t* status, uint64_t* pn_out, uint2* hpm, bool own_hp, hipStream_t s,
                          hipStream_t hot_stream, int cus, const uint32_t* rowseg, uint32_t* sched_s,
-                         uint32_t* sched_hs);
+                         uint32_t* sched_hs, uint64_t bpp = 0);
 const uint32_t* mq_partition_rowseg(uint32_t n, uint32_t n_rows, const uint32_t* counts);
 hipError_t mq_launch_mixed_open_hp(const KeyRow* kt, uint32_t n_rows, const uint8_t* arena, uint64_t arena_len,
                                    const mq_pkt_desc* desc, uint32_t n, uint2* hpm, hipStream_t s);
@@ -971,7 +978,7 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
                          s, cus, nullptr, -1, false, nullptr, bpp);
   } else if (suite_hint == MQ_SUITE_AES128GCM && (kt->rows == 1 || !ws || n > (1u << 30))) {
     e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, n, nullptr, nullptr, nullptr, status, pn_out,
-                      hpm, true, s, s, cus, nullptr, sched_slot(kt->device, s), nullptr);
+                      hpm, true, s, s, cus, nullptr, sched_slot(kt->device, s), nullptr, bpp);
   } else if (suite_hint == MQ_SUITE_MIXED || suite_hint == MQ_SUITE_AES128GCM) {
     // the two index lists (2 x mq_partition_list_cap(n) entries, holes included) are addressed
     // with 32-bit positions: up to 2^30 packets per mixed batch. An AES batch over several key

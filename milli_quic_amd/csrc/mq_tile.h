@@ -343,10 +343,11 @@ __device__ __forceinline__ bool write_unmasked_header(const S& sp, typename S::o
 // Descriptor words of a tile fetched ahead of time (for_tiles): lane 8p + j holds dword j of
 // packet p's descriptor (dw) and, for open, dword j < 2 of its HP mask (hm), and idx = packet p's
 // descriptor index (kListHole for a hole of an index list); octet swizzles rebuild the
-// descriptor, so a prefetch costs three VGPRs.
+// descriptor, so a prefetch costs three VGPRs. Tiles of 16 packets on 4 lanes each (the narrow AES
+// kernels): lane 4p + j holds dwords 2j (dw) and 2j + 1 (dw1).
 struct TilePrefetch {
   bool on;  // wave-uniform
-  uint32_t dw, hm, idx;
+  uint32_t dw, hm, idx, dw1;
 };
 
 template <int K>
@@ -356,15 +357,16 @@ __device__ __forceinline__ uint32_t oct_lane(uint32_t x) {  // lane K of the oct
 
 // Per-lane packet context of tile `tile_id` (descriptor from the prefetch or from memory, HP
 // pre-pass values, validation). Returns false when the tile lies past the batch (wave-uniform).
-template <uint32_t SUITE, bool OPEN, bool SINGLE_KEY>
+template <uint32_t SUITE, bool OPEN, bool SINGLE_KEY, int G = kLanesPerPkt>
 __device__ __forceinline__ bool tile_ctx(uint32_t tile_id, const KeyRow* __restrict__ kt, uint32_t n_rows,
                                          uint64_t arena_len, const mq_pkt_desc* __restrict__ desc, uint32_t n,
                                          const uint32_t* __restrict__ index, const uint32_t* __restrict__ n_dev,
                                          const uint2* __restrict__ hpm, const TilePrefetch& pf, PktCtx& c,
                                          const KeyRow*& row, uint32_t tid = threadIdx.x) {
-  const int lane = tid & (kWave - 1), p = lane / kLanesPerPkt;
+  static_assert(G == 8 || G == 4, "tiles of 8 or 16 packets");
+  const int lane = tid & (kWave - 1), p = lane / G;
   const uint32_t count = n_dev ? *n_dev : n;
-  const uint32_t tile0 = tile_id * kPktsPerTile;
+  const uint32_t tile0 = tile_id * (uint32_t)(kWave / G);
   if (tile0 >= count) return false;  // wave-uniform
   c.tile = tile_id;
   const uint32_t t = tile0 + p;
@@ -374,15 +376,24 @@ __device__ __forceinline__ bool tile_ctx(uint32_t tile_id, const KeyRow* __restr
   if (pf.on) {  // words already in registers
     c.i = c.valid ? pf.idx : 0u;
     if (c.i == kListHole) { c.valid = false; c.i = 0; }
-    const uint32_t w0 = oct_lane<0>(pf.dw), w1 = oct_lane<1>(pf.dw), w2 = oct_lane<2>(pf.dw),
-                   w3 = oct_lane<3>(pf.dw), w4 = oct_lane<4>(pf.dw), w5 = oct_lane<5>(pf.dw),
-                   w6 = oct_lane<6>(pf.dw), w7 = oct_lane<7>(pf.dw);
+    uint32_t w0, w1, w2, w3, w4, w5, w6, w7;
+    if (G == 8) {
+      w0 = oct_lane<0>(pf.dw); w1 = oct_lane<1>(pf.dw); w2 = oct_lane<2>(pf.dw); w3 = oct_lane<3>(pf.dw);
+      w4 = oct_lane<4>(pf.dw); w5 = oct_lane<5>(pf.dw); w6 = oct_lane<6>(pf.dw); w7 = oct_lane<7>(pf.dw);
+    } else {
+      w0 = Grp<4>::lane<0>(pf.dw); w1 = Grp<4>::lane<0>(pf.dw1); w2 = Grp<4>::lane<1>(pf.dw);
+      w3 = Grp<4>::lane<1>(pf.dw1); w4 = Grp<4>::lane<2>(pf.dw); w5 = Grp<4>::lane<2>(pf.dw1);
+      w6 = Grp<4>::lane<3>(pf.dw); w7 = Grp<4>::lane<3>(pf.dw1);
+    }
     c.d.offset = (uint64_t)w1 << 32 | w0;
     c.d.len = w2; c.d.key_id = w3;
     c.d.pn = (uint64_t)w5 << 32 | w4;
     c.d.pn_offset = (uint16_t)w6; c.d.pn_len = (uint8_t)(w6 >> 16); c.d.flags = (uint8_t)(w6 >> 24);
     c.d.reserved = w7;
-    if (OPEN && hpm) { c.hm0 = oct_lane<0>(pf.hm); c.hm1 = oct_lane<1>(pf.hm); }
+    if (OPEN && hpm) {
+      c.hm0 = G == 8 ? oct_lane<0>(pf.hm) : Grp<4>::lane<0>(pf.hm);
+      c.hm1 = G == 8 ? oct_lane<1>(pf.hm) : Grp<4>::lane<1>(pf.hm);
+    }
     if (!c.valid) {
       c.d.offset = 0; c.d.len = 0; c.d.key_id = 0; c.d.pn = 0; c.d.pn_offset = 0; c.d.pn_len = 0;
       c.d.flags = 0; c.d.reserved = 0;
@@ -537,13 +548,14 @@ __device__ __forceinline__ void sched_done(uint32_t* ctr) {
 // tile further ahead still (list entry, then descriptor: two dependent loads off the critical
 // path). Tiles below `base` are not this launch's. With a device-side count (n_dev) the tiles end
 // at that count.
-template <bool OPEN, class F>
+template <bool OPEN, int G = kLanesPerPkt, class F>
 __device__ __forceinline__ void for_tiles(const TileSched& ts, const mq_pkt_desc* __restrict__ desc, uint32_t n,
                                           const uint32_t* __restrict__ index, const uint32_t* __restrict__ n_dev,
                                           const uint2* __restrict__ hpm, F&& body, uint32_t base = 0) {
+  constexpr uint32_t PPT = kWave / G;  // packets per tile
   const uint32_t count = n_dev ? *n_dev : n;
-  const uint32_t tiles = (count + kPktsPerTile - 1) / kPktsPerTile;
-  const uint32_t lane = threadIdx.x & (kWave - 1), p = lane / kLanesPerPkt, j = lane % kLanesPerPkt;
+  const uint32_t tiles = (count + PPT - 1) / PPT;
+  const uint32_t lane = threadIdx.x & (kWave - 1), p = lane / G, j = lane % G;
   constexpr uint32_t kNone = 0xFFFFFFFFu;
   // dynamic schedule (wave-uniform state): the tiles from dyn0 on, in blocks dealt to the heads
   const uint32_t dyn0 = base + ts.waves;
@@ -627,25 +639,32 @@ __device__ __forceinline__ void for_tiles(const TileSched& ts, const mq_pkt_desc
     return tile_of(ch, ce);
   };
   auto idx_of = [&](uint32_t t) -> uint32_t {  // packet p's descriptor index (list: a load)
-    const uint32_t e = t * kPktsPerTile + p;
+    const uint32_t e = t * PPT + p;
     if (t >= tiles || e >= count) return kListHole;
     return index ? index[e] : e;
   };
-  auto fetch = [&](uint32_t ix, uint32_t& dw, uint32_t& hm) {
+  auto fetch = [&](uint32_t ix, uint32_t& dw, uint32_t& dw1, uint32_t& hm) {
     const bool ok = ix != kListHole;
-    dw = ok ? reinterpret_cast<const uint32_t*>(desc)[(size_t)ix * 8 + j] : 0u;
+    if (G == 8) {
+      dw = ok ? reinterpret_cast<const uint32_t*>(desc)[(size_t)ix * 8 + j] : 0u;
+      dw1 = 0;
+    } else {
+      const uint2 v = ok ? reinterpret_cast<const uint2*>(desc)[(size_t)ix * 4 + j] : make_uint2(0, 0);
+      dw = v.x;
+      dw1 = v.y;
+    }
     hm = (OPEN && hpm && ok && j < 2) ? reinterpret_cast<const uint32_t*>(hpm)[(size_t)ix * 2 + j] : 0u;
   };
   uint32_t t = base + ts.g;
   if (ts.ctr && t < tiles) issue();  // resolved right away by next(t): one wait per wave, at its start
   uint32_t t1 = next(t);
-  uint32_t ix0 = idx_of(t), ix1 = idx_of(t1), dw, hm;
-  fetch(ix0, dw, hm);
+  uint32_t ix0 = idx_of(t), ix1 = idx_of(t1), dw, dw1, hm;
+  fetch(ix0, dw, dw1, hm);
   while (t < tiles) {
-    const TilePrefetch pf{true, dw, hm, ix0};
+    const TilePrefetch pf{true, dw, hm, ix0, dw1};
     const uint32_t t2 = next(t1);
     const uint32_t ix2 = idx_of(t2);
-    fetch(ix1, dw, hm);
+    fetch(ix1, dw, dw1, hm);
     body(t, pf);
     t = t1; t1 = t2; ix0 = ix1; ix1 = ix2;
   }

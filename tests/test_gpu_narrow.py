@@ -59,12 +59,12 @@ def oracle_run(orc, keys, arena, desc, open_=False, hint=CHACHA):
     return a, orc.batch_seal(keys, a, desc, hint, threads=8), None
 
 
-def short_batch(n, lmin, lmax, n_keys=1, seed=1, long_frac=0.2, lead=0):
-    """n ChaCha20 packets of random lengths in [lmin, lmax] packed back to back after `lead` bytes:
+def short_batch(n, lmin, lmax, n_keys=1, seed=1, long_frac=0.2, lead=0, suite=CHACHA):
+    """n packets (ChaCha20, or `suite`) of random lengths in [lmin, lmax] packed back to back after `lead` bytes:
     short headers (DCID 8) or long ones (26-B Initial layout), pn_len 1..4, key row i mod n_keys.
     The arena ends exactly at the last packet (its length is usually not a multiple of 16)."""
     rng = np.random.default_rng(seed)
-    keys = workload.uniform_keys(CHACHA, n_keys)
+    keys = workload.uniform_keys(suite, n_keys)
     pn_len = rng.integers(1, 5, size=n).astype(np.uint8)
     long_h = rng.random(n) < long_frac
     pn_off = np.where(long_h, workload.LONG_HDR, workload.SHORT_HDR).astype(np.int64)
@@ -87,17 +87,17 @@ def short_batch(n, lmin, lmax, n_keys=1, seed=1, long_frac=0.2, lead=0):
     return keys, arena, sd, od, pns
 
 
-def roundtrip_vs_oracle(orc, keys, arena, sd, od, pns, modes=(None, "0", "1")):
-    o_out, o_st, _ = oracle_run(orc, keys, arena, sd)
-    o_back, o_st2, o_pn = oracle_run(orc, keys, o_out, od, open_=True)
+def roundtrip_vs_oracle(orc, keys, arena, sd, od, pns, modes=(None, "0", "1"), hint=CHACHA, env=_Env):
+    o_out, o_st, _ = oracle_run(orc, keys, arena, sd, hint=hint)
+    o_back, o_st2, o_pn = oracle_run(orc, keys, o_out, od, open_=True, hint=hint)
     assert (o_st == 0).all() and (o_st2 == 0).all()
     for mode in modes:
-        with _Env(mode):
+        with env(mode):
             for use_ws in (True, False):
-                g_out, g_st, _ = gpu_run(keys, arena, sd, use_ws=use_ws)
+                g_out, g_st, _ = gpu_run(keys, arena, sd, use_ws=use_ws, hint=hint)
                 assert (g_st == o_st).all(), (mode, use_ws, np.nonzero(g_st != o_st)[0][:8])
                 assert g_out.tobytes() == o_out.tobytes(), (mode, use_ws)
-                g_back, g_st, g_pn = gpu_run(keys, o_out, od, open_=True, use_ws=use_ws)
+                g_back, g_st, g_pn = gpu_run(keys, o_out, od, open_=True, use_ws=use_ws, hint=hint)
                 assert (g_st == o_st2).all(), (mode, use_ws)
                 assert g_back.tobytes() == o_back.tobytes(), (mode, use_ws)
                 assert (g_pn == o_pn).all() and (g_pn == pns).all(), (mode, use_ws)
@@ -242,3 +242,89 @@ def test_subrange_batch_len_hint(orc, hinted):
     assert (g_st == 0).all() and (g_pn == w.pns[lo:hi]).all()
     v = g_back.reshape(-1, 1200)[lo:hi, :1184]
     assert v.tobytes() == w.arena.reshape(-1, 1200)[lo:hi, :1184].tobytes()
+
+
+# ---- narrow AES-128-GCM tiles (r06, VERDICT r04 #1 "both suites"): flat single-key batches of short
+# packets run 16 packets per tile on 4 lanes each (mq_aes.hip AesStream G = 4, the H^4 Horner
+# multiplier, the header-protection block in the free slot nblk once a packet has 4 CTR blocks);
+# MQ_AES_NARROW 0 / 1 forces the octet / narrow kernels. Reference: rustcrypto.rs:38-94 (seal /
+# open), :175-186 (header protection), transmit.rs:625-755, recv.rs:340-421.
+AES = _lib.MQ_SUITE_AES128GCM
+
+
+def _EnvAes(v):
+    """MQ_AES_NARROW for the calls inside the block (mq_debug_option)."""
+    return _lib.option("MQ_AES_NARROW", v)
+
+
+@pytest.mark.parametrize("lmin,lmax,n", [
+    (21, 90, 3001),      # nblk < 4 (the late HP block) and >= 4 (HP in slot nblk), a ragged last tile
+    (64, 64, 2048),      # uniform 64 B (the len_sweep shape)
+    (90, 300, 1500),     # several iterations per tile, AAD of 1-2 blocks
+    (21, 640, 4000),     # lean iterations beside short packets in one wave
+])
+def test_aes_narrow_flat_vs_oracle(orc, lmin, lmax, n):
+    keys, arena, sd, od, pns = short_batch(n, lmin, lmax, 1, seed=lmin * 5 + lmax, suite=AES)
+    roundtrip_vs_oracle(orc, keys, arena, sd, od, pns, hint=AES, env=_EnvAes)
+
+
+@pytest.mark.parametrize("lead", [0, 5, 13])
+def test_aes_narrow_uniform_alignments(orc, lead):
+    for L in (64, 256, 448):
+        w = workload.uniform(555, AES, L=L, pn_len=1 + L % 4)
+        arena = np.concatenate([np.full(lead, 0x5A, np.uint8), w.arena])
+        sd, od = w.seal_desc.copy(), w.open_desc.copy()
+        sd["offset"] += lead
+        od["offset"] += lead
+        roundtrip_vs_oracle(orc, w.keys, arena, sd, od, w.pns, modes=(None, "0", "1"), hint=AES, env=_EnvAes)
+
+
+def test_aes_narrow_forced_on_long_packets(orc):
+    # MQ_AES_NARROW=1 on packets up to 4500 B: counters past 255 (no CTR cache), long AAD, many
+    # lean iterations; open over 2048 B with MQ_PKT_NO_RECV_LIMIT
+    keys, arena, sd, od, pns = short_batch(900, 21, 4500, 1, seed=123, long_frac=0.5, suite=AES)
+    od = od.copy()
+    od["flags"] |= _lib.MQ_PKT_NO_RECV_LIMIT
+    roundtrip_vs_oracle(orc, keys, arena, sd, od, pns, modes=("1",), hint=AES, env=_EnvAes)
+
+
+def test_aes_narrow_failures_match_oracle(orc):
+    keys, arena, sd, od, pns = short_batch(2500, 21, 400, 1, seed=6, suite=AES)
+    sealed, st, _ = oracle_run(orc, keys, arena, sd, hint=AES)
+    assert (st == 0).all()
+    rng = np.random.default_rng(9)
+    bad = sealed.copy()
+    for v in rng.choice(len(sd), size=300, replace=False):  # one flipped bit anywhere in the packet
+        o, L = int(sd["offset"][v]), int(sd["len"][v])
+        bad[o + int(rng.integers(0, L))] ^= 1 << int(rng.integers(0, 8))
+    od = od.copy()
+    od["key_id"][3] = 77                   # key id out of range
+    od["len"][4] = 24                      # sample out of range -> Crypto
+    od["offset"][6] = len(bad) - 10        # past the arena end
+    od["pn"][9] = (1 << 62) - 2            # decode_pn above 2^62 - 1 -> ProtocolViolation
+    o_out, o_st, o_pn = oracle_run(orc, keys, bad, od, open_=True, hint=AES)
+    assert (o_st != 0).sum() >= 250
+    for mode in (None, "0", "1"):
+        with _EnvAes(mode):
+            for use_ws in (True, False):
+                g_out, g_st, g_pn = gpu_run(keys, bad, od, open_=True, use_ws=use_ws, hint=AES)
+                assert (g_st == o_st).all(), (mode, use_ws, np.nonzero(g_st != o_st)[0][:8])
+                assert g_out.tobytes() == o_out.tobytes(), (mode, use_ws)
+                ok = o_st == 0
+                assert (g_pn[ok] == o_pn[ok]).all()
+    sd = sd.copy()
+    sd["pn_len"][3] = 0
+    sd["len"][9] = 20
+    sd["key_id"][10] = 1 << 20
+    o_out, o_st, _ = oracle_run(orc, keys, arena, sd, hint=AES)
+    for mode in (None, "1"):
+        with _EnvAes(mode):
+            g_out, g_st, _ = gpu_run(keys, arena, sd, hint=AES)
+            assert (g_st == o_st).all() and g_out.tobytes() == o_out.tobytes()
+
+
+@pytest.mark.parametrize("n", [1, 2, 15, 16, 17, 191, 192, 193, 3073])
+def test_aes_narrow_counts(orc, n):
+    # tiles with one packet, exactly full tiles / workgroups (12 waves x 16 packets), partial ones
+    keys, arena, sd, od, pns = short_batch(n, 21, 200, 1, seed=n + 1000, suite=AES)
+    roundtrip_vs_oracle(orc, keys, arena, sd, od, pns, modes=(None, "1"), hint=AES, env=_EnvAes)
