@@ -647,7 +647,7 @@ __device__ __forceinline__ void aes_stream_tiles(const KeyRow* __restrict__ kt, 
                                                  const uint32_t* __restrict__ index,
                                                  const uint32_t* __restrict__ n_dev, uint8_t* __restrict__ status,
                                                  uint64_t* __restrict__ pn_out, const uint2* __restrict__ hpm,
-                                                 uint32_t skip, const TileSched& ts) {
+                                                 uint32_t skip, const TileSched& ts, uint32_t e0 = 0) {
   const uint32_t w = wave_id();
   static_assert(SINGLE || G == kLanesPerPkt, "narrow tiles: single-key kernels only");
   const int lane = (int)(threadIdx.x & (kWave - 1)), j = lane & (G - 1);
@@ -657,7 +657,7 @@ __device__ __forceinline__ void aes_stream_tiles(const KeyRow* __restrict__ kt, 
     PktCtx c;
     const KeyRow* row;
     if (!tile_ctx<MQ_SUITE_AES128GCM, OPEN, SINGLE, G>(t, kt, n_rows, arena_len, desc, n, index, n_dev, hpm, pf, c,
-                                                       row))
+                                                       row, threadIdx.x, e0))
       return;
     MQ_STAMP(t, 0);
     // CTR caching needs every counter < 256: packets of at most 4080 bytes
@@ -706,7 +706,7 @@ __device__ __forceinline__ void aes_stream_tiles(const KeyRow* __restrict__ kt, 
     }
     MQ_STAMP(t, 7);
     tile_status<OPEN>(c, j, status, pn_out);
-  }, skip);
+  }, skip, e0);
 }
 
 // hot (partition lists only, else null): hot[0] = the hot key's row, hot[1] = the entries of its
@@ -823,7 +823,7 @@ __device__ __forceinline__ uint32_t seg_row_of(const uint32_t* __restrict__ rows
   return lo;
 }
 
-template <bool OPEN>
+template <bool OPEN, int G>
 __device__ __forceinline__ void aes_seg_tiles(const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena,
                                               uint64_t arena_len, const mq_pkt_desc* __restrict__ desc,
                                               const uint32_t* __restrict__ list, const uint32_t* __restrict__ n_dev,
@@ -866,31 +866,36 @@ __device__ __forceinline__ void aes_seg_tiles(const KeyRow* __restrict__ kt, uin
         const KeyRow* ks = kt + row;  // the segment's row as a one-row table (validation uses n_rows)
         if (row != built) {
           __syncthreads();  // the previous segment's tiles are done with the tables
-          aes_key_tables(ks);  // ends with a barrier
+          aes_key_tables<G>(ks);  // ends with a barrier
           built = row;
         }
-        aes_stream_tiles<true, OPEN>(ks, n_rows, arena, arena_len, desc, end, list, nullptr, status, pn_out, hpm,
-                                     e / kPktsPerTile, TileSched{nullptr, w, W, 0});
+        aes_stream_tiles<true, OPEN, G>(ks, n_rows, arena, arena_len, desc, end, list, nullptr, status, pn_out, hpm,
+                                        0, TileSched{nullptr, w, W, 0}, e);
       }
       e = end;
     }
   }
   sched_done(sched);  // after the loop's last barrier
 }
-extern "C" __global__ __launch_bounds__(64 * aes_seg_waves()) void mq_aes_seals_kernel(
-    const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
-    const mq_pkt_desc* __restrict__ desc, const uint32_t* __restrict__ list, const uint32_t* __restrict__ n_dev,
-    const uint32_t* __restrict__ hot, const uint32_t* __restrict__ rowseg, uint8_t* __restrict__ status,
-    uint32_t* __restrict__ sched) {
-  aes_seg_tiles<false>(kt, n_rows, arena, arena_len, desc, list, n_dev, hot, rowseg, status, nullptr, nullptr, sched);
-}
-extern "C" __global__ __launch_bounds__(64 * aes_seg_waves()) void mq_aes_opens_kernel(
-    const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,
-    const mq_pkt_desc* __restrict__ desc, const uint32_t* __restrict__ list, const uint32_t* __restrict__ n_dev,
-    const uint32_t* __restrict__ hot, const uint32_t* __restrict__ rowseg, uint8_t* __restrict__ status,
-    uint64_t* __restrict__ pn_out, const uint2* __restrict__ hpm, uint32_t* __restrict__ sched) {
-  aes_seg_tiles<true>(kt, n_rows, arena, arena_len, desc, list, n_dev, hot, rowseg, status, pn_out, hpm, sched);
-}
+#define MQ_AES_SEG_KERNELS(NAME_SEAL, NAME_OPEN, G)                                                                 \
+  extern "C" __global__ __launch_bounds__(64 * aes_seg_waves()) void NAME_SEAL(                                     \
+      const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,             \
+      const mq_pkt_desc* __restrict__ desc, const uint32_t* __restrict__ list, const uint32_t* __restrict__ n_dev, \
+      const uint32_t* __restrict__ hot, const uint32_t* __restrict__ rowseg, uint8_t* __restrict__ status,         \
+      uint32_t* __restrict__ sched) {                                                                              \
+    aes_seg_tiles<false, G>(kt, n_rows, arena, arena_len, desc, list, n_dev, hot, rowseg, status, nullptr, nullptr, \
+                            sched);                                                                                \
+  }                                                                                                                \
+  extern "C" __global__ __launch_bounds__(64 * aes_seg_waves()) void NAME_OPEN(                                     \
+      const KeyRow* __restrict__ kt, uint32_t n_rows, uint8_t* __restrict__ arena, uint64_t arena_len,             \
+      const mq_pkt_desc* __restrict__ desc, const uint32_t* __restrict__ list, const uint32_t* __restrict__ n_dev, \
+      const uint32_t* __restrict__ hot, const uint32_t* __restrict__ rowseg, uint8_t* __restrict__ status,         \
+      uint64_t* __restrict__ pn_out, const uint2* __restrict__ hpm, uint32_t* __restrict__ sched) {                \
+    aes_seg_tiles<true, G>(kt, n_rows, arena, arena_len, desc, list, n_dev, hot, rowseg, status, pn_out, hpm, sched); \
+  }
+MQ_AES_SEG_KERNELS(mq_aes_seals_kernel, mq_aes_opens_kernel, 8)
+// narrow tiles (16 packets on 4 lanes each) within every key's segment (r06)
+MQ_AES_SEG_KERNELS(mq_aes_sealsn_kernel, mq_aes_opensn_kernel, 4)
 
 extern "C" __global__ __launch_bounds__(256) void mq_aes_hp_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, const uint32_t* __restrict__ key_ids,
@@ -1006,14 +1011,19 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
                          n, index, n_dev, hot, status, sched_s);
     return hipGetLastError();
   }
+  // the hot key's segment of a partition list, and the key-segmented kernels' segments, run narrow
+  // tiles too, unless MQ_AES_NARROW=0
+  const bool hot_narrow = opt(Opt::AesNarrow) != 0;
   if (rowseg && index && hot && n_rows > 1 && !own_hp) {
     const uint32_t blocks = (uint32_t)(cus > 0 ? cus : 256);
     if (open)
-      hipLaunchKernelGGL(mq_aes_opens_kernel, dim3(blocks), dim3(64 * aes_seg_waves()), 0, s, kt, n_rows, arena,
-                         arena_len, desc, index, n_dev, hot, rowseg, status, pn_out, hpm, sched_s);
+      hipLaunchKernelGGL(hot_narrow ? mq_aes_opensn_kernel : mq_aes_opens_kernel, dim3(blocks),
+                         dim3(64 * aes_seg_waves()), 0, s, kt, n_rows, arena, arena_len, desc, index, n_dev, hot,
+                         rowseg, status, pn_out, hpm, sched_s);
     else
-      hipLaunchKernelGGL(mq_aes_seals_kernel, dim3(blocks), dim3(64 * aes_seg_waves()), 0, s, kt, n_rows, arena,
-                         arena_len, desc, index, n_dev, hot, rowseg, status, sched_s);
+      hipLaunchKernelGGL(hot_narrow ? mq_aes_sealsn_kernel : mq_aes_seals_kernel, dim3(blocks),
+                         dim3(64 * aes_seg_waves()), 0, s, kt, n_rows, arena, arena_len, desc, index, n_dev, hot,
+                         rowseg, status, sched_s);
     return hipGetLastError();
   }
   const uint32_t waves = aes_waves(n_rows == 1), blocks = aes_grid(tiles, waves, cus);
@@ -1027,9 +1037,6 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
     if (e != hipSuccess) return e;
   }
   if (!hot) hs = s;
-  // the hot key's segment (a partition list: length classes up to 1350 B in config E) on the
-  // narrow kernels too, unless MQ_AES_NARROW=0
-  const bool hot_narrow = opt(Opt::AesNarrow) != 0;
   // the launch's own HP passes run on s: a forked hot kernel would race them
   if (own_hp && hs != s) return hipErrorInvalidValue;
   // two kernels at once on one stream's slot would share its heads

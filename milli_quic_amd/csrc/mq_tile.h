@@ -362,11 +362,11 @@ __device__ __forceinline__ bool tile_ctx(uint32_t tile_id, const KeyRow* __restr
                                          uint64_t arena_len, const mq_pkt_desc* __restrict__ desc, uint32_t n,
                                          const uint32_t* __restrict__ index, const uint32_t* __restrict__ n_dev,
                                          const uint2* __restrict__ hpm, const TilePrefetch& pf, PktCtx& c,
-                                         const KeyRow*& row, uint32_t tid = threadIdx.x) {
+                                         const KeyRow*& row, uint32_t tid = threadIdx.x, uint32_t e0 = 0) {
   static_assert(G == 8 || G == 4, "tiles of 8 or 16 packets");
   const int lane = tid & (kWave - 1), p = lane / G;
   const uint32_t count = n_dev ? *n_dev : n;
-  const uint32_t tile0 = tile_id * (uint32_t)(kWave / G);
+  const uint32_t tile0 = e0 + tile_id * (uint32_t)(kWave / G);  // its first entry
   if (tile0 >= count) return false;  // wave-uniform
   c.tile = tile_id;
   const uint32_t t = tile0 + p;
@@ -547,14 +547,15 @@ __device__ __forceinline__ void sched_done(uint32_t* ctr) {
 // starts without waiting on a descriptor fetch; with an index list the list entries are read one
 // tile further ahead still (list entry, then descriptor: two dependent loads off the critical
 // path). Tiles below `base` are not this launch's. With a device-side count (n_dev) the tiles end
-// at that count.
+// at that count. Tile t holds entries e0 + PPT t .. e0 + PPT t + PPT - 1 (e0: the key-segmented
+// kernels' segment start, which need not be a multiple of PPT).
 template <bool OPEN, int G = kLanesPerPkt, class F>
 __device__ __forceinline__ void for_tiles(const TileSched& ts, const mq_pkt_desc* __restrict__ desc, uint32_t n,
                                           const uint32_t* __restrict__ index, const uint32_t* __restrict__ n_dev,
-                                          const uint2* __restrict__ hpm, F&& body, uint32_t base = 0) {
+                                          const uint2* __restrict__ hpm, F&& body, uint32_t base = 0, uint32_t e0 = 0) {
   constexpr uint32_t PPT = kWave / G;  // packets per tile
   const uint32_t count = n_dev ? *n_dev : n;
-  const uint32_t tiles = (count + PPT - 1) / PPT;
+  const uint32_t tiles = count > e0 ? (count - e0 + PPT - 1) / PPT : 0u;
   const uint32_t lane = threadIdx.x & (kWave - 1), p = lane / G, j = lane % G;
   constexpr uint32_t kNone = 0xFFFFFFFFu;
   // dynamic schedule (wave-uniform state): the tiles from dyn0 on, in blocks dealt to the heads
@@ -639,7 +640,7 @@ __device__ __forceinline__ void for_tiles(const TileSched& ts, const mq_pkt_desc
     return tile_of(ch, ce);
   };
   auto idx_of = [&](uint32_t t) -> uint32_t {  // packet p's descriptor index (list: a load)
-    const uint32_t e = t * PPT + p;
+    const uint32_t e = e0 + t * PPT + p;
     if (t >= tiles || e >= count) return kListHole;
     return index ? index[e] : e;
   };
