@@ -226,8 +226,8 @@ long mq_debug_option_get(const char* name);
  * this suite_hint (MQ_BATCH_LEN_HINT included): 0 narrow tiles (short packets), 1 octet tiles over
  * 10-KiB images, 2 over 13-KiB, 3 over 20-KiB images; -1 for n = 0. (Diagnostic switches aside.) */
 int mq_debug_chacha_flat_kind(uint64_t arena_len, uint32_t n, uint32_t suite_hint);
-/* The same for a flat single-key AES-128-GCM batch: 0 narrow tiles (16 short packets per wave),
- * 1 octet tiles; -1 for n = 0. */
+/* The same for a flat single-key AES-128-GCM batch: its lanes per packet — 2 (tiles of 32 short
+ * packets), 4 (16 packets) or 8 (octet tiles); -1 for n = 0. */
 int mq_debug_aes_flat_kind(uint64_t arena_len, uint32_t n, uint32_t suite_hint);
 
 /* ---- CryptoProvider::aead / Aead (per packet, host buffers; runs the HIP kernels) ----------- */

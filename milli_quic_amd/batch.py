@@ -179,6 +179,6 @@ def flat_kind(arena_len, n, suite_hint):
 
 
 def aes_flat_kind(arena_len, n, suite_hint):
-    """The flat single-key AES-128-GCM kernel family a batch would run (mq_debug_aes_flat_kind):
-    0 narrow tiles (16 short packets per wave), 1 octet tiles."""
+    """Lanes per packet of the flat single-key AES-128-GCM kernels a batch would run
+    (mq_debug_aes_flat_kind): 2 (32 packets per wave), 4 (16) or 8 (octet tiles)."""
     return _lib.load().mq_debug_aes_flat_kind(int(arena_len), int(n), int(suite_hint))

@@ -161,7 +161,11 @@ enum GhMode { kGhWorkgroup, kGhWave, kGhProduct };
 // multiplier is H^G (the workgroup's byte-position table holds H^G: aes_key_tables<G>).
 template <bool SINGLE, int GH, int G = kLanesPerPkt>
 struct AesStream {
-  static_assert(G == 8 || (G == 4 && GH == kGhWorkgroup), "narrow tiles: single-key kernels only");
+  static_assert(G == 8 || ((G == 4 || G == 2) && GH == kGhWorkgroup), "narrow tiles: single-key kernels only");
+  // seal: the HP sample (slots 1 and 2) is complete after iteration kSmpIt; the HP block can take
+  // slot nblk when that slot lies in a later iteration
+  static constexpr int kSmpIt = G >= 4 ? 0 : 1;
+  static constexpr uint32_t kHpSlotMin = G >= 4 ? (uint32_t)G : 4u;
   using Gp = Grp<G>;
   // AES of slot b (b >= 0) from the CTR cache or full rounds; keystream as little-endian words
   template <bool CACHED, class K>
@@ -266,7 +270,7 @@ struct AesStream {
     k.A = (k.aad_len + 15) >> 4;
     k.nblk = 1 + ((k.P + 15) >> 4);
     k.hp = k.act && !(d.flags & MQ_PKT_NO_HP);
-    const bool hp_slot = k.hp && k.nblk >= (uint32_t)G;  // else after the tag
+    const bool hp_slot = k.hp && k.nblk >= kHpSlotMin;  // else after the tag
     const int it_lo = -(int)Gp::wave_max(k.act ? (k.A + G - 2) / G : 0u);
     const int it_hi = (int)Gp::wave_max(k.act ? k.nblk / G + 1 : 0u);
     nonce_be(row, c.pn, k.nb);
@@ -287,7 +291,7 @@ struct AesStream {
         return ald16(arena + k.pkt + 16ull * (uint32_t)((int)k.A + b - 1));
       return make_uint4(0, 0, 0, 0);
     };
-    uint32_t acc[4] = {0, 0, 0, 0}, ej0[4] = {0, 0, 0, 0}, smp[4] = {0, 0, 0, 0};
+    uint32_t acc[4] = {0, 0, 0, 0}, ej0[4] = {0, 0, 0, 0}, smp[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0};
     uint32_t m0 = 0, m1 = 0;
     bool have_mask = false;
     uint4 cur = data(j + G * it_lo);
@@ -317,7 +321,7 @@ struct AesStream {
       const int b = j + G * it;
       const uint32_t ub = (uint32_t)b;
       const uint4 nxt = data(b + G);  // next iteration's block, in flight during this one
-      if (it >= 1 && it < it_lean) {  // interior iteration (wave-uniform)
+      if (it > kSmpIt && it < it_lean) {  // interior iteration (wave-uniform)
         uint32_t ks[4], ct[4], x[4];
         ctr<CACHED>(key, L, k, cc, ub, ks);
         ct[0] = cur.x ^ ks[0]; ct[1] = cur.y ^ ks[1]; ct[2] = cur.z ^ ks[2]; ct[3] = cur.w ^ ks[3];
@@ -380,10 +384,17 @@ struct AesStream {
 #pragma unroll
         for (int q = 0; q < 4; ++q) ej0[q] = ks[q];
       }
-      if (it == 0) {  // the HP sample: payload bytes [4 - pn_len, 20 - pn_len) from slots 1 and 2
+      if (G == 2 && it == 0) {  // slot 1 (lane 1); slot 2 comes in iteration 1
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s1[q] = Gp::template lane<G - 1>(ct[q]);
+      }
+      if (it == kSmpIt) {  // the HP sample: payload bytes [4 - pn_len, 20 - pn_len) from slots 1 and 2
         uint32_t src[8];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) { src[q] = Gp::template lane<1>(ct[q]); src[4 + q] = Gp::template lane<2>(ct[q]); }
+        for (int q = 0; q < 4; ++q) {
+          src[q] = G == 2 ? s1[q] : Gp::template lane<1 % G>(ct[q]);
+          src[4 + q] = Gp::template lane<2 % G>(ct[q]);
+        }
         const uint32_t o = 4u - (k.hp ? d.pn_len : 4u);
 #pragma unroll
         for (int q = 0; q < 4; ++q) smp[q] = __builtin_amdgcn_alignbyte(src[q + 1], src[q], o);
@@ -786,6 +797,7 @@ MQ_AES_KERNELS(mq_aes_seal_kernel, mq_aes_open_kernel, false, 8)
 MQ_AES_KERNELS(mq_aes_seal1_kernel, mq_aes_open1_kernel, true, 8)
 // narrow single-key kernels (r06): tiles of 16 short packets on 4 lanes each (AesStream G = 4)
 MQ_AES_KERNELS(mq_aes_seal1n_kernel, mq_aes_open1n_kernel, true, 4)
+MQ_AES_KERNELS(mq_aes_seal1n2_kernel, mq_aes_open1n2_kernel, true, 2)
 
 // Key-segmented single-key kernels (r03): for a partition list in the keyed layout whose keys carry
 // many packets each (config C with 1024 keys: 128 tiles per key), every key's segment runs at
@@ -896,6 +908,7 @@ __device__ __forceinline__ void aes_seg_tiles(const KeyRow* __restrict__ kt, uin
 MQ_AES_SEG_KERNELS(mq_aes_seals_kernel, mq_aes_opens_kernel, 8)
 // narrow tiles (16 packets on 4 lanes each) within every key's segment (r06)
 MQ_AES_SEG_KERNELS(mq_aes_sealsn_kernel, mq_aes_opensn_kernel, 4)
+MQ_AES_SEG_KERNELS(mq_aes_sealsn2_kernel, mq_aes_opensn2_kernel, 2)
 
 extern "C" __global__ __launch_bounds__(256) void mq_aes_hp_kernel(
     const KeyRow* __restrict__ kt, uint32_t n_rows, const uint32_t* __restrict__ key_ids,
@@ -978,15 +991,40 @@ static uint32_t aes_grid(uint32_t tiles, uint32_t waves, int cus) {
 // Measured (profiles/r06i_*): seal + open 64 B 150 -> 244 GiB/s, 256 B 421 -> 555, 700 B 651 -> 739,
 // 1200 B 732 -> 768 (config C: 3.18 -> 3.02 ms), 1500 B 758 -> 768; 1600 B 771 -> 759, 2048 B 796 -> 768
 // (r06j), so the octet kernels keep packets over 1536 B.
+// Flat batches up to MQ_AES_NARROW2_MAX bytes per packet take tiles of 32 packets on 2 lanes each
+// (r06l: 64 B 248 -> 339 GiB/s, 128 B 393 -> 505, 256 B 569 -> 619, 448 B equal, 700 B 757 -> 653:
+// a packet's 2 lanes walk 22+ iterations each).
 #ifndef MQ_AES_NARROW_MAX
 #define MQ_AES_NARROW_MAX 1536
 #endif
-constexpr uint64_t kAesNarrowMaxBpp = MQ_AES_NARROW_MAX;
-int mq_aes_flat_narrow(uint64_t bpp) {
+#ifndef MQ_AES_NARROW2_MAX
+#define MQ_AES_NARROW2_MAX 400
+#endif
+constexpr uint64_t kAesNarrowMaxBpp = MQ_AES_NARROW_MAX, kAesNarrow2MaxBpp = MQ_AES_NARROW2_MAX;
+// lanes per packet of the single-key tiles: MQ_AES_NARROW 0 -> 8, 1 -> 4, 2 -> 2; unset: flat
+// batches by their bytes per packet, partition segments (mixed lengths: config E 2.42 ms with 4,
+// 2.47 with 2, r06l) 4
+static int aes_lanes(bool flat, uint64_t bpp) {
   const long f = opt(Opt::AesNarrow);
-  if (f >= 0) return f != 0;
-  return bpp != 0 && bpp <= kAesNarrowMaxBpp;
+  if (f >= 0) return f == 0 ? 8 : f == 2 ? 2 : 4;
+  if (!flat) return 4;
+  if (bpp == 0 || bpp > kAesNarrowMaxBpp) return 8;
+  return bpp <= kAesNarrow2MaxBpp ? 2 : 4;
 }
+int mq_aes_flat_lanes(uint64_t bpp) { return aes_lanes(true, bpp); }
+using AesSealK = void (*)(const KeyRow*, uint32_t, uint8_t*, uint64_t, const mq_pkt_desc*, uint32_t, const uint32_t*,
+                          const uint32_t*, const uint32_t*, uint8_t*, uint32_t*);
+using AesOpenK = void (*)(const KeyRow*, uint32_t, uint8_t*, uint64_t, const mq_pkt_desc*, uint32_t, const uint32_t*,
+                          const uint32_t*, const uint32_t*, uint8_t*, uint64_t*, const uint2*, uint32_t*);
+using AesSegSealK = void (*)(const KeyRow*, uint32_t, uint8_t*, uint64_t, const mq_pkt_desc*, const uint32_t*,
+                             const uint32_t*, const uint32_t*, const uint32_t*, uint8_t*, uint32_t*);
+using AesSegOpenK = void (*)(const KeyRow*, uint32_t, uint8_t*, uint64_t, const mq_pkt_desc*, const uint32_t*,
+                             const uint32_t*, const uint32_t*, const uint32_t*, uint8_t*, uint64_t*, const uint2*,
+                             uint32_t*);
+static AesSealK seal1_of(int g) { return g == 2 ? mq_aes_seal1n2_kernel : g == 4 ? mq_aes_seal1n_kernel : mq_aes_seal1_kernel; }
+static AesOpenK open1_of(int g) { return g == 2 ? mq_aes_open1n2_kernel : g == 4 ? mq_aes_open1n_kernel : mq_aes_open1_kernel; }
+static AesSegSealK seals_of(int g) { return g == 2 ? mq_aes_sealsn2_kernel : g == 4 ? mq_aes_sealsn_kernel : mq_aes_seals_kernel; }
+static AesSegOpenK opens_of(int g) { return g == 2 ? mq_aes_opensn2_kernel : g == 4 ? mq_aes_opensn_kernel : mq_aes_opens_kernel; }
 
 hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* arena, uint64_t arena_len,
                          const mq_pkt_desc* desc, uint32_t n, const uint32_t* index, const uint32_t* n_dev,
@@ -995,8 +1033,9 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
                          uint32_t* sched_hs, uint64_t bpp) {
   const uint32_t tiles = (n + kPktsPerTile - 1) / kPktsPerTile;
   if (tiles == 0) return hipSuccess;
-  if (n_rows == 1 && !index && !n_dev && !hot && mq_aes_flat_narrow(bpp)) {
-    const uint32_t waves = aes_waves(true), blocks = aes_grid((n + 15) / 16, waves, cus);
+  const int gflat = aes_lanes(true, bpp);
+  if (n_rows == 1 && !index && !n_dev && !hot && gflat != 8) {
+    const uint32_t waves = aes_waves(true), ppt = 64u / (uint32_t)gflat, blocks = aes_grid((n + ppt - 1) / ppt, waves, cus);
     if (open && hpm && own_hp) {
       hipLaunchKernelGGL(mq_aes_open_hp_kernel<true>, dim3((n + 255) / 256), dim3(256), 0, s, kt, n_rows, arena,
                          arena_len, desc, n, index, n_dev, hpm);
@@ -1004,24 +1043,24 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
       if (e != hipSuccess) return e;
     }
     if (open)
-      hipLaunchKernelGGL(mq_aes_open1n_kernel, dim3(blocks), dim3(64 * waves), 0, s, kt, n_rows, arena, arena_len, desc,
+      hipLaunchKernelGGL(open1_of(gflat), dim3(blocks), dim3(64 * waves), 0, s, kt, n_rows, arena, arena_len, desc,
                          n, index, n_dev, hot, status, pn_out, hpm, sched_s);
     else
-      hipLaunchKernelGGL(mq_aes_seal1n_kernel, dim3(blocks), dim3(64 * waves), 0, s, kt, n_rows, arena, arena_len, desc,
+      hipLaunchKernelGGL(seal1_of(gflat), dim3(blocks), dim3(64 * waves), 0, s, kt, n_rows, arena, arena_len, desc,
                          n, index, n_dev, hot, status, sched_s);
     return hipGetLastError();
   }
   // the hot key's segment of a partition list, and the key-segmented kernels' segments, run narrow
   // tiles too, unless MQ_AES_NARROW=0
-  const bool hot_narrow = opt(Opt::AesNarrow) != 0;
+  const int ghot = aes_lanes(false, bpp);
   if (rowseg && index && hot && n_rows > 1 && !own_hp) {
     const uint32_t blocks = (uint32_t)(cus > 0 ? cus : 256);
     if (open)
-      hipLaunchKernelGGL(hot_narrow ? mq_aes_opensn_kernel : mq_aes_opens_kernel, dim3(blocks),
+      hipLaunchKernelGGL(opens_of(ghot), dim3(blocks),
                          dim3(64 * aes_seg_waves()), 0, s, kt, n_rows, arena, arena_len, desc, index, n_dev, hot,
                          rowseg, status, pn_out, hpm, sched_s);
     else
-      hipLaunchKernelGGL(hot_narrow ? mq_aes_sealsn_kernel : mq_aes_seals_kernel, dim3(blocks),
+      hipLaunchKernelGGL(seals_of(ghot), dim3(blocks),
                          dim3(64 * aes_seg_waves()), 0, s, kt, n_rows, arena, arena_len, desc, index, n_dev, hot,
                          rowseg, status, sched_s);
     return hipGetLastError();
@@ -1043,14 +1082,14 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
   if (hot && hs == s) sched_hs = nullptr;
   if (open) {
     if (hot)
-      hipLaunchKernelGGL(hot_narrow ? mq_aes_open1n_kernel : mq_aes_open1_kernel, dim3(hot_blocks),
+      hipLaunchKernelGGL(open1_of(ghot), dim3(hot_blocks),
                          dim3(64 * aes_waves(true)), 0, hs, kt, n_rows, arena, arena_len, desc, n, index, n_dev, hot,
                          status, pn_out, hpm, sched_hs);
     hipLaunchKernelGGL(n_rows == 1 ? mq_aes_open1_kernel : mq_aes_open_kernel, dim3(blocks), dim3(64 * waves),
                        0, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, hot, status, pn_out, hpm, sched_s);
   } else {
     if (hot)
-      hipLaunchKernelGGL(hot_narrow ? mq_aes_seal1n_kernel : mq_aes_seal1_kernel, dim3(hot_blocks),
+      hipLaunchKernelGGL(seal1_of(ghot), dim3(hot_blocks),
                          dim3(64 * aes_waves(true)), 0, hs, kt, n_rows, arena, arena_len, desc, n, index, n_dev, hot,
                          status, sched_hs);
     hipLaunchKernelGGL(n_rows == 1 ? mq_aes_seal1_kernel : mq_aes_seal_kernel, dim3(blocks), dim3(64 * waves),

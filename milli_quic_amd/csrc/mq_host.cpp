@@ -23,7 +23,7 @@
 using mq::KeyRow;
 
 int mq_chacha_flat_kind(uint64_t bpp);  // mq_chacha.hip
-int mq_aes_flat_narrow(uint64_t bpp);   // mq_aes.hip
+int mq_aes_flat_lanes(uint64_t bpp);    // mq_aes.hip
 
 // ---- diagnostic switches (mq_opts.h) ---------------------------------------------------------
 namespace {
@@ -73,7 +73,7 @@ extern "C" int mq_debug_chacha_flat_kind(uint64_t arena_len, uint32_t n, uint32_
 extern "C" int mq_debug_aes_flat_kind(uint64_t arena_len, uint32_t n, uint32_t suite_hint) {
   const uint64_t len_hint = suite_hint >> 16;
   if (n == 0) return -1;
-  return mq_aes_flat_narrow(len_hint ? len_hint : (arena_len + n - 1) / n) ? 0 : 1;
+  return mq_aes_flat_lanes(len_hint ? len_hint : (arena_len + n - 1) / n);
 }
 
 extern "C" long mq_debug_option_get(const char* name) {

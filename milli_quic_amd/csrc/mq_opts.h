@@ -21,7 +21,7 @@ enum class Opt : int {
   Resident,           // MQ_RESIDENT: 0 sends per-packet calls through a launch instead of the resident kernel
   ResidentTimeoutUs,  // MQ_RESIDENT_TIMEOUT_US: how long a per-packet call waits for the resident kernel
   RecvSeg,            // MQ_RECV_SEG: receive-walk segment length (0 = one segment per run)
-  AesNarrow,          // MQ_AES_NARROW: 0 / 1 forces the octet / narrow (16 packets per tile) flat AES kernels
+  AesNarrow,          // MQ_AES_NARROW: 0 / 1 / 2 forces 8 / 4 / 2 lanes per packet in the single-key AES kernels
   Count
 };
 

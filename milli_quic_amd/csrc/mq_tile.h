@@ -347,7 +347,7 @@ __device__ __forceinline__ bool write_unmasked_header(const S& sp, typename S::o
 // kernels): lane 4p + j holds dwords 2j (dw) and 2j + 1 (dw1).
 struct TilePrefetch {
   bool on;  // wave-uniform
-  uint32_t dw, hm, idx, dw1;
+  uint32_t dw, hm, idx, dw1, dw2, dw3;  // dw2, dw3: tiles of 32 packets on 2 lanes (dwords 4j .. 4j + 3)
 };
 
 template <int K>
@@ -363,7 +363,7 @@ __device__ __forceinline__ bool tile_ctx(uint32_t tile_id, const KeyRow* __restr
                                          const uint32_t* __restrict__ index, const uint32_t* __restrict__ n_dev,
                                          const uint2* __restrict__ hpm, const TilePrefetch& pf, PktCtx& c,
                                          const KeyRow*& row, uint32_t tid = threadIdx.x, uint32_t e0 = 0) {
-  static_assert(G == 8 || G == 4, "tiles of 8 or 16 packets");
+  static_assert(G == 8 || G == 4 || G == 2, "tiles of 8, 16 or 32 packets");
   const int lane = tid & (kWave - 1), p = lane / G;
   const uint32_t count = n_dev ? *n_dev : n;
   const uint32_t tile0 = e0 + tile_id * (uint32_t)(kWave / G);  // its first entry
@@ -380,10 +380,14 @@ __device__ __forceinline__ bool tile_ctx(uint32_t tile_id, const KeyRow* __restr
     if (G == 8) {
       w0 = oct_lane<0>(pf.dw); w1 = oct_lane<1>(pf.dw); w2 = oct_lane<2>(pf.dw); w3 = oct_lane<3>(pf.dw);
       w4 = oct_lane<4>(pf.dw); w5 = oct_lane<5>(pf.dw); w6 = oct_lane<6>(pf.dw); w7 = oct_lane<7>(pf.dw);
-    } else {
+    } else if (G == 4) {
       w0 = Grp<4>::lane<0>(pf.dw); w1 = Grp<4>::lane<0>(pf.dw1); w2 = Grp<4>::lane<1>(pf.dw);
       w3 = Grp<4>::lane<1>(pf.dw1); w4 = Grp<4>::lane<2>(pf.dw); w5 = Grp<4>::lane<2>(pf.dw1);
       w6 = Grp<4>::lane<3>(pf.dw); w7 = Grp<4>::lane<3>(pf.dw1);
+    } else {
+      w0 = Grp<2>::lane<0>(pf.dw); w1 = Grp<2>::lane<0>(pf.dw1); w2 = Grp<2>::lane<0>(pf.dw2);
+      w3 = Grp<2>::lane<0>(pf.dw3); w4 = Grp<2>::lane<1>(pf.dw); w5 = Grp<2>::lane<1>(pf.dw1);
+      w6 = Grp<2>::lane<1>(pf.dw2); w7 = Grp<2>::lane<1>(pf.dw3);
     }
     c.d.offset = (uint64_t)w1 << 32 | w0;
     c.d.len = w2; c.d.key_id = w3;
@@ -391,8 +395,8 @@ __device__ __forceinline__ bool tile_ctx(uint32_t tile_id, const KeyRow* __restr
     c.d.pn_offset = (uint16_t)w6; c.d.pn_len = (uint8_t)(w6 >> 16); c.d.flags = (uint8_t)(w6 >> 24);
     c.d.reserved = w7;
     if (OPEN && hpm) {
-      c.hm0 = G == 8 ? oct_lane<0>(pf.hm) : Grp<4>::lane<0>(pf.hm);
-      c.hm1 = G == 8 ? oct_lane<1>(pf.hm) : Grp<4>::lane<1>(pf.hm);
+      c.hm0 = G == 8 ? oct_lane<0>(pf.hm) : Grp<G>::template lane<0>(pf.hm);
+      c.hm1 = G == 8 ? oct_lane<1>(pf.hm) : Grp<G>::template lane<1 % G>(pf.hm);
     }
     if (!c.valid) {
       c.d.offset = 0; c.d.len = 0; c.d.key_id = 0; c.d.pn = 0; c.d.pn_offset = 0; c.d.pn_len = 0;
@@ -644,28 +648,34 @@ __device__ __forceinline__ void for_tiles(const TileSched& ts, const mq_pkt_desc
     if (t >= tiles || e >= count) return kListHole;
     return index ? index[e] : e;
   };
-  auto fetch = [&](uint32_t ix, uint32_t& dw, uint32_t& dw1, uint32_t& hm) {
+  auto fetch = [&](uint32_t ix, uint32_t& dw, uint32_t& dw1, uint32_t& dw2, uint32_t& dw3, uint32_t& hm) {
     const bool ok = ix != kListHole;
+    dw1 = dw2 = dw3 = 0;
     if (G == 8) {
       dw = ok ? reinterpret_cast<const uint32_t*>(desc)[(size_t)ix * 8 + j] : 0u;
-      dw1 = 0;
-    } else {
+    } else if (G == 4) {
       const uint2 v = ok ? reinterpret_cast<const uint2*>(desc)[(size_t)ix * 4 + j] : make_uint2(0, 0);
       dw = v.x;
       dw1 = v.y;
+    } else {
+      const uint4 v = ok ? reinterpret_cast<const uint4*>(desc)[(size_t)ix * 2 + j] : make_uint4(0, 0, 0, 0);
+      dw = v.x;
+      dw1 = v.y;
+      dw2 = v.z;
+      dw3 = v.w;
     }
     hm = (OPEN && hpm && ok && j < 2) ? reinterpret_cast<const uint32_t*>(hpm)[(size_t)ix * 2 + j] : 0u;
   };
   uint32_t t = base + ts.g;
   if (ts.ctr && t < tiles) issue();  // resolved right away by next(t): one wait per wave, at its start
   uint32_t t1 = next(t);
-  uint32_t ix0 = idx_of(t), ix1 = idx_of(t1), dw, dw1, hm;
-  fetch(ix0, dw, dw1, hm);
+  uint32_t ix0 = idx_of(t), ix1 = idx_of(t1), dw, dw1, dw2, dw3, hm;
+  fetch(ix0, dw, dw1, dw2, dw3, hm);
   while (t < tiles) {
-    const TilePrefetch pf{true, dw, hm, ix0, dw1};
+    const TilePrefetch pf{true, dw, hm, ix0, dw1, dw2, dw3};
     const uint32_t t2 = next(t1);
     const uint32_t ix2 = idx_of(t2);
-    fetch(ix1, dw, dw1, hm);
+    fetch(ix1, dw, dw1, dw2, dw3, hm);
     body(t, pf);
     t = t1; t1 = t2; ix0 = ix1; ix1 = ix2;
   }

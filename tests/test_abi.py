@@ -108,18 +108,20 @@ def test_flat_chacha_kernel_choice(mqlib):
 
 
 def test_flat_aes_kernel_choice(mqlib):
-    # r06: flat single-key AES-128-GCM batches of packets up to 1536 B run the narrow
-    # tiles (16 packets per wave); MQ_AES_NARROW forces either family
+    # r06: flat single-key AES-128-GCM batches run 2 lanes per packet up to 400 B per packet, 4 up
+    # to 1536 B, else 8; MQ_AES_NARROW 0 / 1 / 2 forces 8 / 4 / 2
     kind = mqlib.mq_debug_aes_flat_kind
     A = _lib.MQ_SUITE_AES128GCM
-    for L, want in ((21, 0), (64, 0), (512, 0), (513, 0), (1200, 0), (1536, 0), (1537, 1), (1 << 20, 1)):
+    for L, want in ((21, 2), (64, 2), (400, 2), (401, 4), (1200, 4), (1536, 4), (1537, 8), (1 << 20, 8)):
         assert kind(L * 1000, 1000, A) == want, L
         assert kind(1 << 40, 1000, A | _lib.MQ_BATCH_LEN_HINT(L)) == want, L
     with _lib.option("MQ_AES_NARROW", 1):
-        assert kind(4000 * 1000, 1000, A) == 0
+        assert kind(4000 * 1000, 1000, A) == 4
+    with _lib.option("MQ_AES_NARROW", 2):
+        assert kind(4000 * 1000, 1000, A) == 2
     with _lib.option("MQ_AES_NARROW", 0):
-        assert kind(64 * 1000, 1000, A) == 1
-    assert kind(64 * 1000, 1000, A) == 0
+        assert kind(64 * 1000, 1000, A) == 8
+    assert kind(64 * 1000, 1000, A) == 2
     assert kind(0, 0, A) == -1
 
 

@@ -244,10 +244,10 @@ def test_subrange_batch_len_hint(orc, hinted):
     assert v.tobytes() == w.arena.reshape(-1, 1200)[lo:hi, :1184].tobytes()
 
 
-# ---- narrow AES-128-GCM tiles (r06, VERDICT r04 #1 "both suites"): flat single-key batches of short
-# packets run 16 packets per tile on 4 lanes each (mq_aes.hip AesStream G = 4, the H^4 Horner
-# multiplier, the header-protection block in the free slot nblk once a packet has 4 CTR blocks);
-# MQ_AES_NARROW 0 / 1 forces the octet / narrow kernels. Reference: rustcrypto.rs:38-94 (seal /
+# ---- narrow AES-128-GCM tiles (r06, VERDICT r04 #1 "both suites"): single-key tiles of 16 packets on
+# 4 lanes each or 32 on 2 (mq_aes.hip AesStream G = 4 / 2, the H^G Horner multiplier, the
+# header-protection block in the free slot nblk once a packet has 4 CTR blocks); MQ_AES_NARROW
+# 0 / 1 / 2 forces 8 / 4 / 2 lanes per packet. Reference: rustcrypto.rs:38-94 (seal /
 # open), :175-186 (header protection), transmit.rs:625-755, recv.rs:340-421.
 AES = _lib.MQ_SUITE_AES128GCM
 
@@ -265,7 +265,7 @@ def _EnvAes(v):
 ])
 def test_aes_narrow_flat_vs_oracle(orc, lmin, lmax, n):
     keys, arena, sd, od, pns = short_batch(n, lmin, lmax, 1, seed=lmin * 5 + lmax, suite=AES)
-    roundtrip_vs_oracle(orc, keys, arena, sd, od, pns, hint=AES, env=_EnvAes)
+    roundtrip_vs_oracle(orc, keys, arena, sd, od, pns, modes=(None, "0", "1", "2"), hint=AES, env=_EnvAes)
 
 
 @pytest.mark.parametrize("lead", [0, 5, 13])
@@ -276,7 +276,7 @@ def test_aes_narrow_uniform_alignments(orc, lead):
         sd, od = w.seal_desc.copy(), w.open_desc.copy()
         sd["offset"] += lead
         od["offset"] += lead
-        roundtrip_vs_oracle(orc, w.keys, arena, sd, od, w.pns, modes=(None, "0", "1"), hint=AES, env=_EnvAes)
+        roundtrip_vs_oracle(orc, w.keys, arena, sd, od, w.pns, modes=(None, "0", "1", "2"), hint=AES, env=_EnvAes)
 
 
 def test_aes_narrow_forced_on_long_packets(orc):
@@ -285,7 +285,7 @@ def test_aes_narrow_forced_on_long_packets(orc):
     keys, arena, sd, od, pns = short_batch(900, 21, 4500, 1, seed=123, long_frac=0.5, suite=AES)
     od = od.copy()
     od["flags"] |= _lib.MQ_PKT_NO_RECV_LIMIT
-    roundtrip_vs_oracle(orc, keys, arena, sd, od, pns, modes=("1",), hint=AES, env=_EnvAes)
+    roundtrip_vs_oracle(orc, keys, arena, sd, od, pns, modes=("1", "2"), hint=AES, env=_EnvAes)
 
 
 def test_aes_narrow_failures_match_oracle(orc):
@@ -304,7 +304,7 @@ def test_aes_narrow_failures_match_oracle(orc):
     od["pn"][9] = (1 << 62) - 2            # decode_pn above 2^62 - 1 -> ProtocolViolation
     o_out, o_st, o_pn = oracle_run(orc, keys, bad, od, open_=True, hint=AES)
     assert (o_st != 0).sum() >= 250
-    for mode in (None, "0", "1"):
+    for mode in (None, "0", "1", "2"):
         with _EnvAes(mode):
             for use_ws in (True, False):
                 g_out, g_st, g_pn = gpu_run(keys, bad, od, open_=True, use_ws=use_ws, hint=AES)
@@ -317,7 +317,7 @@ def test_aes_narrow_failures_match_oracle(orc):
     sd["len"][9] = 20
     sd["key_id"][10] = 1 << 20
     o_out, o_st, _ = oracle_run(orc, keys, arena, sd, hint=AES)
-    for mode in (None, "1"):
+    for mode in (None, "1", "2"):
         with _EnvAes(mode):
             g_out, g_st, _ = gpu_run(keys, arena, sd, hint=AES)
             assert (g_st == o_st).all() and g_out.tobytes() == o_out.tobytes()
@@ -327,4 +327,24 @@ def test_aes_narrow_failures_match_oracle(orc):
 def test_aes_narrow_counts(orc, n):
     # tiles with one packet, exactly full tiles / workgroups (12 waves x 16 packets), partial ones
     keys, arena, sd, od, pns = short_batch(n, 21, 200, 1, seed=n + 1000, suite=AES)
-    roundtrip_vs_oracle(orc, keys, arena, sd, od, pns, modes=(None, "1"), hint=AES, env=_EnvAes)
+    roundtrip_vs_oracle(orc, keys, arena, sd, od, pns, modes=(None, "1", "2"), hint=AES, env=_EnvAes)
+
+
+@pytest.mark.parametrize("cfg,n,n_keys", [("c", 40000, 16), ("c", 20000, 3), ("e", 20000, 0)])
+def test_aes_narrow_partitioned_vs_oracle(orc, cfg, n, n_keys):
+    # partitioned AES (mixed hint): the hot key's segment on the narrow single-key kernel, the
+    # key-segmented kernels with narrow tiles inside every segment (segments start at any multiple
+    # of 8 entries), the multi-key octet kernel after the hot split; MQ_AES_NARROW 0 / 1 / 2 = 8 / 4
+    # / 2 lanes per packet
+    w = workload.config_c(n, n_keys=n_keys) if cfg == "c" else workload.config_e(n, seed=3)
+    hint = _lib.MQ_SUITE_MIXED
+    o_out, o_st, _ = oracle_run(orc, w.keys, w.arena, w.seal_desc, hint=hint)
+    o_back, o_st2, o_pn = oracle_run(orc, w.keys, o_out, w.open_desc, open_=True, hint=hint)
+    assert (o_st == 0).all() and (o_st2 == 0).all()
+    for mode in (None, "0", "1", "2"):
+        with _EnvAes(mode):
+            g_out, g_st, _ = gpu_run(w.keys, w.arena, w.seal_desc, hint=hint)
+            assert (g_st == o_st).all() and g_out.tobytes() == o_out.tobytes(), mode
+            g_back, g_st, g_pn = gpu_run(w.keys, o_out, w.open_desc, open_=True, hint=hint)
+            assert (g_st == o_st2).all() and (g_pn == o_pn).all(), mode
+            assert g_back.tobytes() == o_back.tobytes(), mode
