@@ -1080,15 +1080,30 @@ hipError_t mq_launch_aes(bool open, const KeyRow* kt, uint32_t n_rows, uint8_t* 
   if (own_hp && hs != s) return hipErrorInvalidValue;
   // two kernels at once on one stream's slot would share its heads
   if (hot && hs == s) sched_hs = nullptr;
+  // the hot segment on the key-segmented (slice) kernel: one workgroup per CU walks contiguous slices
+  // of the length-sorted segment (count = the segment's entries, so no row segment is ever reached).
+  // E's hot AES key alone 2.94 -> 2.54 ns per packet, hot + Initial keys 3.03 -> 2.76; the whole
+  // config-E batch unchanged (its ChaCha20 list after the multi-key kernel on s is the longer chain;
+  // profiles/r06q_*). MQ_AES_HOT_SEG=0: the tile kernel.
+  const bool hot_seg = hot && opt(Opt::AesHotSeg) != 0;
+  const uint32_t seg_blocks = (uint32_t)(cus > 0 ? cus : 256);
+  if (hot_seg) {
+    if (open)
+      hipLaunchKernelGGL(opens_of(ghot), dim3(seg_blocks), dim3(64 * aes_seg_waves()), 0, hs, kt, n_rows, arena,
+                         arena_len, desc, index, hot + 1, hot, (const uint32_t*)nullptr, status, pn_out, hpm, sched_hs);
+    else
+      hipLaunchKernelGGL(seals_of(ghot), dim3(seg_blocks), dim3(64 * aes_seg_waves()), 0, hs, kt, n_rows, arena,
+                         arena_len, desc, index, hot + 1, hot, (const uint32_t*)nullptr, status, sched_hs);
+  }
   if (open) {
-    if (hot)
+    if (hot && !hot_seg)
       hipLaunchKernelGGL(open1_of(ghot), dim3(hot_blocks),
                          dim3(64 * aes_waves(true)), 0, hs, kt, n_rows, arena, arena_len, desc, n, index, n_dev, hot,
                          status, pn_out, hpm, sched_hs);
     hipLaunchKernelGGL(n_rows == 1 ? mq_aes_open1_kernel : mq_aes_open_kernel, dim3(blocks), dim3(64 * waves),
                        0, s, kt, n_rows, arena, arena_len, desc, n, index, n_dev, hot, status, pn_out, hpm, sched_s);
   } else {
-    if (hot)
+    if (hot && !hot_seg)
       hipLaunchKernelGGL(seal1_of(ghot), dim3(hot_blocks),
                          dim3(64 * aes_waves(true)), 0, hs, kt, n_rows, arena, arena_len, desc, n, index, n_dev, hot,
                          status, sched_hs);

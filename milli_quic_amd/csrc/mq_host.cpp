@@ -29,7 +29,7 @@ int mq_aes_flat_lanes(uint64_t bpp);    // mq_aes.hip
 namespace {
 const char* const kOptNames[(int)mq::Opt::Count] = {
     "MQ_CC_NARROW", "MQ_CC_LONG",  "MQ_CC_LIST",           "MQ_HP_FORK", "MQ_AES_SEG",
-    "MQ_PROTECT_FUSED", "MQ_RESIDENT", "MQ_RESIDENT_TIMEOUT_US", "MQ_RECV_SEG", "MQ_AES_NARROW"};
+    "MQ_PROTECT_FUSED", "MQ_RESIDENT", "MQ_RESIDENT_TIMEOUT_US", "MQ_RECV_SEG", "MQ_AES_HOT_SEG", "MQ_AES_NARROW"};
 std::atomic<long> g_opts[(int)mq::Opt::Count];
 std::once_flag g_opts_once;
 void opts_init() {  // once: the environment's values (shell-driven diagnostics keep working)
@@ -1026,6 +1026,8 @@ static int batch(bool open, const mq_keytable* kt, uint8_t* arena, uint64_t aren
                                  ? nullptr
                                  : mq_partition_rowseg(n, kt->rows, counts);
     auto fork = fork_enabled() && !rowseg ? side_streams().fork(kt->device, s, 1) : mq::SideStreams<HipBackend>::Fork();
+    // list 1 stays on s: after the hot segment on its side stream instead it cost E 2 % (the slice
+    // kernel) to 10 % (the tile kernel) (profiles/r06r_ab_e_list1_after_hot_rejected.txt)
     hipStream_t s_hot = fork ? fork.side(0) : s, s_list1 = s;
     uint32_t* sched_s = sched_slot(kt->device, s);
     e = mq_launch_aes(open, kt->dev, kt->rows, arena, arena_len, desc, cap, list, counts, counts + 2, status, pn_out,

@@ -21,6 +21,7 @@ enum class Opt : int {
   Resident,           // MQ_RESIDENT: 0 sends per-packet calls through a launch instead of the resident kernel
   ResidentTimeoutUs,  // MQ_RESIDENT_TIMEOUT_US: how long a per-packet call waits for the resident kernel
   RecvSeg,            // MQ_RECV_SEG: receive-walk segment length (0 = one segment per run)
+  AesHotSeg,          // MQ_AES_HOT_SEG: 0 runs a partition's hot AES segment on the tile kernel, not the slice kernel
   AesNarrow,          // MQ_AES_NARROW: 0 / 1 / 2 forces 8 / 4 / 2 lanes per packet in the single-key AES kernels
   Count
 };
