@@ -365,22 +365,38 @@ def end_to_end(torch, batch, kt, w, sd, od, dev, reps=3):
 # kernel — then list 1 (ChaCha20, or the AES hint's leftovers on the multi-key kernel again).
 # mq_host.cpp batch() makes the same launches.
 PARTITION = ("mq_part_init_kernel", "mq_part_count_kernel", "mq_part_rows_kernel", "mq_part_scatter_kernel")
-AES_LIST0 = ("mq_aes_seal1_kernel", "mq_aes_seal_kernel")
+# single-key AES kernels by lanes per packet (r06 narrow tiles: mq_aes.hip aes_lanes)
+AES_SEAL1 = {8: "mq_aes_seal1_kernel", 4: "mq_aes_seal1n_kernel", 2: "mq_aes_seal1n2_kernel"}
+AES_SEALS = {8: "mq_aes_seals_kernel", 4: "mq_aes_sealsn_kernel", 2: "mq_aes_sealsn2_kernel"}
 
 
-def seal_kernels(cfg, n_rows, n=1 << 20, non_aes_rows=None):
+def aes_segment_kernel():
+    """The kernel a partition's hot AES key segment runs on (mq_aes.hip mq_launch_aes): the slice
+    kernel unless MQ_AES_HOT_SEG=0, with 4 lanes per packet unless MQ_AES_NARROW says otherwise."""
+    from milli_quic_amd import _lib
+    lib = _lib.load()
+    f = lib.mq_debug_option_get(b"MQ_AES_NARROW")
+    g = 4 if f < 0 else {0: 8, 2: 2}.get(f, 4)
+    return (AES_SEAL1 if lib.mq_debug_option_get(b"MQ_AES_HOT_SEG") == 0 else AES_SEALS)[g], g
+
+
+def seal_kernels(cfg, n_rows, n=1 << 20, non_aes_rows=None, arena_len=None):
     if cfg == "b":
         return ("mq_chacha_seal1_kernel",) if n_rows == 1 else ("mq_chacha_seal_kernel",)
     if cfg == "c":
         if n_rows == 1:
-            return ("mq_aes_seal1_kernel",)
+            from milli_quic_amd import _lib, batch
+            return (AES_SEAL1[batch.aes_flat_kind(arena_len or 1200 * n, n, _lib.MQ_SUITE_AES128GCM)],)
+        hot, g = aes_segment_kernel()
         if n >= 512 * n_rows:  # mq_host.cpp: keys with >= 512 packets each: the key-segmented kernel
-            return PARTITION + ("mq_aes_seals_kernel", "mq_aes_seal_kernel")
-        return PARTITION + AES_LIST0 + ("mq_aes_seal_kernel",)
+            return PARTITION + (AES_SEALS[g], "mq_aes_seal_kernel")
+        return PARTITION + (hot, "mq_aes_seal_kernel", "mq_aes_seal_kernel")
     if cfg == "e":
         # list 1 on the one-shot grid list kernels (mq_chacha.hip lgrid); a key table with one
         # non-AES row takes the single-key one
-        return PARTITION + AES_LIST0 + ("mq_chacha_seal_lgrid1_kernel" if non_aes_rows == 1 else "mq_chacha_seal_lgrid_kernel",)
+        hot, _ = aes_segment_kernel()
+        return PARTITION + (hot, "mq_aes_seal_kernel",
+                            "mq_chacha_seal_lgrid1_kernel" if non_aes_rows == 1 else "mq_chacha_seal_lgrid_kernel")
     return None
 
 
@@ -513,7 +529,7 @@ def main():
         algo_bytes = 2.0 * wire  # per launch: read + write of every wire byte
         achieved = algo_bytes / (seal_ms * 1e-3) / 1e9
         non_aes = sum(1 for k in w.keys if int(k.suite) != 1)  # MQ_SUITE_AES128GCM = 1
-        kerns = seal_kernels(args.config, len(w.keys), w.n, non_aes)
+        kerns = seal_kernels(args.config, len(w.keys), w.n, non_aes, len(w.arena))
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": load_traffic(args.config, kerns, args.keys) if w.n == 1 << 20 else None,

@@ -12,7 +12,7 @@ import pytest
 pytest.importorskip("torch")
 
 import bench  # noqa: E402
-from milli_quic_amd import shard, workload  # noqa: E402
+from milli_quic_amd import _lib, shard, workload  # noqa: E402
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 
@@ -99,14 +99,23 @@ def test_roofline_seal_composite_traffic():
     profiles/pmc_traffic_<cfg>.json."""
     assert bench.seal_kernels("b", 1) == ("mq_chacha_seal1_kernel",)  # HP inside the tile (r03)
     assert bench.seal_kernels("b", 1024) == ("mq_chacha_seal_kernel",)
-    assert bench.seal_kernels("c", 1) == ("mq_aes_seal1_kernel",)
-    assert bench.seal_kernels("e", 4098) == bench.PARTITION + bench.AES_LIST0 + ("mq_chacha_seal_lgrid_kernel",)
+    # single-key AES: 4 lanes per 1200-B packet, 2 per 64-B packet, 8 over 1536 B (r06 narrow tiles)
+    assert bench.seal_kernels("c", 1) == ("mq_aes_seal1n_kernel",)
+    assert bench.seal_kernels("c", 1, 1 << 20, None, 64 << 20) == ("mq_aes_seal1n2_kernel",)
+    assert bench.seal_kernels("c", 1, 1 << 20, None, 2048 << 20) == ("mq_aes_seal1_kernel",)
+    # the hot AES key's segment on the slice kernel (4 lanes per packet) beside the multi-key kernel
+    hot = ("mq_aes_sealsn_kernel", "mq_aes_seal_kernel")
+    assert bench.seal_kernels("e", 4098) == bench.PARTITION + hot + ("mq_chacha_seal_lgrid_kernel",)
     # config E's table has one non-AES row: its ChaCha20 list runs on the single-key kernel
-    assert bench.seal_kernels("e", 4098, 1 << 20, 1) == bench.PARTITION + bench.AES_LIST0 + ("mq_chacha_seal_lgrid1_kernel",)
+    assert bench.seal_kernels("e", 4098, 1 << 20, 1) == bench.PARTITION + hot + ("mq_chacha_seal_lgrid1_kernel",)
     # 1024 keys over 2^20 packets (>= 512 per row): the key-segmented kernel runs list 0 (r03);
     # 4096 keys: the hot split and the multi-key kernel
-    assert bench.seal_kernels("c", 1024) == bench.PARTITION + ("mq_aes_seals_kernel", "mq_aes_seal_kernel")
-    assert bench.seal_kernels("c", 4096) == bench.PARTITION + bench.AES_LIST0 + ("mq_aes_seal_kernel",)
+    assert bench.seal_kernels("c", 1024) == bench.PARTITION + ("mq_aes_sealsn_kernel", "mq_aes_seal_kernel")
+    assert bench.seal_kernels("c", 4096) == bench.PARTITION + hot + ("mq_aes_seal_kernel",)
+    with _lib.option("MQ_AES_NARROW", 0), _lib.option("MQ_AES_HOT_SEG", 0):
+        assert bench.seal_kernels("c", 1) == ("mq_aes_seal1_kernel",)
+        assert bench.seal_kernels("c", 4096) == bench.PARTITION + ("mq_aes_seal1_kernel", "mq_aes_seal_kernel",
+                                                                   "mq_aes_seal_kernel")
     assert bench.kernel_key("void mq_mixed_hp_kernel(mq::KeyRow const*, unsigned int)") == "mq_mixed_hp_kernel"
     for cfg in ("b", "c"):
         ks = bench.seal_kernels(cfg, 1)
