@@ -215,9 +215,9 @@ int mq_resident_phases(int device, uint32_t* ns, int n);
 const char* mq_status_str(int status);
 /* Diagnostic switches (A/B measurements and tests that run two kernel paths on one batch; no
  * switch changes a result): MQ_CC_NARROW, MQ_CC_LONG, MQ_CC_LIST, MQ_HP_FORK, MQ_AES_SEG,
- * MQ_PROTECT_FUSED, MQ_RESIDENT, MQ_RESIDENT_TIMEOUT_US, MQ_RECV_SEG, MQ_AES_NARROW. Each starts from the
- * environment variable of that name (read once, at the first use of any switch); value < 0 unsets
- * it (the product behaviour). MQ_OK, or MQ_ERR_INVALID_ARG for an unknown name. A batch reads each
+ * MQ_PROTECT_FUSED, MQ_RESIDENT, MQ_RESIDENT_TIMEOUT_US, MQ_RECV_SEG, MQ_AES_HOT_SEG, MQ_AES_NARROW.
+ * Each starts from the environment variable of that name (read once, at the first use of any
+ * switch); value < 0 unsets it (the product behaviour). MQ_OK, or MQ_ERR_INVALID_ARG for an unknown name. A batch reads each
  * switch once per call. */
 int mq_debug_option(const char* name, long value);
 /* The switch's value: -1 unset, -2 unknown name. */
