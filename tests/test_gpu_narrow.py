@@ -348,3 +348,24 @@ def test_aes_narrow_partitioned_vs_oracle(orc, cfg, n, n_keys):
             g_back, g_st, g_pn = gpu_run(w.keys, o_out, w.open_desc, open_=True, hint=hint)
             assert (g_st == o_st2).all() and (g_pn == o_pn).all(), mode
             assert g_back.tobytes() == o_back.tobytes(), mode
+
+
+@pytest.mark.parametrize("hinted", [False, True])
+def test_aes_subrange_batch_len_hint(orc, hinted):
+    # a flat AES batch over part of a larger arena: with MQ_BATCH_LEN_HINT(1200) it runs 4 lanes per
+    # packet (the narrow kernels of a tight arena), without it the arena's 7200 B per descriptor pick
+    # the octet kernels; same bytes either way, only the batch's packets touched
+    w = workload.config_c(24000)
+    lo, hi = 9000, 13000
+    hint = AES | (_lib.MQ_BATCH_LEN_HINT(1200) if hinted else 0)
+    assert batch.aes_flat_kind(len(w.arena), hi - lo, hint) == (4 if hinted else 8)
+    sd, od = w.seal_desc[lo:hi], w.open_desc[lo:hi]
+    o_out, o_st, _ = oracle_run(orc, w.keys, w.arena, sd, hint=AES)
+    assert (o_st == 0).all()
+    g_out, g_st, _ = gpu_run(w.keys, w.arena, sd, hint=hint)
+    assert (g_st == 0).all() and g_out.tobytes() == o_out.tobytes()
+    assert g_out[:1200 * lo].tobytes() == w.arena[:1200 * lo].tobytes()
+    g_back, g_st, g_pn = gpu_run(w.keys, g_out, od, open_=True, hint=hint)
+    assert (g_st == 0).all() and (g_pn == w.pns[lo:hi]).all()
+    v = g_back.reshape(-1, 1200)[lo:hi, :1184]
+    assert v.tobytes() == w.arena.reshape(-1, 1200)[lo:hi, :1184].tobytes()
